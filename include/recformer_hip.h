@@ -1,0 +1,116 @@
+/*
+ * librecformer_hip — C ABI of the MI355X-native Recformer encoder + scorer.
+ *
+ * The reference exposes no C ABI: its boundary is the Python class API of
+ * recformer/models.py (RecformerModel.forward models.py:274-356,
+ * RecformerForSeqRec.forward models.py:547-599). These entry points are what the
+ * build's autograd Functions (recformer_amd/ops.py) bind with ctypes; each one names
+ * the reference computation it replaces. See INTEGRATION.md for the bindings.
+ *
+ * Conventions:
+ *  - all pointers are DEVICE pointers owned by the caller (PyTorch's caching
+ *    allocator); the library never allocates, frees or synchronises;
+ *  - `stream` is the caller's hipStream_t (torch.cuda.current_stream().cuda_stream);
+ *    every call is asynchronous on it and safe to capture in a hipGraph;
+ *  - matrices are row-major with explicit leading dimensions in ELEMENTS;
+ *  - `dtype` selects the storage/compute type of activations and weights:
+ *    RF_F32 (fp32 storage, exact-fp32 MFMA) or RF_BF16 (bf16 storage, fp32 accumulate);
+ *    biases, LayerNorm affine parameters, norms and scores are always fp32;
+ *  - return 0 on success; otherwise rf_last_error() holds a thread-local message.
+ */
+#ifndef RECFORMER_HIP_H
+#define RECFORMER_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* rf_stream_t;
+
+enum { RF_OK = 0, RF_ERR_ARG = 1, RF_ERR_HIP = 2 };
+enum { RF_F32 = 0, RF_BF16 = 1 };
+enum {
+  RF_EPI_NONE = 0,       /* C = A.W^T                                   */
+  RF_EPI_BIAS = 1,       /* C = A.W^T + b              (nn.Linear)      */
+  RF_EPI_BIAS_GELU = 2,  /* C = gelu_erf(A.W^T + b)    (TF:1113-1116)   */
+  RF_EPI_BIAS_RESID = 3, /* C = A.W^T + b + R          (TF:1068-1071 / 1127-1130, pre-LN) */
+  RF_EPI_COS = 4         /* C(f32) = A.W^T * ra[m] * rw[n] * scale (Similarity, models.py:358-369) */
+};
+
+const char* rf_last_error(void);
+int rf_abi_version(void);
+
+/* A2 — RecformerModel.forward prologue, models.py:306-329 (_merge_to_attention_mask
+ * 262-272, _pad_to_window_size 210-260) + create_position_ids_from_input_ids 68-79.
+ * Inputs (B,L) int64 (attention_mask / global_attention_mask / token_type_ids /
+ * position_ids may be NULL = reference defaults). Outputs (B,Lp) int32 ids/pos/type/
+ * item-pos, uint8 flags {0 pad, 1 local, 2 global}, and gidx (B,gmax) int32 = the
+ * positions of each row's global tokens in order, -1 padded (replaces the nonzero()
+ * bookkeeping of TF:869-896 without a host sync). */
+int rf_prepare_inputs(const int64_t* input_ids, const int64_t* attention_mask,
+                      const int64_t* global_attention_mask, const int64_t* token_type_ids,
+                      const int64_t* item_position_ids, const int64_t* position_ids,
+                      int B, int L, int Lp, int pad_id, int gmax,
+                      int32_t* ids, int32_t* pos, int32_t* tt, int32_t* ip, uint8_t* flags,
+                      int32_t* gidx, rf_stream_t stream);
+
+/* A3 — RecformerEmbeddings.forward, models.py:108-138: LN(Ew[id] + Ep[pos] + Et[tt] +
+ * Ei[ip]) for M tokens, one fused pass (tables in `dtype`, LN params fp32). */
+int rf_embed_ln_fwd(int dtype, int M, int D, const int32_t* ids, const int32_t* pos,
+                    const int32_t* tt, const int32_t* ip, const void* word_emb,
+                    const void* pos_emb, const void* type_emb, const void* ipos_emb,
+                    const float* ln_w, const float* ln_b, float eps, void* out,
+                    rf_stream_t stream);
+
+/* A4 linears — nn.Linear / the 9 addmm per layer (TF:504-506, 982-984, 1064-1071,
+ * 1107, 1123) on MFMA: C[M,N] = epi(A[M,K] . W[N,K]^T). The first `scale_cols`
+ * output columns are multiplied by `col_scale` after the bias (the q/sqrt(hd) of
+ * TF:514). EPI_COS writes fp32 C and needs ra (M) / rw (N) inverse norms. */
+int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, const void* W, int ldw,
+            const float* bias, const void* resid, int ldr, void* C, int ldc, int epilogue,
+            int scale_cols, float col_scale, const float* ra, const float* rw,
+            rf_stream_t stream);
+
+/* LayerNorm over rows of D (TF:1071, 1130; nn.LayerNorm eps). mean/rstd (M) optional. */
+int rf_layernorm_fwd(int dtype, int M, int D, const void* x, int ldx, const float* w,
+                     const float* b, float eps, void* y, int ldy, float* mean, float* rstd,
+                     rf_stream_t stream);
+
+/* A5 — LongformerSelfAttention local branch (TF:482-604 with _sliding_chunks_* 759-867,
+ * _mask_invalid_locations 743-757, _concat_with_global_key_attn_probs 898-926,
+ * _compute_attn_output_with_global_indices 928-962). q (pre-scaled), k, v are
+ * (B*Lp, *) row-major with leading dim ld_qkv, head h at column h*hd. hd must be 64.
+ * Output ctx (B*Lp, H*hd), ld_out; padded query rows are written as 0. */
+int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
+                     const void* k, const void* v, int ld_qkv, const uint8_t* flags,
+                     const int32_t* gidx, int gmax, void* out, int ld_out, rf_stream_t stream);
+
+/* A6 — global query rows, _compute_global_attn_output_from_hidden TF:964-1057 + the
+ * overwrite TF:612-629: for every (b, g < count_b): ctx[gidx[b,g], h] =
+ * softmax(qg[b*gmax+g, h] . kg[b, :, h]^T over valid keys) . vg[b, :, h]. */
+int rf_global_attn_fwd(int dtype, int B, int Lp, int H, int hd, const void* qg, int ld_qg,
+                       const void* kg, const void* vg, int ld_kv, const uint8_t* flags,
+                       const int32_t* gidx, int gmax, void* out, int ld_out,
+                       rf_stream_t stream);
+
+/* Row gather: out[r] = x[b*Lp + gidx[b, g]] for r = b*gmax + g (zero rows for -1). Feeds
+ * the query_global projection of the global rows (TF:972-982). */
+int rf_gather_global_rows(int dtype, int B, int Lp, int D, int gmax, const void* x, int ldx,
+                          const int32_t* gidx, void* out, rf_stream_t stream);
+
+/* A8 helpers — 1 / max(||x_m||, eps) per row (torch cosine_similarity clamp, models.py:366). */
+int rf_row_inv_norm(int dtype, int M, int D, const void* x, int ldx, float eps, float* out,
+                    rf_stream_t stream);
+
+/* A8 sampled candidates — similarity_score with candidates (models.py:539-545):
+ * s[b,c] = <z_b, E[cand[b,c]]> * rz[b] * re[cand[b,c]] * inv_temp. */
+int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, const float* rz,
+                      const void* items, int ldi, const float* ri, const int64_t* cand,
+                      float inv_temp, float* scores, rf_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RECFORMER_HIP_H */

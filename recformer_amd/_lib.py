@@ -1,0 +1,67 @@
+"""ctypes binding of librecformer_hip.so (the C ABI declared in include/recformer_hip.h).
+
+The product path has no CPU fallback: if the library is missing or a tensor is not on a
+ROCm device, calls raise immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_void_p
+from typing import Optional
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librecformer_hip.so")
+
+RF_F32, RF_BF16 = 0, 1
+RF_EPI_NONE, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF_EPI_COS = 0, 1, 2, 3, 4
+
+# symbol -> (restype, argtypes); must match include/recformer_hip.h exactly
+P = c_void_p
+SIGNATURES = {
+    "rf_last_error": (ctypes.c_char_p, []),
+    "rf_abi_version": (c_int, []),
+    "rf_prepare_inputs": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
+                                  P, P, P, P, P, P, P]),
+    "rf_embed_ln_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_float, P, P]),
+    "rf_gemm": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, P, c_int, P, c_int,
+                        c_int, c_int, c_float, P, P, P]),
+    "rf_layernorm_fwd": (c_int, [c_int, c_int, c_int, P, c_int, P, P, c_float, P, c_int, P, P, P]),
+    "rf_band_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
+                                 c_int, P, c_int, P]),
+    "rf_global_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P,
+                                   P, c_int, P, c_int, P]),
+    "rf_gather_global_rows": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
+    "rf_row_inv_norm": (c_int, [c_int, c_int, c_int, P, c_int, c_float, P, P]),
+    "rf_cos_score_cand": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P,
+                                  c_float, P, P]),
+}
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+class RecformerHipError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and type the library. Raises if it has not been built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.isfile(path):
+        raise RecformerHipError(
+            f"librecformer_hip.so not found at {path}: build it with "
+            f"`python -c 'import __graft_entry__ as g; g.build()'` (make -C recformer_amd/csrc)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().rf_last_error().decode(errors="replace")
+        raise RecformerHipError(f"{what} failed (rc={rc}): {msg}")

@@ -1,0 +1,79 @@
+// Shared device/host helpers for librecformer_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/recformer_hip.h"
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+namespace rf {
+
+// ---- error plumbing (no C++ exception crosses the C ABI) ------------------------------
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define RF_REQUIRE(cond, ...)                 \
+  do {                                        \
+    if (!(cond)) {                            \
+      ::rf::set_error(__VA_ARGS__);           \
+      return RF_ERR_ARG;                      \
+    }                                         \
+  } while (0)
+
+#define RF_LAUNCH_CHECK(name)                                                         \
+  do {                                                                                \
+    hipError_t _e = hipGetLastError();                                                \
+    if (_e != hipSuccess) {                                                           \
+      ::rf::set_error("%s: launch failed: %s", name, hipGetErrorString(_e));          \
+      return RF_ERR_HIP;                                                              \
+    }                                                                                 \
+    return RF_OK;                                                                     \
+  } while (0)
+
+inline hipStream_t as_stream(rf_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- scalar conversions ---------------------------------------------------------------
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// exact-erf GELU (transformers ACT2FN['gelu'], TF:1115)
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// ---- wave64 reductions ----------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 16-byte global->LDS DMA: LDS destination is (wave-uniform base + lane*16); the global
+// source is per lane (cdna_hip_programming.md §5 'Async global->LDS copy').
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)gsrc,
+      (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Byte offset of 16-B chunk `ch` (0..7) of row `row` in a [rows][64 x bf16] LDS tile
+// (128-B rows) with the XOR swizzle ch ^ (row & 7): conflict-free ds_read_b128 of the
+// MFMA 16x16x32 operand pattern (rows l&15, chunk l>>4) — guide §5.5 T2.
+__device__ __forceinline__ int swz128(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
+
+}  // namespace rf

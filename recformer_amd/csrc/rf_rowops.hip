@@ -1,0 +1,452 @@
+// Row-wise HBM-bound kernels: input prologue, fused embedding+LayerNorm, LayerNorm,
+// inverse row norms, global-row gather, candidate cosine scores.
+// One wave64 per row; each lane owns D/64 elements loaded as 8-16 B vectors
+// (cdna_hip_programming.md Guideline 13). All statistics in fp32.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "rf_common.h"
+
+namespace rf {
+
+static thread_local char g_err[512];
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+void clear_error() { g_err[0] = 0; }
+
+// ------------------------------------------------------------------------------------
+// vector load/store of VEC elements at p (VEC*sizeof(T) bytes, naturally aligned)
+template <typename T, int VEC> struct Vec;
+template <> struct Vec<float, 4> {
+  static __device__ __forceinline__ void load(const float* p, float* o) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float* o) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+};
+template <> struct Vec<float, 2> {
+  static __device__ __forceinline__ void load(const float* p, float* o) {
+    float2 v = *reinterpret_cast<const float2*>(p);
+    o[0] = v.x; o[1] = v.y;
+  }
+  static __device__ __forceinline__ void store(float* p, const float* o) {
+    *reinterpret_cast<float2*>(p) = make_float2(o[0], o[1]);
+  }
+};
+template <> struct Vec<float, 1> {
+  static __device__ __forceinline__ void load(const float* p, float* o) { o[0] = *p; }
+  static __device__ __forceinline__ void store(float* p, const float* o) { *p = o[0]; }
+};
+template <> struct Vec<bf16, 4> {
+  static __device__ __forceinline__ void load(const bf16* p, float* o) {
+    bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float* o) {
+    bf16x4 v;
+    v[0] = (bf16)o[0]; v[1] = (bf16)o[1]; v[2] = (bf16)o[2]; v[3] = (bf16)o[3];
+    *reinterpret_cast<bf16x4*>(p) = v;
+  }
+};
+template <> struct Vec<bf16, 2> {
+  static __device__ __forceinline__ void load(const bf16* p, float* o) {
+    bf16x2 v = *reinterpret_cast<const bf16x2*>(p);
+    o[0] = (float)v[0]; o[1] = (float)v[1];
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float* o) {
+    bf16x2 v;
+    v[0] = (bf16)o[0]; v[1] = (bf16)o[1];
+    *reinterpret_cast<bf16x2*>(p) = v;
+  }
+};
+template <> struct Vec<bf16, 1> {
+  static __device__ __forceinline__ void load(const bf16* p, float* o) { o[0] = (float)*p; }
+  static __device__ __forceinline__ void store(bf16* p, const float* o) { *p = (bf16)o[0]; }
+};
+
+// ------------------------------------------------------------------------------------
+// 256-thread block exclusive scan of one int per thread.
+__device__ __forceinline__ int block_excl_scan256(int v, int* lds /*[8]*/, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) lds[wid] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    int s = lds[w];
+    if (w < wid) base += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+// A2 prologue. One 256-thread block per sequence.
+__global__ void __launch_bounds__(256) k_prepare(
+    const int64_t* __restrict__ ids_in, const int64_t* __restrict__ am_in,
+    const int64_t* __restrict__ gm_in, const int64_t* __restrict__ tt_in,
+    const int64_t* __restrict__ ip_in, const int64_t* __restrict__ pos_in, int L, int Lp,
+    int pad_id, int gmax, int32_t* __restrict__ ids, int32_t* __restrict__ pos,
+    int32_t* __restrict__ tt, int32_t* __restrict__ ip, uint8_t* __restrict__ flags,
+    int32_t* __restrict__ gidx) {
+  __shared__ int scan_lds[8];
+  const int b = blockIdx.x;
+  const int per = (Lp + 255) / 256;
+  const int p0 = threadIdx.x * per;
+  const int p1 = min(p0 + per, Lp);
+  const int64_t* idr = ids_in + (int64_t)b * L;
+  int cnt_tok = 0, cnt_glob = 0;
+  for (int p = p0; p < p1; ++p) {
+    int64_t id = p < L ? idr[p] : pad_id;
+    cnt_tok += (id != pad_id);
+    if (p < L) {
+      int64_t am = am_in ? am_in[(int64_t)b * L + p] : 1;
+      int64_t m = gm_in ? am * (gm_in[(int64_t)b * L + p] + 1) : am;
+      cnt_glob += (m > 1);
+    }
+  }
+  int tot_tok, tot_glob;
+  int run_tok = block_excl_scan256(cnt_tok, scan_lds, &tot_tok);
+  int run_glob = block_excl_scan256(cnt_glob, scan_lds, &tot_glob);
+  for (int p = p0; p < p1; ++p) {
+    const int64_t o = (int64_t)b * Lp + p;
+    const int64_t i = (int64_t)b * L + p;
+    int64_t id = p < L ? idr[p] : pad_id;
+    int nonpad = id != pad_id;
+    run_tok += nonpad;
+    int32_t posv;
+    if (pos_in)
+      posv = p < L ? (int32_t)pos_in[i] : pad_id;
+    else
+      posv = nonpad ? run_tok + pad_id : pad_id;
+    uint8_t f = 0;
+    int32_t ttv = 0, ipv = pad_id;
+    if (p < L) {
+      int64_t am = am_in ? am_in[i] : 1;
+      int64_t m = gm_in ? am * (gm_in[i] + 1) : am;
+      f = m <= 0 ? 0 : (m == 1 ? 1 : 2);
+      ttv = tt_in ? (int32_t)tt_in[i] : 0;
+      ipv = (int32_t)ip_in[i];
+      if (f == 2) {
+        if (run_glob < gmax) gidx[(int64_t)b * gmax + run_glob] = p;
+        ++run_glob;
+      }
+    }
+    ids[o] = (int32_t)id;
+    pos[o] = posv;
+    tt[o] = ttv;
+    ip[o] = ipv;
+    flags[o] = f;
+  }
+  for (int g = tot_glob + threadIdx.x; g < gmax; g += 256) gidx[(int64_t)b * gmax + g] = -1;
+}
+
+// ------------------------------------------------------------------------------------
+// Fused embedding gather + LayerNorm (A3). One wave per token.
+template <typename T, int VEC, int NCH>
+__global__ void __launch_bounds__(256) k_embed_ln(
+    int M, const int32_t* __restrict__ ids, const int32_t* __restrict__ pos,
+    const int32_t* __restrict__ tt, const int32_t* __restrict__ ip, const T* __restrict__ we,
+    const T* __restrict__ pe, const T* __restrict__ te, const T* __restrict__ ie,
+    const float* __restrict__ lw, const float* __restrict__ lb, float eps, T* __restrict__ out) {
+  constexpr int D = 64 * VEC * NCH;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int64_t r0 = (int64_t)ids[row] * D, r1 = (int64_t)pos[row] * D;
+  const int64_t r2 = (int64_t)tt[row] * D, r3 = (int64_t)ip[row] * D;
+  float x[NCH][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = c * 64 * VEC + lane * VEC;
+    float a[VEC], b2[VEC], c2[VEC], d2[VEC];
+    Vec<T, VEC>::load(we + r0 + e, a);
+    Vec<T, VEC>::load(pe + r1 + e, b2);
+    Vec<T, VEC>::load(te + r2 + e, c2);
+    Vec<T, VEC>::load(ie + r3 + e, d2);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      // summation order of models.py:135: ((word + pos) + type) + item_pos
+      x[c][j] = ((a[j] + b2[j]) + c2[j]) + d2[j];
+      s += x[c][j];
+    }
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float v = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float d = x[c][j] - mean;
+      v += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(v) * (1.0f / D) + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = c * 64 * VEC + lane * VEC;
+    float w[VEC], bb[VEC], y[VEC];
+    Vec<float, VEC>::load(lw + e, w);
+    Vec<float, VEC>::load(lb + e, bb);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) y[j] = (x[c][j] - mean) * rstd * w[j] + bb[j];
+    Vec<T, VEC>::store(out + (int64_t)row * D + e, y);
+  }
+}
+
+template <typename T, int VEC, int NCH>
+__global__ void __launch_bounds__(256) k_layernorm(int M, const T* __restrict__ x, int ldx,
+                                                    const float* __restrict__ lw,
+                                                    const float* __restrict__ lb, float eps,
+                                                    T* __restrict__ y, int ldy,
+                                                    float* __restrict__ mean_out,
+                                                    float* __restrict__ rstd_out) {
+  constexpr int D = 64 * VEC * NCH;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float xv[NCH][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    Vec<T, VEC>::load(x + (int64_t)row * ldx + c * 64 * VEC + lane * VEC, xv[c]);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) s += xv[c][j];
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float v = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float d = xv[c][j] - mean;
+      v += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(v) * (1.0f / D) + eps);
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = c * 64 * VEC + lane * VEC;
+    float w[VEC], bb[VEC], o[VEC];
+    Vec<float, VEC>::load(lw + e, w);
+    Vec<float, VEC>::load(lb + e, bb);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (xv[c][j] - mean) * rstd * w[j] + bb[j];
+    Vec<T, VEC>::store(y + (int64_t)row * ldy + e, o);
+  }
+}
+
+template <typename T, int VEC, int NCH>
+__global__ void __launch_bounds__(256) k_row_inv_norm(int M, const T* __restrict__ x, int ldx,
+                                                       float eps, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    float xv[VEC];
+    Vec<T, VEC>::load(x + (int64_t)row * ldx + c * 64 * VEC + lane * VEC, xv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) s += xv[j] * xv[j];
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[row] = 1.0f / fmaxf(sqrtf(s), eps);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_gather_rows(int Lp, int D, int gmax, const T* __restrict__ x,
+                                                      int ldx, const int32_t* __restrict__ gidx,
+                                                      T* __restrict__ out) {
+  const int r = blockIdx.x;  // r = b*gmax + g
+  const int b = r / gmax;
+  const int p = gidx[r];
+  for (int e = threadIdx.x; e < D; e += 256)
+    out[(int64_t)r * D + e] = p >= 0 ? x[((int64_t)b * Lp + p) * ldx + e] : from_f32<T>(0.f);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_cos_cand(int B, int C, int D, const T* __restrict__ z,
+                                                   int ldz, const float* __restrict__ rz,
+                                                   const T* __restrict__ items, int ldi,
+                                                   const float* __restrict__ ri,
+                                                   const int64_t* __restrict__ cand,
+                                                   float inv_temp, float* __restrict__ scores) {
+  const int lane = threadIdx.x & 63;
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (idx >= B * C) return;
+  const int b = idx / C;
+  const int64_t n = cand[idx];
+  float s = 0.f;
+  for (int e = lane; e < D; e += 64) s += to_f32(z[(int64_t)b * ldz + e]) * to_f32(items[n * ldi + e]);
+  s = wave_sum(s);
+  if (lane == 0) scores[idx] = s * rz[b] * ri[n] * inv_temp;
+}
+
+// ------------------------------------------------------------------------------------
+// D dispatch: 64*VEC*NCH == D
+#define RF_ROW_DISPATCH(D, LAUNCH)                                      \
+  do {                                                                  \
+    switch (D) {                                                        \
+      case 64: LAUNCH(1, 1); break;                                     \
+      case 128: LAUNCH(2, 1); break;                                    \
+      case 256: LAUNCH(4, 1); break;                                    \
+      case 384: LAUNCH(2, 3); break;                                    \
+      case 512: LAUNCH(4, 2); break;                                    \
+      case 768: LAUNCH(4, 3); break;                                    \
+      case 1024: LAUNCH(4, 4); break;                                   \
+      default:                                                          \
+        ::rf::set_error("row kernel: unsupported width D=%d", (int)D);  \
+        return RF_ERR_ARG;                                              \
+    }                                                                   \
+  } while (0)
+
+}  // namespace rf
+
+using namespace rf;
+
+extern "C" {
+
+const char* rf_last_error(void) { return rf::g_err; }
+int rf_abi_version(void) { return 1; }
+
+int rf_prepare_inputs(const int64_t* input_ids, const int64_t* attention_mask,
+                      const int64_t* global_attention_mask, const int64_t* token_type_ids,
+                      const int64_t* item_position_ids, const int64_t* position_ids, int B,
+                      int L, int Lp, int pad_id, int gmax, int32_t* ids, int32_t* pos,
+                      int32_t* tt, int32_t* ip, uint8_t* flags, int32_t* gidx,
+                      rf_stream_t stream) {
+  RF_REQUIRE(input_ids && item_position_ids && ids && pos && tt && ip && flags,
+             "rf_prepare_inputs: null pointer");
+  RF_REQUIRE(B > 0 && L > 0 && Lp >= L, "rf_prepare_inputs: bad shape B=%d L=%d Lp=%d", B, L, Lp);
+  RF_REQUIRE(gmax == 0 || gidx, "rf_prepare_inputs: gidx required when gmax>0");
+  k_prepare<<<B, 256, 0, as_stream(stream)>>>(input_ids, attention_mask, global_attention_mask,
+                                               token_type_ids, item_position_ids, position_ids,
+                                               L, Lp, pad_id, gmax, ids, pos, tt, ip, flags,
+                                               gidx);
+  RF_LAUNCH_CHECK("rf_prepare_inputs");
+}
+
+int rf_embed_ln_fwd(int dtype, int M, int D, const int32_t* ids, const int32_t* pos,
+                    const int32_t* tt, const int32_t* ip, const void* word_emb,
+                    const void* pos_emb, const void* type_emb, const void* ipos_emb,
+                    const float* ln_w, const float* ln_b, float eps, void* out,
+                    rf_stream_t stream) {
+  RF_REQUIRE(M >= 0, "rf_embed_ln_fwd: bad M");
+  if (M == 0) return RF_OK;
+  dim3 grid((M + 3) / 4);
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16) {
+#define L_(V, N)                                                                              \
+  k_embed_ln<bf16, V, N><<<grid, 256, 0, s>>>(M, ids, pos, tt, ip, (const bf16*)word_emb,      \
+                                               (const bf16*)pos_emb, (const bf16*)type_emb,    \
+                                               (const bf16*)ipos_emb, ln_w, ln_b, eps, (bf16*)out)
+    RF_ROW_DISPATCH(D, L_);
+#undef L_
+  } else if (dtype == RF_F32) {
+#define L_(V, N)                                                                                \
+  k_embed_ln<float, V, N><<<grid, 256, 0, s>>>(M, ids, pos, tt, ip, (const float*)word_emb,      \
+                                                (const float*)pos_emb, (const float*)type_emb,   \
+                                                (const float*)ipos_emb, ln_w, ln_b, eps,         \
+                                                (float*)out)
+    RF_ROW_DISPATCH(D, L_);
+#undef L_
+  } else {
+    RF_REQUIRE(false, "rf_embed_ln_fwd: bad dtype %d", dtype);
+  }
+  RF_LAUNCH_CHECK("rf_embed_ln_fwd");
+}
+
+int rf_layernorm_fwd(int dtype, int M, int D, const void* x, int ldx, const float* w,
+                     const float* b, float eps, void* y, int ldy, float* mean, float* rstd,
+                     rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && ldx >= D && ldy >= D, "rf_layernorm_fwd: bad shape");
+  if (M == 0) return RF_OK;
+  dim3 grid((M + 3) / 4);
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16) {
+#define L_(V, N) \
+  k_layernorm<bf16, V, N><<<grid, 256, 0, s>>>(M, (const bf16*)x, ldx, w, b, eps, (bf16*)y, ldy, mean, rstd)
+    RF_ROW_DISPATCH(D, L_);
+#undef L_
+  } else if (dtype == RF_F32) {
+#define L_(V, N) \
+  k_layernorm<float, V, N><<<grid, 256, 0, s>>>(M, (const float*)x, ldx, w, b, eps, (float*)y, ldy, mean, rstd)
+    RF_ROW_DISPATCH(D, L_);
+#undef L_
+  } else {
+    RF_REQUIRE(false, "rf_layernorm_fwd: bad dtype %d", dtype);
+  }
+  RF_LAUNCH_CHECK("rf_layernorm_fwd");
+}
+
+int rf_row_inv_norm(int dtype, int M, int D, const void* x, int ldx, float eps, float* out,
+                    rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && ldx >= D, "rf_row_inv_norm: bad shape");
+  if (M == 0) return RF_OK;
+  dim3 grid((M + 3) / 4);
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16) {
+#define L_(V, N) k_row_inv_norm<bf16, V, N><<<grid, 256, 0, s>>>(M, (const bf16*)x, ldx, eps, out)
+    RF_ROW_DISPATCH(D, L_);
+#undef L_
+  } else if (dtype == RF_F32) {
+#define L_(V, N) k_row_inv_norm<float, V, N><<<grid, 256, 0, s>>>(M, (const float*)x, ldx, eps, out)
+    RF_ROW_DISPATCH(D, L_);
+#undef L_
+  } else {
+    RF_REQUIRE(false, "rf_row_inv_norm: bad dtype %d", dtype);
+  }
+  RF_LAUNCH_CHECK("rf_row_inv_norm");
+}
+
+int rf_gather_global_rows(int dtype, int B, int Lp, int D, int gmax, const void* x, int ldx,
+                          const int32_t* gidx, void* out, rf_stream_t stream) {
+  RF_REQUIRE(B >= 0 && gmax >= 0 && ldx >= D, "rf_gather_global_rows: bad shape");
+  if (B == 0 || gmax == 0) return RF_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16)
+    k_gather_rows<bf16><<<B * gmax, 256, 0, s>>>(Lp, D, gmax, (const bf16*)x, ldx, gidx, (bf16*)out);
+  else if (dtype == RF_F32)
+    k_gather_rows<float><<<B * gmax, 256, 0, s>>>(Lp, D, gmax, (const float*)x, ldx, gidx, (float*)out);
+  else
+    RF_REQUIRE(false, "rf_gather_global_rows: bad dtype %d", dtype);
+  RF_LAUNCH_CHECK("rf_gather_global_rows");
+}
+
+int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, const float* rz,
+                      const void* items, int ldi, const float* ri, const int64_t* cand,
+                      float inv_temp, float* scores, rf_stream_t stream) {
+  RF_REQUIRE(B >= 0 && C >= 0 && D > 0, "rf_cos_score_cand: bad shape");
+  if (B == 0 || C == 0) return RF_OK;
+  dim3 grid((B * C + 3) / 4);
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16)
+    k_cos_cand<bf16><<<grid, 256, 0, s>>>(B, C, D, (const bf16*)z, ldz, rz, (const bf16*)items, ldi,
+                                          ri, cand, inv_temp, scores);
+  else if (dtype == RF_F32)
+    k_cos_cand<float><<<grid, 256, 0, s>>>(B, C, D, (const float*)z, ldz, rz, (const float*)items,
+                                           ldi, ri, cand, inv_temp, scores);
+  else
+    RF_REQUIRE(false, "rf_cos_score_cand: bad dtype %d", dtype);
+  RF_LAUNCH_CHECK("rf_cos_score_cand");
+}
+
+}  // extern "C"

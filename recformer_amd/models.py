@@ -1,0 +1,489 @@
+"""Drop-in Recformer model classes on the MI355X HIP kernels.
+
+Mirrors the reference Python API (recformer/models.py): same class names, constructor
+arguments, forward() keyword signatures and return types, and the same state-dict keys
+(models.py:82-356 plus the transformers Longformer layer names TF:446-1172), so
+finetune.py / evaluate_seq.py / checkpoints load unchanged. The arithmetic runs in
+hand-written HIP kernels through ops.py; there is no PyTorch/CPU fallback.
+
+Compute dtype: bf16 when the parameters are bf16 or a CUDA autocast context with a
+16-bit dtype is active (fp16 autocast is computed in bf16: gfx950 kernels are bf16);
+fp32 otherwise (exact-fp32 MFMA GEMMs).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Any, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .config import RecformerConfig
+
+__all__ = [
+    "RecformerConfig", "RecformerModel", "RecformerForSeqRec", "RecformerForPretraining",
+    "RecformerPretrainingOutput", "RecformerModelOutput", "RecformerEmbeddings",
+    "RecformerPooler", "Similarity", "create_position_ids_from_input_ids",
+]
+
+
+# ----------------------------------------------------------------------------------
+# outputs
+class _Output:
+    """Tuple/attribute hybrid like transformers' ModelOutput."""
+
+    _fields: Tuple[str, ...] = ()
+
+    def to_tuple(self):
+        return tuple(getattr(self, f) for f in self._fields if getattr(self, f) is not None)
+
+    def __getitem__(self, i):
+        if isinstance(i, str):
+            return getattr(self, i)
+        return self.to_tuple()[i]
+
+    def __iter__(self):
+        return iter(self.to_tuple())
+
+    def keys(self):
+        return [f for f in self._fields if getattr(self, f) is not None]
+
+
+@dataclass
+class RecformerModelOutput(_Output):
+    """Fields of LongformerBaseModelOutputWithPooling (TF:79)."""
+
+    last_hidden_state: Optional[torch.Tensor] = None
+    pooler_output: Optional[torch.Tensor] = None
+    hidden_states: Optional[Tuple[torch.Tensor, ...]] = None
+    attentions: Optional[Tuple[torch.Tensor, ...]] = None
+    global_attentions: Optional[Tuple[torch.Tensor, ...]] = None
+    _fields = ("last_hidden_state", "pooler_output", "hidden_states", "attentions", "global_attentions")
+
+
+LongformerBaseModelOutputWithPooling = RecformerModelOutput
+
+
+@dataclass
+class RecformerPretrainingOutput:
+    """models.py:57-66."""
+
+    cl_correct_num: float = 0.0
+    cl_total_num: float = 1e-5
+    loss: Optional[torch.FloatTensor] = None
+    logits: torch.FloatTensor = None
+    hidden_states: Optional[Tuple[torch.FloatTensor]] = None
+    attentions: Optional[Tuple[torch.FloatTensor]] = None
+    global_attentions: Optional[Tuple[torch.FloatTensor]] = None
+
+
+def create_position_ids_from_input_ids(input_ids, padding_idx):
+    """models.py:68-79 (host-side helper kept for API compatibility; the HIP path computes
+    the same ids inside rf_prepare_inputs)."""
+    mask = input_ids.ne(padding_idx).int()
+    incremental_indices = torch.cumsum(mask, dim=1).type_as(mask) * mask
+    return incremental_indices.long() + padding_idx
+
+
+# ----------------------------------------------------------------------------------
+# modules (parameter containers with the reference names)
+class RecformerEmbeddings(nn.Module):
+    """models.py:82-138 — parameter layout only; compute is rf_embed_ln_fwd."""
+
+    def __init__(self, config: RecformerConfig):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(config.vocab_size, config.hidden_size, padding_idx=config.pad_token_id)
+        self.position_embeddings = nn.Embedding(config.max_position_embeddings, config.hidden_size,
+                                                padding_idx=config.pad_token_id)
+        self.token_type_embeddings = nn.Embedding(config.token_type_size, config.hidden_size)
+        self.item_position_embeddings = nn.Embedding(config.max_item_embeddings, config.hidden_size)
+        self.LayerNorm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.dropout = nn.Dropout(config.hidden_dropout_prob)
+        self.register_buffer("position_ids", torch.arange(config.max_position_embeddings).expand((1, -1)))
+        self.position_embedding_type = getattr(config, "position_embedding_type", "absolute")
+        self.padding_idx = config.pad_token_id
+
+
+class _SelfAttention(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        d = config.hidden_size
+        self.query = nn.Linear(d, d)
+        self.key = nn.Linear(d, d)
+        self.value = nn.Linear(d, d)
+        self.query_global = nn.Linear(d, d)
+        self.key_global = nn.Linear(d, d)
+        self.value_global = nn.Linear(d, d)
+
+
+class _DenseLN(nn.Module):
+    def __init__(self, d_in, d_out, eps):
+        super().__init__()
+        self.dense = nn.Linear(d_in, d_out)
+        self.LayerNorm = nn.LayerNorm(d_out, eps=eps)
+
+
+class _Attention(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.self = _SelfAttention(config)
+        self.output = _DenseLN(config.hidden_size, config.hidden_size, config.layer_norm_eps)
+
+
+class _Intermediate(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.dense = nn.Linear(config.hidden_size, config.intermediate_size)
+
+
+class RecformerLayer(nn.Module):
+    """One LongformerLayer (TF:1134-1172) — names match the reference state dict."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.attention = _Attention(config)
+        self.intermediate = _Intermediate(config)
+        self.output = _DenseLN(config.intermediate_size, config.hidden_size, config.layer_norm_eps)
+
+
+class RecformerEncoder(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.layer = nn.ModuleList([RecformerLayer(config) for _ in range(config.num_hidden_layers)])
+
+
+class RecformerPooler(nn.Module):
+    """models.py:155-171."""
+
+    def __init__(self, config: RecformerConfig):
+        super().__init__()
+        self.pooler_type = config.pooler_type
+
+    def forward(self, attention_mask: torch.Tensor, hidden_states: torch.Tensor) -> torch.Tensor:
+        if self.pooler_type == "cls":
+            return hidden_states[:, 0]
+        if self.pooler_type == "avg":
+            return (hidden_states * attention_mask.unsqueeze(-1)).sum(1) / attention_mask.sum(-1).unsqueeze(-1)
+        raise NotImplementedError
+
+
+class Similarity(nn.Module):
+    """models.py:358-369 — cos(x, y)/temp. Used on the HIP path through ops.cos_scores."""
+
+    def __init__(self, config: RecformerConfig):
+        super().__init__()
+        self.temp = config.temp
+
+    def forward(self, x, y):
+        return nn.functional.cosine_similarity(x, y, dim=-1) / self.temp
+
+
+def _init_weights(module: nn.Module, std: float) -> None:
+    """LongformerPreTrainedModel._init_weights semantics (normal(0, std), zero bias, LN 1/0)."""
+    for m in module.modules():
+        if isinstance(m, nn.Linear):
+            m.weight.data.normal_(0.0, std)
+            if m.bias is not None:
+                m.bias.data.zero_()
+        elif isinstance(m, nn.Embedding):
+            m.weight.data.normal_(0.0, std)
+            if m.padding_idx is not None:
+                m.weight.data[m.padding_idx].zero_()
+        elif isinstance(m, nn.LayerNorm):
+            m.bias.data.zero_()
+            m.weight.data.fill_(1.0)
+
+
+# ----------------------------------------------------------------------------------
+def _compute_dtype(param_dtype: torch.dtype) -> torch.dtype:
+    if torch.is_autocast_enabled("cuda"):
+        return torch.bfloat16
+    if param_dtype in (torch.bfloat16, torch.float16):
+        return torch.bfloat16
+    return torch.float32
+
+
+class _PackedWeights:
+    """Compute-dtype copies of the layer weights in the layouts the kernels read.
+
+    Per layer: W_qkv5 = [Wq; Wk; Wv; Wkg; Wvg] (5d x d) so one MFMA GEMM produces q, k, v
+    and the global-path k/v over all tokens (TF:504-506, 983-984); biases fp32. Rebuilt
+    whenever any parameter's version counter or storage changes (e.g. after an optimizer
+    step or load_state_dict).
+    """
+
+    def __init__(self):
+        self.key = None
+        self.data = None
+
+    @staticmethod
+    def _sig(model: "RecformerModel", dtype):
+        return (dtype,) + tuple((p.data_ptr(), p._version) for p in model.parameters())
+
+    def get(self, model: "RecformerModel", dtype: torch.dtype):
+        sig = self._sig(model, dtype)
+        if sig != self.key:
+            self.data = self._build(model, dtype)
+            self.key = sig
+        return self.data
+
+    @staticmethod
+    @torch.no_grad()
+    def _build(model: "RecformerModel", dt: torch.dtype):
+        f32 = torch.float32
+        emb = model.embeddings
+        pk = {
+            "word": emb.word_embeddings.weight.to(dt).contiguous(),
+            "pos": emb.position_embeddings.weight.to(dt).contiguous(),
+            "type": emb.token_type_embeddings.weight.to(dt).contiguous(),
+            "ipos": emb.item_position_embeddings.weight.to(dt).contiguous(),
+            "ln_w": emb.LayerNorm.weight.to(f32).contiguous(),
+            "ln_b": emb.LayerNorm.bias.to(f32).contiguous(),
+            "layers": [],
+        }
+        for lyr in model.encoder.layer:
+            sa = lyr.attention.self
+            lin = [sa.query, sa.key, sa.value, sa.key_global, sa.value_global]
+            pk["layers"].append({
+                "w_qkv": torch.cat([m.weight for m in lin], 0).to(dt).contiguous(),
+                "b_qkv": torch.cat([m.bias for m in lin], 0).to(f32).contiguous(),
+                "w_qg": sa.query_global.weight.to(dt).contiguous(),
+                "b_qg": sa.query_global.bias.to(f32).contiguous(),
+                "w_o": lyr.attention.output.dense.weight.to(dt).contiguous(),
+                "b_o": lyr.attention.output.dense.bias.to(f32).contiguous(),
+                "ln1_w": lyr.attention.output.LayerNorm.weight.to(f32).contiguous(),
+                "ln1_b": lyr.attention.output.LayerNorm.bias.to(f32).contiguous(),
+                "w_1": lyr.intermediate.dense.weight.to(dt).contiguous(),
+                "b_1": lyr.intermediate.dense.bias.to(f32).contiguous(),
+                "w_2": lyr.output.dense.weight.to(dt).contiguous(),
+                "b_2": lyr.output.dense.bias.to(f32).contiguous(),
+                "ln2_w": lyr.output.LayerNorm.weight.to(f32).contiguous(),
+                "ln2_b": lyr.output.LayerNorm.bias.to(f32).contiguous(),
+            })
+        return pk
+
+
+class RecformerModel(nn.Module):
+    """models.py:174-356 on HIP kernels."""
+
+    def __init__(self, config: RecformerConfig):
+        super().__init__()
+        self.config = config
+        if isinstance(config.attention_window, int):
+            assert config.attention_window % 2 == 0, "`config.attention_window` has to be an even value"
+            assert config.attention_window > 0, "`config.attention_window` has to be positive"
+            config.attention_window = [config.attention_window] * config.num_hidden_layers
+        else:
+            assert len(config.attention_window) == config.num_hidden_layers, (
+                "`len(config.attention_window)` should equal `config.num_hidden_layers`. "
+                f"Expected {config.num_hidden_layers}, given {len(config.attention_window)}")
+        self.embeddings = RecformerEmbeddings(config)
+        self.encoder = RecformerEncoder(config)
+        self.pooler = RecformerPooler(config)
+        _init_weights(self, config.initializer_range)
+        self._packed = _PackedWeights()
+
+    def get_input_embeddings(self):
+        return self.embeddings.word_embeddings
+
+    def set_input_embeddings(self, value):
+        self.embeddings.word_embeddings = value
+
+    @property
+    def dtype(self) -> torch.dtype:
+        return self.embeddings.word_embeddings.weight.dtype
+
+    def _window(self) -> int:
+        w = self.config.attention_window
+        return w if isinstance(w, int) else max(w)
+
+    def forward(
+        self,
+        input_ids: Optional[torch.Tensor] = None,
+        attention_mask: Optional[torch.Tensor] = None,
+        global_attention_mask: Optional[torch.Tensor] = None,
+        head_mask: Optional[torch.Tensor] = None,
+        token_type_ids: Optional[torch.Tensor] = None,
+        position_ids: Optional[torch.Tensor] = None,
+        item_position_ids: Optional[torch.Tensor] = None,
+        inputs_embeds: Optional[torch.Tensor] = None,
+        output_attentions: Optional[bool] = None,
+        output_hidden_states: Optional[bool] = None,
+        return_dict: Optional[bool] = None,
+    ):
+        cfg = self.config
+        output_attentions = output_attentions if output_attentions is not None else cfg.output_attentions
+        output_hidden_states = (output_hidden_states if output_hidden_states is not None
+                                else cfg.output_hidden_states)
+        return_dict = return_dict if return_dict is not None else cfg.use_return_dict
+        if input_ids is not None and inputs_embeds is not None:
+            raise ValueError("You cannot specify both input_ids and inputs_embeds at the same time")
+        if input_ids is None:
+            raise NotImplementedError("recformer_amd: inputs_embeds is not supported on the HIP path")
+        if head_mask is not None:
+            raise NotImplementedError("recformer_amd: head_mask is not supported (callers pass None)")
+        if output_attentions:
+            raise NotImplementedError("recformer_amd: output_attentions is not supported on the HIP path")
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("recformer_amd: training forward/backward is not built yet")
+
+        last, hidden_all = self._encode(input_ids, attention_mask, global_attention_mask,
+                                        token_type_ids, position_ids, item_position_ids,
+                                        output_hidden_states)
+        pooled = self.pooler(attention_mask, last)
+        if not return_dict:
+            out = (last, pooled)
+            if output_hidden_states:
+                out = out + (hidden_all,)
+            return out
+        return RecformerModelOutput(last_hidden_state=last, pooler_output=pooled, hidden_states=hidden_all)
+
+    @torch.no_grad()
+    def _encode(self, input_ids, attention_mask, global_attention_mask, token_type_ids,
+                position_ids, item_position_ids, output_hidden_states):
+        cfg = self.config
+        B, L = input_ids.shape
+        W = self._window()
+        Lp = L + (W - L % W) % W
+        D, H = cfg.hidden_size, cfg.num_attention_heads
+        hd = D // H
+        dt = _compute_dtype(self.dtype)
+        pk = self._packed.get(self, dt)
+
+        # number of global slots (one host read per forward; the reference does ~265)
+        if global_attention_mask is not None:
+            gm = global_attention_mask != 0
+            if attention_mask is not None:
+                gm = gm & (attention_mask > 0)
+            gmax = int(gm.sum(1).max().item()) if B > 0 else 0
+        else:
+            gmax = 0
+        ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
+            input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
+            position_ids, Lp, cfg.pad_token_id, gmax)
+        h = ops.embed_ln(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
+                         pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps)
+        hidden_all = [h] if output_hidden_states else None
+        scale = 1.0 / math.sqrt(hd)
+        windows = cfg.window_per_layer()
+        for li, lw in enumerate(pk["layers"]):
+            half_w = windows[li] // 2
+            nq = 5 * D if gmax > 0 else 3 * D
+            qkv = ops.gemm(h, lw["w_qkv"][:nq], lw["b_qkv"][:nq], ops.RF_EPI_BIAS,
+                           scale_cols=D, col_scale=scale, tag="gemm_qkv")
+            ctx = ops.band_attention(qkv[:, 0:D], qkv[:, D:2 * D], qkv[:, 2 * D:3 * D], flags,
+                                     gidx, B, Lp, H, half_w, tag="band_attn")
+            if gmax > 0:
+                hg = ops.gather_global_rows(h, gidx, B, Lp)
+                qg = ops.gemm(hg, lw["w_qg"], lw["b_qg"], ops.RF_EPI_BIAS, scale_cols=D, col_scale=scale)
+                ops.global_attention(qg, qkv[:, 3 * D:4 * D], qkv[:, 4 * D:5 * D], flags, gidx,
+                                     B, Lp, H, ctx, tag="global_attn")
+            t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h, tag="gemm_out")
+            a = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], cfg.layer_norm_eps, out=t, tag="layernorm")
+            f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
+            t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a, tag="gemm_ffn2")
+            h = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], cfg.layer_norm_eps, out=t2, tag="layernorm")
+            if output_hidden_states:
+                hidden_all.append(h)
+        last = h.view(B, Lp, D)[:, :L]
+        if output_hidden_states:
+            hidden_all = tuple(x.view(B, Lp, D)[:, :L] for x in hidden_all)
+        return last, hidden_all
+
+
+class RecformerForSeqRec(nn.Module):
+    """models.py:524-599 on HIP kernels (scores via normalize + MFMA GEMM, never the
+    (B,N,d) broadcast of nn.CosineSimilarity)."""
+
+    def __init__(self, config: RecformerConfig):
+        super().__init__()
+        self.config = config
+        self.longformer = RecformerModel(config)
+        self.sim = Similarity(config)
+        self._item_cache_key = None
+        self._item_cache = None
+
+    def init_item_embedding(self, embeddings: Optional[torch.Tensor] = None):
+        """models.py:533-537."""
+        self.item_embedding = nn.Embedding(num_embeddings=self.config.item_num,
+                                           embedding_dim=self.config.hidden_size)
+        if embeddings is not None:
+            self.item_embedding = nn.Embedding.from_pretrained(embeddings, freeze=True)
+            print("Initalize item embeddings from vectors.")
+        self._item_cache_key = None
+
+    def _items(self, dt: torch.dtype):
+        w = self.item_embedding.weight
+        key = (w.data_ptr(), w._version, dt, w.device)
+        if key != self._item_cache_key:
+            with torch.no_grad():
+                table = w.detach().to(dt).contiguous()
+                self._item_cache = (table, ops.row_inv_norm(table))
+            self._item_cache_key = key
+        return self._item_cache
+
+    def similarity_score(self, pooler_output, candidates=None):
+        """models.py:539-545: (B,N) or (B,C) fp32 scores = cos / temp."""
+        dt = pooler_output.dtype if pooler_output.dtype in (torch.bfloat16, torch.float32) else torch.bfloat16
+        z = pooler_output.to(dt).contiguous()
+        table, rnorm = self._items(dt)
+        inv_t = 1.0 / self.config.temp
+        if candidates is None:
+            return ops.cos_scores(z, table, inv_t, items_rnorm=rnorm)
+        return ops.cos_scores_cand(z, table, candidates, inv_t, items_rnorm=rnorm)
+
+    def forward(self, input_ids=None, attention_mask=None, global_attention_mask=None, head_mask=None,
+                token_type_ids=None, position_ids=None, item_position_ids=None, inputs_embeds=None,
+                output_attentions=None, output_hidden_states=None, return_dict=None, candidates=None,
+                labels=None):
+        batch_size = input_ids.size(0)
+        outputs = self.longformer(input_ids, attention_mask=attention_mask,
+                                  global_attention_mask=global_attention_mask, head_mask=head_mask,
+                                  token_type_ids=token_type_ids, position_ids=position_ids,
+                                  item_position_ids=item_position_ids, inputs_embeds=inputs_embeds,
+                                  output_attentions=output_attentions,
+                                  output_hidden_states=output_hidden_states, return_dict=True)
+        pooler_output = outputs.pooler_output
+        if labels is None:
+            return self.similarity_score(pooler_output, candidates)
+        loss_fct = nn.CrossEntropyLoss()
+        if self.config.finetune_negative_sample_size <= 0:
+            logits = self.similarity_score(pooler_output)
+            return loss_fct(logits, labels)
+        # sampled softmax: candidates from the CPU global RNG as models.py:594
+        candidates = torch.cat((labels.unsqueeze(-1), torch.randint(
+            0, self.config.item_num, size=(batch_size, self.config.finetune_negative_sample_size)
+        ).to(labels.device)), dim=-1)
+        logits = self.similarity_score(pooler_output, candidates)
+        target = torch.zeros_like(labels, device=labels.device)
+        return loss_fct(logits, target)
+
+
+class RecformerForPretraining(nn.Module):
+    """models.py:372-520 — parameter layout (longformer + lm_head) for checkpoint
+    compatibility. Its training step arrives with the backward kernels."""
+
+    def __init__(self, config: RecformerConfig):
+        super().__init__()
+        self.config = config
+        self.longformer = RecformerModel(config)
+        self.lm_head = _LMHead(config)
+        self.sim = Similarity(config)
+
+    def forward(self, *args: Any, **kwargs: Any):
+        raise NotImplementedError("recformer_amd: RecformerForPretraining.forward needs the backward "
+                                  "kernels (SURVEY.md §8a A10); not built yet")
+
+
+class _LMHead(nn.Module):
+    """LongformerLMHead parameter names (TF:1265-1285): dense, layer_norm, decoder, bias."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.dense = nn.Linear(config.hidden_size, config.hidden_size)
+        self.layer_norm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.decoder = nn.Linear(config.hidden_size, config.vocab_size)
+        self.bias = nn.Parameter(torch.zeros(config.vocab_size))
+        self.decoder.bias = self.bias

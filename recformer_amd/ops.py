@@ -1,0 +1,275 @@
+"""Tensor-level wrappers over the C ABI (include/recformer_hip.h).
+
+Each function takes torch tensors that already live on a ROCm device, validates shape /
+dtype / contiguity on the host, and launches on torch's current stream. Buffers are
+allocated by PyTorch's caching allocator; the library never allocates or syncs.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF_EPI_COS,
+                   RF_EPI_NONE, RF_F32, check)
+
+__all__ = [
+    "dtype_code", "prepare_inputs", "embed_ln", "gemm", "layernorm", "band_attention",
+    "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
+    "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
+]
+
+
+# ---- optional per-launch timing (bench.py): HIP events recorded on the launch stream ----
+_TIMING: Optional[Dict[str, List[Tuple[torch.cuda.Event, torch.cuda.Event]]]] = None
+
+
+def enable_timing(on: bool = True) -> None:
+    global _TIMING
+    _TIMING = {} if on else None
+
+
+def timing_results() -> Dict[str, List[float]]:
+    """Per-tag launch durations in ms (synchronises)."""
+    if not _TIMING:
+        return {}
+    torch.cuda.synchronize()
+    return {k: [s.elapsed_time(e) for s, e in v] for k, v in _TIMING.items()}
+
+
+@contextlib.contextmanager
+def _region(tag: Optional[str]):
+    if _TIMING is None or tag is None:
+        yield
+        return
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    yield
+    e.record()
+    _TIMING.setdefault(tag, []).append((s, e))
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.bfloat16:
+        return RF_BF16
+    if dt == torch.float32:
+        return RF_F32
+    raise TypeError(f"recformer_amd: unsupported compute dtype {dt} (bf16 or fp32)")
+
+
+def _dev(*ts: Optional[torch.Tensor]) -> None:
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.RecformerHipError(
+                "recformer_amd kernels need ROCm device tensors (no CPU fallback); got a CPU tensor")
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _rowmajor(t: torch.Tensor, name: str) -> int:
+    """Leading dimension of a 2-D row-major view (unit column stride)."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a 2-D row-major tensor, got shape {tuple(t.shape)} "
+                         f"strides {t.stride()}")
+    return t.stride(0)
+
+
+def prepare_inputs(input_ids, attention_mask, global_attention_mask, token_type_ids,
+                   item_position_ids, position_ids, Lp: int, pad_id: int, gmax: int):
+    """A2 prologue (models.py:306-329). Returns int32 ids/pos/tt/ip (B,Lp), uint8 flags,
+    int32 gidx (B,gmax)."""
+    lib = _lib.load()
+    _dev(input_ids)
+    B, L = input_ids.shape
+    dev = input_ids.device
+
+    def i64(t):
+        if t is None:
+            return None
+        _dev(t)
+        if t.shape != (B, L):
+            raise ValueError(f"input of shape {tuple(t.shape)} does not match input_ids {(B, L)}")
+        return t.to(torch.int64).contiguous()
+
+    ids_in = i64(input_ids)
+    am, gm, tt_in, ip_in, pos_in = (i64(attention_mask), i64(global_attention_mask),
+                                    i64(token_type_ids), i64(item_position_ids), i64(position_ids))
+    if ip_in is None:
+        raise ValueError("item_position_ids is required (RecformerEmbeddings, models.py:132)")
+    ids = torch.empty(B, Lp, dtype=torch.int32, device=dev)
+    pos = torch.empty_like(ids)
+    tt = torch.empty_like(ids)
+    ip = torch.empty_like(ids)
+    flags = torch.empty(B, Lp, dtype=torch.uint8, device=dev)
+    gidx = torch.empty(B, max(gmax, 1), dtype=torch.int32, device=dev)
+    check(lib.rf_prepare_inputs(_p(ids_in), _p(am), _p(gm), _p(tt_in), _p(ip_in), _p(pos_in), B, L,
+                                Lp, pad_id, gmax, _p(ids), _p(pos), _p(tt), _p(ip), _p(flags),
+                                _p(gidx), _stream(ids)), "rf_prepare_inputs")
+    return ids, pos, tt, ip, flags, gidx[:, :gmax]
+
+
+def embed_ln(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, ln_b, eps: float):
+    lib = _lib.load()
+    _dev(ids, word)
+    M = ids.numel()
+    D = word.shape[1]
+    for t in (word, posemb, typeemb, iposemb):
+        if not t.is_contiguous() or t.dtype != word.dtype or t.shape[1] != D:
+            raise ValueError("embedding tables must be contiguous, same dtype and width")
+    out = torch.empty(M, D, dtype=word.dtype, device=word.device)
+    check(lib.rf_embed_ln_fwd(dtype_code(word.dtype), M, D, _p(ids), _p(pos), _p(tt), _p(ip),
+                              _p(word), _p(posemb), _p(typeemb), _p(iposemb),
+                              _p(ln_w.float().contiguous()), _p(ln_b.float().contiguous()),
+                              float(eps), _p(out), _stream(out)), "rf_embed_ln_fwd")
+    return out
+
+
+def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+         epilogue: int = RF_EPI_BIAS, resid: Optional[torch.Tensor] = None,
+         scale_cols: int = 0, col_scale: float = 1.0, out: Optional[torch.Tensor] = None,
+         ra: Optional[torch.Tensor] = None, rw: Optional[torch.Tensor] = None,
+         tag: Optional[str] = None) -> torch.Tensor:
+    """C = epi(a . w^T); a (M,K), w (N,K) row-major, same dtype."""
+    lib = _lib.load()
+    _dev(a, w, bias, resid)
+    if a.dtype != w.dtype:
+        raise TypeError(f"gemm: dtype mismatch {a.dtype} vs {w.dtype}")
+    M, K = a.shape
+    N, K2 = w.shape
+    if K != K2:
+        raise ValueError(f"gemm: K mismatch {K} vs {K2}")
+    lda, ldw = _rowmajor(a, "a"), _rowmajor(w, "w")
+    odt = torch.float32 if epilogue == RF_EPI_COS else a.dtype
+    if out is None:
+        out = torch.empty(M, N, dtype=odt, device=a.device)
+    ldc = _rowmajor(out, "out")
+    ldr = 0
+    if resid is not None:
+        ldr = _rowmajor(resid, "resid")
+        if resid.dtype != a.dtype or resid.shape != (M, N):
+            raise ValueError("gemm: residual must match output shape/dtype")
+    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
+        raise TypeError("gemm: bias must be contiguous fp32")
+    with _region(tag):
+        rc = lib.rf_gemm(dtype_code(a.dtype), M, N, K, _p(a), lda, _p(w), ldw, _p(bias), _p(resid),
+                         ldr, _p(out), ldc, epilogue, scale_cols, float(col_scale), _p(ra), _p(rw),
+                         _stream(out))
+    check(rc, "rf_gemm")
+    return out
+
+
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
+              out: Optional[torch.Tensor] = None, stats: bool = False, tag: Optional[str] = None):
+    lib = _lib.load()
+    _dev(x)
+    M, D = x.shape
+    ldx = _rowmajor(x, "x")
+    if out is None:
+        out = torch.empty(M, D, dtype=x.dtype, device=x.device)
+    mean = rstd = None
+    if stats:
+        mean = torch.empty(M, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    with _region(tag):
+        rc = lib.rf_layernorm_fwd(dtype_code(x.dtype), M, D, _p(x), ldx, _p(w), _p(b), float(eps),
+                                  _p(out), _rowmajor(out, "out"), _p(mean), _p(rstd), _stream(x))
+    check(rc, "rf_layernorm_fwd")
+    return (out, mean, rstd) if stats else out
+
+
+def band_attention(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int,
+                   out: Optional[torch.Tensor] = None, tag: Optional[str] = None):
+    """q/k/v: (B*Lp, >=H*64) row-major views sharing one leading dim (e.g. column slices of
+    the fused projection output)."""
+    lib = _lib.load()
+    _dev(q, k, v, flags)
+    ld = _rowmajor(q, "q")
+    if _rowmajor(k, "k") != ld or _rowmajor(v, "v") != ld:
+        raise ValueError("band_attention: q/k/v must share a leading dimension")
+    D = H * 64
+    if out is None:
+        out = torch.empty(B * Lp, D, dtype=q.dtype, device=q.device)
+    gmax = gidx.shape[1]
+    with _region(tag):
+        rc = lib.rf_band_attn_fwd(dtype_code(q.dtype), B, Lp, H, 64, half_w, _p(q), _p(k), _p(v), ld,
+                                  _p(flags), _p(gidx) if gmax else None, gmax, _p(out),
+                                  _rowmajor(out, "out"), _stream(out))
+    check(rc, "rf_band_attn_fwd")
+    return out
+
+
+def global_attention(qg, kg, vg, flags, gidx, B: int, Lp: int, H: int, out: torch.Tensor,
+                     tag: Optional[str] = None):
+    lib = _lib.load()
+    gmax = gidx.shape[1]
+    if gmax == 0:
+        return out
+    ld = _rowmajor(kg, "kg")
+    if _rowmajor(vg, "vg") != ld:
+        raise ValueError("global_attention: kg/vg must share a leading dimension")
+    with _region(tag):
+        rc = lib.rf_global_attn_fwd(dtype_code(qg.dtype), B, Lp, H, 64, _p(qg), _rowmajor(qg, "qg"),
+                                    _p(kg), _p(vg), ld, _p(flags), _p(gidx.contiguous()), gmax,
+                                    _p(out), _rowmajor(out, "out"), _stream(out))
+    check(rc, "rf_global_attn_fwd")
+    return out
+
+
+def gather_global_rows(x, gidx, B: int, Lp: int):
+    lib = _lib.load()
+    gmax = gidx.shape[1]
+    D = x.shape[1]
+    out = torch.empty(B * gmax, D, dtype=x.dtype, device=x.device)
+    check(lib.rf_gather_global_rows(dtype_code(x.dtype), B, Lp, D, gmax, _p(x), _rowmajor(x, "x"),
+                                    _p(gidx.contiguous()), _p(out), _stream(out)),
+          "rf_gather_global_rows")
+    return out
+
+
+def row_inv_norm(x: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(x)
+    M, D = x.shape
+    out = torch.empty(M, dtype=torch.float32, device=x.device)
+    check(lib.rf_row_inv_norm(dtype_code(x.dtype), M, D, _p(x), _rowmajor(x, "x"), float(eps),
+                              _p(out), _stream(x)), "rf_row_inv_norm")
+    return out
+
+
+def cos_scores(z: torch.Tensor, items: torch.Tensor, inv_temp: float,
+               z_rnorm: Optional[torch.Tensor] = None,
+               items_rnorm: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(B,N) fp32 = cos(z_b, items_n) * inv_temp on the MFMA GEMM (Similarity, models.py:358-369)."""
+    if z_rnorm is None:
+        z_rnorm = row_inv_norm(z)
+    if items_rnorm is None:
+        items_rnorm = row_inv_norm(items)
+    return gemm(z, items, None, RF_EPI_COS, col_scale=inv_temp, ra=z_rnorm, rw=items_rnorm)
+
+
+def cos_scores_cand(z: torch.Tensor, items: torch.Tensor, cand: torch.Tensor, inv_temp: float,
+                    z_rnorm: Optional[torch.Tensor] = None,
+                    items_rnorm: Optional[torch.Tensor] = None) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(z, items, cand)
+    B, D = z.shape
+    C = cand.shape[1]
+    if z_rnorm is None:
+        z_rnorm = row_inv_norm(z)
+    if items_rnorm is None:
+        items_rnorm = row_inv_norm(items)
+    cand = cand.to(torch.int64).contiguous()
+    out = torch.empty(B, C, dtype=torch.float32, device=z.device)
+    check(lib.rf_cos_score_cand(dtype_code(z.dtype), B, C, D, _p(z), _rowmajor(z, "z"), _p(z_rnorm),
+                                _p(items), _rowmajor(items, "items"), _p(items_rnorm), _p(cand),
+                                float(inv_temp), _p(out), _stream(out)), "rf_cos_score_cand")
+    return out

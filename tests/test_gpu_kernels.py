@@ -1,0 +1,166 @@
+"""Tier (ii): each HIP kernel (through the C ABI) against an fp32 reference of the same op.
+
+Tolerances: fp32 kernels 1e-4 (exact-f32 MFMA, different summation order); bf16 kernels
+are compared against the fp32 op on the SAME bf16-rounded inputs, so the only error is
+bf16 output rounding (~2^-9 relative) plus bf16 P in the attention PV product.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import restatement as R
+from recformer_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(shape, dev, dt, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(dev).to(dt)
+
+
+def _tol(dt):
+    return 1e-4 if dt == torch.float32 else 2e-2
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(64, 128, 64), (200, 200, 768), (1024, 768, 768), (320, 3840, 768), (256, 768, 3072)])
+@pytest.mark.parametrize("epi", [ops.RF_EPI_NONE, ops.RF_EPI_BIAS, ops.RF_EPI_BIAS_GELU, ops.RF_EPI_BIAS_RESID])
+def test_gemm_epilogues(dev, dt, M, N, K, epi):
+    a = _rand((M, K), dev, dt, seed=1)
+    w = _rand((N, K), dev, dt, 0.05, seed=2)
+    b = _rand((N,), dev, torch.float32, seed=3)
+    r = _rand((M, N), dev, dt, seed=4)
+    sc = N // 3
+    out = ops.gemm(a, w, b if epi else None, epi, resid=r if epi == ops.RF_EPI_BIAS_RESID else None,
+                   scale_cols=sc, col_scale=0.125)
+    ref = a.float() @ w.float().t()
+    if epi:
+        ref = ref + b
+    ref[:, :sc] *= 0.125
+    if epi == ops.RF_EPI_BIAS_GELU:
+        ref = F.gelu(ref)
+    if epi == ops.RF_EPI_BIAS_RESID:
+        ref = ref + r.float()
+    err = (out.float() - ref).abs().max().item()
+    assert err <= _tol(dt) * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_strided_views(dev, dt):
+    """Column slices of a fused buffer as A (the q/k/v views) and as W (packed weights)."""
+    big = _rand((256, 5 * 128), dev, dt, seed=5)
+    a = big[:, 128:256]
+    w = _rand((3 * 64, 128), dev, dt, 0.1, seed=6)[:128]
+    out = ops.gemm(a, w, None, ops.RF_EPI_NONE)
+    ref = a.float() @ w.float().t()
+    assert (out.float() - ref).abs().max().item() <= _tol(dt) * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("D", [128, 768])
+def test_layernorm(dev, dt, D):
+    x = _rand((333, D), dev, dt, 3.0, seed=7) + 1.0
+    w = _rand((D,), dev, torch.float32, seed=8)
+    b = _rand((D,), dev, torch.float32, seed=9)
+    y, mean, rstd = ops.layernorm(x, w, b, 1e-5, stats=True)
+    ref = F.layer_norm(x.float(), (D,), w, b, 1e-5)
+    assert (y.float() - ref).abs().max().item() <= (1e-4 if dt == torch.float32 else 3e-2)
+    assert torch.allclose(mean, x.float().mean(1), atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_embed_ln_and_prepare(dev, dt):
+    from recformer_amd.synth import synth_batch
+    B, L, D, V = 3, 200, 768, 500
+    bt = synth_batch(B, L, V, seed=3, lens=[200, 130, 7], extra_globals=((0, 9), (1, 50)))
+    bt = {k: v.to(dev) for k, v in bt.items()}
+    Lp = 256
+    gmax = 2
+    ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
+        bt["input_ids"], bt["attention_mask"], bt["global_attention_mask"], bt["token_type_ids"],
+        bt["item_position_ids"], None, Lp, 1, gmax)
+    ids_r, merged, tt_r, ip_r, pad = R.prepare_inputs(*(bt[k].cpu() for k in (
+        "input_ids", "attention_mask", "global_attention_mask", "token_type_ids", "item_position_ids")), 64, 1)
+    assert torch.equal(ids.cpu().long(), ids_r) and torch.equal(tt.cpu().long(), tt_r)
+    assert torch.equal(ip.cpu().long(), ip_r)
+    ref_flags = torch.where(merged > 1, 2, torch.where(merged == 1, 1, 0))
+    assert torch.equal(flags.cpu().long(), ref_flags)
+    m = (ids_r != 1).int()
+    pos_r = (torch.cumsum(m, 1) * m).long() + 1
+    assert torch.equal(pos.cpu().long(), pos_r)
+    assert gidx.cpu().tolist() == [[0, 9], [0, 50], [0, -1]]
+    tabs = [_rand((n, D), dev, dt, 0.02, seed=10 + i) for i, n in enumerate((V, 300, 4, 51))]
+    lw = _rand((D,), dev, torch.float32, seed=20)
+    lb = _rand((D,), dev, torch.float32, seed=21)
+    out = ops.embed_ln(ids, pos, tt, ip, *tabs, lw, lb, 1e-5)
+    x = (tabs[0].float()[ids.long()] + tabs[1].float()[pos.long()] + tabs[2].float()[tt.long()]
+         + tabs[3].float()[ip.long()])
+    ref = F.layer_norm(x, (D,), lw, lb, 1e-5).view(-1, D)
+    assert (out.float() - ref).abs().max().item() <= (1e-4 if dt == torch.float32 else 3e-2)
+
+
+def _attn_case(dev, dt, B, Lp, H, lens, globals_, seed):
+    D = H * 64
+    qkv = _rand((B * Lp, 5 * D), dev, dt, 1.0, seed=seed)
+    merged = torch.zeros(B, Lp, dtype=torch.long)
+    for b, n in enumerate(lens):
+        merged[b, :n] = 1
+    for b, p in globals_:
+        if p < lens[b]:
+            merged[b, p] = 2
+    flags = merged.to(torch.uint8).to(dev)
+    G = int((merged > 1).sum(1).max())
+    gidx = torch.full((B, max(G, 1)), -1, dtype=torch.int32)
+    for b in range(B):
+        pos = torch.nonzero(merged[b] > 1).flatten()
+        gidx[b, :pos.numel()] = pos.int()
+    gidx = gidx[:, :G].to(dev)
+    return qkv, merged, flags, gidx, G
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [
+    dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
+    dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
+    dict(B=1, Lp=128, H=1, lens=[128], globals_=()),
+    dict(B=1, Lp=1024, H=12, lens=[1024], globals_=((0, 0),)),
+])
+def test_band_and_global_attention(dev, dt, case):
+    B, Lp, H = case["B"], case["Lp"], case["H"]
+    D = H * 64
+    qkv, merged, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, case["lens"], case["globals_"], 7)
+    q, k, v, kg, vg = (qkv[:, i * D:(i + 1) * D] for i in range(5))
+    ctx = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, 32)
+    qg = None
+    if G:
+        qg_rows = _rand((B * G, D), dev, dt, 1.0, seed=8)
+        ops.global_attention(qg_rows, kg, vg, flags, gidx, B, Lp, H, ctx)
+        qg = qg_rows.float().cpu().view(B, G, H, 64).transpose(1, 2)
+
+    def hv(x):
+        return x.float().cpu().view(B, Lp, H, 64).transpose(1, 2)
+
+    ref = R.band_global_attention(hv(q), hv(k), hv(v), merged, 32, qg,
+                                  hv(kg) if G else None, hv(vg) if G else None)
+    ref = ref.transpose(1, 2).reshape(B * Lp, D)
+    err = (ctx.float().cpu() - ref).abs().max().item()
+    assert err <= (1e-4 if dt == torch.float32 else 3e-2), err
+    # padded query rows are exactly zero
+    pad_rows = (merged.view(-1) == 0)
+    assert ctx.float().cpu()[pad_rows].abs().max().item() == 0.0 if pad_rows.any() else True
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_cos_scores(dev, dt):
+    z = _rand((37, 768), dev, dt, seed=30)
+    E = _rand((1000, 768), dev, dt, seed=31)
+    s = ops.cos_scores(z, E, 20.0)
+    ref = F.cosine_similarity(z.float().unsqueeze(1), E.float().unsqueeze(0), dim=-1) * 20.0
+    assert (s - ref).abs().max().item() <= (1e-4 if dt == torch.float32 else 2e-2)
+    cand = torch.randint(0, 1000, (37, 65), device=dev)
+    sc = ops.cos_scores_cand(z, E, cand, 20.0)
+    refc = torch.gather(ref, 1, cand)
+    assert (sc - refc).abs().max().item() <= (1e-4 if dt == torch.float32 else 2e-2)

@@ -1,0 +1,74 @@
+"""Host-side checks that need no GPU: config, drop-in state-dict layout, the C ABI
+library exports, and the product path failing loudly without a ROCm device."""
+import os
+import re
+
+import pytest
+import torch
+
+import recformer_amd
+from recformer_amd import RecformerConfig, RecformerForPretraining, RecformerForSeqRec, RecformerModel
+from recformer_amd import _lib
+from tests.common import C1, manifest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_config_preset_and_roundtrip(tmp_path):
+    c = RecformerConfig.from_pretrained("allenai/longformer-base-4096")
+    assert (c.hidden_size, c.num_hidden_layers, c.vocab_size, c.max_position_embeddings) == (768, 12, 50265, 4098)
+    assert c.layer_norm_eps == 1e-5 and c.pad_token_id == 1 and c.temp == 0.05
+    # the attribute writes finetune.py:202-209 performs
+    c.max_attr_num, c.max_attr_length, c.max_item_embeddings = 3, 32, 51
+    c.attention_window, c.max_token_num, c.item_num = [64] * 12, 1024, 10
+    c.save_pretrained(str(tmp_path))
+    d = RecformerConfig.from_pretrained(str(tmp_path))
+    assert d.to_dict() == c.to_dict()
+    with pytest.raises(OSError):
+        RecformerConfig.from_pretrained("no/such-model")
+
+
+@pytest.mark.parametrize("cls", [RecformerModel, RecformerForSeqRec, RecformerForPretraining])
+def test_state_dict_layout_matches_reference(cls):
+    ref = manifest()["state_dict_layout_C1"][cls.__name__]
+    ours = {k: [list(v.shape), str(v.dtype)] for k, v in cls(RecformerConfig(**C1)).state_dict().items()}
+    assert ours == ref
+
+
+def test_reference_checkpoint_loads_strict():
+    m = RecformerForSeqRec(RecformerConfig(**C1))
+    sd = m.state_dict()
+    m2 = RecformerForSeqRec(RecformerConfig(**C1))
+    m2.load_state_dict(sd, strict=True)
+
+
+def _header_functions():
+    with open(os.path.join(ROOT, "include", "recformer_hip.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(rf_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = _header_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _lib.SIGNATURES, f"{n} declared in the header but not typed in _lib.py"
+    assert set(_lib.SIGNATURES) == set(names)
+    assert lib.rf_abi_version() == 1
+
+
+def test_argument_errors_come_back_as_messages():
+    lib = _lib.load()
+    # bad shape is rejected host-side before any launch (no GPU needed)
+    rc = lib.rf_gemm(1, 64, 64, 63, None, 63, None, 63, None, None, 0, None, 64, 0, 0, 1.0, None, None, None)
+    assert rc != 0
+    assert b"multiple" in lib.rf_last_error()
+
+
+def test_product_path_has_no_cpu_fallback():
+    m = RecformerModel(RecformerConfig(**C1)).eval()
+    ids = torch.zeros(1, 64, dtype=torch.long)
+    with pytest.raises(_lib.RecformerHipError):
+        m(input_ids=ids, item_position_ids=ids)

@@ -1,0 +1,45 @@
+"""Tier (i): the CPU restatement (oracle/restatement.py) against golden fixtures made by
+the real reference (oracle/gen_golden.py). Pins the oracle before it is trusted."""
+import pytest
+import torch
+
+from oracle import restatement as R
+from tests.common import (BASE, C1, batch_of, checksums, errs, hashed_model, load_golden,
+                          manifest)
+from recformer_amd.hashinit import hash_tensor
+
+
+@pytest.mark.parametrize("name", ["c1_full", "c1_ragged", "c1_l200"])
+def test_c1_variants(name):
+    g = load_golden(name)
+    m = hashed_model(C1, seed=1)
+    assert checksums(m) == pytest.approx(manifest()[name]["checksums"], rel=0, abs=1e-9)
+    h, p = R.model_forward(m.state_dict(), m.config, **batch_of(g))
+    assert h.shape == g["last_hidden_state"].shape
+    assert errs(h, g["last_hidden_state"])["max"] <= 1e-5
+    assert errs(p, g["pooler_output"])["max"] <= 1e-5
+
+
+def test_one_layer_768():
+    g = load_golden("l1_768")
+    m = hashed_model(dict(BASE, num_hidden_layers=1, attention_window=[64]), seed=4)
+    assert checksums(m) == pytest.approx(manifest()["l1_768"]["checksums"], rel=0, abs=1e-6)
+    h, _ = R.model_forward(m.state_dict(), m.config, **batch_of(g))
+    assert errs(h, g["last_hidden_state"])["max"] <= 1e-5
+
+
+@pytest.mark.slow
+def test_12l_768_scores_and_losses():
+    torch.set_num_threads(8)
+    g = load_golden("c2_12l")
+    m = hashed_model(BASE, seed=2)
+    h, p = R.model_forward(m.state_dict(), m.config, **batch_of(g))
+    assert errs(p, g["pooler_output"])["max"] <= 1e-4
+    assert errs(h[:, g["rows"]], g["hidden_rows"])["max"] <= 1e-4
+    items = hash_tensor("catalog", (1000, 768), "weight", seed=3, std=1.0)
+    s = R.cosine_scores(p, items, 0.05)
+    assert errs(s, g["scores"])["max"] <= 1e-3
+    assert abs(float(R.seqrec_loss(s, g["labels"])) - float(g["loss_full"])) <= 1e-4
+    sc = R.cosine_scores(p, items[g["candidates"]], 0.05)
+    assert errs(sc, g["scores_cand"])["max"] <= 1e-3
+    assert abs(float(R.seqrec_loss(sc, torch.zeros(2, dtype=torch.long))) - float(g["loss_sampled"])) <= 1e-4
