@@ -31,6 +31,7 @@ typedef void* rf_stream_t;
 
 enum { RF_OK = 0, RF_ERR_ARG = 1, RF_ERR_HIP = 2 };
 enum { RF_F32 = 0, RF_BF16 = 1 };
+enum { RF_IO_C_F32 = 1, RF_IO_R_F32 = 2 }; /* rf_gemm io_flags (bf16 GEMMs): C / residual in fp32 */
 enum {
   RF_EPI_NONE = 0,       /* C = A.W^T                                   */
   RF_EPI_BIAS = 1,       /* C = A.W^T + b              (nn.Linear)      */
@@ -57,26 +58,31 @@ int rf_prepare_inputs(const int64_t* input_ids, const int64_t* attention_mask,
                       int32_t* gidx, rf_stream_t stream);
 
 /* A3 — RecformerEmbeddings.forward, models.py:108-138: LN(Ew[id] + Ep[pos] + Et[tt] +
- * Ei[ip]) for M tokens, one fused pass (tables in `dtype`, LN params fp32). */
-int rf_embed_ln_fwd(int dtype, int M, int D, const int32_t* ids, const int32_t* pos,
-                    const int32_t* tt, const int32_t* ip, const void* word_emb,
-                    const void* pos_emb, const void* type_emb, const void* ipos_emb,
-                    const float* ln_w, const float* ln_b, float eps, void* out,
-                    rf_stream_t stream);
+ * Ei[ip]) for M tokens, one fused pass. Tables in table_dtype, LN params fp32, output in
+ * out_dtype plus an optional fp32 copy out32 (M x D; the bf16 path's residual stream). */
+int rf_embed_ln_fwd(int table_dtype, int out_dtype, int M, int D, const int32_t* ids,
+                    const int32_t* pos, const int32_t* tt, const int32_t* ip,
+                    const void* word_emb, const void* pos_emb, const void* type_emb,
+                    const void* ipos_emb, const float* ln_w, const float* ln_b, float eps,
+                    void* out, float* out32, rf_stream_t stream);
 
 /* A4 linears — nn.Linear / the 9 addmm per layer (TF:504-506, 982-984, 1064-1071,
  * 1107, 1123) on MFMA: C[M,N] = epi(A[M,K] . W[N,K]^T). The first `scale_cols`
  * output columns are multiplied by `col_scale` after the bias (the q/sqrt(hd) of
- * TF:514). EPI_COS writes fp32 C and needs ra (M) / rw (N) inverse norms. */
+ * TF:514). C and the residual R are stored in `dtype`, or in fp32 when io_flags has
+ * RF_IO_C_F32 / RF_IO_R_F32 (the bf16 path keeps the residual stream and the pre-LayerNorm
+ * sums in fp32, as the reference's autocast does: LayerNorm outputs fp32 there).
+ * EPI_COS always writes fp32 C and needs ra (M) / rw (N) inverse norms. */
 int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, const void* W, int ldw,
-            const float* bias, const void* resid, int ldr, void* C, int ldc, int epilogue,
-            int scale_cols, float col_scale, const float* ra, const float* rw,
+            const float* bias, const void* resid, int ldr, void* C, int ldc, int io_flags,
+            int epilogue, int scale_cols, float col_scale, const float* ra, const float* rw,
             rf_stream_t stream);
 
-/* LayerNorm over rows of D (TF:1071, 1130; nn.LayerNorm eps). mean/rstd (M) optional. */
-int rf_layernorm_fwd(int dtype, int M, int D, const void* x, int ldx, const float* w,
-                     const float* b, float eps, void* y, int ldy, float* mean, float* rstd,
-                     rf_stream_t stream);
+/* LayerNorm over rows of D (TF:1071, 1130; nn.LayerNorm eps); x in x_dtype, y in y_dtype,
+ * optional fp32 copy y32 (M x D, contiguous); mean/rstd (M) optional. */
+int rf_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, int ldx,
+                     const float* w, const float* b, float eps, void* y, int ldy, float* y32,
+                     float* mean, float* rstd, rf_stream_t stream);
 
 /* A5 — LongformerSelfAttention local branch (TF:482-604 with _sliding_chunks_* 759-867,
  * _mask_invalid_locations 743-757, _concat_with_global_key_attn_probs 898-926,

@@ -13,6 +13,7 @@ from typing import Optional
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librecformer_hip.so")
 
 RF_F32, RF_BF16 = 0, 1
+RF_IO_C_F32, RF_IO_R_F32 = 1, 2
 RF_EPI_NONE, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF_EPI_COS = 0, 1, 2, 3, 4
 
 # symbol -> (restype, argtypes); must match include/recformer_hip.h exactly
@@ -22,10 +23,12 @@ SIGNATURES = {
     "rf_abi_version": (c_int, []),
     "rf_prepare_inputs": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                   P, P, P, P, P, P, P]),
-    "rf_embed_ln_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_float, P, P]),
+    "rf_embed_ln_fwd": (c_int, [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_float,
+                                P, P, P]),
     "rf_gemm": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, P, c_int, P, c_int,
-                        c_int, c_int, c_float, P, P, P]),
-    "rf_layernorm_fwd": (c_int, [c_int, c_int, c_int, P, c_int, P, P, c_float, P, c_int, P, P, P]),
+                        c_int, c_int, c_int, c_float, P, P, P]),
+    "rf_layernorm_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_float, P, c_int, P,
+                                 P, P, P]),
     "rf_band_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
                                  c_int, P, c_int, P]),
     "rf_global_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P,

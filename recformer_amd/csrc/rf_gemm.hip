@@ -26,7 +26,7 @@ struct EpiArgs {
   const float* rw;
 };
 
-template <typename TIN, int EPI>
+template <typename TIN, int EPI, bool CF32, bool RF32>
 __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, float v) {
   if (row >= e.M || col >= e.N) return;
   if (EPI == RF_EPI_COS) {
@@ -36,8 +36,16 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, fl
   if (EPI != RF_EPI_NONE) v += e.bias[col];
   if (col < e.scale_cols) v *= e.col_scale;
   if (EPI == RF_EPI_BIAS_GELU) v = gelu_erf(v);
-  if (EPI == RF_EPI_BIAS_RESID) v += to_f32(reinterpret_cast<const TIN*>(e.R)[(int64_t)row * e.ldr + col]);
-  reinterpret_cast<TIN*>(e.C)[(int64_t)row * e.ldc + col] = from_f32<TIN>(v);
+  if (EPI == RF_EPI_BIAS_RESID) {
+    if (RF32)
+      v += reinterpret_cast<const float*>(e.R)[(int64_t)row * e.ldr + col];
+    else
+      v += to_f32(reinterpret_cast<const TIN*>(e.R)[(int64_t)row * e.ldr + col]);
+  }
+  if (CF32)
+    reinterpret_cast<float*>(e.C)[(int64_t)row * e.ldc + col] = v;
+  else
+    reinterpret_cast<TIN*>(e.C)[(int64_t)row * e.ldc + col] = from_f32<TIN>(v);
 }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -50,7 +58,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
 constexpr int GB_TILE_BYTES = GB_M * GB_K * 2;  // 16 KiB per operand tile
 
-template <int EPI>
+template <int EPI, bool CF32, bool RF32>
 __global__ void __launch_bounds__(256) k_gemm_bf16(int K, const bf16* __restrict__ A, int lda,
                                                     const bf16* __restrict__ W, int ldw, EpiArgs e,
                                                     int nTn) {
@@ -125,7 +133,7 @@ __global__ void __launch_bounds__(256) k_gemm_bf16(int K, const bf16* __restrict
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        epi_store<bf16, EPI>(e, m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r,
+        epi_store<bf16, EPI, CF32, RF32>(e, m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r,
                              n0 + wn * 64 + j * 16 + (lane & 15), acc[i][j][r]);
 }
 
@@ -191,7 +199,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int K, const float* __restrict
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        epi_store<float, EPI>(e, m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r,
+        epi_store<float, EPI, false, false>(e, m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r,
                               n0 + wn * 32 + j * 16 + (lane & 15), acc[i][j][r]);
 }
 
@@ -201,7 +209,7 @@ using namespace rf;
 
 extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, const void* W,
                        int ldw, const float* bias, const void* resid, int ldr, void* C, int ldc,
-                       int epilogue, int scale_cols, float col_scale, const float* ra,
+                       int io_flags, int epilogue, int scale_cols, float col_scale, const float* ra,
                        const float* rw, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && N > 0 && K > 0, "rf_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   RF_REQUIRE(lda >= K && ldw >= K && ldc >= N, "rf_gemm: bad leading dims");
@@ -217,10 +225,31 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
     RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0, "rf_gemm(bf16): lda/ldw must be multiples of 8");
     const int nTm = (M + GB_M - 1) / GB_M, nTn = (N + GB_N - 1) / GB_N;
     const size_t lds = 4 * GB_TILE_BYTES;
+    const bool cf = io_flags & RF_IO_C_F32, rf = io_flags & RF_IO_R_F32;
+    const dim3 grid(nTm * nTn);
+    const bf16* Ab = (const bf16*)A;
+    const bf16* Wb = (const bf16*)W;
     switch (epilogue) {
-#define C_(E) case E: k_gemm_bf16<E><<<nTm * nTn, 256, lds, s>>>(K, (const bf16*)A, lda, (const bf16*)W, ldw, e, nTn); break;
-      C_(RF_EPI_NONE) C_(RF_EPI_BIAS) C_(RF_EPI_BIAS_GELU) C_(RF_EPI_BIAS_RESID) C_(RF_EPI_COS)
-#undef C_
+      case RF_EPI_NONE:
+        if (cf) k_gemm_bf16<RF_EPI_NONE, true, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        else k_gemm_bf16<RF_EPI_NONE, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        break;
+      case RF_EPI_BIAS:
+        if (cf) k_gemm_bf16<RF_EPI_BIAS, true, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        else k_gemm_bf16<RF_EPI_BIAS, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        break;
+      case RF_EPI_BIAS_GELU:
+        k_gemm_bf16<RF_EPI_BIAS_GELU, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        break;
+      case RF_EPI_BIAS_RESID:
+        if (cf && rf) k_gemm_bf16<RF_EPI_BIAS_RESID, true, true><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        else if (cf) k_gemm_bf16<RF_EPI_BIAS_RESID, true, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        else if (rf) k_gemm_bf16<RF_EPI_BIAS_RESID, false, true><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        else k_gemm_bf16<RF_EPI_BIAS_RESID, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        break;
+      case RF_EPI_COS:
+        k_gemm_bf16<RF_EPI_COS, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        break;
     }
   } else if (dtype == RF_F32) {
     RF_REQUIRE(K % GF_K == 0, "rf_gemm(f32): K=%d must be a multiple of %d", K, GF_K);

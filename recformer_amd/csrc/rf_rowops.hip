@@ -156,13 +156,16 @@ __global__ void __launch_bounds__(256) k_prepare(
 }
 
 // ------------------------------------------------------------------------------------
-// Fused embedding gather + LayerNorm (A3). One wave per token.
-template <typename T, int VEC, int NCH>
+// Fused embedding gather + LayerNorm (A3). One wave per token. Tables in TT (fp32 keeps the
+// reference's fp32 embedding sum under autocast), output in T plus an optional fp32 copy
+// (the fp32 residual stream of the bf16 path).
+template <typename TT, typename T, int VEC, int NCH>
 __global__ void __launch_bounds__(256) k_embed_ln(
     int M, const int32_t* __restrict__ ids, const int32_t* __restrict__ pos,
-    const int32_t* __restrict__ tt, const int32_t* __restrict__ ip, const T* __restrict__ we,
-    const T* __restrict__ pe, const T* __restrict__ te, const T* __restrict__ ie,
-    const float* __restrict__ lw, const float* __restrict__ lb, float eps, T* __restrict__ out) {
+    const int32_t* __restrict__ tt, const int32_t* __restrict__ ip, const TT* __restrict__ we,
+    const TT* __restrict__ pe, const TT* __restrict__ te, const TT* __restrict__ ie,
+    const float* __restrict__ lw, const float* __restrict__ lb, float eps, T* __restrict__ out,
+    float* __restrict__ out32) {
   constexpr int D = 64 * VEC * NCH;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -175,10 +178,10 @@ __global__ void __launch_bounds__(256) k_embed_ln(
   for (int c = 0; c < NCH; ++c) {
     const int e = c * 64 * VEC + lane * VEC;
     float a[VEC], b2[VEC], c2[VEC], d2[VEC];
-    Vec<T, VEC>::load(we + r0 + e, a);
-    Vec<T, VEC>::load(pe + r1 + e, b2);
-    Vec<T, VEC>::load(te + r2 + e, c2);
-    Vec<T, VEC>::load(ie + r3 + e, d2);
+    Vec<TT, VEC>::load(we + r0 + e, a);
+    Vec<TT, VEC>::load(pe + r1 + e, b2);
+    Vec<TT, VEC>::load(te + r2 + e, c2);
+    Vec<TT, VEC>::load(ie + r3 + e, d2);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       // summation order of models.py:135: ((word + pos) + type) + item_pos
@@ -205,14 +208,16 @@ __global__ void __launch_bounds__(256) k_embed_ln(
 #pragma unroll
     for (int j = 0; j < VEC; ++j) y[j] = (x[c][j] - mean) * rstd * w[j] + bb[j];
     Vec<T, VEC>::store(out + (int64_t)row * D + e, y);
+    if (out32) Vec<float, VEC>::store(out32 + (int64_t)row * D + e, y);
   }
 }
 
-template <typename T, int VEC, int NCH>
-__global__ void __launch_bounds__(256) k_layernorm(int M, const T* __restrict__ x, int ldx,
+template <typename TX, typename T, int VEC, int NCH>
+__global__ void __launch_bounds__(256) k_layernorm(int M, const TX* __restrict__ x, int ldx,
                                                     const float* __restrict__ lw,
                                                     const float* __restrict__ lb, float eps,
                                                     T* __restrict__ y, int ldy,
+                                                    float* __restrict__ y32,
                                                     float* __restrict__ mean_out,
                                                     float* __restrict__ rstd_out) {
   constexpr int D = 64 * VEC * NCH;
@@ -223,7 +228,7 @@ __global__ void __launch_bounds__(256) k_layernorm(int M, const T* __restrict__ 
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    Vec<T, VEC>::load(x + (int64_t)row * ldx + c * 64 * VEC + lane * VEC, xv[c]);
+    Vec<TX, VEC>::load(x + (int64_t)row * ldx + c * 64 * VEC + lane * VEC, xv[c]);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) s += xv[c][j];
   }
@@ -250,6 +255,7 @@ __global__ void __launch_bounds__(256) k_layernorm(int M, const T* __restrict__ 
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o[j] = (xv[c][j] - mean) * rstd * w[j] + bb[j];
     Vec<T, VEC>::store(y + (int64_t)row * ldy + e, o);
+    if (y32) Vec<float, VEC>::store(y32 + (int64_t)row * D + e, o);
   }
 }
 
@@ -318,6 +324,33 @@ __global__ void __launch_bounds__(256) k_cos_cand(int B, int C, int D, const T* 
     }                                                                   \
   } while (0)
 
+template <typename TT, typename T>
+static int launch_embed(int M, int D, const int32_t* ids, const int32_t* pos, const int32_t* tt,
+                        const int32_t* ip, const void* we, const void* pe, const void* te,
+                        const void* ie, const float* lw, const float* lb, float eps, void* out,
+                        float* out32, hipStream_t s) {
+  dim3 grid((M + 3) / 4);
+#define L_(V, N)                                                                                 \
+  k_embed_ln<TT, T, V, N><<<grid, 256, 0, s>>>(M, ids, pos, tt, ip, (const TT*)we, (const TT*)pe, \
+                                               (const TT*)te, (const TT*)ie, lw, lb, eps, (T*)out, \
+                                               out32)
+  RF_ROW_DISPATCH(D, L_);
+#undef L_
+  RF_LAUNCH_CHECK("rf_embed_ln_fwd");
+}
+
+template <typename TX, typename T>
+static int launch_ln(int M, int D, const void* x, int ldx, const float* w, const float* b,
+                     float eps, void* y, int ldy, float* y32, float* mean, float* rstd,
+                     hipStream_t s) {
+  dim3 grid((M + 3) / 4);
+#define L_(V, N) \
+  k_layernorm<TX, T, V, N><<<grid, 256, 0, s>>>(M, (const TX*)x, ldx, w, b, eps, (T*)y, ldy, y32, mean, rstd)
+  RF_ROW_DISPATCH(D, L_);
+#undef L_
+  RF_LAUNCH_CHECK("rf_layernorm_fwd");
+}
+
 }  // namespace rf
 
 using namespace rf;
@@ -344,57 +377,38 @@ int rf_prepare_inputs(const int64_t* input_ids, const int64_t* attention_mask,
   RF_LAUNCH_CHECK("rf_prepare_inputs");
 }
 
-int rf_embed_ln_fwd(int dtype, int M, int D, const int32_t* ids, const int32_t* pos,
-                    const int32_t* tt, const int32_t* ip, const void* word_emb,
+int rf_embed_ln_fwd(int table_dtype, int out_dtype, int M, int D, const int32_t* ids,
+                    const int32_t* pos, const int32_t* tt, const int32_t* ip, const void* word_emb,
                     const void* pos_emb, const void* type_emb, const void* ipos_emb,
-                    const float* ln_w, const float* ln_b, float eps, void* out,
+                    const float* ln_w, const float* ln_b, float eps, void* out, float* out32,
                     rf_stream_t stream) {
   RF_REQUIRE(M >= 0, "rf_embed_ln_fwd: bad M");
   if (M == 0) return RF_OK;
-  dim3 grid((M + 3) / 4);
   hipStream_t s = as_stream(stream);
-  if (dtype == RF_BF16) {
-#define L_(V, N)                                                                              \
-  k_embed_ln<bf16, V, N><<<grid, 256, 0, s>>>(M, ids, pos, tt, ip, (const bf16*)word_emb,      \
-                                               (const bf16*)pos_emb, (const bf16*)type_emb,    \
-                                               (const bf16*)ipos_emb, ln_w, ln_b, eps, (bf16*)out)
-    RF_ROW_DISPATCH(D, L_);
-#undef L_
-  } else if (dtype == RF_F32) {
-#define L_(V, N)                                                                                \
-  k_embed_ln<float, V, N><<<grid, 256, 0, s>>>(M, ids, pos, tt, ip, (const float*)word_emb,      \
-                                                (const float*)pos_emb, (const float*)type_emb,   \
-                                                (const float*)ipos_emb, ln_w, ln_b, eps,         \
-                                                (float*)out)
-    RF_ROW_DISPATCH(D, L_);
-#undef L_
-  } else {
-    RF_REQUIRE(false, "rf_embed_ln_fwd: bad dtype %d", dtype);
-  }
-  RF_LAUNCH_CHECK("rf_embed_ln_fwd");
+  if (table_dtype == RF_F32 && out_dtype == RF_F32)
+    return launch_embed<float, float>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, s);
+  if (table_dtype == RF_F32 && out_dtype == RF_BF16)
+    return launch_embed<float, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, s);
+  if (table_dtype == RF_BF16 && out_dtype == RF_BF16)
+    return launch_embed<bf16, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, s);
+  RF_REQUIRE(false, "rf_embed_ln_fwd: unsupported dtypes table=%d out=%d", table_dtype, out_dtype);
 }
 
-int rf_layernorm_fwd(int dtype, int M, int D, const void* x, int ldx, const float* w,
-                     const float* b, float eps, void* y, int ldy, float* mean, float* rstd,
-                     rf_stream_t stream) {
+int rf_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, int ldx,
+                     const float* w, const float* b, float eps, void* y, int ldy, float* y32,
+                     float* mean, float* rstd, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && ldx >= D && ldy >= D, "rf_layernorm_fwd: bad shape");
   if (M == 0) return RF_OK;
-  dim3 grid((M + 3) / 4);
   hipStream_t s = as_stream(stream);
-  if (dtype == RF_BF16) {
-#define L_(V, N) \
-  k_layernorm<bf16, V, N><<<grid, 256, 0, s>>>(M, (const bf16*)x, ldx, w, b, eps, (bf16*)y, ldy, mean, rstd)
-    RF_ROW_DISPATCH(D, L_);
-#undef L_
-  } else if (dtype == RF_F32) {
-#define L_(V, N) \
-  k_layernorm<float, V, N><<<grid, 256, 0, s>>>(M, (const float*)x, ldx, w, b, eps, (float*)y, ldy, mean, rstd)
-    RF_ROW_DISPATCH(D, L_);
-#undef L_
-  } else {
-    RF_REQUIRE(false, "rf_layernorm_fwd: bad dtype %d", dtype);
-  }
-  RF_LAUNCH_CHECK("rf_layernorm_fwd");
+  if (x_dtype == RF_BF16 && y_dtype == RF_BF16)
+    return launch_ln<bf16, bf16>(M, D, x, ldx, w, b, eps, y, ldy, y32, mean, rstd, s);
+  if (x_dtype == RF_F32 && y_dtype == RF_BF16)
+    return launch_ln<float, bf16>(M, D, x, ldx, w, b, eps, y, ldy, y32, mean, rstd, s);
+  if (x_dtype == RF_F32 && y_dtype == RF_F32)
+    return launch_ln<float, float>(M, D, x, ldx, w, b, eps, y, ldy, y32, mean, rstd, s);
+  if (x_dtype == RF_BF16 && y_dtype == RF_F32)
+    return launch_ln<bf16, float>(M, D, x, ldx, w, b, eps, y, ldy, y32, mean, rstd, s);
+  RF_REQUIRE(false, "rf_layernorm_fwd: bad dtypes %d/%d", x_dtype, y_dtype);
 }
 
 int rf_row_inv_norm(int dtype, int M, int D, const void* x, int ldx, float eps, float* out,

@@ -234,11 +234,12 @@ class _PackedWeights:
     def _build(model: "RecformerModel", dt: torch.dtype):
         f32 = torch.float32
         emb = model.embeddings
+        # embedding tables stay fp32: the reference sums fp32 embeddings even under autocast
         pk = {
-            "word": emb.word_embeddings.weight.to(dt).contiguous(),
-            "pos": emb.position_embeddings.weight.to(dt).contiguous(),
-            "type": emb.token_type_embeddings.weight.to(dt).contiguous(),
-            "ipos": emb.item_position_embeddings.weight.to(dt).contiguous(),
+            "word": emb.word_embeddings.weight.to(f32).contiguous(),
+            "pos": emb.position_embeddings.weight.to(f32).contiguous(),
+            "type": emb.token_type_embeddings.weight.to(f32).contiguous(),
+            "ipos": emb.item_position_embeddings.weight.to(f32).contiguous(),
             "ln_w": emb.LayerNorm.weight.to(f32).contiguous(),
             "ln_b": emb.LayerNorm.bias.to(f32).contiguous(),
             "layers": [],
@@ -340,6 +341,13 @@ class RecformerModel(nn.Module):
             return out
         return RecformerModelOutput(last_hidden_state=last, pooler_output=pooled, hidden_states=hidden_all)
 
+    def _ln(self, t, w, b, dt, mixed):
+        if mixed:
+            return ops.layernorm(t, w, b, self.config.layer_norm_eps, out_dtype=dt, want_f32=True,
+                                 tag="layernorm")
+        y = ops.layernorm(t, w, b, self.config.layer_norm_eps, out=t, tag="layernorm")
+        return y, y
+
     @torch.no_grad()
     def _encode(self, input_ids, attention_mask, global_attention_mask, token_type_ids,
                 position_ids, item_position_ids, output_hidden_states):
@@ -363,9 +371,14 @@ class RecformerModel(nn.Module):
         ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
             input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
             position_ids, Lp, cfg.pad_token_id, gmax)
-        h = ops.embed_ln(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
-                         pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps)
-        hidden_all = [h] if output_hidden_states else None
+        # bf16 path: GEMM operands in bf16, residual stream / LN outputs in fp32 (as the
+        # reference's autocast run); fp32 path: everything fp32 (h32 is h).
+        mixed = dt != torch.float32
+        h, h32 = ops.embed_ln(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
+                              pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps, out_dtype=dt, want_f32=mixed)
+        if not mixed:
+            h32 = h
+        hidden_all = [h32] if output_hidden_states else None
         scale = 1.0 / math.sqrt(hd)
         windows = cfg.window_per_layer()
         for li, lw in enumerate(pk["layers"]):
@@ -380,14 +393,18 @@ class RecformerModel(nn.Module):
                 qg = ops.gemm(hg, lw["w_qg"], lw["b_qg"], ops.RF_EPI_BIAS, scale_cols=D, col_scale=scale)
                 ops.global_attention(qg, qkv[:, 3 * D:4 * D], qkv[:, 4 * D:5 * D], flags, gidx,
                                      B, Lp, H, ctx, tag="global_attn")
-            t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h, tag="gemm_out")
-            a = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], cfg.layer_norm_eps, out=t, tag="layernorm")
+            # pre-LN residual sums are kept in fp32 (the reference's autocast residual stream is
+            # fp32); LayerNorm re-emits the compute dtype for the next GEMM.
+            t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h32, out_f32=True,
+                         tag="gemm_out")
+            a, a32 = self._ln(t, lw["ln1_w"], lw["ln1_b"], dt, mixed)
             f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
-            t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a, tag="gemm_ffn2")
-            h = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], cfg.layer_norm_eps, out=t2, tag="layernorm")
+            t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a32, out_f32=True,
+                          tag="gemm_ffn2")
+            h, h32 = self._ln(t2, lw["ln2_w"], lw["ln2_b"], dt, mixed)
             if output_hidden_states:
-                hidden_all.append(h)
-        last = h.view(B, Lp, D)[:, :L]
+                hidden_all.append(h32)
+        last = h32.view(B, Lp, D)[:, :L]
         if output_hidden_states:
             hidden_all = tuple(x.view(B, Lp, D)[:, :L] for x in hidden_all)
         return last, hidden_all

@@ -117,7 +117,9 @@ def prepare_inputs(input_ids, attention_mask, global_attention_mask, token_type_
     return ids, pos, tt, ip, flags, gidx[:, :gmax]
 
 
-def embed_ln(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, ln_b, eps: float):
+def embed_ln(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, ln_b, eps: float,
+             out_dtype: Optional[torch.dtype] = None, want_f32: bool = False):
+    """Returns (out in out_dtype, fp32 copy or None)."""
     lib = _lib.load()
     _dev(ids, word)
     M = ids.numel()
@@ -125,20 +127,22 @@ def embed_ln(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, ln_b, eps: 
     for t in (word, posemb, typeemb, iposemb):
         if not t.is_contiguous() or t.dtype != word.dtype or t.shape[1] != D:
             raise ValueError("embedding tables must be contiguous, same dtype and width")
-    out = torch.empty(M, D, dtype=word.dtype, device=word.device)
-    check(lib.rf_embed_ln_fwd(dtype_code(word.dtype), M, D, _p(ids), _p(pos), _p(tt), _p(ip),
-                              _p(word), _p(posemb), _p(typeemb), _p(iposemb),
+    odt = out_dtype or word.dtype
+    out = torch.empty(M, D, dtype=odt, device=word.device)
+    out32 = torch.empty(M, D, dtype=torch.float32, device=word.device) if want_f32 else None
+    check(lib.rf_embed_ln_fwd(dtype_code(word.dtype), dtype_code(odt), M, D, _p(ids), _p(pos), _p(tt),
+                              _p(ip), _p(word), _p(posemb), _p(typeemb), _p(iposemb),
                               _p(ln_w.float().contiguous()), _p(ln_b.float().contiguous()),
-                              float(eps), _p(out), _stream(out)), "rf_embed_ln_fwd")
-    return out
+                              float(eps), _p(out), _p(out32), _stream(out)), "rf_embed_ln_fwd")
+    return out, out32
 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
          epilogue: int = RF_EPI_BIAS, resid: Optional[torch.Tensor] = None,
          scale_cols: int = 0, col_scale: float = 1.0, out: Optional[torch.Tensor] = None,
          ra: Optional[torch.Tensor] = None, rw: Optional[torch.Tensor] = None,
-         tag: Optional[str] = None) -> torch.Tensor:
-    """C = epi(a . w^T); a (M,K), w (N,K) row-major, same dtype."""
+         tag: Optional[str] = None, out_f32: bool = False) -> torch.Tensor:
+    """C = epi(a . w^T); a (M,K), w (N,K) row-major, same dtype. out_f32 stores C in fp32."""
     lib = _lib.load()
     _dev(a, w, bias, resid)
     if a.dtype != w.dtype:
@@ -148,42 +152,58 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
     if K != K2:
         raise ValueError(f"gemm: K mismatch {K} vs {K2}")
     lda, ldw = _rowmajor(a, "a"), _rowmajor(w, "w")
-    odt = torch.float32 if epilogue == RF_EPI_COS else a.dtype
+    odt = torch.float32 if (epilogue == RF_EPI_COS or out_f32) else a.dtype
+    io = 0
+    if out is not None and out.dtype != odt:
+        raise TypeError(f"gemm: out must be {odt}")
     if out is None:
         out = torch.empty(M, N, dtype=odt, device=a.device)
     ldc = _rowmajor(out, "out")
     ldr = 0
     if resid is not None:
         ldr = _rowmajor(resid, "resid")
-        if resid.dtype != a.dtype or resid.shape != (M, N):
-            raise ValueError("gemm: residual must match output shape/dtype")
+        if resid.dtype not in (a.dtype, torch.float32) or resid.shape != (M, N):
+            raise ValueError("gemm: residual must be (M,N) in the compute dtype or fp32")
+        if resid.dtype == torch.float32 and a.dtype != torch.float32:
+            io |= _lib.RF_IO_R_F32
+    if odt == torch.float32 and a.dtype != torch.float32 and epilogue != RF_EPI_COS:
+        io |= _lib.RF_IO_C_F32
     if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
         raise TypeError("gemm: bias must be contiguous fp32")
     with _region(tag):
         rc = lib.rf_gemm(dtype_code(a.dtype), M, N, K, _p(a), lda, _p(w), ldw, _p(bias), _p(resid),
-                         ldr, _p(out), ldc, epilogue, scale_cols, float(col_scale), _p(ra), _p(rw),
+                         ldr, _p(out), ldc, io, epilogue, scale_cols, float(col_scale), _p(ra), _p(rw),
                          _stream(out))
     check(rc, "rf_gemm")
     return out
 
 
 def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
-              out: Optional[torch.Tensor] = None, stats: bool = False, tag: Optional[str] = None):
+              out: Optional[torch.Tensor] = None, stats: bool = False, tag: Optional[str] = None,
+              out_dtype: Optional[torch.dtype] = None, want_f32: bool = False):
+    """y = LN(x) in out_dtype (default x.dtype); want_f32 also returns an fp32 copy.
+    Returns y, or (y, y32) with want_f32, or (y, mean, rstd) with stats."""
     lib = _lib.load()
     _dev(x)
     M, D = x.shape
     ldx = _rowmajor(x, "x")
     if out is None:
-        out = torch.empty(M, D, dtype=x.dtype, device=x.device)
+        out = torch.empty(M, D, dtype=out_dtype or x.dtype, device=x.device)
+    y32 = torch.empty(M, D, dtype=torch.float32, device=x.device) if want_f32 else None
     mean = rstd = None
     if stats:
         mean = torch.empty(M, dtype=torch.float32, device=x.device)
         rstd = torch.empty(M, dtype=torch.float32, device=x.device)
     with _region(tag):
-        rc = lib.rf_layernorm_fwd(dtype_code(x.dtype), M, D, _p(x), ldx, _p(w), _p(b), float(eps),
-                                  _p(out), _rowmajor(out, "out"), _p(mean), _p(rstd), _stream(x))
+        rc = lib.rf_layernorm_fwd(dtype_code(x.dtype), dtype_code(out.dtype), M, D, _p(x), ldx,
+                                  _p(w), _p(b), float(eps), _p(out), _rowmajor(out, "out"), _p(y32),
+                                  _p(mean), _p(rstd), _stream(x))
     check(rc, "rf_layernorm_fwd")
-    return (out, mean, rstd) if stats else out
+    if stats:
+        return out, mean, rstd
+    if want_f32:
+        return out, y32
+    return out
 
 
 def band_attention(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int,

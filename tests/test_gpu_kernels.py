@@ -48,6 +48,27 @@ def test_gemm_epilogues(dev, dt, M, N, K, epi):
     assert err <= _tol(dt) * max(1.0, ref.abs().max().item()), err
 
 
+def test_gemm_bf16_fp32_output_and_mixed_layernorm(dev):
+    """bf16 GEMM writing the fp32 pre-LN residual sum, then LN fp32 -> bf16."""
+    a = _rand((300, 768), dev, torch.bfloat16, seed=11)
+    w = _rand((768, 768), dev, torch.bfloat16, 0.05, seed=12)
+    b = _rand((768,), dev, torch.float32, seed=13)
+    r = _rand((300, 768), dev, torch.bfloat16, seed=14)
+    t = ops.gemm(a, w, b, ops.RF_EPI_BIAS_RESID, resid=r, out_f32=True)
+    assert t.dtype == torch.float32
+    ref = a.float() @ w.float().t() + b + r.float()
+    assert (t - ref).abs().max().item() <= 1e-3
+    lw = _rand((768,), dev, torch.float32, seed=15)
+    lb = _rand((768,), dev, torch.float32, seed=16)
+    y, y32 = ops.layernorm(t, lw, lb, 1e-5, out_dtype=torch.bfloat16, want_f32=True)
+    assert y.dtype == torch.bfloat16 and y32.dtype == torch.float32
+    assert (y32 - F.layer_norm(ref, (768,), lw, lb, 1e-5)).abs().max().item() <= 1e-3
+    t2 = ops.gemm(a, w, b, ops.RF_EPI_BIAS_RESID, resid=y32, out_f32=True)
+    assert (t2 - (a.float() @ w.float().t() + b + y32)).abs().max().item() <= 1e-3
+    yr = F.layer_norm(ref, (768,), lw, lb, 1e-5)
+    assert (y.float() - yr).abs().max().item() <= 2 ** -8 * yr.abs().max().item() + 1e-3
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gemm_strided_views(dev, dt):
     """Column slices of a fused buffer as A (the q/k/v views) and as W (packed weights)."""
@@ -67,12 +88,15 @@ def test_layernorm(dev, dt, D):
     b = _rand((D,), dev, torch.float32, seed=9)
     y, mean, rstd = ops.layernorm(x, w, b, 1e-5, stats=True)
     ref = F.layer_norm(x.float(), (D,), w, b, 1e-5)
-    assert (y.float() - ref).abs().max().item() <= (1e-4 if dt == torch.float32 else 3e-2)
+    # bf16: output rounding only (half an ulp = 2^-9 relative)
+    tol = 1e-4 if dt == torch.float32 else 2 ** -8 * ref.abs().max().item()
+    assert (y.float() - ref).abs().max().item() <= tol
     assert torch.allclose(mean, x.float().mean(1), atol=1e-4)
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_embed_ln_and_prepare(dev, dt):
+@pytest.mark.parametrize("tdt,dt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.bfloat16, torch.bfloat16)])
+def test_embed_ln_and_prepare(dev, tdt, dt):
     from recformer_amd.synth import synth_batch
     B, L, D, V = 3, 200, 768, 500
     bt = synth_batch(B, L, V, seed=3, lens=[200, 130, 7], extra_globals=((0, 9), (1, 50)))
@@ -92,14 +116,16 @@ def test_embed_ln_and_prepare(dev, dt):
     pos_r = (torch.cumsum(m, 1) * m).long() + 1
     assert torch.equal(pos.cpu().long(), pos_r)
     assert gidx.cpu().tolist() == [[0, 9], [0, 50], [0, -1]]
-    tabs = [_rand((n, D), dev, dt, 0.02, seed=10 + i) for i, n in enumerate((V, 300, 4, 51))]
+    tabs = [_rand((n, D), dev, tdt, 0.02, seed=10 + i) for i, n in enumerate((V, 300, 4, 51))]
     lw = _rand((D,), dev, torch.float32, seed=20)
     lb = _rand((D,), dev, torch.float32, seed=21)
-    out = ops.embed_ln(ids, pos, tt, ip, *tabs, lw, lb, 1e-5)
+    out, out32 = ops.embed_ln(ids, pos, tt, ip, *tabs, lw, lb, 1e-5, out_dtype=dt, want_f32=True)
     x = (tabs[0].float()[ids.long()] + tabs[1].float()[pos.long()] + tabs[2].float()[tt.long()]
          + tabs[3].float()[ip.long()])
     ref = F.layer_norm(x, (D,), lw, lb, 1e-5).view(-1, D)
-    assert (out.float() - ref).abs().max().item() <= (1e-4 if dt == torch.float32 else 3e-2)
+    tol = 1e-4 if dt == torch.float32 else 2 ** -8 * ref.abs().max().item()
+    assert (out.float() - ref).abs().max().item() <= tol
+    assert (out32 - ref).abs().max().item() <= 1e-4
 
 
 def _attn_case(dev, dt, B, Lp, H, lens, globals_, seed):

@@ -62,7 +62,7 @@ def test_library_exports_every_header_symbol():
 def test_argument_errors_come_back_as_messages():
     lib = _lib.load()
     # bad shape is rejected host-side before any launch (no GPU needed)
-    rc = lib.rf_gemm(1, 64, 64, 63, None, 63, None, 63, None, None, 0, None, 64, 0, 0, 1.0, None, None, None)
+    rc = lib.rf_gemm(1, 64, 64, 63, None, 63, None, 63, None, None, 0, None, 64, 0, 0, 0, 1.0, None, None, None)
     assert rc != 0
     assert b"multiple" in lib.rf_last_error()
 
