@@ -101,6 +101,20 @@ int rf_global_attn_fwd(int dtype, int B, int Lp, int H, int hd, const void* qg, 
                        const int32_t* gidx, int gmax, void* out, int ld_out,
                        rf_stream_t stream);
 
+/* A6, production form — the same global rows through the key/value-projection fold
+ * (exact algebra, different rounding; SURVEY.md §7 'Global-path algebra'):
+ *   s_j = (Wkg_h^T qg_h) . h_j + qg_h . bkg_h over valid keys j,
+ *   ctx[gidx[b,g], h] = Wvg_h (sum_j softmax(s)_j h_j) + bvg_h.
+ * h is the layer input (B*Lp, D) (leading dim ldh), wkg/wvg (D, D) nn.Linear weights in
+ * dtype, bkg/bvg fp32. Replaces key_global/value_global over all L tokens (TF:983-984).
+ * workspace: rf_global_fold_workspace(B, Lp, D, H, gmax) bytes of device memory. */
+size_t rf_global_fold_workspace(int B, int Lp, int D, int H, int gmax);
+int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, const void* qg, int ld_qg,
+                            const void* h, int ldh, const void* wkg, const float* bkg,
+                            const void* wvg, const float* bvg, const uint8_t* flags,
+                            const int32_t* gidx, int gmax, void* workspace, void* out,
+                            int ld_out, rf_stream_t stream);
+
 /* Row gather: out[r] = x[b*Lp + gidx[b, g]] for r = b*gmax + g (zero rows for -1). Feeds
  * the query_global projection of the global rows (TF:972-982). */
 int rf_gather_global_rows(int dtype, int B, int Lp, int D, int gmax, const void* x, int ldx,

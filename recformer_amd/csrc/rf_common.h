@@ -46,8 +46,22 @@ template <typename T> __device__ __forceinline__ T from_f32(float x);
 template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 
-// exact-erf GELU (transformers ACT2FN['gelu'], TF:1115)
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// erf with |error| <= 1.5e-7 (Abramowitz & Stegun 7.1.26): one v_rcp, one v_exp and a
+// degree-5 Horner chain — ~4x fewer VALU issues than the libm erff, which dominated the
+// FFN1 GEMM epilogue (it runs after the MFMA loop, so its VALU cost is not hidden).
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float y = fmaf(-p * t, __expf(-ax * ax), 1.0f);
+  return copysignf(y, x);
+}
+
+// exact-erf GELU (transformers ACT2FN['gelu'] = x * Phi(x), TF:1115), |error| < 1e-6 |x|
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
 // ---- wave64 reductions ----------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {

@@ -3,11 +3,19 @@
 // Replaces the nn.Linear addmm's of the Longformer layer (TF:504-506, 982-984,
 // 1064-1071, 1107, 1123) and the scoring product of Similarity (models.py:358-369).
 //
-// bf16 path: 128x128x64 block tile, 4 waves (2x2) of 64x64, v_mfma_f32_16x16x32_bf16,
-// operands staged HBM->LDS by 16-B global_load_lds (lane-linear LDS image, XOR swizzle
-// applied on the per-lane SOURCE address and on the ds_read_b128 — guide §5.4 rule 21,
-// §5.5 T2), two LDS buffers so the next K tile's DMA overlaps this tile's MFMAs,
-// bijective XCD-aware block remap (guide §5 'XCD swizzle must be bijective').
+// bf16 path (k_gemm_bf16<BM,BN,WM,WN,...>): v_mfma_f32_16x16x32_bf16, BK = 64. Operands are
+// DMA'd HBM->LDS by 16-B global_load_lds into a lane-linear image; the XOR swizzle that
+// makes the ds_read_b128 operand reads conflict-free is applied to the per-lane SOURCE
+// address and to the read (guide §5.4 rule 21, §5.5 T2). Two LDS stages: tile k+1's DMA
+// is in flight while tile k's MFMAs run. Blocks are remapped bijectively so consecutive
+// tiles (sharing an A panel) land on one XCD's L2 (guide §5 T1).
+//   * 256x256 tile, 8 waves of 128x64 — the production shape: 128 flop per staged byte,
+//     so the L2->LDS stream needs ~20 TB/s at MFMA peak (a 128^2 tile would need ~39 TB/s,
+//     above what the XCD L2s deliver);
+//   * 128x128 tile, 4 waves of 64x64 — for small M or N (global rows, scoring).
+// Epilogue: each wave stages 16-row slabs of fp32 accumulators through LDS and writes
+// whole rows with 16-B vector stores (bias / q-scale / GELU / residual / cosine scale
+// applied in fp32 on the way).
 // fp32 path: exact-f32 v_mfma_f32_16x16x4_f32, 64x64x16 tiles, register staging.
 #include "rf_common.h"
 
@@ -26,6 +34,7 @@ struct EpiArgs {
   const float* rw;
 };
 
+// scalar epilogue (fp32 kernel and ragged tails)
 template <typename TIN, int EPI, bool CF32, bool RF32>
 __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, float v) {
   if (row >= e.M || col >= e.N) return;
@@ -55,49 +64,129 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // ------------------------------------------------------------------------------------
 // bf16
-constexpr int GB_M = 128, GB_N = 128, GB_K = 64;
-constexpr int GB_TILE_BYTES = GB_M * GB_K * 2;  // 16 KiB per operand tile
+constexpr int GB_K = 64;
+constexpr int EPI_LD = 68;  // fp32 staging row stride (floats): conflict-free write + b128 read
 
+// 16 consecutive columns [c0, c0+16) of one output row: vector epilogue.
 template <int EPI, bool CF32, bool RF32>
-__global__ void __launch_bounds__(256) k_gemm_bf16(int K, const bf16* __restrict__ A, int lda,
-                                                    const bf16* __restrict__ W, int ldw, EpiArgs e,
-                                                    int nTn) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (A tile + W tile) = 64 KiB
-  const int nwg = gridDim.x;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int tm = wg / nTn, tn = wg - tm * nTn;
-  const int m0 = tm * GB_M, n0 = tn * GB_N;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-
-  // per-lane staging sources: wave stages chunks c = wave*4+i (8 rows each) of each tile
-  const bf16* asrc[4];
-  const bf16* wsrc[4];
+__device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, float* v) {
+  if (row >= e.M) return;
+  if (c0 + 16 > e.N) {  // ragged right edge: scalar path
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wave * 4 + i) * 8 + (lane >> 3);
+    for (int k = 0; k < 16; ++k) epi_store<bf16, EPI, CF32, RF32>(e, row, c0 + k, v[k]);
+    return;
+  }
+  if (EPI == RF_EPI_COS) {
+    const float s = e.ra[row] * e.col_scale;
+    float* out = reinterpret_cast<float*>(e.C) + (int64_t)row * e.ldc + c0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 w = *reinterpret_cast<const float4*>(e.rw + c0 + 4 * q);
+      *reinterpret_cast<float4*>(out + 4 * q) =
+          make_float4(v[4 * q] * s * w.x, v[4 * q + 1] * s * w.y, v[4 * q + 2] * s * w.z, v[4 * q + 3] * s * w.w);
+    }
+    return;
+  }
+  if (EPI != RF_EPI_NONE) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(e.bias + c0 + 4 * q);
+      v[4 * q] += b.x; v[4 * q + 1] += b.y; v[4 * q + 2] += b.z; v[4 * q + 3] += b.w;
+    }
+  }
+  if (c0 < e.scale_cols) {
+    // scale_cols is a multiple of 16 on every call site (head-aligned q columns)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] *= e.col_scale;
+  }
+  if (EPI == RF_EPI_BIAS_GELU) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = gelu_erf(v[k]);
+  }
+  if (EPI == RF_EPI_BIAS_RESID) {
+    if (RF32) {
+      const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)row * e.ldr + c0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(r + 4 * q);
+        v[4 * q] += x.x; v[4 * q + 1] += x.y; v[4 * q + 2] += x.z; v[4 * q + 3] += x.w;
+      }
+    } else {
+      const bf16* r = reinterpret_cast<const bf16*>(e.R) + (int64_t)row * e.ldr + c0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const bf16x8 x = *reinterpret_cast<const bf16x8*>(r + 8 * q);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[8 * q + k] += (float)x[k];
+      }
+    }
+  }
+  if (CF32) {
+    float* out = reinterpret_cast<float*>(e.C) + (int64_t)row * e.ldc + c0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(out + 4 * q) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  } else {
+    bf16* out = reinterpret_cast<bf16*>(e.C) + (int64_t)row * e.ldc + c0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      bf16x8 x;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = (bf16)v[8 * q + k];
+      *reinterpret_cast<bf16x8*>(out + 8 * q) = x;
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, bool CF32, bool RF32>
+__global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64)
+    k_gemm_bf16(int K, const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw,
+                EpiArgs e, int nTn) {
+  constexpr int NWN = BN / WN;
+  constexpr int NWAVES = (BM / WM) * NWN;
+  constexpr int FM = WM / 16, FN = WN / 16;          // 16x16 fragments per wave
+  constexpr int A_BYTES = BM * GB_K * 2, B_BYTES = BN * GB_K * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int CHUNKS = (BM + BN) / 8;              // 1-KiB DMA pieces per stage
+  constexpr int CPW = CHUNKS / NWAVES;               // per wave
+  constexpr int ACH = BM / 8;                        // A pieces come first
+  static_assert(CHUNKS % NWAVES == 0, "staging split");
+  static_assert(NWAVES * 16 * EPI_LD * 4 <= 2 * STAGE, "epilogue scratch");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = wg / nTn, tn = wg - tm * nTn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / NWN, wn = wave % NWN;
+
+  // per-lane DMA sources: wave stages pieces c = wave*CPW + i (8 rows of 128 B each)
+  const bf16* src[CPW];
+  int dst[CPW];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) {
+    const int c = wave * CPW + i;
+    const bool isA = c < ACH;
+    const int row = (isA ? c : c - ACH) * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ (row & 7);
-    const int ar = min(m0 + row, e.M - 1);
-    const int wr = min(n0 + row, e.N - 1);
-    asrc[i] = A + (int64_t)ar * lda + ch * 8;
-    wsrc[i] = W + (int64_t)wr * ldw + ch * 8;
+    if (isA)
+      src[i] = A + (int64_t)min(m0 + row, e.M - 1) * lda + ch * 8;
+    else
+      src[i] = W + (int64_t)min(n0 + row, e.N - 1) * ldw + ch * 8;
+    dst[i] = isA ? c * 1024 : A_BYTES + (c - ACH) * 1024;
   }
   auto stage = [&](int kt, int buf) {
-    char* as = smem + buf * 2 * GB_TILE_BYTES;
-    char* ws = as + GB_TILE_BYTES;
+    char* base = smem + buf * STAGE;
     const int koff = kt * GB_K;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      glds16(asrc[i] + koff, as + (wave * 4 + i) * 1024);
-      glds16(wsrc[i] + koff, ws + (wave * 4 + i) * 1024);
-    }
+    for (int i = 0; i < CPW; ++i) glds16(src[i] + koff, base + dst[i]);
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / GB_K;
   stage(0, 0);
@@ -106,35 +195,53 @@ __global__ void __launch_bounds__(256) k_gemm_bf16(int K, const bf16* __restrict
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    const char* as = smem + cur * 2 * GB_TILE_BYTES;
-    const char* ws = as + GB_TILE_BYTES;
+    const char* as = smem + cur * STAGE;
+    const char* ws = as + A_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int ch = 4 * s + (lane >> 4);
-      bf16x8 a[4], b[4];
+      bf16x8 a[FM], b[FN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = *reinterpret_cast<const bf16x8*>(as + swz128(wm * 64 + i * 16 + (lane & 15), ch));
-        b[i] = *reinterpret_cast<const bf16x8*>(ws + swz128(wn * 64 + i * 16 + (lane & 15), ch));
-      }
+      for (int i = 0; i < FM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(as + swz128(wm * WM + i * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < FN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(ws + swz128(wn * WN + j * 16 + (lane & 15), ch));
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     wait_vmcnt0();
     __syncthreads();
   }
 
+  // ---- epilogue: per wave, 16-row slabs through LDS, then row-major vector stores ----
+  float* scr = reinterpret_cast<float*>(smem) + wave * 16 * EPI_LD;
+  const int rr = lane >> 2, cc = (lane & 3) * 16;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j0 = 0; j0 < FN; j0 += 4) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        epi_store<bf16, EPI, CF32, RF32>(e, m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r,
-                             n0 + wn * 64 + j * 16 + (lane & 15), acc[i][j][r]);
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          scr[((lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[i][j0 + j][r];
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(scr + rr * EPI_LD + cc + 4 * q);
+        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
+      epi_row16<EPI, CF32, RF32>(e, m0 + wm * WM + i * 16 + rr, n0 + wn * WN + j0 * 16 + cc, v);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -200,7 +307,34 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int K, const float* __restrict
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         epi_store<float, EPI, false, false>(e, m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r,
-                              n0 + wn * 32 + j * 16 + (lane & 15), acc[i][j][r]);
+                                            n0 + wn * 32 + j * 16 + (lane & 15), acc[i][j][r]);
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, bool CF32, bool RF32>
+static void launch_bf16(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
+                        const EpiArgs& e, hipStream_t s) {
+  constexpr int threads = (BM / WM) * (BN / WN) * 64;
+  constexpr size_t lds = 2 * (size_t)(BM + BN) * GB_K * 2;
+  static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_bf16<BM, BN, WM, WN, EPI, CF32, RF32>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  const int nTm = (M + BM - 1) / BM, nTn = (N + BN - 1) / BN;
+  k_gemm_bf16<BM, BN, WM, WN, EPI, CF32, RF32><<<nTm * nTn, threads, lds, s>>>(
+      K, (const bf16*)A, lda, (const bf16*)W, ldw, e, nTn);
+}
+
+template <int EPI, bool CF32, bool RF32>
+static void dispatch_tile(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
+                          const EpiArgs& e, hipStream_t s) {
+  // 256x256 when the grid still covers the chip; 128x128 for skinny problems
+  const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  if (tiles256 >= 128)
+    launch_bf16<256, 256, 128, 64, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+  else
+    launch_bf16<128, 128, 64, 64, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
 }
 
 }  // namespace rf
@@ -223,32 +357,30 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
   if (dtype == RF_BF16) {
     RF_REQUIRE(K % GB_K == 0, "rf_gemm(bf16): K=%d must be a multiple of %d", K, GB_K);
     RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0, "rf_gemm(bf16): lda/ldw must be multiples of 8");
-    const int nTm = (M + GB_M - 1) / GB_M, nTn = (N + GB_N - 1) / GB_N;
-    const size_t lds = 4 * GB_TILE_BYTES;
+    RF_REQUIRE(ldc % 8 == 0 && (resid == nullptr || ldr % 8 == 0),
+               "rf_gemm(bf16): ldc/ldr must be multiples of 8 (16-B vector epilogue)");
+    RF_REQUIRE(scale_cols % 16 == 0, "rf_gemm(bf16): scale_cols must be a multiple of 16");
     const bool cf = io_flags & RF_IO_C_F32, rf = io_flags & RF_IO_R_F32;
-    const dim3 grid(nTm * nTn);
-    const bf16* Ab = (const bf16*)A;
-    const bf16* Wb = (const bf16*)W;
     switch (epilogue) {
       case RF_EPI_NONE:
-        if (cf) k_gemm_bf16<RF_EPI_NONE, true, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
-        else k_gemm_bf16<RF_EPI_NONE, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        if (cf) dispatch_tile<RF_EPI_NONE, true, false>(M, N, K, A, lda, W, ldw, e, s);
+        else dispatch_tile<RF_EPI_NONE, false, false>(M, N, K, A, lda, W, ldw, e, s);
         break;
       case RF_EPI_BIAS:
-        if (cf) k_gemm_bf16<RF_EPI_BIAS, true, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
-        else k_gemm_bf16<RF_EPI_BIAS, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        if (cf) dispatch_tile<RF_EPI_BIAS, true, false>(M, N, K, A, lda, W, ldw, e, s);
+        else dispatch_tile<RF_EPI_BIAS, false, false>(M, N, K, A, lda, W, ldw, e, s);
         break;
       case RF_EPI_BIAS_GELU:
-        k_gemm_bf16<RF_EPI_BIAS_GELU, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        dispatch_tile<RF_EPI_BIAS_GELU, false, false>(M, N, K, A, lda, W, ldw, e, s);
         break;
       case RF_EPI_BIAS_RESID:
-        if (cf && rf) k_gemm_bf16<RF_EPI_BIAS_RESID, true, true><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
-        else if (cf) k_gemm_bf16<RF_EPI_BIAS_RESID, true, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
-        else if (rf) k_gemm_bf16<RF_EPI_BIAS_RESID, false, true><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
-        else k_gemm_bf16<RF_EPI_BIAS_RESID, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        if (cf && rf) dispatch_tile<RF_EPI_BIAS_RESID, true, true>(M, N, K, A, lda, W, ldw, e, s);
+        else if (cf) dispatch_tile<RF_EPI_BIAS_RESID, true, false>(M, N, K, A, lda, W, ldw, e, s);
+        else if (rf) dispatch_tile<RF_EPI_BIAS_RESID, false, true>(M, N, K, A, lda, W, ldw, e, s);
+        else dispatch_tile<RF_EPI_BIAS_RESID, false, false>(M, N, K, A, lda, W, ldw, e, s);
         break;
       case RF_EPI_COS:
-        k_gemm_bf16<RF_EPI_COS, false, false><<<grid, 256, lds, s>>>(K, Ab, lda, Wb, ldw, e, nTn);
+        dispatch_tile<RF_EPI_COS, false, false>(M, N, K, A, lda, W, ldw, e, s);
         break;
     }
   } else if (dtype == RF_F32) {

@@ -381,9 +381,12 @@ class RecformerModel(nn.Module):
         hidden_all = [h32] if output_hidden_states else None
         scale = 1.0 / math.sqrt(hd)
         windows = cfg.window_per_layer()
+        # global rows: the key/value-projection fold by default; `config.global_attention_fold
+        # = False` keeps the reference's structure (k_g/v_g projected over all tokens).
+        fold = getattr(cfg, "global_attention_fold", True)
         for li, lw in enumerate(pk["layers"]):
             half_w = windows[li] // 2
-            nq = 5 * D if gmax > 0 else 3 * D
+            nq = 5 * D if (gmax > 0 and not fold) else 3 * D
             qkv = ops.gemm(h, lw["w_qkv"][:nq], lw["b_qkv"][:nq], ops.RF_EPI_BIAS,
                            scale_cols=D, col_scale=scale, tag="gemm_qkv")
             ctx = ops.band_attention(qkv[:, 0:D], qkv[:, D:2 * D], qkv[:, 2 * D:3 * D], flags,
@@ -391,8 +394,13 @@ class RecformerModel(nn.Module):
             if gmax > 0:
                 hg = ops.gather_global_rows(h, gidx, B, Lp)
                 qg = ops.gemm(hg, lw["w_qg"], lw["b_qg"], ops.RF_EPI_BIAS, scale_cols=D, col_scale=scale)
-                ops.global_attention(qg, qkv[:, 3 * D:4 * D], qkv[:, 4 * D:5 * D], flags, gidx,
-                                     B, Lp, H, ctx, tag="global_attn")
+                if fold:
+                    ops.global_attention_fold(qg, h, lw["w_qkv"][3 * D:4 * D], lw["b_qkv"][3 * D:4 * D],
+                                              lw["w_qkv"][4 * D:5 * D], lw["b_qkv"][4 * D:5 * D],
+                                              flags, gidx, B, Lp, H, ctx, tag="global_attn")
+                else:
+                    ops.global_attention(qg, qkv[:, 3 * D:4 * D], qkv[:, 4 * D:5 * D], flags, gidx,
+                                         B, Lp, H, ctx, tag="global_attn")
             # pre-LN residual sums are kept in fp32 (the reference's autocast residual stream is
             # fp32); LayerNorm re-emits the compute dtype for the next GEMM.
             t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h32, out_f32=True,

@@ -244,6 +244,30 @@ def global_attention(qg, kg, vg, flags, gidx, B: int, Lp: int, H: int, out: torc
     return out
 
 
+def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int,
+                          out: torch.Tensor, tag: Optional[str] = None):
+    """Global query rows through the key/value-projection fold (rf_global_attn_fold_fwd):
+    overwrites ctx rows at the global positions."""
+    lib = _lib.load()
+    gmax = gidx.shape[1]
+    if gmax == 0:
+        return out
+    _dev(qg, h, wkg, wvg, flags)
+    D = h.shape[1]
+    ws_bytes = lib.rf_global_fold_workspace(B, Lp, D, H, gmax)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=h.device)
+    for t in (wkg, wvg):
+        if not t.is_contiguous() or t.dtype != h.dtype:
+            raise ValueError("global_attention_fold: weights must be contiguous in the compute dtype")
+    with _region(tag):
+        rc = lib.rf_global_attn_fold_fwd(dtype_code(h.dtype), B, Lp, D, H, _p(qg), _rowmajor(qg, "qg"),
+                                         _p(h), _rowmajor(h, "h"), _p(wkg), _p(bkg), _p(wvg), _p(bvg),
+                                         _p(flags), _p(gidx.contiguous()), gmax, _p(ws), _p(out),
+                                         _rowmajor(out, "out"), _stream(out))
+    check(rc, "rf_global_attn_fold_fwd")
+    return out
+
+
 def gather_global_rows(x, gidx, B: int, Lp: int):
     lib = _lib.load()
     gmax = gidx.shape[1]

@@ -33,7 +33,7 @@ def test_gemm_epilogues(dev, dt, M, N, K, epi):
     w = _rand((N, K), dev, dt, 0.05, seed=2)
     b = _rand((N,), dev, torch.float32, seed=3)
     r = _rand((M, N), dev, dt, seed=4)
-    sc = N // 3
+    sc = (N // 3) // 16 * 16          # head-aligned q columns
     out = ops.gemm(a, w, b if epi else None, epi, resid=r if epi == ops.RF_EPI_BIAS_RESID else None,
                    scale_cols=sc, col_scale=0.125)
     ref = a.float() @ w.float().t()
@@ -190,3 +190,41 @@ def test_cos_scores(dev, dt):
     sc = ops.cos_scores_cand(z, E, cand, 20.0)
     refc = torch.gather(ref, 1, cand)
     assert (sc - refc).abs().max().item() <= (1e-4 if dt == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [
+    dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
+    dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
+    dict(B=2, Lp=1024, H=12, lens=[1024, 333], globals_=((0, 0), (1, 0))),
+])
+def test_global_attention_fold(dev, dt, case):
+    """Fold form (u = Wkg^T qg over h, out = Wvg (sum p h) + b) vs the reference structure
+    (k_g = Wkg h + b over all tokens, softmax, p . v_g), both on the same inputs in fp32."""
+    B, Lp, H = case["B"], case["Lp"], case["H"]
+    D = H * 64
+    _, merged, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, case["lens"], case["globals_"], 3)
+    h = _rand((B * Lp, D), dev, dt, 1.0, seed=40)
+    wkg = _rand((D, D), dev, dt, 0.05, seed=41)
+    wvg = _rand((D, D), dev, dt, 0.05, seed=42)
+    bkg = _rand((D,), dev, torch.float32, 0.1, seed=43)
+    bvg = _rand((D,), dev, torch.float32, 0.1, seed=44)
+    qg = _rand((B * G, D), dev, dt, 1.0, seed=45)
+    ctx = torch.zeros(B * Lp, D, dtype=dt, device=dev)
+    ops.global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, ctx)
+    hf = h.float().cpu()
+    kg = (hf @ wkg.float().cpu().t() + bkg.cpu()).view(B, Lp, H, 64).transpose(1, 2)
+    vg = (hf @ wvg.float().cpu().t() + bvg.cpu()).view(B, Lp, H, 64).transpose(1, 2)
+    q = qg.float().cpu().view(B, G, H, 64).transpose(1, 2)
+    valid = (merged > 0)
+    s = torch.matmul(q, kg.transpose(-1, -2)).masked_fill(~valid.view(B, 1, 1, Lp), float("-inf"))
+    og = torch.matmul(torch.softmax(s, -1), vg)                 # (B,H,G,64)
+    got = ctx.float().cpu().view(B, Lp, H, 64)
+    gl = gidx.cpu()
+    for b in range(B):
+        for g in range(G):
+            p = int(gl[b, g])
+            if p < 0:
+                continue
+            err = (got[b, p] - og[b, :, g]).abs().max().item()
+            assert err <= (1e-4 if dt == torch.float32 else 2e-2), (b, g, err)
