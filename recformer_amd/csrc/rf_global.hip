@@ -3,34 +3,56 @@
 //
 // The reference projects key_global / value_global over ALL L tokens of every layer
 // (TF:983-984) only to serve the G global query rows (TF:964-1057). Per head h:
-//     s_j   = qg_h . (Wkg_h h_j + bkg_h) = u_h . h_j + c_h,   u_h = Wkg_h^T qg_h, c_h = qg_h . bkg_h
+//     s_j   = qg_h . (Wkg_h h_j + bkg_h) = u_h . h_j + c_h,   u_h = Wkg_h^T qg_h
 //     out_h = sum_j p_j (Wvg_h h_j + bvg_h) = Wvg_h w_h + bvg_h,  w_h = sum_j p_j h_j  (sum p = 1)
-// so the two d x d projections over L tokens (4 L d^2 flops/layer, 2/5 of the fused QKV
-// GEMM) collapse to two per-head GEMVs plus one streaming pass over h. Same algebra,
-// different rounding (fp32 throughout here; checked against the oracle in the tests).
+// c_h = qg_h . bkg_h is the same for every key j, so softmax removes it. The two d x d
+// projections over L tokens (4 L d^2 flops/layer, 2/5 of the fused QKV GEMM) collapse to
+// per-head GEMVs plus one streaming pass over h. Same algebra, different rounding.
 //
-//   k_gfold_u       (H, B*G):    u = Wkg_h^T qg_h, c = qg_h . bkg_h        (fp32 workspace)
-//   k_gfold_partial (Lp/CH, B*G): per CH-row chunk: s = u.h_j + c (masked to valid keys),
-//                                chunk max/sum per head, w_part = sum_j p_j h_j
-//   k_gfold_out     (H, B*G):    merge chunks (log-sum-exp), out = Wvg_h w_h + bvg_h,
-//                                written into ctx at the global token's row
+//   k_gfold_u        (16, R):     u_h = Wkg_h^T qg_h  (bf16 path: bf16 [R][16][D], heads>=H = 0;
+//                                                      fp32 path: fp32 [R][H][D+4])
+//   k_gfold_partial  (Lp/64, R):  one 64-row chunk of h: s = u.h_j over valid keys, chunk
+//                                 max / sum per head, w_part[c][h] = sum_j p_j h_j[c].
+//                                 bf16: the 64 x D chunk is DMA'd to LDS once; S^T = H.U^T and
+//                                 W^T = H^T.P^T run on v_mfma_f32_16x16x32_bf16 (H^T and P^T
+//                                 through ds_read_b64_tr_b16), like the band-attention kernel
+//                                 with "keys = values = h" and the heads as 16 queries.
+//   k_gfold_out      (H, R):      log-sum-exp merge of the chunks, out = Wvg_h w_h + bvg_h,
+//                                 written into ctx at the global token's row (TF:621-629).
 #include "rf_common.h"
 
 namespace rf {
 
 constexpr float GF_NEG_INF = -__builtin_inff();
-constexpr int GF_CH = 64;     // rows per partial chunk
-constexpr int GF_HMAX = 16;   // heads handled per block (H <= 16)
+constexpr int GF_CH = 256;    // rows per chunk (bf16 kernel walks it in 64-row sub-chunks)
+constexpr int GF_CHF = 64;    // rows per chunk of the fp32 VALU kernel
+constexpr int GF_HP = 16;     // heads padded to one MFMA column tile (H <= 16)
 
 struct GfoldWs {
-  float* u;      // [R][H][Dp]   (Dp = D + 4, padded rows)
-  float* c;      // [R][H]
-  float* m;      // [R][nch][H]
-  float* l;      // [R][nch][H]
-  float* w;      // [R][nch][H][D]
+  bf16* u16;     // [R][2 planes hi/lo][16][D]
+  float* u32;    // [R][H][D+4]
+  float* m;      // [R][nch][16]
+  float* l;      // [R][nch][16]
+  float* w;      // [R][nch][16][D]
 };
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+inline GfoldWs gfold_carve(void* ws, int R, int nch, int H, int D) {
+  char* p = (char*)ws;
+  GfoldWs w;
+  w.u16 = (bf16*)p; p += align256((size_t)R * 2 * GF_HP * D * 2);
+  w.u32 = (float*)p; p += align256((size_t)R * H * (D + 4) * 4);
+  w.m = (float*)p; p += align256((size_t)R * nch * GF_HP * 4);
+  w.l = (float*)p; p += align256((size_t)R * nch * GF_HP * 4);
+  w.w = (float*)p;
+  return w;
+}
+
+inline size_t gfold_bytes(int R, int nch, int H, int D) {
+  return align256((size_t)R * 2 * GF_HP * D * 2) + align256((size_t)R * H * (D + 4) * 4) +
+         2 * align256((size_t)R * nch * GF_HP * 4) + (size_t)R * nch * D * GF_HP * 4;
+}
 
 __device__ __forceinline__ void load4(const float* p, float* x) {
   const float4 v = *reinterpret_cast<const float4*>(p);
@@ -41,53 +63,205 @@ __device__ __forceinline__ void load4(const bf16* p, float* x) {
   x[0] = (float)v[0]; x[1] = (float)v[1]; x[2] = (float)v[2]; x[3] = (float)v[3];
 }
 
-__host__ __device__ inline GfoldWs gfold_carve(void* ws, int R, int nch, int H, int D) {
-  char* p = (char*)ws;
-  GfoldWs w;
-  w.u = (float*)p; p += align256((size_t)R * H * (D + 4) * 4);
-  w.c = (float*)p; p += align256((size_t)R * H * 4);
-  w.m = (float*)p; p += align256((size_t)R * nch * H * 4);
-  w.l = (float*)p; p += align256((size_t)R * nch * H * 4);
-  w.w = (float*)p;
-  return w;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_g;
+__device__ __forceinline__ bf16x4 tr_read_g(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_g*)p);
 }
 
-inline size_t gfold_bytes(int R, int nch, int H, int D) {
-  return align256((size_t)R * H * (D + 4) * 4) + align256((size_t)R * H * 4) +
-         2 * align256((size_t)R * nch * H * 4) + (size_t)R * nch * H * D * 4;
-}
-
+// ---- u = Wkg_h^T qg_h ------------------------------------------------------------------
+// grid (16 heads, ceil(D/256)): a thread owns one column k of Wkg_h (64 weights in registers,
+// read once for all R global rows); the R query rows of head h are staged in LDS.
+// bf16 path writes u as hi + lo bf16 planes (u ~= hi + lo to ~16 mantissa bits), so the MFMA
+// score product keeps fp32-like precision in u: s = hi.h + lo.h.
 template <typename T>
-__global__ void __launch_bounds__(256) k_gfold_u(int D, int H, int gmax, const T* __restrict__ qg,
+__global__ void __launch_bounds__(256) k_gfold_u(int D, int H, int R, const T* __restrict__ qg,
                                                   int ld_qg, const T* __restrict__ wkg,
-                                                  const float* __restrict__ bkg,
-                                                  const int32_t* __restrict__ gidx, GfoldWs ws) {
-  __shared__ float qs[64];
-  const int h = blockIdx.x, r = blockIdx.y;
-  if (gidx[r] < 0) return;
-  const int t = threadIdx.x;
-  if (t < 64) qs[t] = to_f32(qg[(int64_t)r * ld_qg + h * 64 + t]);
-  __syncthreads();
-  const T* wb = wkg + (int64_t)h * 64 * D;
-  float* urow = ws.u + ((int64_t)r * H + h) * (D + 4);
-  for (int k = t; k < D; k += 256) {
-    float a = 0.f;
-#pragma unroll 8
-    for (int d = 0; d < 64; ++d) a = fmaf(qs[d], to_f32(wb[(int64_t)d * D + k]), a);
-    urow[k] = a;
+                                                  const int32_t* __restrict__ gidx, GfoldWs ws,
+                                                  bool out_bf16) {
+  __shared__ float qs[64 * 64];
+  const int h = blockIdx.x;
+  const int k = blockIdx.y * 64 + (threadIdx.x & 63);   // column of Wkg_h
+  const int rgrp = threadIdx.x >> 6;                      // rows r = rgrp (mod 4)
+  const bool kin = k < D;
+  float w[64];
+  if (h < H) {
+#pragma unroll
+    for (int d = 0; d < 64; ++d) w[d] = kin ? to_f32(wkg[(int64_t)(h * 64 + d) * D + k]) : 0.f;
   }
-  if (t < 64) {
-    float cv = wave_sum(qs[t] * bkg[h * 64 + t]);
-    if (t == 0) ws.c[(int64_t)r * H + h] = cv;
+  for (int r0 = 0; r0 < R; r0 += 64) {
+    const int nr = min(64, R - r0);
+    __syncthreads();
+    if (h < H)
+      for (int i = threadIdx.x; i < nr * 64; i += 256)
+        qs[i] = to_f32(qg[(int64_t)(r0 + (i >> 6)) * ld_qg + h * 64 + (i & 63)]);
+    __syncthreads();
+    for (int rr = rgrp; rr < nr; rr += 4) {
+      const int r = r0 + rr;
+      if (!kin || gidx[r] < 0) continue;
+      float a = 0.f;
+      if (h < H) {
+#pragma unroll
+        for (int d = 0; d < 64; ++d) a = fmaf(qs[rr * 64 + d], w[d], a);
+      }
+      if (out_bf16) {
+        const bf16 hi = (bf16)a;
+        ws.u16[((int64_t)r * 2 * GF_HP + h) * D + k] = hi;
+        ws.u16[((int64_t)r * 2 * GF_HP + GF_HP + h) * D + k] = (bf16)(a - (float)hi);
+      } else if (h < H) {
+        ws.u32[((int64_t)r * H + h) * (D + 4) + k] = a;
+      }
+    }
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) k_gfold_partial(int Lp, int D, int H, int gmax,
-                                                        const T* __restrict__ hs, int ldh,
-                                                        const uint8_t* __restrict__ flags,
-                                                        const int32_t* __restrict__ gidx,
-                                                        GfoldWs ws) {
+// ---- bf16 partial: MFMA over a 64-row chunk -----------------------------------------------
+// LDS image of the chunk: segment-major [D/64][64 rows][128 B] with the 16-B slot XOR
+// (row & 7) inside each 128-B segment (lane-linear DMA pieces of 8 rows x 128 B).
+__device__ __forceinline__ int gimg(int row, int col) {
+  return (((col >> 6) * 64 + row) << 7) + ((((col >> 3) & 7) ^ (row & 7)) << 4) + ((col & 7) << 1);
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
+                                                             const bf16* __restrict__ hs, int ldh,
+                                                             const uint8_t* __restrict__ flags,
+                                                             const int32_t* __restrict__ gidx,
+                                                             GfoldWs ws, int H) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NK = D / 32;
+  constexpr int nseg = D >> 6;
+  constexpr int nmt = D >> 6;  // 16-column tiles of W per wave (D/16 tiles over 4 waves)
+  const int ch = blockIdx.x, r = blockIdx.y, nch = gridDim.x;
+  if (gidx[r] < 0) return;
+  const int b = r / gmax;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int q4 = li >> 2, p4 = li & 3;
+  // u fragments (B operand of S^T = H.U^T): hi and lo planes, issued before the first DMA wait
+  bf16x8 uh[NK], ul[NK];
+  {
+    const bf16* uhi = ws.u16 + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
+    const bf16* ulo = uhi + (int64_t)GF_HP * D;
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+      uh[s] = *reinterpret_cast<const bf16x8*>(uhi + 32 * s);
+      ul[s] = *reinterpret_cast<const bf16x8*>(ulo + 32 * s);
+    }
+  }
+  char* pimg = smem + nseg * 64 * 128;                         // P [64 rows][16 heads] bf16
+  float* red = reinterpret_cast<float*>(pimg + 64 * 16 * 2);    // [max 4x16][sum 4x16][m 16][alpha 16]
+  float* m_run = red + 128;
+  float* alpha_s = red + 144;
+  const bf16* hb = hs + (int64_t)b * Lp * ldh;
+  if (threadIdx.x < 16) m_run[threadIdx.x] = GF_NEG_INF;
+  float l_run = 0.f;  // per head li (valid in wave 0, g == 0)
+  f32x4 acc[nmt];
+#pragma unroll
+  for (int i = 0; i < nmt; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int row_begin = ch * GF_CH;
+  const int row_end = min(row_begin + GF_CH, Lp);
+  for (int j0 = row_begin; j0 < row_end; j0 += 64) {
+    __syncthreads();  // previous sub-chunk's LDS reads are done
+    for (int p = wave; p < nseg * 8; p += 4) {
+      const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
+      const int chk = (lane & 7) ^ (row & 7);
+      const int jr = min(j0 + row, Lp - 1);
+      glds16(hb + (int64_t)jr * ldh + seg * 64 + chk * 8, smem + (seg * 64 + (p & 7) * 8) * 128);
+    }
+    wait_vmcnt0();
+    __syncthreads();
+
+    // S^T[j = 16*wave + 4g + q][head = li]
+    f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int arow = 16 * wave + li;
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + gimg(arow, 32 * s + 8 * g));
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, uh[s], st, 0, 0, 0);
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ul[s], st, 0, 0, 0);
+    }
+    float mx = GF_NEG_INF;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + 16 * wave + 4 * g + q;
+      const bool ok = j < Lp && flags[(int64_t)b * Lp + j] != 0;
+      st[q] = ok ? st[q] : GF_NEG_INF;
+      mx = fmaxf(mx, st[q]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (g == 0) red[wave * 16 + li] = mx;
+    __syncthreads();
+    const float m_old = m_run[li];
+    const float m_new = fmaxf(m_old, fmaxf(fmaxf(red[li], red[16 + li]), fmaxf(red[32 + li], red[48 + li])));
+    const float mu = (m_new == GF_NEG_INF) ? 0.f : m_new;
+    float ls = 0.f;
+    bf16* pt = reinterpret_cast<bf16*>(pimg);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float p = __expf(st[q] - mu);
+      ls += p;
+      pt[(16 * wave + 4 * g + q) * 16 + li] = (bf16)p;
+    }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    if (g == 0) red[64 + wave * 16 + li] = ls;
+    __syncthreads();  // P, sums and every wave's read of m_run are done
+    if (wave == 0 && g == 0) {
+      const float a = __expf(m_old - mu);  // 0 when m_old = -inf
+      l_run = l_run * a + red[64 + li] + red[80 + li] + red[96 + li] + red[112 + li];
+      alpha_s[li] = a;
+      m_run[li] = m_new;
+    }
+    __syncthreads();
+    // rescale W rows (head 4g + q) by alpha, then W[head][c] += sum_j p[j][head] h[j][c]
+    float al[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) al[q] = alpha_s[4 * g + q];
+    bf16x8 pa[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int rb = 32 * s + 8 * g + q4;
+      const bf16x4 v0 = tr_read_g(pimg + (rb * 16 + 4 * p4) * 2);
+      const bf16x4 v1 = tr_read_g(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
+      pa[s] = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < nmt; ++i) {
+      const int col = (wave * nmt + i) * 16 + 4 * p4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[i][q] *= al[q];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int rb = 32 * s + 8 * g + q4;
+        const bf16x4 v0 = tr_read_g(smem + gimg(rb, col));
+        const bf16x4 v1 = tr_read_g(smem + gimg(rb + 4, col));
+        const bf16x8 hb8 = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[s], hb8, acc[i], 0, 0, 0);
+      }
+    }
+  }
+  if (wave == 0 && g == 0) {
+    ws.m[((int64_t)r * nch + ch) * GF_HP + li] = m_run[li];
+    ws.l[((int64_t)r * nch + ch) * GF_HP + li] = l_run;
+  }
+  float* wout = ws.w + ((int64_t)r * nch + ch) * GF_HP * D;
+#pragma unroll
+  for (int i = 0; i < nmt; ++i) {
+    const int c0 = (wave * nmt + i) * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * g + q < H) wout[(int64_t)(4 * g + q) * D + c0 + li] = acc[i][q];
+  }
+}
+
+// ---- fp32 partial (VALU; parity path) ------------------------------------------------------
+__global__ void __launch_bounds__(256) k_gfold_partial_f32(int Lp, int D, int H, int gmax,
+                                                            const float* __restrict__ hs, int ldh,
+                                                            const uint8_t* __restrict__ flags,
+                                                            const int32_t* __restrict__ gidx,
+                                                            GfoldWs ws) {
   extern __shared__ __attribute__((aligned(16))) float sm[];  // u: H x (D+4), p: H x CH
   const int ch = blockIdx.x, r = blockIdx.y, nch = gridDim.x;
   if (gidx[r] < 0) return;
@@ -96,19 +270,17 @@ __global__ void __launch_bounds__(256) k_gfold_partial(int Lp, int D, int H, int
   const int Dp = D + 4;
   float* us = sm;
   float* ps = sm + H * Dp;
-  const float* ug = ws.u + (int64_t)r * H * Dp;
+  const float* ug = ws.u32 + (int64_t)r * H * Dp;
   for (int i = t; i < H * Dp; i += 256) us[i] = ug[i];
   __syncthreads();
-
-  const int j0 = ch * GF_CH;
-  const T* hb = hs + (int64_t)b * Lp * ldh;
-  // ---- scores: thread -> (row j = t/4, heads hg, hg+4, hg+8, ...) ----
+  const int j0 = ch * GF_CHF;
+  const float* hb = hs + (int64_t)b * Lp * ldh;
   {
     const int jl = t >> 2, hg = t & 3;
     const int j = j0 + jl;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     if (j < Lp) {
-      const T* hr = hb + (int64_t)j * ldh;
+      const float* hr = hb + (int64_t)j * ldh;
       for (int k = 0; k < D; k += 4) {
         float x[4];
         load4(hr + k, x);
@@ -126,47 +298,44 @@ __global__ void __launch_bounds__(256) k_gfold_partial(int Lp, int D, int H, int
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int hh = hg + 4 * i;
-      if (hh < H) ps[hh * GF_CH + jl] = ok ? s[i] + ws.c[(int64_t)r * H + hh] : GF_NEG_INF;
+      if (hh < H) ps[hh * GF_CHF+ jl] = ok ? s[i] : GF_NEG_INF;
     }
   }
   __syncthreads();
-  // ---- chunk softmax statistics per head (one wave per head, lane = row) ----
   for (int hh = wave; hh < H; hh += 4) {
-    const float sv = ps[hh * GF_CH + lane];
+    const float sv = ps[hh * GF_CHF+ lane];
     const float mx = wave_max(sv);
     const float mu = (mx == GF_NEG_INF) ? 0.f : mx;
     const float p = __expf(sv - mu);
     const float lsum = wave_sum(p);
-    ps[hh * GF_CH + lane] = p;
+    ps[hh * GF_CHF+ lane] = p;
     if (lane == 0) {
-      ws.m[((int64_t)r * nch + ch) * H + hh] = mx;
-      ws.l[((int64_t)r * nch + ch) * H + hh] = lsum;
+      ws.m[((int64_t)r * nch + ch) * GF_HP + hh] = mx;
+      ws.l[((int64_t)r * nch + ch) * GF_HP + hh] = lsum;
     }
   }
   __syncthreads();
-  // ---- w_part[h][k] = sum_j p[h][j] h[j][k]; thread -> columns k = t + 256 i ----
-  const int jn = min(GF_CH, Lp - j0);
-  for (int k0 = 0; k0 < D; k0 += 256) {
-    const int k = k0 + t;
-    if (k >= D) break;
-    float acc[GF_HMAX];
+  const int jn = min(GF_CHF, Lp - j0);
+  float* wout = ws.w + ((int64_t)r * nch + ch) * D * GF_HP;
+  for (int k = t; k < D; k += 256) {
+    float acc[GF_HP];
 #pragma unroll
-    for (int hh = 0; hh < GF_HMAX; ++hh) acc[hh] = 0.f;
+    for (int hh = 0; hh < GF_HP; ++hh) acc[hh] = 0.f;
     for (int jl = 0; jl < jn; ++jl) {
-      const float x = to_f32(hb[(int64_t)(j0 + jl) * ldh + k]);
+      const float x = hb[(int64_t)(j0 + jl) * ldh + k];
 #pragma unroll
-      for (int hh = 0; hh < GF_HMAX; ++hh)
-        if (hh < H) acc[hh] = fmaf(ps[hh * GF_CH + jl], x, acc[hh]);
+      for (int hh = 0; hh < GF_HP; ++hh)
+        if (hh < H) acc[hh] = fmaf(ps[hh * GF_CHF+ jl], x, acc[hh]);
     }
-    float* wout = ws.w + (((int64_t)r * nch + ch) * H) * D + k;
 #pragma unroll
-    for (int hh = 0; hh < GF_HMAX; ++hh)
-      if (hh < H) wout[(int64_t)hh * D] = acc[hh];
+    for (int hh = 0; hh < GF_HP; ++hh)
+      if (hh < H) wout[(int64_t)hh * D + k] = acc[hh];
   }
 }
 
+// ---- merge chunks + out = Wvg_h w_h + bvg_h -------------------------------------------------
 template <typename T>
-__global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int H, int gmax, int nch,
+__global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int gmax, int nch,
                                                     const T* __restrict__ wvg,
                                                     const float* __restrict__ bvg,
                                                     const int32_t* __restrict__ gidx, GfoldWs ws,
@@ -178,17 +347,17 @@ __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int H, int gma
   const int pos = gidx[r];
   if (pos < 0) return;
   const int b = r / gmax;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   if (t < 64) {
     float mx = GF_NEG_INF;
-    for (int c = t; c < nch; c += 64) mx = fmaxf(mx, ws.m[((int64_t)r * nch + c) * H + h]);
+    for (int c = t; c < nch; c += 64) mx = fmaxf(mx, ws.m[((int64_t)r * nch + c) * GF_HP + h]);
     mx = wave_max(mx);
     float ls = 0.f;
     for (int c = t; c < nch; c += 64) {
-      const float mc = ws.m[((int64_t)r * nch + c) * H + h];
+      const float mc = ws.m[((int64_t)r * nch + c) * GF_HP + h];
       const float sc = (mc == GF_NEG_INF) ? 0.f : __expf(mc - mx);
       scl[c] = sc;
-      ls += sc * ws.l[((int64_t)r * nch + c) * H + h];
+      ls += sc * ws.l[((int64_t)r * nch + c) * GF_HP + h];
     }
     ls = wave_sum(ls);
     if (t == 0) lsum_s = ls;
@@ -197,18 +366,22 @@ __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int H, int gma
   const float inv = lsum_s > 0.f ? 1.0f / lsum_s : 0.f;
   for (int k = t; k < D; k += 256) {
     float a = 0.f;
-    for (int c = 0; c < nch; ++c) a = fmaf(scl[c], ws.w[(((int64_t)r * nch + c) * H + h) * D + k], a);
+    for (int c = 0; c < nch; ++c) a = fmaf(scl[c], ws.w[(((int64_t)r * nch + c) * GF_HP + h) * D + k], a);
     wsm[k] = a * inv;
   }
   __syncthreads();
-  // out[d] = Wvg[h*64+d] . w + bvg: 4 threads per output row of Wvg
-  const int d = t >> 2, qtr = t & 3;
-  const T* wr = wvg + (int64_t)(h * 64 + d) * D;
-  float a = 0.f;
-  for (int k = qtr; k < D; k += 4) a = fmaf(to_f32(wr[k]), wsm[k], a);
-  a += __shfl_xor(a, 1, 64);
-  a += __shfl_xor(a, 2, 64);
-  if (qtr == 0) out[((int64_t)b * Lp + pos) * ldo + h * 64 + d] = from_f32<T>(a + bvg[h * 64 + d]);
+  // one wave per 16 output rows of Wvg_h; lanes stride the row with 4-element vectors
+  for (int d = wave * 16; d < wave * 16 + 16; ++d) {
+    const T* wr = wvg + (int64_t)(h * 64 + d) * D;
+    float a = 0.f;
+    for (int k = 4 * lane; k < D; k += 256) {
+      float x[4];
+      load4(wr + k, x);
+      a = fmaf(x[0], wsm[k], fmaf(x[1], wsm[k + 1], fmaf(x[2], wsm[k + 2], fmaf(x[3], wsm[k + 3], a))));
+    }
+    a = wave_sum(a);
+    if (lane == 0) out[((int64_t)b * Lp + pos) * ldo + h * 64 + d] = from_f32<T>(a + bvg[h * 64 + d]);
+  }
 }
 
 }  // namespace rf
@@ -216,8 +389,8 @@ __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int H, int gma
 using namespace rf;
 
 extern "C" size_t rf_global_fold_workspace(int B, int Lp, int D, int H, int gmax) {
-  if (B <= 0 || gmax <= 0) return 0;
-  const int nch = (Lp + GF_CH - 1) / GF_CH;
+  if (B <= 0 || gmax <= 0 || Lp <= 0) return 0;
+  const int nch = (Lp + GF_CHF - 1) / GF_CHF;  // the larger chunk count of the two paths
   return gfold_bytes(B * gmax, nch, H, D);
 }
 
@@ -227,32 +400,50 @@ extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, c
                                        const uint8_t* flags, const int32_t* gidx, int gmax,
                                        void* workspace, void* out, int ld_out,
                                        rf_stream_t stream) {
+  (void)bkg;  // softmax-invariant (see header comment)
   RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0, "rf_global_attn_fold_fwd: bad shape");
   RF_REQUIRE(D == H * 64, "rf_global_attn_fold_fwd: D=%d must be H*64", D);
-  RF_REQUIRE(H <= GF_HMAX, "rf_global_attn_fold_fwd: at most %d heads", GF_HMAX);
-  RF_REQUIRE(D % 4 == 0 && ldh >= D && ld_qg >= D && ld_out >= D, "rf_global_attn_fold_fwd: dims");
+  RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_fwd: at most %d heads", GF_HP);
+  RF_REQUIRE(ldh >= D && ld_qg >= D && ld_out >= D, "rf_global_attn_fold_fwd: dims");
   if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
   RF_REQUIRE(workspace && gidx && flags, "rf_global_attn_fold_fwd: null workspace/gidx/flags");
   const int R = B * gmax;
-  const int nch = (Lp + GF_CH - 1) / GF_CH;
+  const int chunk = dtype == RF_BF16 ? GF_CH : GF_CHF;
+  const int nch = (Lp + chunk - 1) / chunk;
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
-  const size_t lds_p = (size_t)(H * (D + 4) + H * GF_CH) * sizeof(float);
-  RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold_fwd: D too large for LDS");
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
   if (dtype == RF_BF16) {
-    (void)hipFuncSetAttribute((const void*)k_gfold_partial<bf16>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);
-    k_gfold_u<bf16><<<dim3(H, R), 256, 0, s>>>(D, H, gmax, (const bf16*)qg, ld_qg, (const bf16*)wkg, bkg, gidx, ws);
-    k_gfold_partial<bf16><<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const bf16*)h, ldh, flags, gidx, ws);
-    k_gfold_out<bf16><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, H, gmax, nch, (const bf16*)wvg, bvg, gidx, ws,
+    RF_REQUIRE(ldh % 8 == 0, "rf_global_attn_fold_fwd(bf16): ldh must be a multiple of 8");
+    const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + 160 * sizeof(float);
+    RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold_fwd: D too large for LDS");
+    k_gfold_u<bf16><<<dim3(GF_HP, (D + 63) / 64), 256, 0, s>>>(D, H, R, (const bf16*)qg, ld_qg,
+                                                                  (const bf16*)wkg, gidx, ws, true);
+#define GP_(DD)                                                                               \
+  case DD:                                                                                    \
+    (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<DD>,                          \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
+    k_gfold_partial_bf16<DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const bf16*)h, ldh,  \
+                                                              flags, gidx, ws, H);            \
+    break;
+    switch (D) {
+      GP_(64) GP_(128) GP_(192) GP_(256) GP_(384) GP_(512) GP_(768) GP_(1024)
+      default:
+        RF_REQUIRE(false, "rf_global_attn_fold_fwd(bf16): unsupported hidden size %d", D);
+    }
+#undef GP_
+    k_gfold_out<bf16><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const bf16*)wvg, bvg, gidx, ws,
                                                       (bf16*)out, ld_out);
   } else if (dtype == RF_F32) {
-    (void)hipFuncSetAttribute((const void*)k_gfold_partial<float>,
+    RF_REQUIRE(ldh % 4 == 0, "rf_global_attn_fold_fwd(f32): ldh must be a multiple of 4");
+    const size_t lds_p = (size_t)(H * (D + 4) + H * GF_CHF) * sizeof(float);
+    RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold_fwd: D too large for LDS");
+    (void)hipFuncSetAttribute((const void*)k_gfold_partial_f32,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);
-    k_gfold_u<float><<<dim3(H, R), 256, 0, s>>>(D, H, gmax, (const float*)qg, ld_qg, (const float*)wkg, bkg, gidx, ws);
-    k_gfold_partial<float><<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const float*)h, ldh, flags, gidx, ws);
-    k_gfold_out<float><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, H, gmax, nch, (const float*)wvg, bvg, gidx, ws,
+    k_gfold_u<float><<<dim3(H, (D + 63) / 64), 256, 0, s>>>(D, H, R, (const float*)qg, ld_qg,
+                                                               (const float*)wkg, gidx, ws, false);
+    k_gfold_partial_f32<<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const float*)h, ldh, flags, gidx, ws);
+    k_gfold_out<float><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const float*)wvg, bvg, gidx, ws,
                                                        (float*)out, ld_out);
   } else {
     RF_REQUIRE(false, "rf_global_attn_fold_fwd: bad dtype %d", dtype);

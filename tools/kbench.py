@@ -59,7 +59,12 @@ def attn_bench():
     ctx = torch.empty(B * L, D, device=dev, dtype=torch.bfloat16)
     qg = torch.randn(B, D, device=dev).bfloat16()
     t = timeit(lambda: ops.global_attention(qg, qkv[:, 3 * D:4 * D], qkv[:, 4 * D:], flags, gidx, B, L, H, ctx))
-    print(f"global_attn B={B} L={L}: {t*1e6:.1f} us", flush=True)
+    print(f"global_attn (reference structure, kg/vg precomputed) B={B} L={L}: {t*1e6:.1f} us", flush=True)
+    h = qkv[:, :D]
+    w = (torch.randn(2 * D, D, device=dev) * 0.05).bfloat16()
+    bb = torch.zeros(2 * D, device=dev)
+    t = timeit(lambda: ops.global_attention_fold(qg, h, w[:D], bb[:D], w[D:], bb[D:], flags, gidx, B, L, H, ctx))
+    print(f"global_attn_fold B={B} L={L}: {t*1e6:.1f} us (reads h once: {B*L*D*2/t/1e9:.0f} GB/s)", flush=True)
 
 
 if __name__ == "__main__":
