@@ -37,7 +37,8 @@ enum {
   RF_EPI_BIAS = 1,       /* C = A.W^T + b              (nn.Linear)      */
   RF_EPI_BIAS_GELU = 2,  /* C = gelu_erf(A.W^T + b)    (TF:1113-1116)   */
   RF_EPI_BIAS_RESID = 3, /* C = A.W^T + b + R          (TF:1068-1071 / 1127-1130, pre-LN) */
-  RF_EPI_COS = 4         /* C(f32) = A.W^T * ra[m] * rw[n] * scale (Similarity, models.py:358-369) */
+  RF_EPI_COS = 4,        /* C(f32) = A.W^T * ra[m] * rw[n] * scale (Similarity, models.py:358-369) */
+  RF_EPI_BIAS_RESID_LN = 5 /* C(f32) = A.W^T + b + LN(R): rf_gemm_resid_ln only */
 };
 
 const char* rf_last_error(void);
@@ -77,6 +78,15 @@ int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, const void* 
             const float* bias, const void* resid, int ldr, void* C, int ldc, int io_flags,
             int epilogue, int scale_cols, float col_scale, const float* ra, const float* rw,
             rf_stream_t stream);
+
+/* The residual-add linears (attention output TF:1068-1071, FFN output TF:1127-1130) with the
+ * residual given as the PREVIOUS LayerNorm's fp32 input rows R and its row statistics:
+ * C(f32) = A.W^T + b + ((R - mean) * rstd * gamma + beta) — the same expression the LayerNorm
+ * kernel evaluates, so the LN output never needs an fp32 copy in HBM. */
+int rf_gemm_resid_ln(int dtype, int M, int N, int K, const void* A, int lda, const void* W,
+                     int ldw, const float* bias, const float* resid_pre, int ldr,
+                     const float* r_mean, const float* r_rstd, const float* r_gamma,
+                     const float* r_beta, float* C, int ldc, rf_stream_t stream);
 
 /* LayerNorm over rows of D (TF:1071, 1130; nn.LayerNorm eps); x in x_dtype, y in y_dtype,
  * optional fp32 copy y32 (M x D, contiguous); mean/rstd (M) optional. */

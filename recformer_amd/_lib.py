@@ -27,7 +27,9 @@ SIGNATURES = {
                                 P, P, P]),
     "rf_gemm": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, P, c_int, P, c_int,
                         c_int, c_int, c_int, c_float, P, P, P]),
-    "rf_layernorm_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_float, P, c_int, P,
+    "rf_gemm_resid_ln": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, P, c_int, P, P,
+                                 P, P, P, c_int, P]),
+    "rf_layernorm_fwd":(c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_float, P, c_int, P,
                                  P, P, P]),
     "rf_band_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
                                  c_int, P, c_int, P]),

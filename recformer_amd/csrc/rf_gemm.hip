@@ -17,6 +17,8 @@
 // whole rows with 16-B vector stores (bias / q-scale / GELU / residual / cosine scale
 // applied in fp32 on the way).
 // fp32 path: exact-f32 v_mfma_f32_16x16x4_f32, 64x64x16 tiles, register staging.
+#include <stdlib.h>
+
 #include "rf_common.h"
 
 namespace rf {
@@ -32,6 +34,12 @@ struct EpiArgs {
   float col_scale;
   const float* ra;
   const float* rw;
+  // RF_EPI_BIAS_RESID_LN: residual = LayerNorm(R) recomputed from the fp32 pre-LN rows R and
+  // the row statistics the LayerNorm kernel stored (no fp32 copy of the LN output in HBM)
+  const float* lmean;
+  const float* lrstd;
+  const float* lgamma;
+  const float* lbeta;
 };
 
 // scalar epilogue (fp32 kernel and ragged tails)
@@ -51,6 +59,10 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, fl
     else
       v += to_f32(reinterpret_cast<const TIN*>(e.R)[(int64_t)row * e.ldr + col]);
   }
+  if (EPI == RF_EPI_BIAS_RESID_LN) {
+    const float x = reinterpret_cast<const float*>(e.R)[(int64_t)row * e.ldr + col];
+    v += (x - e.lmean[row]) * e.lrstd[row] * e.lgamma[col] + e.lbeta[col];
+  }
   if (CF32)
     reinterpret_cast<float*>(e.C)[(int64_t)row * e.ldc + col] = v;
   else
@@ -64,7 +76,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // ------------------------------------------------------------------------------------
 // bf16
-constexpr int GB_K = 64;
 constexpr int EPI_LD = 68;  // fp32 staging row stride (floats): conflict-free write + b128 read
 
 // 16 consecutive columns [c0, c0+16) of one output row: vector epilogue.
@@ -121,6 +132,21 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
       }
     }
   }
+  if (EPI == RF_EPI_BIAS_RESID_LN) {
+    // same expression as the LayerNorm kernel's output: (x - mean) * rstd * gamma + beta
+    const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)row * e.ldr + c0;
+    const float mu = e.lmean[row], rs = e.lrstd[row];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 x = *reinterpret_cast<const float4*>(r + 4 * q);
+      const float4 gm = *reinterpret_cast<const float4*>(e.lgamma + c0 + 4 * q);
+      const float4 bt = *reinterpret_cast<const float4*>(e.lbeta + c0 + 4 * q);
+      v[4 * q] += (x.x - mu) * rs * gm.x + bt.x;
+      v[4 * q + 1] += (x.y - mu) * rs * gm.y + bt.y;
+      v[4 * q + 2] += (x.z - mu) * rs * gm.z + bt.z;
+      v[4 * q + 3] += (x.w - mu) * rs * gm.w + bt.w;
+    }
+  }
   if (CF32) {
     float* out = reinterpret_cast<float*>(e.C) + (int64_t)row * e.ldc + c0;
 #pragma unroll
@@ -138,20 +164,55 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool CF32, bool RF32>
-__global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64)
+// Operand tile geometry for a BK-deep stage: rows of BK bf16 (BK*2 bytes), 16-B chunks.
+//  BK = 64: 128-B rows, chunk slot = c ^ (r & 7)            (guide §5.5 T2)
+//  BK = 32:  64-B rows, chunk slot = c ^ f(r), f = (-(r>>2)) & 3: makes every 16-lane group
+//            of the ds_read_b128 operand read (rows l&15, chunk l>>4) hit 16 distinct slots.
+template <int BK> struct TileGeo;
+template <> struct TileGeo<64> {
+  static constexpr int ROWB = 128, PIECE_ROWS = 8;
+  static __device__ __forceinline__ int slot(int r, int c) { return c ^ (r & 7); }
+};
+template <> struct TileGeo<32> {
+  static constexpr int ROWB = 64, PIECE_ROWS = 16;
+  static __device__ __forceinline__ int slot(int r, int c) { return c ^ ((-(r >> 2)) & 3); }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// NSTAGE-deep LDS ring, prefetch distance NSTAGE-1. Each wave waits only for ITS pieces of
+// the tile it is about to read (counted vmcnt, the younger tiles stay in flight across the
+// raw s_barrier — guide §5 'Pipelining across barriers'), then the barrier publishes every
+// wave's pieces. The slot refilled in iteration kt was last read in kt-1, which every wave
+// has finished before passing this iteration's barrier.
+constexpr int gemm_min_waves(int bm, int bn, int wm, int wn, int bk, int nstage) {
+  // waves per SIMD the LDS budget admits (1..8): lets the register allocator size for it
+  return (163840 / (nstage * (bm + bn) * bk * 2)) * ((bm / wm) * (bn / wn)) / 4 < 1
+             ? 1
+             : ((163840 / (nstage * (bm + bn) * bk * 2)) * ((bm / wm) * (bn / wn)) / 4 > 8
+                    ? 8
+                    : (163840 / (nstage * (bm + bn) * bk * 2)) * ((bm / wm) * (bn / wn)) / 4);
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
+__global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, gemm_min_waves(BM, BN, WM, WN, BK, NSTAGE))
     k_gemm_bf16(int K, const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw,
                 EpiArgs e, int nTn) {
+  using G = TileGeo<BK>;
   constexpr int NWN = BN / WN;
   constexpr int NWAVES = (BM / WM) * NWN;
   constexpr int FM = WM / 16, FN = WN / 16;          // 16x16 fragments per wave
-  constexpr int A_BYTES = BM * GB_K * 2, B_BYTES = BN * GB_K * 2;
+  constexpr int A_BYTES = BM * G::ROWB, B_BYTES = BN * G::ROWB;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int CHUNKS = (BM + BN) / 8;              // 1-KiB DMA pieces per stage
+  constexpr int CHUNKS = (BM + BN) / G::PIECE_ROWS;  // 1-KiB DMA pieces per stage
   constexpr int CPW = CHUNKS / NWAVES;               // per wave
-  constexpr int ACH = BM / 8;                        // A pieces come first
+  constexpr int ACH = BM / G::PIECE_ROWS;            // A pieces come first
+  constexpr int LPR = G::ROWB / 16;                  // lanes per row in a piece
   static_assert(CHUNKS % NWAVES == 0, "staging split");
-  static_assert(NWAVES * 16 * EPI_LD * 4 <= 2 * STAGE, "epilogue scratch");
+  static_assert(NWAVES * 16 * EPI_LD * 4 <= NSTAGE * STAGE, "epilogue scratch");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -160,15 +221,14 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / NWN, wn = wave % NWN;
 
-  // per-lane DMA sources: wave stages pieces c = wave*CPW + i (8 rows of 128 B each)
   const bf16* src[CPW];
   int dst[CPW];
 #pragma unroll
   for (int i = 0; i < CPW; ++i) {
     const int c = wave * CPW + i;
     const bool isA = c < ACH;
-    const int row = (isA ? c : c - ACH) * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ (row & 7);
+    const int row = (isA ? c : c - ACH) * G::PIECE_ROWS + lane / LPR;
+    const int ch = G::slot(row, lane % LPR);  // slot is an involution on the chunk index
     if (isA)
       src[i] = A + (int64_t)min(m0 + row, e.M - 1) * lda + ch * 8;
     else
@@ -177,7 +237,7 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64)
   }
   auto stage = [&](int kt, int buf) {
     char* base = smem + buf * STAGE;
-    const int koff = kt * GB_K;
+    const int koff = kt * BK;
 #pragma unroll
     for (int i = 0; i < CPW; ++i) glds16(src[i] + koff, base + dst[i]);
   };
@@ -188,34 +248,108 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / GB_K;
-  stage(0, 0);
-  wait_vmcnt0();
-  __syncthreads();
+  const int nk = K / BK;
+  if constexpr (BK == 32 && NSTAGE == 4) {
+    // Register-pipelined ring: iteration kt computes tile kt from fragment set X while the
+    // ds_reads of tile kt+1 fill set Y and the DMA of tile kt+3 is in flight, so neither the
+    // LDS latency nor the HBM/L2 latency sits on the MFMA stream (guide T14 idea applied to
+    // the LDS->register stage). Slot (kt+3)%4 = (kt-1)%4 was last read (frag prefetch of tile
+    // kt-1) in iteration kt-2 and drained by that wave's lgkmcnt(0) before iteration kt-1's
+    // barrier.
+    auto read_frags = [&](int kt, bf16x8 (&a)[FM], bf16x8 (&b)[FN]) {
+      const char* as = smem + (kt & 3) * STAGE;
+      const char* ws = as + A_BYTES;
+      const int ch = lane >> 4;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * WM + i * 16 + (lane & 15);
+        a[i] = *reinterpret_cast<const bf16x8*>(as + r * G::ROWB + (G::slot(r, ch) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * WN + j * 16 + (lane & 15);
+        b[j] = *reinterpret_cast<const bf16x8*>(ws + r * G::ROWB + (G::slot(r, ch) << 4));
+      }
+    };
+    auto mma = [&](const bf16x8 (&a)[FM], const bf16x8 (&b)[FN]) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    };
+    auto sync_tile = [&](int kt) {  // tile kt landed in every wave's pieces
+      const int ahead = nk - 1 - kt;  // tiles kt+1.. that may still be in flight (at most 1)
+      if (ahead >= 1) wait_vmcnt<CPW>();
+      else wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (i < nk) stage(i, i);
+    // tile 0 landed (tiles 1, 2 may be in flight)
+    if (nk >= 3) wait_vmcnt<2 * CPW>();
+    else if (nk == 2) wait_vmcnt<CPW>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_frags(0, a0, b0);
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      sync_tile(kt + 1);
+      if (kt + 3 < nk) stage(kt + 3, (kt + 3) & 3);
+      read_frags(kt + 1, a1, b1);
+      mma(a0, b0);
+      if (kt + 2 < nk) {
+        sync_tile(kt + 2);
+        if (kt + 4 < nk) stage(kt + 4, (kt + 4) & 3);
+        read_frags(kt + 2, a0, b0);
+      }
+      mma(a1, b1);
+    }
+    if (kt < nk) mma(a0, b0);
+  } else {
+#pragma unroll
+  for (int i = 0; i < NSTAGE - 1; ++i)
+    if (i < nk) stage(i, i);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    const char* as = smem + cur * STAGE;
+    // tiles kt+1 .. min(kt+NSTAGE-2, nk-1) may stay in flight
+    const int ahead = min(NSTAGE - 2, nk - 1 - kt);
+    if (NSTAGE >= 4 && ahead >= 2) wait_vmcnt<2 * CPW>();
+    else if (NSTAGE >= 3 && ahead >= 1) wait_vmcnt<CPW>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    const char* as = smem + (kt % NSTAGE) * STAGE;
     const char* ws = as + A_BYTES;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BK / 32; ++s) {
       const int ch = 4 * s + (lane >> 4);
       bf16x8 a[FM], b[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(as + swz128(wm * WM + i * 16 + (lane & 15), ch));
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * WM + i * 16 + (lane & 15);
+        a[i] = *reinterpret_cast<const bf16x8*>(as + r * G::ROWB + (G::slot(r, ch) << 4));
+      }
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(ws + swz128(wn * WN + j * 16 + (lane & 15), ch));
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * WN + j * 16 + (lane & 15);
+        b[j] = *reinterpret_cast<const bf16x8*>(ws + r * G::ROWB + (G::slot(r, ch) << 4));
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    wait_vmcnt0();
-    __syncthreads();
   }
+  }
+  __syncthreads();  // every wave is done with the ring before it becomes epilogue scratch
 
   // ---- epilogue: per wave, 16-row slabs through LDS, then row-major vector stores ----
   float* scr = reinterpret_cast<float*>(smem) + wave * 16 * EPI_LD;
@@ -310,31 +444,50 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int K, const float* __restrict
                                             n0 + wn * 32 + j * 16 + (lane & 15), acc[i][j][r]);
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool CF32, bool RF32>
+template <int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
 static void launch_bf16(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                         const EpiArgs& e, hipStream_t s) {
   constexpr int threads = (BM / WM) * (BN / WN) * 64;
-  constexpr size_t lds = 2 * (size_t)(BM + BN) * GB_K * 2;
+  constexpr size_t lds = (size_t)NSTAGE * (BM + BN) * BK * 2;
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_bf16<BM, BN, WM, WN, EPI, CF32, RF32>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_gemm_bf16<BM, BN, WM, WN, BK, NSTAGE, EPI, CF32, RF32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   const int nTm = (M + BM - 1) / BM, nTn = (N + BN - 1) / BN;
-  k_gemm_bf16<BM, BN, WM, WN, EPI, CF32, RF32><<<nTm * nTn, threads, lds, s>>>(
+  k_gemm_bf16<BM, BN, WM, WN, BK, NSTAGE, EPI, CF32, RF32><<<nTm * nTn, threads, lds, s>>>(
       K, (const bf16*)A, lda, (const bf16*)W, ldw, e, nTn);
 }
+
+// Variant selector for A/B timing (RF_GEMM_VARIANT): 1 -> 256^2 BK64 x2 (default, fastest
+// measured), 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 -> 256x128 / 128^2 tiles.
+static int gemm_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("RF_GEMM_VARIANT");
+    v = s ? atoi(s) : 1;
+  }
+  return v;
+}
+
 
 template <int EPI, bool CF32, bool RF32>
 static void dispatch_tile(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                           const EpiArgs& e, hipStream_t s) {
   // 256x256 when the grid still covers the chip; 128x128 for skinny problems
   const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-  if (tiles256 >= 128)
-    launch_bf16<256, 256, 128, 64, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
-  else
-    launch_bf16<128, 128, 64, 64, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+  if (tiles256 >= 128) {
+    switch (gemm_variant()) {
+      case 1: launch_bf16<256, 256, 128, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 2: launch_bf16<256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 3: launch_bf16<128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 4: launch_bf16<256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      default: launch_bf16<256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+    }
+  } else {
+    launch_bf16<128, 128, 64, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+  }
 }
 
 }  // namespace rf
@@ -352,10 +505,11 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
   RF_REQUIRE(epilogue != RF_EPI_BIAS_RESID || (resid && ldr >= N), "rf_gemm: residual required");
   RF_REQUIRE(epilogue != RF_EPI_COS || (ra && rw), "rf_gemm: norms required for EPI_COS");
   if (M == 0) return RF_OK;
-  EpiArgs e{M, N, bias, resid, ldr, C, ldc, scale_cols, col_scale, ra, rw};
+  EpiArgs e{M, N, bias, resid, ldr, C, ldc, scale_cols, col_scale, ra, rw,
+            nullptr, nullptr, nullptr, nullptr};
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16) {
-    RF_REQUIRE(K % GB_K == 0, "rf_gemm(bf16): K=%d must be a multiple of %d", K, GB_K);
+    RF_REQUIRE(K % 64 == 0, "rf_gemm(bf16): K=%d must be a multiple of 64", K);
     RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0, "rf_gemm(bf16): lda/ldw must be multiples of 8");
     RF_REQUIRE(ldc % 8 == 0 && (resid == nullptr || ldr % 8 == 0),
                "rf_gemm(bf16): ldc/ldr must be multiples of 8 (16-B vector epilogue)");
@@ -396,4 +550,33 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
     RF_REQUIRE(false, "rf_gemm: bad dtype %d", dtype);
   }
   RF_LAUNCH_CHECK("rf_gemm");
+}
+
+extern "C" int rf_gemm_resid_ln(int dtype, int M, int N, int K, const void* A, int lda,
+                                const void* W, int ldw, const float* bias, const float* resid_pre,
+                                int ldr, const float* r_mean, const float* r_rstd,
+                                const float* r_gamma, const float* r_beta, float* C, int ldc,
+                                rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && N > 0 && K > 0, "rf_gemm_resid_ln: bad shape M=%d N=%d K=%d", M, N, K);
+  RF_REQUIRE(lda >= K && ldw >= K && ldc >= N && ldr >= N, "rf_gemm_resid_ln: bad leading dims");
+  RF_REQUIRE(bias && resid_pre && r_mean && r_rstd && r_gamma && r_beta && C,
+             "rf_gemm_resid_ln: null pointer");
+  if (M == 0) return RF_OK;
+  EpiArgs e{M, N, bias, resid_pre, ldr, C, ldc, 0, 1.0f, nullptr, nullptr,
+            r_mean, r_rstd, r_gamma, r_beta};
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16) {
+    RF_REQUIRE(K % 64 == 0, "rf_gemm_resid_ln(bf16): K=%d must be a multiple of 64", K);
+    RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0 && ldr % 8 == 0,
+               "rf_gemm_resid_ln(bf16): leading dims must be multiples of 8");
+    dispatch_tile<RF_EPI_BIAS_RESID_LN, true, true>(M, N, K, A, lda, W, ldw, e, s);
+  } else if (dtype == RF_F32) {
+    RF_REQUIRE(K % GF_K == 0 && lda % 4 == 0 && ldw % 4 == 0, "rf_gemm_resid_ln(f32): alignment");
+    const int nTm = (M + GF_M - 1) / GF_M, nTn = (N + GF_N - 1) / GF_N;
+    k_gemm_f32<RF_EPI_BIAS_RESID_LN><<<nTm * nTn, 256, 0, s>>>(K, (const float*)A, lda, (const float*)W,
+                                                              ldw, e, nTn);
+  } else {
+    RF_REQUIRE(false, "rf_gemm_resid_ln: bad dtype %d", dtype);
+  }
+  RF_LAUNCH_CHECK("rf_gemm_resid_ln");
 }

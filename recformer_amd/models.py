@@ -341,13 +341,6 @@ class RecformerModel(nn.Module):
             return out
         return RecformerModelOutput(last_hidden_state=last, pooler_output=pooled, hidden_states=hidden_all)
 
-    def _ln(self, t, w, b, dt, mixed):
-        if mixed:
-            return ops.layernorm(t, w, b, self.config.layer_norm_eps, out_dtype=dt, want_f32=True,
-                                 tag="layernorm")
-        y = ops.layernorm(t, w, b, self.config.layer_norm_eps, out=t, tag="layernorm")
-        return y, y
-
     @torch.no_grad()
     def _encode(self, input_ids, attention_mask, global_attention_mask, token_type_ids,
                 position_ids, item_position_ids, output_hidden_states):
@@ -384,6 +377,9 @@ class RecformerModel(nn.Module):
         # global rows: the key/value-projection fold by default; `config.global_attention_fold
         # = False` keeps the reference's structure (k_g/v_g projected over all tokens).
         fold = getattr(cfg, "global_attention_fold", True)
+        eps = cfg.layer_norm_eps
+        nl = len(pk["layers"])
+        res = None  # (pre-LN rows, mean, rstd, gamma, beta) of the residual, bf16 path
         for li, lw in enumerate(pk["layers"]):
             half_w = windows[li] // 2
             nq = 5 * D if (gmax > 0 and not fold) else 3 * D
@@ -401,15 +397,35 @@ class RecformerModel(nn.Module):
                 else:
                     ops.global_attention(qg, qkv[:, 3 * D:4 * D], qkv[:, 4 * D:5 * D], flags, gidx,
                                          B, Lp, H, ctx, tag="global_attn")
-            # pre-LN residual sums are kept in fp32 (the reference's autocast residual stream is
-            # fp32); LayerNorm re-emits the compute dtype for the next GEMM.
-            t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h32, out_f32=True,
-                         tag="gemm_out")
-            a, a32 = self._ln(t, lw["ln1_w"], lw["ln1_b"], dt, mixed)
-            f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
-            t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a32, out_f32=True,
-                          tag="gemm_ffn2")
-            h, h32 = self._ln(t2, lw["ln2_w"], lw["ln2_b"], dt, mixed)
+            if not mixed:
+                t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h32,
+                             tag="gemm_out")
+                a = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], eps, out=t, tag="layernorm")
+                f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
+                t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a, tag="gemm_ffn2")
+                h = h32 = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out=t2, tag="layernorm")
+            else:
+                # bf16 path: the residual stream stays fp32 (the reference's autocast LayerNorm
+                # outputs fp32). It is never materialised: the residual-add GEMMs recompute
+                # LN(x) = (x - mean) * rstd * gamma + beta from the fp32 pre-LN rows x and the
+                # row stats the LayerNorm kernel wrote; LayerNorm itself only emits bf16.
+                if res is None:
+                    t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h32,
+                                 out_f32=True, tag="gemm_out")
+                else:
+                    t = ops.gemm_resid_ln(ctx, lw["w_o"], lw["b_o"], *res, tag="gemm_out")
+                a, m1, r1 = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], eps, out_dtype=dt, stats=True,
+                                          tag="layernorm")
+                f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
+                t2 = ops.gemm_resid_ln(f, lw["w_2"], lw["b_2"], t, m1, r1, lw["ln1_w"], lw["ln1_b"],
+                                       tag="gemm_ffn2")
+                if li == nl - 1 or output_hidden_states:
+                    h, h32, m2, r2 = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out_dtype=dt,
+                                                   stats=True, want_f32=True, tag="layernorm")
+                else:
+                    h, m2, r2 = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out_dtype=dt,
+                                              stats=True, tag="layernorm")
+                res = (t2, m2, r2, lw["ln2_w"], lw["ln2_b"])
             if output_hidden_states:
                 hidden_all.append(h32)
         last = h32.view(B, Lp, D)[:, :L]

@@ -178,6 +178,26 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
     return out
 
 
+def gemm_resid_ln(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, resid_pre: torch.Tensor,
+                  mean: torch.Tensor, rstd: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
+                  tag: Optional[str] = None) -> torch.Tensor:
+    """fp32 C = a . w^T + bias + LayerNorm(resid_pre) with the stored row stats (mean, rstd)."""
+    lib = _lib.load()
+    _dev(a, w, bias, resid_pre, mean, rstd)
+    M, K = a.shape
+    N = w.shape[0]
+    if resid_pre.dtype != torch.float32 or resid_pre.shape != (M, N):
+        raise ValueError("gemm_resid_ln: resid_pre must be the fp32 (M, N) pre-LayerNorm rows")
+    out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    with _region(tag):
+        rc = lib.rf_gemm_resid_ln(dtype_code(a.dtype), M, N, K, _p(a), _rowmajor(a, "a"), _p(w),
+                                  _rowmajor(w, "w"), _p(bias), _p(resid_pre),
+                                  _rowmajor(resid_pre, "resid_pre"), _p(mean), _p(rstd), _p(gamma),
+                                  _p(beta), _p(out), N, _stream(out))
+    check(rc, "rf_gemm_resid_ln")
+    return out
+
+
 def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
               out: Optional[torch.Tensor] = None, stats: bool = False, tag: Optional[str] = None,
               out_dtype: Optional[torch.dtype] = None, want_f32: bool = False):
@@ -199,6 +219,8 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
                                   _p(w), _p(b), float(eps), _p(out), _rowmajor(out, "out"), _p(y32),
                                   _p(mean), _p(rstd), _stream(x))
     check(rc, "rf_layernorm_fwd")
+    if stats and want_f32:
+        return out, y32, mean, rstd
     if stats:
         return out, mean, rstd
     if want_f32:

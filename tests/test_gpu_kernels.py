@@ -70,6 +70,23 @@ def test_gemm_bf16_fp32_output_and_mixed_layernorm(dev):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_resid_ln(dev, dt):
+    """Residual = LayerNorm(previous pre-LN rows) recomputed in the GEMM epilogue."""
+    M, N, K = 300, 768, 768
+    a = _rand((M, K), dev, dt, seed=21)
+    w = _rand((N, K), dev, dt, 0.05, seed=22)
+    b = _rand((N,), dev, torch.float32, seed=23)
+    x = _rand((M, N), dev, torch.float32, 2.0, seed=24) + 0.5
+    g = _rand((N,), dev, torch.float32, seed=25)
+    be = _rand((N,), dev, torch.float32, seed=26)
+    y, mean, rstd = ops.layernorm(x, g, be, 1e-5, out_dtype=dt, stats=True)
+    out = ops.gemm_resid_ln(a, w, b, x, mean, rstd, g, be)
+    ref = a.float() @ w.float().t() + b + F.layer_norm(x, (N,), g, be, 1e-5)
+    assert out.dtype == torch.float32
+    assert (out - ref).abs().max().item() <= (1e-4 if dt == torch.float32 else 1e-3) * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gemm_strided_views(dev, dt):
     """Column slices of a fused buffer as A (the q/k/v views) and as W (packed weights)."""
     big = _rand((256, 5 * 128), dev, dt, seed=5)
