@@ -52,11 +52,28 @@ def parse():
     return ap.parse_args()
 
 
-def gemm_flops_per_seq(L, d, ffn, layers, gmax=1):
-    # per layer: fused q,k,v,k_g,v_g (5 d x d over all L tokens) + q_g (d x d on G rows)
-    # + out-proj (d x d) + FFN (2 d x ffn); 2 flops per MAC
-    per_layer = 2 * L * d * (5 * d) + 2 * gmax * d * d + 2 * L * d * d + 2 * 2 * L * d * ffn
+def gemm_flops_per_seq(L, d, ffn, layers, gmax=1, fold=True):
+    # per layer: fused q,k,v (3 d x d over all L tokens; + k_g, v_g when the global
+    # projections are not folded) + q_g (d x d on G rows) + out-proj (d x d) + FFN (2 d x ffn);
+    # 2 flops per MAC. The global fold's own work (u = Wkg^T qg, P.H, Wvg GEMV) is excluded.
+    per_layer = 2 * L * d * ((3 if fold else 5) * d) + 2 * gmax * d * d + 2 * L * d * d + 2 * 2 * L * d * ffn
     return per_layer * layers
+
+
+def pmc_traffic(B, L, layers):
+    """Per-launch HBM bytes per kernel tag from the newest committed PMC profile of this exact
+    workload (profiles/r*/bench_pmc_summary.json, tools/profile_bench.sh), or {}."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bench_pmc_summary.json")),
+                       reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if doc.get("config") == {"batch": B, "seq_len": L, "layers": layers}:
+            return {k: v.get("hbm_bytes") for k, v in doc["tags"].items()}, os.path.relpath(path, ROOT)
+    return {}, None
 
 
 def cpu_baseline(sd_cpu, cfg, items_cpu, L, target_s, threads):
@@ -103,7 +120,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from recformer_amd import RecformerConfig, RecformerForSeqRec, ops
+    from recformer_amd import RecformerConfig, RecformerForSeqRec, dp, ops
     from recformer_amd.synth import BASE, synth_batch
 
     L, B = args.seq_len, args.batch
@@ -145,10 +162,7 @@ def main():
         ops.enable_timing(False)
     assert scores.shape == (B, args.catalog)
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tmax = float(t.item())
+    tmax = dp.max_over_ranks(elapsed, device=dev)
     total_seqs = B * world * args.steps
     value = total_seqs / tmax
 
@@ -158,6 +172,7 @@ def main():
         roofline = None
         attn_roof = None
         kernels = {}
+        traffic, traffic_src = pmc_traffic(B, L, args.layers)
         if kt:
             for k, v in kt.items():
                 kernels[k] = {"launches": len(v), "avg_us": 1e3 * sum(v) / len(v),
@@ -166,13 +181,15 @@ def main():
             dom = max(gemms, key=lambda k: sum(gemms[k])) if gemms else None
             if dom:
                 Mrows = B * L
-                nflops = {"gemm_qkv": 2 * Mrows * d * 5 * d, "gemm_out": 2 * Mrows * d * d,
+                nqkv = 3 if getattr(cfg, "global_attention_fold", True) else 5
+                nflops = {"gemm_qkv": 2 * Mrows * d * nqkv * d, "gemm_out": 2 * Mrows * d * d,
                           "gemm_ffn1": 2 * Mrows * d * ffn, "gemm_ffn2": 2 * Mrows * ffn * d}[dom]
                 avg_s = sum(gemms[dom]) / len(gemms[dom]) / 1e3
                 ach = nflops / avg_s / 1e12
                 roofline = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1),
                             "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                            "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                            "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": traffic.get(dom),
+                            "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                             "algorithmic_per_launch": f"{nflops / 1e9:.2f} GFLOP (2*M*N*K, M=B*L={Mrows})"}
             if "band_attn" in kt:
                 v = kt["band_attn"]
@@ -181,9 +198,10 @@ def main():
                 gbs = nbytes / avg_s / 1e9
                 attn_roof = {"kernel": "band_attn", "bound": "hbm", "achieved": round(gbs, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                             "traffic": None,
+                             "traffic": traffic.get("band_attn"),
+                             "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                              "algorithmic_per_launch": f"{nbytes / 1e6:.1f} MB (8*B*L*d bytes)"}
-        flops_seq = gemm_flops_per_seq(L, d, ffn, args.layers)
+        flops_seq = gemm_flops_per_seq(L, d, ffn, args.layers, fold=getattr(cfg, "global_attention_fold", True))
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "user-seq/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / args.steps, 3),

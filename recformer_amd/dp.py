@@ -1,0 +1,76 @@
+"""Data-parallel plumbing for the encode+score path.
+
+User sequences are independent, so inference shards a batch of sequences across ranks with
+no data-path collective; the item catalog is replicated. The only collectives are host-side
+bookkeeping: the max-over-ranks step time (bench) and, for evaluation drivers that want the
+whole batch's scores on every rank, an all-gather of per-rank score rows in batch order
+(the reference evaluates on one device, finetune.py:66-96, so the gathered result must equal
+the single-device one row for row).
+
+Works with any torch.distributed backend: `nccl` (RCCL over xGMI) on MI355X, `gloo` on CPU
+(tests/test_dp.py).
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> Tuple[int, int]:
+    """(rank, world_size); (0, 1) when torch.distributed is not initialised."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_range(n: int, rank: int, world_size: int) -> Tuple[int, int]:
+    """Contiguous, balanced [start, stop) of n items for `rank` (sizes differ by at most 1,
+    lower ranks take the remainder)."""
+    if world_size < 1 or not 0 <= rank < world_size:
+        raise ValueError(f"bad rank {rank} / world {world_size}")
+    q, r = divmod(n, world_size)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def shard_batch(batch: Dict[str, torch.Tensor], rank: int, world_size: int) -> Dict[str, torch.Tensor]:
+    """This rank's rows of every (B, ...) tensor in a collator batch dict (views, no copy)."""
+    sizes = {v.shape[0] for v in batch.values() if torch.is_tensor(v) and v.dim() > 0}
+    if len(sizes) != 1:
+        raise ValueError(f"batch tensors disagree on the batch dimension: {sizes}")
+    a, b = shard_range(sizes.pop(), rank, world_size)
+    return {k: (v[a:b] if torch.is_tensor(v) and v.dim() > 0 else v) for k, v in batch.items()}
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    """Max of a host scalar over all ranks (the bench's step time)."""
+    rank, ws = world()
+    if ws == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_rows(local: torch.Tensor, total: int) -> torch.Tensor:
+    """All-gather per-rank row blocks (from shard_batch's split of `total` rows) into the full
+    (total, ...) tensor in the original row order, on every rank. Ragged shards are padded to
+    the largest shard for the collective and trimmed after."""
+    rank, ws = world()
+    if ws == 1:
+        return local
+    q = -(-total // ws)
+    a, b = shard_range(total, rank, ws)
+    if local.shape[0] != b - a:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, its shard is {b - a}")
+    pad = local.new_zeros((q,) + tuple(local.shape[1:]))
+    pad[: b - a] = local
+    parts = [torch.empty_like(pad) for _ in range(ws)]
+    dist.all_gather(parts, pad.contiguous())
+    out = []
+    for r in range(ws):
+        ra, rb = shard_range(total, r, ws)
+        out.append(parts[r][: rb - ra])
+    return torch.cat(out, 0)
