@@ -13,9 +13,9 @@
 //     so the L2->LDS stream needs ~20 TB/s at MFMA peak (a 128^2 tile would need ~39 TB/s,
 //     above what the XCD L2s deliver);
 //   * 128x128 tile, 4 waves of 64x64 — for small M or N (global rows, scoring).
-// Epilogue: each wave stages 16-row slabs of fp32 accumulators through LDS and writes
-// whole rows with 16-B vector stores (bias / q-scale / GELU / residual / cosine scale
-// applied in fp32 on the way).
+// Epilogue: whole rows of 16 columns per lane with 16-B vector stores (bias / q-scale /
+// GELU / residual / LayerNorm-recompute / cosine scale applied in fp32 on the way) — straight
+// from the accumulators in the ping-pong kernel, through LDS slabs in k_gemm_bf16.
 // fp32 path: exact-f32 v_mfma_f32_16x16x4_f32, 64x64x16 tiles, register staging.
 #include <stdlib.h>
 
@@ -52,7 +52,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, fl
   }
   if (EPI != RF_EPI_NONE) v += e.bias[col];
   if (col < e.scale_cols) v *= e.col_scale;
-  if (EPI == RF_EPI_BIAS_GELU) v = gelu_erf(v);
+  if (EPI == RF_EPI_BIAS_GELU) v = (CF32 || sizeof(TIN) == 4) ? gelu_erf(v) : gelu_bf16out(v);
   if (EPI == RF_EPI_BIAS_RESID) {
     if (RF32)
       v += reinterpret_cast<const float*>(e.R)[(int64_t)row * e.ldr + col];
@@ -78,9 +78,25 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // bf16
 constexpr int EPI_LD = 68;  // fp32 staging row stride (floats): conflict-free write + b128 read
 
-// 16 consecutive columns [c0, c0+16) of one output row: vector epilogue.
+// bias[c0, c0+16) as 4 float4 loads (zeros for EPI_NONE / EPI_COS or a ragged right edge)
+template <int EPI>
+__device__ __forceinline__ void load_bias16(const EpiArgs& e, int c0, float* b) {
+  if (EPI == RF_EPI_NONE || EPI == RF_EPI_COS || c0 + 16 > e.N) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b[k] = 0.f;
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 x = *reinterpret_cast<const float4*>(e.bias + c0 + 4 * q);
+    b[4 * q] = x.x; b[4 * q + 1] = x.y; b[4 * q + 2] = x.z; b[4 * q + 3] = x.w;
+  }
+}
+
+// 16 consecutive columns [c0, c0+16) of one output row: vector epilogue. `bv` is the bias
+// slice from load_bias16 (hoisted by the caller).
 template <int EPI, bool CF32, bool RF32>
-__device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, float* v) {
+__device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, float* v, const float* bv) {
   if (row >= e.M) return;
   if (c0 + 16 > e.N) {  // ragged right edge: scalar path
 #pragma unroll
@@ -100,10 +116,7 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
   }
   if (EPI != RF_EPI_NONE) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 b = *reinterpret_cast<const float4*>(e.bias + c0 + 4 * q);
-      v[4 * q] += b.x; v[4 * q + 1] += b.y; v[4 * q + 2] += b.z; v[4 * q + 3] += b.w;
-    }
+    for (int k = 0; k < 16; ++k) v[k] += bv[k];
   }
   if (c0 < e.scale_cols) {
     // scale_cols is a multiple of 16 on every call site (head-aligned q columns)
@@ -112,7 +125,7 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
   }
   if (EPI == RF_EPI_BIAS_GELU) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = gelu_erf(v[k]);
+    for (int k = 0; k < 16; ++k) v[k] = CF32 ? gelu_erf(v[k]) : gelu_bf16out(v[k]);
   }
   if (EPI == RF_EPI_BIAS_RESID) {
     if (RF32) {
@@ -151,7 +164,7 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
     float* out = reinterpret_cast<float*>(e.C) + (int64_t)row * e.ldc + c0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<float4*>(out + 4 * q) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      *reinterpret_cast<f32x4*>(out + 4 * q) = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
   } else {
     bf16* out = reinterpret_cast<bf16*>(e.C) + (int64_t)row * e.ldc + c0;
 #pragma unroll
@@ -373,7 +386,9 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, gemm_min_waves(BM,
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_wave_barrier();
-      epi_row16<EPI, CF32, RF32>(e, m0 + wm * WM + i * 16 + rr, n0 + wn * WN + j0 * 16 + cc, v);
+      float bv[16];
+      load_bias16<EPI>(e, n0 + wn * WN + j0 * 16 + cc, bv);
+      epi_row16<EPI, CF32, RF32>(e, m0 + wm * WM + i * 16 + rr, n0 + wn * WN + j0 * 16 + cc, v, bv);
     }
   }
 }
@@ -444,6 +459,254 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int K, const float* __restrict
                                             n0 + wn * 32 + j * 16 + (lane & 15), acc[i][j][r]);
 }
 
+// ------------------------------------------------------------------------------------
+// bf16 256x256 ping-pong kernel (guide §5 "256² 8-phase template", rebuilt here).
+//
+// 8 waves = two groups of four (wr = wave>>2 owns output rows wr*128.., wc = wave&3 owns
+// columns wc*64..), one wave of each group per SIMD. Group 1 runs one barrier behind group 0,
+// so on every SIMD one wave issues its LDS reads and DMA while the other runs its MFMAs.
+// Each K-tile (BK = 64) is 4 phases; a phase = [ds_read the register sub-tile it needs,
+// DMA one 16-KiB half-tile, (counted vmcnt)] barrier [16 MFMAs on one 64x32 C-quadrant]
+// barrier. LDS: 2 buffers (even / odd K-tile) x 4 halves {A rows 0-127, A rows 128-255,
+// W rows 0-127, W rows 128-255} x 16 KiB = 128 KiB; each half is 128 rows x 128 B with the
+// chunk swizzle c ^ (r & 7) applied on the DMA source address.
+// Reads per K-tile:  P1 a0 + a1 (16) + b0 (4) -> (a0,b0);  P2 b1 (4) -> (a0,b1);
+//                    P3 -> (a1,b1);  P4 -> (a1,b0)   (every read of a buffer happens in P1-P2).
+// DMA per iteration (K-tiles t = 2i in buffer 0, t+1 in buffer 1):  P1 W1-half of t+1;
+// P2..P5 A0, A1, W0, W1 of t+2;  P6..P8 A0, A1, W0 of t+3. Restaging a half waits >= 1 phase
+// after its last read when only the leading group reads it (A0), >= 2 phases otherwise (the
+// lgkmcnt(0) before each MFMA block retires a wave's reads; the stagger adds one phase).
+// vmcnt(6) in P4 and P8 (3 half-tiles = 6 DMAs stay in flight) retires the buffer that is
+// read from the next phase on.
+constexpr int PP_HALF = 128 * 128;  // bytes per half-tile
+
+// W-row order in LDS: within each 64-row band, LDS row 16f + i (N-fragment f, MFMA row i)
+// holds W row 16(i>>2) + 4f + (i&3), so that MFMA output row i = 4g + r of fragment f is
+// output column 16g + 4f + r: lane group g ends up owning 16 consecutive columns.
+__device__ __forceinline__ int wperm(int rho) {
+  const int f = (rho >> 4) & 3, i = rho & 15;
+  return (rho & ~63) + 16 * (i >> 2) + 4 * f + (i & 3);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n from the small set the ping-pong kernel uses
+template <int S>
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  if (n == 0) wait_vmcnt<0>();
+  else if (n == 6) wait_vmcnt<6>();
+  else if (n == 8) wait_vmcnt<8>();
+  else if (n == S) wait_vmcnt<S>();
+  else if (n == 6 + S) wait_vmcnt<6 + S>();
+  else if (n == 8 + S) wait_vmcnt<8 + S>();
+  else wait_vmcnt<0>();
+}
+
+// Persistent: one workgroup per CU walks tiles v = blockIdx.x, +gridDim.x, ... (the same
+// XCD-aware tile order as one-tile-per-block). The next tile's prologue DMAs are issued
+// BEFORE the current tile's epilogue, so (vmcnt retiring in issue order) the next tile can
+// start while the epilogue's S stores are still draining: the prologue wait and the first
+// P4 wait count them as allowed-outstanding (interior tiles only, where S is exact).
+template <int EPI, bool CF32, bool RF32>
+__global__ void __launch_bounds__(512, 1)
+    k_gemm_pp(int K, const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw, EpiArgs e,
+              int nTm, int nTn) {
+  constexpr int S = (CF32 || EPI == RF_EPI_COS) ? 32 : 16;  // epilogue stores per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles = nTm * nTn;
+  int v = blockIdx.x;
+  if (v >= tiles) return;
+  int m0 = 0, n0 = 0;
+  auto set_tile = [&](int vv) {
+    const int wg = xcd_remap(vv, tiles);
+    const int tm = wg / nTn;
+    m0 = tm * 256;
+    n0 = (wg - tm * nTn) * 256;
+  };
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // DMA sources: this thread's two 8-row pieces of each half (rows 16*wave + 8p + lane/8),
+  // chunk (lane&7) ^ (row&7) = (lane&7) ^ (lane>>3); rows clamped into the matrix. Offsets
+  // are recomputed per DMA (a few VALU ops in the load phase) to keep VGPRs for the MMA.
+  // The per-lane row terms are laundered through an empty asm at every K-step so the compiler
+  // recomputes the few address ops per DMA instead of hoisting 8+ live offsets out of the
+  // tile loop (VGPRs belong to the MMA operands and accumulators).
+  int xa = 16 * wave + (lane >> 3);               // A piece row (p = 0; p = 1 is +8)
+  int xw0 = wperm(xa), xw1 = wperm(xa + 8);        // permuted W piece rows
+  int pch = ((lane & 7) ^ (lane >> 3)) * 8;
+  const int nk = K >> 6;
+  auto launder = [&]() { asm volatile("" : "+v"(xa), "+v"(xw0), "+v"(xw1), "+v"(pch)); };
+  // half index: 0 = A rows 0-127, 1 = A rows 128-255, 2 = W rows 0-127, 3 = W rows 128-255
+  auto dma = [&](int t, int half) {
+    if (t >= nk) return;  // wave-uniform
+    char* dst = smem + ((t & 1) * 4 + half) * PP_HALF + wave * 2048;
+    const bool isA = half < 2;
+    const bf16* base = isA ? A : W;
+    const int ld = isA ? lda : ldw;
+    const int lim = (isA ? e.M : e.N) - 1;
+    const int r0 = (isA ? m0 : n0) + (half & 1) * 128;
+    const int ra = r0 + (isA ? xa : xw0), rb = r0 + (isA ? xa + 8 : xw1);
+    glds16(base + (min(ra, lim) * ld + t * 64 + pch), dst);
+    glds16(base + (min(rb, lim) * ld + t * 64 + pch), dst + 1024);
+  };
+  auto prologue_dma = [&]() {  // K-tiles 0 and 1 complete
+    dma(0, 0); dma(0, 1); dma(0, 2); dma(0, 3);
+    dma(1, 0); dma(1, 1); dma(1, 2); dma(1, 3);
+  };
+
+  // fragment read offsets: row l&15 of a 16-row block, chunk ks*4 + (l>>4), swizzled
+  const int lr = lane & 15;
+  const int off0 = lr * 128 + (((lane >> 4) ^ (lane & 7)) << 4);
+  const int off1 = lr * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
+  const int aBase = wr * PP_HALF;                                      // A-half of this group
+  const int bBase = (2 + (wc >> 1)) * PP_HALF + (wc & 1) * 64 * 128;  // W-half, 64-row band
+
+  bf16x8 a[2][4][2], b[2][2][2];
+  f32x4 acc[8][4];
+
+  auto read_a = [&](int buf, int qm) {
+    const char* base = smem + buf * 4 * PP_HALF + aBase + qm * 64 * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[qm][i][0] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + off0);
+      a[qm][i][1] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + off1);
+    }
+  };
+  auto read_b = [&](int buf, int qn) {
+    const char* base = smem + buf * 4 * PP_HALF + bBase + qn * 32 * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      b[qn][j][0] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + off0);
+      b[qn][j][1] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + off1);
+    }
+  };
+  auto mma = [&](int qm, int qn) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm * 4 + i][qn * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[qn][j][ks], a[qm][i][ks], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // the MFMA half of a phase: barrier, retire this phase's LDS reads, MFMAs at raised priority
+  auto compute = [&](int qm, int qn, bool live) {
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (live) {
+      __builtin_amdgcn_s_setprio(1);
+      mma(qm, qn);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bar();
+  };
+
+  set_tile(v);
+  prologue_dma();
+  int relax = 0;  // S stores of the previous (interior) tile may still be outstanding
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    wait_vm_rt<S>((nk > 1 ? 8 : 0) + relax);  // K-tile 0 landed
+    bar();
+    if (wr == 1) bar();  // group 1 runs one barrier behind
+
+    for (int t = 0; t < nk; t += 2) {
+      const bool odd_live = t + 1 < nk;
+      launder();
+      // ---- even K-tile t (buffer 0) ----
+      read_a(0, 0); read_b(0, 0); read_a(0, 1);
+      if (t > 0) dma(t + 1, 3);
+      compute(0, 0, true);
+      read_b(0, 1); dma(t + 2, 0);
+      compute(0, 1, true);
+      dma(t + 2, 1);
+      compute(1, 1, true);
+      dma(t + 2, 2);
+      wait_vm_rt<S>((t + 2 < nk ? 6 : 0) + (t == 0 ? relax : 0));  // retires tile t+1 (buffer 1)
+      compute(1, 0, true);
+      // ---- odd K-tile t+1 (buffer 1) ----
+      read_a(1, 0); read_b(1, 0); read_a(1, 1); dma(t + 2, 3);
+      compute(0, 0, odd_live);
+      read_b(1, 1); dma(t + 3, 0);
+      compute(0, 1, odd_live);
+      dma(t + 3, 1);
+      compute(1, 1, odd_live);
+      dma(t + 3, 2);
+      wait_vm_rt<S>(t + 3 < nk ? 6 : 0);  // retires tile t+2 (buffer 0)
+      compute(1, 0, odd_live);
+    }
+    if (wr == 0) bar();  // equalise the barrier count of the two groups: every LDS read is done
+
+    const int em0 = m0, en0 = n0;
+    const bool interior = (em0 + 256 <= e.M) && (en0 + 256 <= e.N);
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const int erow = em0 + wr * 128 + (el & 15), ecol = en0 + wc * 64 + 16 * (el >> 4);
+    float bv[16];
+    load_bias16<EPI>(e, ecol, bv);  // issued before the next tile's DMAs: its wait skips them
+    v += gridDim.x;
+    const bool has_next = v < tiles;
+    if (has_next) {
+      set_tile(v);
+      launder();
+      prologue_dma();
+    }
+    asm volatile("" ::: "memory");
+    // Epilogue straight from the accumulators: with W as the MFMA's first operand and the W
+    // rows permuted (wperm), lane l holds 16 consecutive columns 16(l>>4).. of row l&15 of
+    // every 16-row block — whole 16-B vectors, no LDS.
+#pragma unroll
+    for (int mf = 0; mf < 8; ++mf) {
+      float vv[16];
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vv[4 * f + r] = acc[mf][f][r];
+      epi_row16<EPI, CF32, RF32>(e, erow + mf * 16, ecol, vv, bv);
+    }
+    asm volatile("" ::: "memory");
+    if (!has_next) break;
+    relax = interior ? S : 0;
+  }
+  wait_vmcnt<0>();
+}
+
+static int num_cus() {
+  static int n[16] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) dev = 0;
+  if (!n[dev]) {
+    int c = 0;
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    n[dev] = c > 0 ? c : 256;
+  }
+  return n[dev];
+}
+
+template <int EPI, bool CF32, bool RF32>
+static void launch_pp(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
+                      hipStream_t s) {
+  constexpr size_t lds = 8 * PP_HALF;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_pp<EPI, CF32, RF32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  const int nTm = (M + 255) / 256, nTn = (N + 255) / 256;
+  const int grid = min(nTm * nTn, num_cus());
+  k_gemm_pp<EPI, CF32, RF32><<<grid, 512, lds, s>>>(K, (const bf16*)A, lda, (const bf16*)W, ldw, e, nTm, nTn);
+}
+
 template <int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
 static void launch_bf16(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                         const EpiArgs& e, hipStream_t s) {
@@ -460,15 +723,11 @@ static void launch_bf16(int M, int N, int K, const void* A, int lda, const void*
       K, (const bf16*)A, lda, (const bf16*)W, ldw, e, nTn);
 }
 
-// Variant selector for A/B timing (RF_GEMM_VARIANT): 1 -> 256^2 BK64 x2 (default, fastest
-// measured), 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 -> 256x128 / 128^2 tiles.
+// Variant selector for A/B timing (RF_GEMM_VARIANT): 5 -> 256^2 ping-pong (default), 1 -> 256^2
+// BK64 x2, 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 -> 256x128 / 128^2 tiles.
 static int gemm_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = getenv("RF_GEMM_VARIANT");
-    v = s ? atoi(s) : 1;
-  }
-  return v;
+  const char* s = getenv("RF_GEMM_VARIANT");  // read per call so A/B tools can switch
+  return s ? atoi(s) : 5;
 }
 
 
@@ -483,6 +742,7 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
       case 2: launch_bf16<256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 3: launch_bf16<128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 4: launch_bf16<256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 5: launch_pp<EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       default: launch_bf16<256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
     }
   } else {
