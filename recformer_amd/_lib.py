@@ -10,7 +10,8 @@ import os
 from ctypes import c_float, c_int, c_void_p
 from typing import Optional
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librecformer_hip.so")
+LIB_PATH = os.environ.get("RF_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                        "librecformer_hip.so")  # env: diagnostic builds
 
 RF_F32, RF_BF16 = 0, 1
 RF_IO_C_F32, RF_IO_R_F32 = 1, 2

@@ -40,6 +40,8 @@ struct EpiArgs {
   const float* lrstd;
   const float* lgamma;
   const float* lbeta;
+  unsigned long long* stamps;  // diagnostic s_memtime stamps (tools only), nullptr = off
+  int gn;                      // ping-pong kernel: column tiles per raster group (0 = all)
 };
 
 // scalar epilogue (fp32 kernel and ragged tails)
@@ -515,12 +517,20 @@ __global__ void __launch_bounds__(512, 1)
   int v = blockIdx.x;
   if (v >= tiles) return;
   int m0 = 0, n0 = 0;
-  auto set_tile = [&](int vv) {
+  // Tile order: XCD-contiguous ranges (xcd_remap) of a column-grouped raster: GN columns of
+  // tiles at a time, all row panels down, so the tiles one XCD runs concurrently share a W
+  // slice of GN x 256 rows that stays resident in its L2 across rounds.
+  const int GN = e.gn > 0 ? min(e.gn, nTn) : nTn;
+  auto tile_origin = [&](int vv, int& om0, int& on0) {
     const int wg = xcd_remap(vv, tiles);
-    const int tm = wg / nTn;
-    m0 = tm * 256;
-    n0 = (wg - tm * nTn) * 256;
+    const int g = wg / (nTm * GN);
+    const int gw = min(GN, nTn - g * GN);  // width of this (possibly last, narrower) group
+    const int rem = wg - g * nTm * GN;
+    const int tm = rem / gw;
+    om0 = tm * 256;
+    on0 = (g * GN + rem - tm * gw) * 256;
   };
+  auto set_tile = [&](int vv) { tile_origin(vv, m0, n0); };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave >> 2, wc = wave & 3;
 
@@ -536,17 +546,28 @@ __global__ void __launch_bounds__(512, 1)
   const int nk = K >> 6;
   auto launder = [&]() { asm volatile("" : "+v"(xa), "+v"(xw0), "+v"(xw1), "+v"(pch)); };
   // half index: 0 = A rows 0-127, 1 = A rows 128-255, 2 = W rows 0-127, 3 = W rows 128-255
+  // K-tiles nk, nk+1 of the current tile are K-tiles 0, 1 of the NEXT tile when `pf` is set
+  // (nk even, so the buffer parity carries over): the last iteration's idle DMA slots prefetch
+  // the next tile's prologue behind this tile's MFMAs.
+  int nm0 = 0, nn0 = 0;
+  bool pf = false;
   auto dma = [&](int t, int half) {
-    if (t >= nk) return;  // wave-uniform
+    int kt = t, bm0 = m0, bn0 = n0;
+    if (t >= nk) {  // wave-uniform
+      if (!pf || t >= nk + 2) return;
+      kt = t - nk;
+      bm0 = nm0;
+      bn0 = nn0;
+    }
     char* dst = smem + ((t & 1) * 4 + half) * PP_HALF + wave * 2048;
     const bool isA = half < 2;
     const bf16* base = isA ? A : W;
     const int ld = isA ? lda : ldw;
     const int lim = (isA ? e.M : e.N) - 1;
-    const int r0 = (isA ? m0 : n0) + (half & 1) * 128;
+    const int r0 = (isA ? bm0 : bn0) + (half & 1) * 128;
     const int ra = r0 + (isA ? xa : xw0), rb = r0 + (isA ? xa + 8 : xw1);
-    glds16(base + (min(ra, lim) * ld + t * 64 + pch), dst);
-    glds16(base + (min(rb, lim) * ld + t * 64 + pch), dst + 1024);
+    glds16(base + (min(ra, lim) * ld + kt * 64 + pch), dst);
+    glds16(base + (min(rb, lim) * ld + kt * 64 + pch), dst + 1024);
   };
   auto prologue_dma = [&]() {  // K-tiles 0 and 1 complete
     dma(0, 0); dma(0, 1); dma(0, 2); dma(0, 3);
@@ -606,6 +627,16 @@ __global__ void __launch_bounds__(512, 1)
     bar();
   };
 
+  // diagnostic timeline (tools/gemm_stamps.py): wave 0 records s_memtime at 6 points of each
+  // tile into LDS past the ring (no vmcnt traffic), copied out at the end
+  unsigned long long* stl = reinterpret_cast<unsigned long long*>(smem + 8 * PP_HALF);
+  int tix = 0;
+  auto stamp = [&](int k) {
+    if (e.stamps != nullptr && wave == 0) {
+      const unsigned long long tt = __builtin_amdgcn_s_memtime();
+      if (lane == 0 && tix < 16) stl[tix * 8 + k] = tt;
+    }
+  };
   set_tile(v);
   prologue_dma();
   int relax = 0;  // S stores of the previous (interior) tile may still be outstanding
@@ -616,7 +647,12 @@ __global__ void __launch_bounds__(512, 1)
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     wait_vm_rt<S>((nk > 1 ? 8 : 0) + relax);  // K-tile 0 landed
     bar();
+    stamp(0);
     if (wr == 1) bar();  // group 1 runs one barrier behind
+    const bool has_next = v + (int)gridDim.x < tiles;
+    pf = has_next && !(nk & 1);
+    if (has_next) tile_origin(v + gridDim.x, nm0, nn0);
+    const int lim = nk + (pf ? 2 : 0);  // DMA-able virtual K-tiles
 
     for (int t = 0; t < nk; t += 2) {
       const bool odd_live = t + 1 < nk;
@@ -630,7 +666,8 @@ __global__ void __launch_bounds__(512, 1)
       dma(t + 2, 1);
       compute(1, 1, true);
       dma(t + 2, 2);
-      wait_vm_rt<S>((t + 2 < nk ? 6 : 0) + (t == 0 ? relax : 0));  // retires tile t+1 (buffer 1)
+      wait_vm_rt<S>((t + 2 < lim ? 6 : 0) + (t == 0 ? relax : 0));  // retires tile t+1 (buffer 1)
+      if (t == 0) stamp(1);
       compute(1, 0, true);
       // ---- odd K-tile t+1 (buffer 1) ----
       read_a(1, 0); read_b(1, 0); read_a(1, 1); dma(t + 2, 3);
@@ -640,10 +677,12 @@ __global__ void __launch_bounds__(512, 1)
       dma(t + 3, 1);
       compute(1, 1, odd_live);
       dma(t + 3, 2);
-      wait_vm_rt<S>(t + 3 < nk ? 6 : 0);  // retires tile t+2 (buffer 0)
+      if (t + 2 < nk) wait_vm_rt<S>(t + 3 < lim ? 6 : 0);  // retires tile t+2 (buffer 0)
+      if (t == 0) stamp(2);
       compute(1, 0, odd_live);
     }
     if (wr == 0) bar();  // equalise the barrier count of the two groups: every LDS read is done
+    stamp(3);
 
     const int em0 = m0, en0 = n0;
     const bool interior = (em0 + 256 <= e.M) && (en0 + 256 <= e.N);
@@ -653,13 +692,14 @@ __global__ void __launch_bounds__(512, 1)
     float bv[16];
     load_bias16<EPI>(e, ecol, bv);  // issued before the next tile's DMAs: its wait skips them
     v += gridDim.x;
-    const bool has_next = v < tiles;
     if (has_next) {
       set_tile(v);
       launder();
-      prologue_dma();
+      if (pf) dma(1, 3);  // the rest of the next tile's K-tiles 0, 1 went out in the last iteration
+      else prologue_dma();
     }
     asm volatile("" ::: "memory");
+    stamp(4);
     // Epilogue straight from the accumulators: with W as the MFMA's first operand and the W
     // rows permuted (wperm), lane l holds 16 consecutive columns 16(l>>4).. of row l&15 of
     // every 16-row block — whole 16-B vectors, no LDS.
@@ -673,10 +713,16 @@ __global__ void __launch_bounds__(512, 1)
       epi_row16<EPI, CF32, RF32>(e, erow + mf * 16, ecol, vv, bv);
     }
     asm volatile("" ::: "memory");
+    stamp(5);
+    ++tix;
     if (!has_next) break;
     relax = interior ? S : 0;
   }
   wait_vmcnt<0>();
+  if (e.stamps != nullptr && wave == 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = lane; i < 16 * 8; i += 64) e.stamps[blockIdx.x * 128 + i] = stl[i];
+  }
 }
 
 static int num_cus() {
@@ -695,7 +741,7 @@ static int num_cus() {
 template <int EPI, bool CF32, bool RF32>
 static void launch_pp(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
                       hipStream_t s) {
-  constexpr size_t lds = 8 * PP_HALF;
+  constexpr size_t lds = 8 * PP_HALF + 1024;  // ring + diagnostic stamp area
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)k_gemm_pp<EPI, CF32, RF32>,
@@ -725,6 +771,13 @@ static void launch_bf16(int M, int N, int K, const void* A, int lda, const void*
 
 // Variant selector for A/B timing (RF_GEMM_VARIANT): 5 -> 256^2 ping-pong (default), 1 -> 256^2
 // BK64 x2, 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 -> 256x128 / 128^2 tiles.
+static unsigned long long* g_stamps = nullptr;  // set by rf_debug_gemm_stamps (tools only)
+
+static int gemm_gn() {  // measured: 4 beats the full-width raster by ~4% on the FFN1 shape
+  const char* s = getenv("RF_GEMM_GN");
+  return s ? atoi(s) : 4;
+}
+
 static int gemm_variant() {
   const char* s = getenv("RF_GEMM_VARIANT");  // read per call so A/B tools can switch
   return s ? atoi(s) : 5;
@@ -766,7 +819,7 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
   RF_REQUIRE(epilogue != RF_EPI_COS || (ra && rw), "rf_gemm: norms required for EPI_COS");
   if (M == 0) return RF_OK;
   EpiArgs e{M, N, bias, resid, ldr, C, ldc, scale_cols, col_scale, ra, rw,
-            nullptr, nullptr, nullptr, nullptr};
+            nullptr, nullptr, nullptr, nullptr, g_stamps, gemm_gn()};
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16) {
     RF_REQUIRE(K % 64 == 0, "rf_gemm(bf16): K=%d must be a multiple of 64", K);
@@ -823,7 +876,7 @@ extern "C" int rf_gemm_resid_ln(int dtype, int M, int N, int K, const void* A, i
              "rf_gemm_resid_ln: null pointer");
   if (M == 0) return RF_OK;
   EpiArgs e{M, N, bias, resid_pre, ldr, C, ldc, 0, 1.0f, nullptr, nullptr,
-            r_mean, r_rstd, r_gamma, r_beta};
+            r_mean, r_rstd, r_gamma, r_beta, g_stamps, gemm_gn()};
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16) {
     RF_REQUIRE(K % 64 == 0, "rf_gemm_resid_ln(bf16): K=%d must be a multiple of 64", K);
@@ -840,3 +893,7 @@ extern "C" int rf_gemm_resid_ln(int dtype, int M, int N, int K, const void* A, i
   }
   RF_LAUNCH_CHECK("rf_gemm_resid_ln");
 }
+
+// Diagnostic only (tools/gemm_stamps.py): device buffer of >= gridDim*128 uint64 that the
+// ping-pong GEMM fills with per-tile s_memtime stamps; nullptr disables. Not part of the ABI.
+extern "C" void rf_debug_gemm_stamps(void* buf) { g_stamps = reinterpret_cast<unsigned long long*>(buf); }
