@@ -14,6 +14,8 @@
 // keys j with |i-j| <= 32 that are valid and NOT global, plus every global key of its
 // sequence (local K/V). Padded query rows are written as exactly 0. Global query rows are
 // computed here too and then overwritten by k_global_attn (TF:612-629).
+#include <stdlib.h>
+
 #include "rf_common.h"
 
 namespace rf {
@@ -37,6 +39,24 @@ __device__ __forceinline__ int swz_el(int row, int col) {
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// Two ds_read_b64_tr_b16 + lgkmcnt(0) as one asm statement. With an LDS-DMA in flight hipcc
+// treats the transposed-read builtin as possibly aliasing it and waits vmcnt(0) first, which
+// would drain the prefetch pipeline; as asm the read is ordered only by the kernel's own
+// counted vmcnt + barrier protocol (the slots read here were retired before the barrier).
+__device__ __forceinline__ void tr_read2(uint32_t a0, uint32_t a1, bf16x4& v0, bf16x4& v1) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %2\n\t"
+      "ds_read_b64_tr_b16 %1, %3\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v0), "=&v"(v1)
+      : "v"(a0), "v"(a1)
+      : "memory");
+}
+
 __device__ __forceinline__ bf16x4 tr_read(const char* lds_base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds_base + off));
 }
@@ -47,9 +67,14 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __re
                                                          const uint8_t* __restrict__ flags,
                                                          const int32_t* __restrict__ gidx,
                                                          int gmax, bf16* __restrict__ out,
-                                                         int ldo) {
+                                                         int ldo, int H) {
   __shared__ __attribute__((aligned(16))) char smem[AT_LDS];
-  const int i0 = blockIdx.x * 64, h = blockIdx.y, b = blockIdx.z;
+  // 1-D grid, XCD-remapped: the Lp/64 query blocks of one (sequence, head) are consecutive
+  // on one XCD, so the half-overlapping K/V windows of neighbouring blocks hit its L2
+  const int nqb = Lp >> 6;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = wg % nqb, bh = wg / nqb;
+  const int i0 = qb * 64, h = bh % H, b = bh / H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int64_t rb = (int64_t)b * Lp;
@@ -237,6 +262,279 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __re
 }
 
 // ------------------------------------------------------------------------------------
+// Local branch, bf16, pipelined sliding window (k_band_attn_pipe): one workgroup walks a run
+// of consecutive 64-query blocks of one (sequence, head). Keys are staged in 64-row chunks
+// c = rows [64c-32, 64c+32): query block x needs chunks x and x+1, so each chunk is DMA'd
+// once (not twice, as with one window per block) into a 3-slot ring, and Q blocks into a
+// 2-slot ring. At the end of block x the slot it no longer needs receives chunk x+3 and
+// Q(x+2), then O(x) is stored: loads run two blocks ahead and the stores, issued last, are
+// never waited for by the next block's counted vmcnt. Key masks (valid & local, and valid)
+// are 64-bit ballots per chunk computed once in the prologue. Needs gmax <= 32.
+constexpr int AP_Q = 0;          // 2 x 64 rows x 128 B
+constexpr int AP_KV = 16384;     // 3 x (K 64 x 128 B, V 64 x 128 B)
+constexpr int AP_KG = 65536;     // 32 x 128 B
+constexpr int AP_VG = 69632;     // 32 x 128 B
+constexpr int AP_GP = 73728;     // 32 x int
+constexpr int AP_MK = 73856;     // per chunk {local mask, valid mask} uint64
+
+__device__ __forceinline__ void wait_vm_small(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_band_attn_pipe(int Lp, int H, int qpb, const bf16* __restrict__ q,
+                                                         const bf16* __restrict__ k,
+                                                         const bf16* __restrict__ v, int ld,
+                                                         const uint8_t* __restrict__ flags,
+                                                         const int32_t* __restrict__ gidx, int gmax,
+                                                         bf16* __restrict__ out, int ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nqb = Lp >> 6;
+  const int nparts = (nqb + qpb - 1) / qpb;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int part = wg % nparts, bh = wg / nparts;
+  const int h = bh % H, b = bh / H;
+  const int x0 = part * qpb, x1 = min(nqb, x0 + qpb);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t rb = (int64_t)b * Lp;
+  const int hoff = h * 64;
+  int* gp = reinterpret_cast<int*>(smem + AP_GP);
+  unsigned long long* mk = reinterpret_cast<unsigned long long*>(smem + AP_MK);
+
+  // ---- prologue: chunk masks, global keys ----
+  for (int c = x0 + wave; c <= x1; c += 4) {
+    const int row = 64 * c - 32 + lane;
+    const int f = (row >= 0 && row < Lp) ? flags[rb + row] : 0;
+    const unsigned long long ml = __ballot(f == 1), mv = __ballot(f != 0);
+    if (lane == 0) {
+      mk[2 * (c - x0)] = ml;
+      mk[2 * (c - x0) + 1] = mv;
+    }
+  }
+  if (gmax > 0) {
+    const int row = wave * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ (row & 7);
+    const int p = row < gmax ? gidx[(int64_t)b * gmax + row] : -1;
+    const int64_t off = (rb + (p >= 0 ? p : 0)) * ld + hoff + ch * 8;
+    glds16(k + off, smem + AP_KG + wave * 1024);
+    glds16(v + off, smem + AP_VG + wave * 1024);
+    if (threadIdx.x < 32) gp[threadIdx.x] = (int)threadIdx.x < gmax ? gidx[(int64_t)b * gmax + threadIdx.x] : -1;
+  }
+  auto dma_chunk = [&](int c) {  // 4 DMAs per wave: K pieces 2w, 2w+1 and V pieces 2w, 2w+1
+    char* base = smem + AP_KV + (c % 3) * 16384;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pc = 2 * wave + j;
+      const int row = pc * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ (row & 7);
+      const int kp = min(max(64 * c - 32 + row, 0), Lp - 1);
+      const int64_t off = (rb + kp) * ld + hoff + ch * 8;
+      glds16(k + off, base + pc * 1024);
+      glds16(v + off, base + 8192 + pc * 1024);
+    }
+  };
+  auto dma_q = [&](int x) {  // 2 DMAs per wave
+    char* base = smem + AP_Q + (x & 1) * 8192;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pc = 2 * wave + j;
+      const int row = pc * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ (row & 7);
+      const int64_t off = (rb + 64 * x + row) * ld + hoff + ch * 8;
+      glds16(q + off, base + pc * 1024);
+    }
+  };
+  dma_q(x0);
+  dma_chunk(x0);
+  dma_chunk(x0 + 1);  // x0 + 1 <= x1 always
+  if (x0 + 1 < x1) dma_q(x0 + 1);
+  if (x0 + 2 <= x1) dma_chunk(x0 + 2);
+
+  const int ks = min(16 * wave, 32);  // first window row of the wave's 96-key span
+  const int myw = 32 + 16 * wave + li;  // this lane's query row inside the 128-row window
+  for (int x = x0; x < x1; ++x) {
+    wait_vm_small((x + 2 <= x1 ? 4 : 0) + (x + 1 < x1 ? 2 : 0) + (x > x0 ? 4 : 0));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int i0 = 64 * x;
+    const int myq = i0 + 16 * wave + li;
+    const unsigned long long ml0 = mk[2 * (x - x0)], ml1 = mk[2 * (x - x0) + 2];
+    const unsigned long long mv0 = mk[2 * (x - x0) + 1], mv1 = mk[2 * (x - x0) + 3];
+    const char* qs = smem + AP_Q + (x & 1) * 8192;
+    bf16x8 qf[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      qf[s2] = *reinterpret_cast<const bf16x8*>(qs + swz128(16 * wave + li, 4 * s2 + g));
+    // LDS base of window row group starting at kr (16-aligned): chunk x + (kr >> 6)
+    auto kslot = [&](int kr) { return smem + AP_KV + ((x + (kr >> 6)) % 3) * 16384; };
+
+    // ---- window segment: 6 key tiles of 16 ----
+    f32x4 st[6];
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const int kr0 = ks + 16 * t;
+      const char* kb = kslot(kr0);
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + swz128((kr0 & 63) + li, 4 * s2 + g));
+        st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s2], st[t], 0, 0, 0);
+      }
+    }
+    // allowed keys as three 32-bit words over the wave's 96-row span [ks, ks+96):
+    // valid & local (chunk ballots, wave-uniform) & band |kr - myw| <= 32 (per lane), then
+    // shifted right by 4g so element (t, r) is bit 16(t&1) + r of word t>>1.
+    unsigned int aw[3];
+    {
+      const unsigned long long lo = ks ? ((ml0 >> ks) | (ml1 << (64 - ks))) : ml0;
+      const unsigned long long hi = ml1 >> ks;
+      const unsigned int kv[3] = {(unsigned int)lo, (unsigned int)(lo >> 32), (unsigned int)hi};
+      const int blo = myw - 32 - ks;  // band = relative rows [blo, blo + 64]
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        const int a = blo - 32 * w, z = blo + 65 - 32 * w;  // band bits [a, z) of this word
+        const unsigned int from = a <= 0 ? ~0u : (a >= 32 ? 0u : (~0u << a));
+        const unsigned int below = z >= 32 ? ~0u : (z <= 0 ? 0u : ((1u << z) - 1u));
+        aw[w] = (kv[w] & from & below) >> (4 * g);
+      }
+    }
+    float mx = RF_NEG_INF;
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = (aw[t >> 1] >> (16 * (t & 1) + r)) & 1u;
+        const float sv = ok ? st[t][r] : RF_NEG_INF;
+        st[t][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float m = mx;
+    float lsum = 0.f;
+    {
+      const float mu = (m == RF_NEG_INF) ? 0.f : m;
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f((st[t][r] - mu) * LOG2E);
+          st[t][r] = p;
+          lsum += p;
+        }
+    }
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[j] = (bf16)st[2 * s2 + (j >> 2)][j & 3];
+      const int ga = ks + 32 * s2, gb = ga + 16;  // the two 16-row key groups of this k-step
+      const char* va = kslot(ga) + 8192;
+      const char* vb = kslot(gb) + 8192;
+      const int rr = 4 * g + (li >> 2);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = 16 * dt + 4 * (li & 3);
+        bf16x4 v0, v1;
+        tr_read2(lds_addr(va + swz_el((ga & 63) + rr, col)), lds_addr(vb + swz_el((gb & 63) + rr, col)), v0, v1);
+        bf16x8 vf;
+        vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v0[2]; vf[3] = v0[3];
+        vf[4] = v1[0]; vf[5] = v1[1]; vf[6] = v1[2]; vf[7] = v1[3];
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+      }
+    }
+
+    // ---- global keys (local K/V at the global positions, staged once) ----
+    if (gmax > 0) {
+      f32x4 sg[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        sg[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(smem + AP_KG + swz128(16 * t + li, 4 * s2 + g));
+          sg[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s2], sg[t], 0, 0, 0);
+        }
+      }
+      float cmx = RF_NEG_INF;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = gp[16 * t + 4 * g + r] >= 0;
+          const float sv = ok ? sg[t][r] : RF_NEG_INF;
+          sg[t][r] = sv;
+          cmx = fmaxf(cmx, sv);
+        }
+      cmx = fmaxf(cmx, __shfl_xor(cmx, 16, 64));
+      cmx = fmaxf(cmx, __shfl_xor(cmx, 32, 64));
+      const float mn = fmaxf(m, cmx);
+      const float mu = (mn == RF_NEG_INF) ? 0.f : mn;
+      const float alpha = __builtin_amdgcn_exp2f((m - mu) * LOG2E);
+      lsum *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f((sg[t][r] - mu) * LOG2E);
+          sg[t][r] = p;
+          lsum += p;
+        }
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[j] = (bf16)sg[j >> 2][j & 3];
+      const int r0 = 4 * g + (li >> 2);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = 16 * dt + 4 * (li & 3);
+        bf16x4 v0, v1;
+        tr_read2(lds_addr(smem + AP_VG + swz_el(r0, col)), lds_addr(smem + AP_VG + swz_el(r0 + 16, col)), v0, v1);
+        bf16x8 vf;
+        vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v0[2]; vf[3] = v0[3];
+        vf[4] = v1[0]; vf[5] = v1[1]; vf[6] = v1[2]; vf[7] = v1[3];
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+      }
+    }
+
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    const unsigned long long qmw = (myw >> 6) ? mv1 : mv0;
+    const bool qvalid = (qmw >> (myw & 63)) & 1ull;
+    const float inv = (qvalid && lsum > 0.f) ? 1.0f / lsum : 0.f;
+
+    // every wave is done with chunk slot x%3 and Q slot x&1: refill them two blocks ahead
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (x + 3 <= x1) dma_chunk(x + 3);
+    if (x + 2 < x1) dma_q(x + 2);
+
+    bf16* orow = out + (rb + myq) * ldo + hoff + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(qvalid ? o[dt][r] * inv : 0.f);
+      *reinterpret_cast<bf16x4*>(orow + 16 * dt) = w;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ------------------------------------------------------------------------------------
 // Local branch, generic element type, VALU (fp32 parity path; any even window).
 // One wave per (query, head): lanes own keys; scores reduced with wave shuffles.
 template <typename T>
@@ -388,9 +686,25 @@ extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int hal
     RF_REQUIRE(half_w == 32, "rf_band_attn_fwd(bf16): window must be 64 (half 32), got half %d", half_w);
     RF_REQUIRE(Lp % 64 == 0, "rf_band_attn_fwd(bf16): Lp=%d must be a multiple of 64", Lp);
     RF_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0, "rf_band_attn_fwd(bf16): alignment");
-    dim3 grid(Lp / 64, H, B);
-    k_band_attn_bf16<<<grid, 256, 0, s>>>(Lp, (const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                          ld_qkv, flags, gidx, gmax, (bf16*)out, ld_out);
+    if (gmax <= 32 && !getenv("RF_BAND_ONESHOT")) {
+      // pipelined: runs of qpb query blocks per workgroup, >= ~3 workgroups per CU slot
+      const int nqb = Lp / 64;
+      const int qpb = nqb >= 16 ? (nqb + 1) / 2 : nqb;
+      const int nparts = (nqb + qpb - 1) / qpb;
+      const size_t lds = AP_MK + (size_t)(qpb + 1) * 16;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_band_attn_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, 80000);
+        attr = true;
+      }
+      RF_REQUIRE(lds <= 80000, "rf_band_attn_fwd(bf16): Lp=%d too long for the pipelined kernel", Lp);
+      k_band_attn_pipe<<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
+                                                         (const bf16*)v, ld_qkv, flags, gidx, gmax,
+                                                         (bf16*)out, ld_out);
+    } else {
+      k_band_attn_bf16<<<(Lp / 64) * H * B, 256, 0, s>>>(Lp, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                         ld_qkv, flags, gidx, gmax, (bf16*)out, ld_out, H);
+    }
   } else if (dtype == RF_F32) {
     RF_REQUIRE(half_w > 0, "rf_band_attn_fwd: bad half window");
     dim3 grid((Lp + 3) / 4, H, B);

@@ -73,6 +73,14 @@ __device__ __forceinline__ float gelu_bf16out(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * p));
 }
 
+// Bijective XCD-aware remap of a 1-D block id (guide §5 T1): the hardware deals block ids
+// round-robin over the 8 XCDs; the returned index is contiguous per XCD, so blocks that share
+// data (neighbouring tiles, windows) run on one XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 // ---- wave64 reductions ----------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -71,10 +71,6 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, fl
     reinterpret_cast<TIN*>(e.C)[(int64_t)row * e.ldc + col] = from_f32<TIN>(v);
 }
 
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
 
 // ------------------------------------------------------------------------------------
 // bf16
