@@ -69,47 +69,48 @@ __device__ __forceinline__ bf16x4 tr_read_g(const char* p) {
 }
 
 // ---- u = Wkg_h^T qg_h ------------------------------------------------------------------
-// grid (16 heads, ceil(D/256)): a thread owns one column k of Wkg_h (64 weights in registers,
-// read once for all R global rows); the R query rows of head h are staged in LDS.
-// bf16 path writes u as hi + lo bf16 planes (u ~= hi + lo to ~16 mantissa bits), so the MFMA
-// score product keeps fp32-like precision in u: s = hi.h + lo.h.
+// grid (16 heads, R): one block per (head, global row); thread t owns columns 4t..4t+3 of
+// Wkg_h (64 rows x D), reads them with 8-B vector loads (L2-resident weights) and dots them
+// with the head's 64 query values (LDS broadcast). bf16 path writes u as hi + lo bf16 planes
+// (u ~= hi + lo to ~16 mantissa bits) so the MFMA score product keeps fp32-like precision
+// in u: s = hi.h + lo.h; heads >= H are written as zeros (padding of the 16-head tile).
 template <typename T>
 __global__ void __launch_bounds__(256) k_gfold_u(int D, int H, int R, const T* __restrict__ qg,
                                                   int ld_qg, const T* __restrict__ wkg,
                                                   const int32_t* __restrict__ gidx, GfoldWs ws,
                                                   bool out_bf16) {
-  __shared__ float qs[64 * 64];
-  const int h = blockIdx.x;
-  const int k = blockIdx.y * 64 + (threadIdx.x & 63);   // column of Wkg_h
-  const int rgrp = threadIdx.x >> 6;                      // rows r = rgrp (mod 4)
-  const bool kin = k < D;
-  float w[64];
-  if (h < H) {
+  __shared__ float qs[64];
+  const int h = blockIdx.x, r = blockIdx.y;
+  if (gidx[r] < 0) return;
+  const int t = threadIdx.x;
+  if (h < H && t < 64) qs[t] = to_f32(qg[(int64_t)r * ld_qg + h * 64 + t]);
+  __syncthreads();
+  for (int k = 4 * t; k < D; k += 4 * blockDim.x) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (h < H) {
+      const T* wp = wkg + (int64_t)(h * 64) * D + k;
+#pragma unroll 16
+      for (int d = 0; d < 64; ++d) {
+        float x[4];
+        load4(wp + (int64_t)d * D, x);
+        const float qd = qs[d];
 #pragma unroll
-    for (int d = 0; d < 64; ++d) w[d] = kin ? to_f32(wkg[(int64_t)(h * 64 + d) * D + k]) : 0.f;
-  }
-  for (int r0 = 0; r0 < R; r0 += 64) {
-    const int nr = min(64, R - r0);
-    __syncthreads();
-    if (h < H)
-      for (int i = threadIdx.x; i < nr * 64; i += 256)
-        qs[i] = to_f32(qg[(int64_t)(r0 + (i >> 6)) * ld_qg + h * 64 + (i & 63)]);
-    __syncthreads();
-    for (int rr = rgrp; rr < nr; rr += 4) {
-      const int r = r0 + rr;
-      if (!kin || gidx[r] < 0) continue;
-      float a = 0.f;
-      if (h < H) {
+        for (int i = 0; i < 4; ++i) a[i] = fmaf(qd, x[i], a[i]);
+      }
+    }
+    if (out_bf16) {
+      bf16* hi = ws.u16 + ((int64_t)r * 2 * GF_HP + h) * D + k;
+      bf16* lo = hi + (int64_t)GF_HP * D;
+      bf16x4 vh, vl;
 #pragma unroll
-        for (int d = 0; d < 64; ++d) a = fmaf(qs[rr * 64 + d], w[d], a);
+      for (int i = 0; i < 4; ++i) {
+        vh[i] = (bf16)a[i];
+        vl[i] = (bf16)(a[i] - (float)vh[i]);
       }
-      if (out_bf16) {
-        const bf16 hi = (bf16)a;
-        ws.u16[((int64_t)r * 2 * GF_HP + h) * D + k] = hi;
-        ws.u16[((int64_t)r * 2 * GF_HP + GF_HP + h) * D + k] = (bf16)(a - (float)hi);
-      } else if (h < H) {
-        ws.u32[((int64_t)r * H + h) * (D + 4) + k] = a;
-      }
+      *reinterpret_cast<bf16x4*>(hi) = vh;
+      *reinterpret_cast<bf16x4*>(lo) = vl;
+    } else if (h < H) {
+      *reinterpret_cast<float4*>(ws.u32 + ((int64_t)r * H + h) * (D + 4) + k) = make_float4(a[0], a[1], a[2], a[3]);
     }
   }
 }
@@ -347,7 +348,7 @@ __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int gmax, int 
   const int pos = gidx[r];
   if (pos < 0) return;
   const int b = r / gmax;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x;
   if (t < 64) {
     float mx = GF_NEG_INF;
     for (int c = t; c < nch; c += 64) mx = fmaxf(mx, ws.m[((int64_t)r * nch + c) * GF_HP + h]);
@@ -370,17 +371,22 @@ __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int gmax, int 
     wsm[k] = a * inv;
   }
   __syncthreads();
-  // one wave per 16 output rows of Wvg_h; lanes stride the row with 4-element vectors
-  for (int d = wave * 16; d < wave * 16 + 16; ++d) {
+  // GEMV out[d] = Wvg_h[d, :] . w: 4 threads per output row d (64 rows), each a quarter of the
+  // row in interleaved 8-element vectors, all loads issued up front; partial sums via shuffles
+  {
+    const int d = t >> 2, part = t & 3;
     const T* wr = wvg + (int64_t)(h * 64 + d) * D;
     float a = 0.f;
-    for (int k = 4 * lane; k < D; k += 256) {
-      float x[4];
+    for (int k = 8 * part; k < D; k += 32) {
+      float x[8];
       load4(wr + k, x);
-      a = fmaf(x[0], wsm[k], fmaf(x[1], wsm[k + 1], fmaf(x[2], wsm[k + 2], fmaf(x[3], wsm[k + 3], a))));
+      load4(wr + k + 4, x + 4);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a = fmaf(x[i], wsm[k + i], a);
     }
-    a = wave_sum(a);
-    if (lane == 0) out[((int64_t)b * Lp + pos) * ldo + h * 64 + d] = from_f32<T>(a + bvg[h * 64 + d]);
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (part == 0) out[((int64_t)b * Lp + pos) * ldo + h * 64 + d] = from_f32<T>(a + bvg[h * 64 + d]);
   }
 }
 
@@ -417,8 +423,8 @@ extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, c
     RF_REQUIRE(ldh % 8 == 0, "rf_global_attn_fold_fwd(bf16): ldh must be a multiple of 8");
     const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + 160 * sizeof(float);
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold_fwd: D too large for LDS");
-    k_gfold_u<bf16><<<dim3(GF_HP, (D + 63) / 64), 256, 0, s>>>(D, H, R, (const bf16*)qg, ld_qg,
-                                                                  (const bf16*)wkg, gidx, ws, true);
+    k_gfold_u<bf16><<<dim3(GF_HP, R), 192, 0, s>>>(D, H, R, (const bf16*)qg, ld_qg, (const bf16*)wkg, gidx,
+                                                    ws, true);
 #define GP_(DD)                                                                               \
   case DD:                                                                                    \
     (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<DD>,                          \
@@ -440,8 +446,8 @@ extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, c
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold_fwd: D too large for LDS");
     (void)hipFuncSetAttribute((const void*)k_gfold_partial_f32,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);
-    k_gfold_u<float><<<dim3(H, (D + 63) / 64), 256, 0, s>>>(D, H, R, (const float*)qg, ld_qg,
-                                                               (const float*)wkg, gidx, ws, false);
+    k_gfold_u<float><<<dim3(H, R), 192, 0, s>>>(D, H, R, (const float*)qg, ld_qg, (const float*)wkg, gidx,
+                                                 ws, false);
     k_gfold_partial_f32<<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const float*)h, ldh, flags, gidx, ws);
     k_gfold_out<float><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const float*)wvg, bvg, gidx, ws,
                                                        (float*)out, ld_out);
