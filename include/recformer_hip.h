@@ -140,6 +140,13 @@ int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, co
                       const void* items, int ldi, const float* ri, const int64_t* cand,
                       float inv_temp, float* scores, rf_stream_t stream);
 
+/* A9/A10 losses — torch CrossEntropyLoss rows (models.py:494-510 contrastive + MLM, :589-597
+ * SeqRec): loss[m] = logsumexp(x[m, :N]) - x[m, label[m]] in fp32 (0 where label == ignore_index;
+ * the caller divides the sum by the non-ignored count, as mean reduction does); optional
+ * argmax[m] (first maximum, torch.argmax) for cl_correct_num (models.py:497). ldx in elements. */
+int rf_cross_entropy_fwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,
+                         int64_t ignore_index, float* loss, int32_t* argmax, rf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -102,6 +102,36 @@ def main():
          **batch)
     manifest["l1_768"] = dict(config="BASE-1L", weight_seed=4, checksums=checksums(ref))
 
+    # --- pretraining (A10): two views + MLM, world size 1 -----------------------------------
+    pre = M.RecformerForPretraining(make_reference_config(**C1)).eval()
+    hash_init_(pre.longformer, seed=1)
+    hash_init_(pre.lm_head, seed=6)
+    with torch.no_grad():  # 4.28 ties decoder.bias to lm_head.bias; 5.15 keeps two: make them equal
+        pre.lm_head.decoder.bias.copy_(pre.lm_head.bias)
+    va = synth_batch(4, 256, C1["vocab_size"], seed=44, lens=[256, 180, 97, 40])
+    vb = synth_batch(4, 64, C1["vocab_size"], seed=45, lens=[64, 33, 64, 12])
+    g = torch.Generator().manual_seed(46)
+
+    def mlm(view, mask_id=3):
+        ids = view["input_ids"].clone()
+        sel = (torch.rand(ids.shape, generator=g) < 0.15) & (view["attention_mask"] == 1)
+        sel[:, 0] = False
+        labels = torch.where(sel, ids, torch.full_like(ids, -100))
+        return torch.where(sel, torch.full_like(ids, mask_id), ids), labels
+
+    mia, mla = mlm(va)
+    mib, mlb = mlm(vb)
+    sfx = lambda d, x: {k + "_" + x: v for k, v in d.items()}  # noqa: E731
+    with torch.no_grad():
+        out = pre(**sfx(va, "a"), **sfx(vb, "b"), mlm_input_ids_a=mia, mlm_labels_a=mla,
+                  mlm_input_ids_b=mib, mlm_labels_b=mlb)
+        out_nomlm = pre(**sfx(va, "a"), **sfx(vb, "b"))
+    save("c1_pretrain.npz", loss=out.loss, logits=out.logits, cl_correct_num=out.cl_correct_num,
+         loss_contrastive=out_nomlm.loss, mlm_input_ids_a=mia, mlm_labels_a=mla, mlm_input_ids_b=mib,
+         mlm_labels_b=mlb, **sfx(va, "a"), **sfx(vb, "b"))
+    manifest["c1_pretrain"] = dict(config="C1", weight_seed=1, head_seed=6,
+                                   checksums=checksums(pre))
+
     # state-dict layout of the drop-in classes
     layout = {}
     for cls in ("RecformerModel", "RecformerForSeqRec", "RecformerForPretraining"):

@@ -221,3 +221,31 @@ def cosine_scores(z: Tensor, items: Tensor, temp: float) -> Tensor:
 def seqrec_loss(scores: Tensor, labels: Tensor) -> Tensor:
     """models.py:587-597 — CrossEntropy over scores (full or sampled with target 0)."""
     return F.cross_entropy(scores, labels)
+
+
+def lm_head_forward(sd: Dict[str, Tensor], x: Tensor, eps: float) -> Tensor:
+    """LongformerLMHead.forward TF:1277-1285 (4.28 ties decoder.bias to bias): dense -> exact
+    GELU -> LayerNorm -> decoder; sd holds the lm_head.* parameters without the prefix."""
+    t = F.gelu(x @ sd["dense.weight"].t() + sd["dense.bias"])
+    t = F.layer_norm(t, (t.shape[-1],), sd["layer_norm.weight"], sd["layer_norm.bias"], eps)
+    return t @ sd["decoder.weight"].t() + sd["bias"]
+
+
+def pretrain_forward(sd_lf: Dict[str, Tensor], sd_head: Dict[str, Tensor], cfg, a: Dict[str, Tensor],
+                     b: Dict[str, Tensor], mlm_a=None, mlm_labels_a=None, mlm_b=None, mlm_labels_b=None):
+    """RecformerForPretraining.forward models.py:380-520 at world size 1: contrastive
+    CE(cos(z_a, z_b)/temp, arange) + mlm_weight * CE(lm_head(h_mlm), labels, ignore -100) per view.
+    Returns (loss, cos_sim, correct_num)."""
+    _, z1 = model_forward(sd_lf, cfg, **a)
+    _, z2 = model_forward(sd_lf, cfg, **b)
+    cos_sim = F.cosine_similarity(z1.unsqueeze(1), z2.unsqueeze(0), dim=-1) / cfg.temp
+    labels = torch.arange(cos_sim.size(0))
+    loss = F.cross_entropy(cos_sim, labels)
+    correct = (cos_sim.argmax(1) == labels).sum()
+    for view, ids, lab in ((a, mlm_a, mlm_labels_a), (b, mlm_b, mlm_labels_b)):
+        if ids is None or lab is None:
+            continue
+        h, _ = model_forward(sd_lf, cfg, **dict(view, input_ids=ids))
+        scores = lm_head_forward(sd_head, h, cfg.layer_norm_eps)
+        loss = loss + cfg.mlm_weight * F.cross_entropy(scores.reshape(-1, scores.shape[-1]), lab.reshape(-1))
+    return loss, cos_sim, correct

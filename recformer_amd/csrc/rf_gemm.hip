@@ -478,12 +478,122 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int K, const float* __restrict
 // read from the next phase on.
 constexpr int PP_HALF = 128 * 128;  // bytes per half-tile
 
-// W-row order in LDS: within each 64-row band, LDS row 16f + i (N-fragment f, MFMA row i)
-// holds W row 16(i>>2) + 4f + (i&3), so that MFMA output row i = 4g + r of fragment f is
-// output column 16g + 4f + r: lane group g ends up owning 16 consecutive columns.
+// W-row order in LDS (per 128-row half): LDS row 16f + j (N-fragment f = 0..7, MFMA column j)
+// holds the W row that makes lane group c = l&15 own whole vectors of output columns:
+//   bf16 output: column 8j + f          -> lane c holds columns 8c..8c+7 (one 16-B store)
+//   fp32 output: column 64(f>>2) + 4j + (f&3) -> columns 4c..4c+3 and 64+4c..: two 16-B
+//                stores, each instruction writing 4 full 256-B row segments.
+// Each store instruction then writes whole 128-B lines (4 rows x 16 lanes): measured 2.3-3.6x
+// the per-CU store rate of the 16-row x 4-lane pattern (tools/micro/store_pattern.hip).
+template <bool OUT32>
 __device__ __forceinline__ int wperm(int rho) {
-  const int f = (rho >> 4) & 3, i = rho & 15;
-  return (rho & ~63) + 16 * (i >> 2) + 4 * f + (i & 3);
+  const int f = (rho >> 4) & 7, j = rho & 15;
+  return OUT32 ? 64 * (f >> 2) + 4 * j + (f & 3) : 8 * j + f;
+}
+
+// n (4 or 8) consecutive columns [c0, c0 + n) of one output row; bv/gm/bt = bias / LN gamma /
+// LN beta for those columns (hoisted by the caller). Mirrors epi_row16 / epi_store.
+template <int EPI, bool CF32, bool RF32, int NV>
+__device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float* v, const float* bv,
+                                        const float* gm, const float* bt) {
+  if (row >= e.M) return;
+  if (c0 + NV > e.N) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) epi_store<bf16, EPI, CF32, RF32>(e, row, c0 + k, v[k]);
+    return;
+  }
+  if (EPI == RF_EPI_COS) {
+    const float sc = e.ra[row] * e.col_scale;
+    float* out = reinterpret_cast<float*>(e.C) + (int64_t)row * e.ldc + c0;
+#pragma unroll
+    for (int q = 0; q < NV / 4; ++q)
+      *reinterpret_cast<f32x4*>(out + 4 * q) =
+          f32x4{v[4 * q] * sc * bv[4 * q], v[4 * q + 1] * sc * bv[4 * q + 1], v[4 * q + 2] * sc * bv[4 * q + 2],
+                v[4 * q + 3] * sc * bv[4 * q + 3]};
+    return;
+  }
+  if (EPI != RF_EPI_NONE) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += bv[k];
+  }
+  if (c0 < e.scale_cols) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] *= e.col_scale;
+  }
+  if (EPI == RF_EPI_BIAS_GELU) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = CF32 ? gelu_erf(v[k]) : gelu_bf16out(v[k]);
+  }
+  if (EPI == RF_EPI_BIAS_RESID) {
+    if (RF32) {
+      const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)row * e.ldr + c0;
+#pragma unroll
+      for (int q = 0; q < NV / 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(r + 4 * q);
+        v[4 * q] += x.x; v[4 * q + 1] += x.y; v[4 * q + 2] += x.z; v[4 * q + 3] += x.w;
+      }
+    } else {
+      const bf16* r = reinterpret_cast<const bf16*>(e.R) + (int64_t)row * e.ldr + c0;
+#pragma unroll
+      for (int q = 0; q < NV / 4; ++q) {
+        const bf16x4 x = *reinterpret_cast<const bf16x4*>(r + 4 * q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 * q + k] += (float)x[k];
+      }
+    }
+  }
+  if (EPI == RF_EPI_BIAS_RESID_LN) {
+    const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)row * e.ldr + c0;
+    const float mu = e.lmean[row], rs = e.lrstd[row];
+#pragma unroll
+    for (int q = 0; q < NV / 4; ++q) {
+      const float4 x = *reinterpret_cast<const float4*>(r + 4 * q);
+      v[4 * q] += (x.x - mu) * rs * gm[4 * q] + bt[4 * q];
+      v[4 * q + 1] += (x.y - mu) * rs * gm[4 * q + 1] + bt[4 * q + 1];
+      v[4 * q + 2] += (x.z - mu) * rs * gm[4 * q + 2] + bt[4 * q + 2];
+      v[4 * q + 3] += (x.w - mu) * rs * gm[4 * q + 3] + bt[4 * q + 3];
+    }
+  }
+  if (CF32) {
+    float* out = reinterpret_cast<float*>(e.C) + (int64_t)row * e.ldc + c0;
+#pragma unroll
+    for (int q = 0; q < NV / 4; ++q)
+      *reinterpret_cast<f32x4*>(out + 4 * q) = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+  } else {
+    bf16* out = reinterpret_cast<bf16*>(e.C) + (int64_t)row * e.ldc + c0;
+    if (NV == 8) {
+      bf16x8 x;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = (bf16)v[k];
+      *reinterpret_cast<bf16x8*>(out) = x;
+    } else {
+      bf16x4 x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = (bf16)v[k];
+      *reinterpret_cast<bf16x4*>(out) = x;
+    }
+  }
+}
+
+// per-column epilogue vectors (bias or, for EPI_COS, the item inverse norms; LN gamma / beta)
+template <int EPI, int NV>
+__device__ __forceinline__ void load_cols(const EpiArgs& e, int c0, float* bv, float* gm, float* bt) {
+  const bool in = c0 + NV <= e.N;
+#pragma unroll
+  for (int q = 0; q < NV / 4; ++q) {
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f), g = b, t = b;
+    if (in) {
+      if (EPI == RF_EPI_COS) b = *reinterpret_cast<const float4*>(e.rw + c0 + 4 * q);
+      else if (EPI != RF_EPI_NONE) b = *reinterpret_cast<const float4*>(e.bias + c0 + 4 * q);
+      if (EPI == RF_EPI_BIAS_RESID_LN) {
+        g = *reinterpret_cast<const float4*>(e.lgamma + c0 + 4 * q);
+        t = *reinterpret_cast<const float4*>(e.lbeta + c0 + 4 * q);
+      }
+    }
+    bv[4 * q] = b.x; bv[4 * q + 1] = b.y; bv[4 * q + 2] = b.z; bv[4 * q + 3] = b.w;
+    gm[4 * q] = g.x; gm[4 * q + 1] = g.y; gm[4 * q + 2] = g.z; gm[4 * q + 3] = g.w;
+    bt[4 * q] = t.x; bt[4 * q + 1] = t.y; bt[4 * q + 2] = t.z; bt[4 * q + 3] = t.w;
+  }
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n from the small set the ping-pong kernel uses
@@ -498,16 +608,17 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
   else wait_vmcnt<0>();
 }
 
-// Persistent: one workgroup per CU walks tiles v = blockIdx.x, +gridDim.x, ... (the same
-// XCD-aware tile order as one-tile-per-block). The next tile's prologue DMAs are issued
-// BEFORE the current tile's epilogue, so (vmcnt retiring in issue order) the next tile can
-// start while the epilogue's S stores are still draining: the prologue wait and the first
-// P4 wait count them as allowed-outstanding (interior tiles only, where S is exact).
+// Persistent: one workgroup per CU walks tiles v = blockIdx.x, +gridDim.x, ... The next tile's
+// prologue DMAs are issued BEFORE the current tile's epilogue (most of them during its last
+// K-iteration), so (vmcnt retiring in issue order) the next tile can start while the
+// epilogue's S stores are still draining: the prologue wait and the first P4 wait count them
+// as allowed-outstanding (interior tiles only, where S is exact).
 template <int EPI, bool CF32, bool RF32>
 __global__ void __launch_bounds__(512, 1)
     k_gemm_pp(int K, const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw, EpiArgs e,
               int nTm, int nTn) {
-  constexpr int S = (CF32 || EPI == RF_EPI_COS) ? 32 : 16;  // epilogue stores per wave
+  constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;  // fp32 output layout
+  constexpr int S = OUT32 ? 32 : 16;                  // epilogue stores per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles = nTm * nTn;
   int v = blockIdx.x;
@@ -528,7 +639,8 @@ __global__ void __launch_bounds__(512, 1)
   };
   auto set_tile = [&](int vv) { tile_origin(vv, m0, n0); };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
+  // wave (wr, wc) owns output rows 64wr.. and columns 128wc..; group = wr >> 1 (waves 0-3 / 4-7)
+  const int grp = wave >> 2, wr = wave >> 1, wc = wave & 1;
 
   // DMA sources: this thread's two 8-row pieces of each half (rows 16*wave + 8p + lane/8),
   // chunk (lane&7) ^ (row&7) = (lane&7) ^ (lane>>3); rows clamped into the matrix. Offsets
@@ -537,7 +649,7 @@ __global__ void __launch_bounds__(512, 1)
   // recomputes the few address ops per DMA instead of hoisting 8+ live offsets out of the
   // tile loop (VGPRs belong to the MMA operands and accumulators).
   int xa = 16 * wave + (lane >> 3);               // A piece row (p = 0; p = 1 is +8)
-  int xw0 = wperm(xa), xw1 = wperm(xa + 8);        // permuted W piece rows
+  int xw0 = wperm<OUT32>(xa), xw1 = wperm<OUT32>(xa + 8);  // permuted W piece rows
   int pch = ((lane & 7) ^ (lane >> 3)) * 8;
   const int nk = K >> 6;
   auto launder = [&]() { asm volatile("" : "+v"(xa), "+v"(xw0), "+v"(xw1), "+v"(pch)); };
@@ -574,24 +686,25 @@ __global__ void __launch_bounds__(512, 1)
   const int lr = lane & 15;
   const int off0 = lr * 128 + (((lane >> 4) ^ (lane & 7)) << 4);
   const int off1 = lr * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
-  const int aBase = wr * PP_HALF;                                      // A-half of this group
-  const int bBase = (2 + (wc >> 1)) * PP_HALF + (wc & 1) * 64 * 128;  // W-half, 64-row band
+  const int aBase = grp * PP_HALF + (wr & 1) * 64 * 128;  // A-half of the group, 64-row band
+  const int bBase = (2 + wc) * PP_HALF;                    // the whole W-half
 
-  bf16x8 a[2][4][2], b[2][2][2];
-  f32x4 acc[8][4];
+  // quadrant (qm, qn) = 32 rows x 64 columns of the wave's 64 x 128 tile
+  bf16x8 a[2][2][2], b[2][4][2];
+  f32x4 acc[4][8];
 
   auto read_a = [&](int buf, int qm) {
-    const char* base = smem + buf * 4 * PP_HALF + aBase + qm * 64 * 128;
+    const char* base = smem + buf * 4 * PP_HALF + aBase + qm * 32 * 128;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 2; ++i) {
       a[qm][i][0] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + off0);
       a[qm][i][1] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + off1);
     }
   };
   auto read_b = [&](int buf, int qn) {
-    const char* base = smem + buf * 4 * PP_HALF + bBase + qn * 32 * 128;
+    const char* base = smem + buf * 4 * PP_HALF + bBase + qn * 64 * 128;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < 4; ++j) {
       b[qn][j][0] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + off0);
       b[qn][j][1] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + off1);
     }
@@ -600,11 +713,11 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[qm * 4 + i][qn * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[qn][j][ks], a[qm][i][ks], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+          acc[qm * 2 + i][qn * 4 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[qm][i][ks], b[qn][j][ks], acc[qm * 2 + i][qn * 4 + j], 0, 0, 0);
   };
   auto bar = [&]() {
     __builtin_amdgcn_s_barrier();
@@ -638,13 +751,13 @@ __global__ void __launch_bounds__(512, 1)
   int relax = 0;  // S stores of the previous (interior) tile may still be outstanding
   for (;;) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     wait_vm_rt<S>((nk > 1 ? 8 : 0) + relax);  // K-tile 0 landed
     bar();
     stamp(0);
-    if (wr == 1) bar();  // group 1 runs one barrier behind
+    if (grp == 1) bar();  // group 1 runs one barrier behind
     const bool has_next = v + (int)gridDim.x < tiles;
     pf = has_next && !(nk & 1);
     if (has_next) tile_origin(v + gridDim.x, nm0, nn0);
@@ -677,16 +790,24 @@ __global__ void __launch_bounds__(512, 1)
       if (t == 0) stamp(2);
       compute(1, 0, odd_live);
     }
-    if (wr == 0) bar();  // equalise the barrier count of the two groups: every LDS read is done
+    if (grp == 0) bar();  // equalise the barrier count of the two groups: every LDS read is done
     stamp(3);
 
     const int em0 = m0, en0 = n0;
     const bool interior = (em0 + 256 <= e.M) && (en0 + 256 <= e.N);
     int el = lane;
     asm volatile("" : "+v"(el));
-    const int erow = em0 + wr * 128 + (el & 15), ecol = en0 + wc * 64 + 16 * (el >> 4);
-    float bv[16];
-    load_bias16<EPI>(e, ecol, bv);  // issued before the next tile's DMAs: its wait skips them
+    // lane (c = l&15, g = l>>4) holds rows 4g + r of each 16-row block mf and the columns
+    // [8c, 8c+8) (bf16) or [4c, 4c+4) u [64+4c, 64+4c+4) (fp32) of the wave's 128 (wperm)
+    const int erow = em0 + wr * 64 + 4 * (el >> 4);
+    const int ecol = en0 + wc * 128 + (OUT32 ? 4 : 8) * (el & 15);
+    float bv[8], gm[8], bt[8];  // column vectors, loaded before the next tile's DMAs
+    if (OUT32) {
+      load_cols<EPI, 4>(e, ecol, bv, gm, bt);
+      load_cols<EPI, 4>(e, ecol + 64, bv + 4, gm + 4, bt + 4);
+    } else {
+      load_cols<EPI, 8>(e, ecol, bv, gm, bt);
+    }
     v += gridDim.x;
     if (has_next) {
       set_tile(v);
@@ -696,18 +817,22 @@ __global__ void __launch_bounds__(512, 1)
     }
     asm volatile("" ::: "memory");
     stamp(4);
-    // Epilogue straight from the accumulators: with W as the MFMA's first operand and the W
-    // rows permuted (wperm), lane l holds 16 consecutive columns 16(l>>4).. of row l&15 of
-    // every 16-row block — whole 16-B vectors, no LDS.
+    // Epilogue straight from the accumulators: whole-line vector stores, no LDS
 #pragma unroll
-    for (int mf = 0; mf < 8; ++mf) {
-      float vv[16];
+    for (int mf = 0; mf < 4; ++mf)
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
+      for (int r = 0; r < 4; ++r) {
+        float vv[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) vv[4 * f + r] = acc[mf][f][r];
-      epi_row16<EPI, CF32, RF32>(e, erow + mf * 16, ecol, vv, bv);
-    }
+        for (int f = 0; f < 8; ++f) vv[f] = acc[mf][f][r];
+        const int row = erow + mf * 16 + r;
+        if (OUT32) {
+          epi_seg<EPI, CF32, RF32, 4>(e, row, ecol, vv, bv, gm, bt);
+          epi_seg<EPI, CF32, RF32, 4>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4);
+        } else {
+          epi_seg<EPI, CF32, RF32, 8>(e, row, ecol, vv, bv, gm, bt);
+        }
+      }
     asm volatile("" ::: "memory");
     stamp(5);
     ++tix;

@@ -324,6 +324,59 @@ __global__ void __launch_bounds__(256) k_cos_cand(int B, int C, int D, const T* 
     }                                                                   \
   } while (0)
 
+// Cross entropy of one logits row against an integer label (torch CrossEntropyLoss with
+// ignore_index, the losses of models.py:494-510 and :589-597): loss = logsumexp(x) - x[label],
+// 0 for ignored rows; also the row's argmax (first max, as torch.argmax) for cl_correct_num.
+// One block per row: streaming max/sum-exp in registers, online rescale, 16-B loads.
+template <typename T>
+__global__ void __launch_bounds__(256) k_cross_entropy(int N, const T* __restrict__ x, int64_t ldx,
+                                                        const int64_t* __restrict__ labels, int64_t ignore,
+                                                        float* __restrict__ loss, int32_t* __restrict__ amax) {
+  __shared__ float sm[8], ss[8];
+  __shared__ int si[8];
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const T* xr = x + (int64_t)row * ldx;
+  float m = -__builtin_inff(), l = 0.f;
+  int im = 0x7fffffff;
+  for (int c = t; c < N; c += 256) {
+    const float v = to_f32(xr[c]);
+    if (v > m) {
+      l = l * __expf(m - v) + 1.f;
+      m = v;
+      im = c;
+    } else {
+      l += __expf(v - m);
+    }
+  }
+  // wave merge (max, argmax first index, rescaled sum)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(l, o, 64);
+    const int i2 = __shfl_xor(im, o, 64);
+    const float mn = fmaxf(m, m2);
+    l = (m == -__builtin_inff() ? 0.f : l * __expf(m - mn)) + (m2 == -__builtin_inff() ? 0.f : l2 * __expf(m2 - mn));
+    im = (m2 > m || (m2 == m && i2 < im)) ? i2 : im;
+    m = mn;
+  }
+  if (lane == 0) { sm[wave] = m; ss[wave] = l; si[wave] = im; }
+  __syncthreads();
+  if (t == 0) {
+    float M = sm[0], Lq = ss[0];
+    int I = si[0];
+    for (int w = 1; w < 4; ++w) {
+      const float mn = fmaxf(M, sm[w]);
+      Lq = (M == -__builtin_inff() ? 0.f : Lq * __expf(M - mn)) + (sm[w] == -__builtin_inff() ? 0.f : ss[w] * __expf(sm[w] - mn));
+      I = (sm[w] > M || (sm[w] == M && si[w] < I)) ? si[w] : I;
+      M = mn;
+    }
+    const int64_t lab = labels[row];
+    float out = 0.f;
+    if (lab != ignore) out = (M + __logf(Lq)) - to_f32(xr[lab]);
+    loss[row] = out;
+    if (amax) amax[row] = I;
+  }
+}
+
 template <typename TT, typename T>
 static int launch_embed(int M, int D, const int32_t* ids, const int32_t* pos, const int32_t* tt,
                         const int32_t* ip, const void* we, const void* pe, const void* te,
@@ -461,6 +514,21 @@ int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, co
   else
     RF_REQUIRE(false, "rf_cos_score_cand: bad dtype %d", dtype);
   RF_LAUNCH_CHECK("rf_cos_score_cand");
+}
+
+int rf_cross_entropy_fwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,
+                         int64_t ignore_index, float* loss, int32_t* argmax, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && N > 0 && ldx >= N, "rf_cross_entropy_fwd: bad shape");
+  RF_REQUIRE(logits && labels && loss, "rf_cross_entropy_fwd: null pointer");
+  if (M == 0) return RF_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16)
+    k_cross_entropy<bf16><<<M, 256, 0, s>>>(N, (const bf16*)logits, ldx, labels, ignore_index, loss, argmax);
+  else if (dtype == RF_F32)
+    k_cross_entropy<float><<<M, 256, 0, s>>>(N, (const float*)logits, ldx, labels, ignore_index, loss, argmax);
+  else
+    RF_REQUIRE(false, "rf_cross_entropy_fwd: bad dtype %d", dtype);
+  RF_LAUNCH_CHECK("rf_cross_entropy_fwd");
 }
 
 }  // extern "C"

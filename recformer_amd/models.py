@@ -489,22 +489,25 @@ class RecformerForSeqRec(nn.Module):
         pooler_output = outputs.pooler_output
         if labels is None:
             return self.similarity_score(pooler_output, candidates)
-        loss_fct = nn.CrossEntropyLoss()
         if self.config.finetune_negative_sample_size <= 0:
             logits = self.similarity_score(pooler_output)
-            return loss_fct(logits, labels)
+            return ops.cross_entropy(logits, labels)  # CrossEntropyLoss, models.py:589-591
         # sampled softmax: candidates from the CPU global RNG as models.py:594
         candidates = torch.cat((labels.unsqueeze(-1), torch.randint(
             0, self.config.item_num, size=(batch_size, self.config.finetune_negative_sample_size)
         ).to(labels.device)), dim=-1)
         logits = self.similarity_score(pooler_output, candidates)
         target = torch.zeros_like(labels, device=labels.device)
-        return loss_fct(logits, target)
+        return ops.cross_entropy(logits, target)  # models.py:595-597
 
 
 class RecformerForPretraining(nn.Module):
-    """models.py:372-520 — parameter layout (longformer + lm_head) for checkpoint
-    compatibility. Its training step arrives with the backward kernels."""
+    """models.py:370-520: two-view contrastive loss (cos(z_a, z_b) / temp, CrossEntropy against
+    arange, cl_correct_num) plus mlm_weight x the masked-LM losses of LongformerLMHead
+    (TF:1265-1285: dense -> exact GELU -> LayerNorm -> decoder) on the MLM-input encodings.
+    Every encoder pass, the head's GEMMs / LayerNorm and both cross entropies run on the HIP
+    kernels. The distributed all_gather of z (models.py:474-490) applies in training only;
+    training needs the backward path, which is not built yet."""
 
     def __init__(self, config: RecformerConfig):
         super().__init__()
@@ -512,10 +515,69 @@ class RecformerForPretraining(nn.Module):
         self.longformer = RecformerModel(config)
         self.lm_head = _LMHead(config)
         self.sim = Similarity(config)
+        self._head_key = None
+        self._head = None
 
-    def forward(self, *args: Any, **kwargs: Any):
-        raise NotImplementedError("recformer_amd: RecformerForPretraining.forward needs the backward "
-                                  "kernels (SURVEY.md §8a A10); not built yet")
+    def _head_weights(self, dt: torch.dtype):
+        m = self.lm_head
+        key = (dt,) + tuple((p.data_ptr(), p._version) for p in m.parameters())
+        if key != self._head_key:
+            with torch.no_grad():
+                self._head = {
+                    "w_d": m.dense.weight.to(dt).contiguous(), "b_d": m.dense.bias.float().contiguous(),
+                    "ln_w": m.layer_norm.weight.float().contiguous(), "ln_b": m.layer_norm.bias.float().contiguous(),
+                    "w_dec": m.decoder.weight.to(dt).contiguous(), "b_dec": m.decoder.bias.float().contiguous(),
+                }
+            self._head_key = key
+        return self._head
+
+    def lm_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """LongformerLMHead.forward (TF:1277-1285) -> (B*L, vocab) logits in the compute dtype."""
+        dt = _compute_dtype(self.longformer.dtype)
+        w = self._head_weights(dt)
+        x = hidden.reshape(-1, hidden.shape[-1]).to(dt).contiguous()
+        t = ops.gemm(x, w["w_d"], w["b_d"], ops.RF_EPI_BIAS_GELU)
+        t = ops.layernorm(t, w["ln_w"], w["ln_b"], self.config.layer_norm_eps)
+        return ops.gemm(t, w["w_dec"], w["b_dec"], ops.RF_EPI_BIAS)
+
+    def forward(self, input_ids_a=None, attention_mask_a=None, global_attention_mask_a=None,
+                token_type_ids_a=None, item_position_ids_a=None, mlm_input_ids_a=None, mlm_labels_a=None,
+                input_ids_b=None, attention_mask_b=None, global_attention_mask_b=None, token_type_ids_b=None,
+                item_position_ids_b=None, mlm_input_ids_b=None, mlm_labels_b=None, head_mask=None,
+                position_ids=None, inputs_embeds=None, labels=None, output_attentions=None,
+                output_hidden_states=None, return_dict=None):
+        batch_size = input_ids_a.size(0)
+
+        def enc(ids, am, gm, tt, ip):
+            return self.longformer(ids, attention_mask=am, global_attention_mask=gm, head_mask=head_mask,
+                                   token_type_ids=tt, position_ids=position_ids, item_position_ids=ip,
+                                   inputs_embeds=inputs_embeds, output_attentions=output_attentions,
+                                   output_hidden_states=output_hidden_states, return_dict=True)
+
+        outputs_a = enc(input_ids_a, attention_mask_a, global_attention_mask_a, token_type_ids_a, item_position_ids_a)
+        outputs_b = enc(input_ids_b, attention_mask_b, global_attention_mask_b, token_type_ids_b, item_position_ids_b)
+        mlm_outputs_a = (enc(mlm_input_ids_a, attention_mask_a, global_attention_mask_a, token_type_ids_a,
+                             item_position_ids_a) if mlm_input_ids_a is not None else None)
+        mlm_outputs_b = (enc(mlm_input_ids_b, attention_mask_b, global_attention_mask_b, token_type_ids_b,
+                             item_position_ids_b) if mlm_input_ids_b is not None else None)
+
+        z1, z2 = outputs_a.pooler_output, outputs_b.pooler_output
+        if torch.distributed.is_available() and torch.distributed.is_initialized() and self.training:
+            raise NotImplementedError("recformer_amd: distributed pretraining needs the backward path")
+        dt = _compute_dtype(self.longformer.dtype)
+        z1c, z2c = z1.to(dt).contiguous(), z2.to(dt).contiguous()
+        cos_sim = ops.cos_scores(z1c, z2c, 1.0 / self.config.temp)  # Similarity(z1[:,None], z2[None])
+        cl_labels = torch.arange(cos_sim.size(0), device=cos_sim.device)
+        loss, amax = ops.cross_entropy(cos_sim, cl_labels, want_argmax=True)
+        correct_num = (amax == cl_labels).sum()
+        for mo, ml in ((mlm_outputs_a, mlm_labels_a), (mlm_outputs_b, mlm_labels_b)):
+            if mo is not None and ml is not None:
+                scores = self.lm_logits(mo.last_hidden_state)
+                loss = loss + self.config.mlm_weight * ops.cross_entropy(scores, ml.reshape(-1))
+        return RecformerPretrainingOutput(loss=loss, logits=cos_sim, cl_correct_num=correct_num,
+                                          cl_total_num=batch_size, hidden_states=outputs_a.hidden_states,
+                                          attentions=outputs_a.attentions,
+                                          global_attentions=outputs_a.global_attentions)
 
 
 class _LMHead(nn.Module):

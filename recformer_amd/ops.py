@@ -18,6 +18,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF
 __all__ = [
     "dtype_code", "prepare_inputs", "embed_ln", "gemm", "layernorm", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
+    "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
 ]
 
@@ -157,7 +158,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
     if out is not None and out.dtype != odt:
         raise TypeError(f"gemm: out must be {odt}")
     if out is None:
-        out = torch.empty(M, N, dtype=odt, device=a.device)
+        # 16-B aligned rows for the vector epilogue: pad the leading dim, return the (M, N) view
+        n8 = (N + 7) // 8 * 8
+        out = torch.empty(M, n8, dtype=odt, device=a.device)[:, :N]
     ldc = _rowmajor(out, "out")
     ldr = 0
     if resid is not None:
@@ -339,3 +342,30 @@ def cos_scores_cand(z: torch.Tensor, items: torch.Tensor, cand: torch.Tensor, in
                                 _p(items), _rowmajor(items, "items"), _p(items_rnorm), _p(cand),
                                 float(inv_temp), _p(out), _stream(out)), "rf_cos_score_cand")
     return out
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100,
+                  reduction: str = "mean", want_argmax: bool = False):
+    """torch.nn.functional.cross_entropy over rows of a (M, N) fp32/bf16 logits view, in fp32 on
+    the HIP kernel (rf_cross_entropy_fwd); mean over the non-ignored rows (nan if none, as torch).
+    want_argmax also returns the int64 row argmax (models.py:497)."""
+    lib = _lib.load()
+    _dev(logits, labels)
+    M, N = logits.shape
+    labels = labels.reshape(-1).to(torch.int64).contiguous()
+    if labels.numel() != M:
+        raise ValueError(f"cross_entropy: {labels.numel()} labels for {M} rows")
+    rows = torch.empty(M, dtype=torch.float32, device=logits.device)
+    amax = torch.empty(M, dtype=torch.int32, device=logits.device) if want_argmax else None
+    check(lib.rf_cross_entropy_fwd(dtype_code(logits.dtype), M, N, _p(logits), _rowmajor(logits, "logits"),
+                                   _p(labels), int(ignore_index), _p(rows), _p(amax), _stream(rows)),
+          "rf_cross_entropy_fwd")
+    if reduction == "none":
+        loss = rows
+    elif reduction == "sum":
+        loss = rows.sum()
+    else:
+        loss = rows.sum() / (labels != ignore_index).sum().to(torch.float32)
+    if want_argmax:
+        return loss, amax.to(torch.int64)
+    return loss

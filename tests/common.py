@@ -45,3 +45,17 @@ def errs(a, b):
     d = (a - b)
     return dict(max=float(d.abs().max()), mean=float(d.abs().mean()),
                 rel=float(d.norm() / max(b.norm(), 1e-30)))
+
+
+def hashed_pretrain(kw=C1, seed_lf=1, seed_head=6):
+    """RecformerForPretraining with the golden fixture's weights (oracle/gen_golden.py)."""
+    from recformer_amd import RecformerForPretraining
+    m = RecformerForPretraining(RecformerConfig(**kw)).eval()
+    hash_init_(m.longformer, seed=seed_lf)
+    hash_init_(m.lm_head, seed=seed_head)
+    return m
+
+
+def pretrain_inputs(g):
+    keys = [k for k in g if k.endswith("_a") or k.endswith("_b")]
+    return {k: g[k] for k in keys}

@@ -245,3 +245,25 @@ def test_global_attention_fold(dev, dt, case):
                 continue
             err = (got[b, p] - og[b, :, g]).abs().max().item()
             assert err <= (1e-4 if dt == torch.float32 else 2e-2), (b, g, err)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N", [4, 1000, 50265])
+def test_cross_entropy(dev, dt, N):
+    """rf_cross_entropy_fwd vs torch cross_entropy (mean over non-ignored, ignore -100) + argmax."""
+    torch.manual_seed(N)
+    M = 37
+    x = (torch.randn(M, N, device=dev) * 3).to(dt)
+    lab = torch.randint(0, N, (M,), device=dev)
+    lab[::5] = -100
+    loss, am = ops.cross_entropy(x, lab, want_argmax=True)
+    ref = F.cross_entropy(x.float(), lab, ignore_index=-100)
+    assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+    assert torch.equal(am, x.float().argmax(1))
+    rows = ops.cross_entropy(x, lab, reduction="none")
+    refr = F.cross_entropy(x.float(), lab, ignore_index=-100, reduction="none")
+    assert (rows - refr).abs().max().item() <= 1e-4
+    # strided (padded leading dim) logits view
+    xp = torch.zeros(M, N + 5, device=dev, dtype=dt)
+    xp[:, :N] = x
+    assert abs(float(ops.cross_entropy(xp[:, :N], lab)) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))

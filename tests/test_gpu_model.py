@@ -129,3 +129,26 @@ def test_return_tuple_and_hidden_states(dev):
     assert len(t) == 3 and len(t[2]) == C1["num_hidden_layers"] + 1
     assert errs(t[0], g["last_hidden_state"])["max"] <= 1e-3
     assert torch.equal(t[2][-1], t[0])
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast"])
+def test_pretrain_golden(dev, mode):
+    """A10: RecformerForPretraining.forward (two views + MLM on both) vs the reference run."""
+    from tests.common import hashed_pretrain, pretrain_inputs
+    g = load_golden("c1_pretrain")
+    model, ctx = _prep(hashed_pretrain(), dev, mode)
+    kw = {k: v.to(dev) for k, v in pretrain_inputs(g).items()}
+    with torch.no_grad(), ctx:
+        out = model(**kw)
+        out0 = model(**{k: v for k, v in kw.items() if not k.startswith("mlm_")})
+    loss, loss0 = float(out.loss), float(out0.loss)
+    if mode == "fp32":
+        assert abs(loss - float(g["loss"])) <= 1e-4, (loss, float(g["loss"]))
+        assert abs(loss0 - float(g["loss_contrastive"])) <= 1e-4
+        assert errs(out.logits, g["logits"])["max"] <= 1e-3
+    else:
+        assert abs(loss - float(g["loss"])) <= 1e-2 * max(1.0, abs(float(g["loss"])))
+        assert abs(loss0 - float(g["loss_contrastive"])) <= 1e-2 * max(1.0, abs(float(g["loss_contrastive"])))
+        assert errs(out.logits, g["logits"])["max"] <= 0.2  # cos / 0.05: 1e-2 in cosine
+    assert int(out.cl_correct_num) == int(g["cl_correct_num"])
+    assert out.cl_total_num == 4

@@ -43,3 +43,25 @@ def test_12l_768_scores_and_losses():
     sc = R.cosine_scores(p, items[g["candidates"]], 0.05)
     assert errs(sc, g["scores_cand"])["max"] <= 1e-3
     assert abs(float(R.seqrec_loss(sc, torch.zeros(2, dtype=torch.long))) - float(g["loss_sampled"])) <= 1e-4
+
+
+def test_pretrain_two_views_mlm():
+    """A10: RecformerForPretraining loss / cos logits / correct count vs the reference run."""
+    from tests.common import hashed_pretrain
+    g = load_golden("c1_pretrain")
+    m = hashed_pretrain()
+    assert checksums(m) == pytest.approx(manifest()["c1_pretrain"]["checksums"], rel=0, abs=1e-9)
+    cfg = m.config
+    sd_lf = m.longformer.state_dict()
+    sd_head = m.lm_head.state_dict()
+    va = {k[:-2]: g[k] for k in ("input_ids_a", "attention_mask_a", "global_attention_mask_a",
+                                 "token_type_ids_a", "item_position_ids_a")}
+    vb = {k[:-2]: g[k] for k in ("input_ids_b", "attention_mask_b", "global_attention_mask_b",
+                                 "token_type_ids_b", "item_position_ids_b")}
+    loss, cos, correct = R.pretrain_forward(sd_lf, sd_head, cfg, va, vb, g["mlm_input_ids_a"], g["mlm_labels_a"],
+                                            g["mlm_input_ids_b"], g["mlm_labels_b"])
+    assert abs(float(loss) - float(g["loss"])) <= 1e-5
+    assert errs(cos, g["logits"])["max"] <= 1e-4
+    assert int(correct) == int(g["cl_correct_num"])
+    loss0, _, _ = R.pretrain_forward(sd_lf, sd_head, cfg, va, vb)
+    assert abs(float(loss0) - float(g["loss_contrastive"])) <= 1e-5

@@ -20,6 +20,16 @@ __global__ void __launch_bounds__(512) k_store(__bf16* C, int M, int N, int nTn,
         __bf16* p = C + (size_t)(r0 + mf * 16 + (lane & 15)) * N + c0 + 16 * (lane >> 4);
         *reinterpret_cast<bf16x8*>(p) = val;
         *reinterpret_cast<bf16x8*>(p + 8) = val;
+      } else if (P == 2) {
+        // MFMA-native non-swapped layout with a 4-column W permutation: lane (c = l&15, g = l>>4)
+        // holds 4 consecutive columns 4c.. of rows 4g + r: one 8-B store per r, 4 full rows
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 v4;
+        for (int k = 0; k < 4; ++k) v4[k] = val[k];
+        for (int r = 0; r < 4; ++r) {
+          __bf16* p = C + (size_t)(r0 + mf * 16 + 4 * (lane >> 4) + r) * N + c0 + 4 * (lane & 15);
+          *reinterpret_cast<bf16x4*>(p) = v4;
+        }
       } else {
         for (int h = 0; h < 2; ++h) {
           __bf16* p = C + (size_t)(r0 + mf * 16 + 8 * h + (lane >> 3)) * N + c0 + 8 * (lane & 7);
@@ -36,16 +46,18 @@ int main() {
   hipMalloc(&C, (size_t)M * N * 2);
   hipEvent_t a, b;
   hipEventCreate(&a); hipEventCreate(&b);
-  for (int P = 0; P < 2; ++P) {
-    for (int grid : {256, 512, 1024}) {
+  for (int P = 0; P < 3; ++P) {
+    for (int grid : {32, 64, 128, 256}) {
       for (int it = 0; it < 3; ++it) {
         if (P == 0) k_store<0><<<grid, 512>>>(C, M, N, nTn, tiles);
-        else k_store<1><<<grid, 512>>>(C, M, N, nTn, tiles);
+        else if (P == 1) k_store<1><<<grid, 512>>>(C, M, N, nTn, tiles);
+        else k_store<2><<<grid, 512>>>(C, M, N, nTn, tiles);
       }
       hipEventRecord(a);
       for (int it = 0; it < 10; ++it) {
         if (P == 0) k_store<0><<<grid, 512>>>(C, M, N, nTn, tiles);
-        else k_store<1><<<grid, 512>>>(C, M, N, nTn, tiles);
+        else if (P == 1) k_store<1><<<grid, 512>>>(C, M, N, nTn, tiles);
+        else k_store<2><<<grid, 512>>>(C, M, N, nTn, tiles);
       }
       hipEventRecord(b);
       hipEventSynchronize(b);

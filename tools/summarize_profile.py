@@ -28,8 +28,9 @@ def tagger():
 
     def tag(name, grid):
         m = re.search(r"k_gemm_bf16<(\d+), (\d+), \d+, \d+, \d+, \d+, (\d+),", name)
-        if m:
-            bm, epi = int(m.group(1)), int(m.group(3))
+        mp = re.search(r"k_gemm_pp<(\d+),", name)
+        if m or mp:
+            bm, epi = (int(m.group(1)), int(m.group(3))) if m else (256, int(mp.group(1)))
             if epi == 5:
                 t = "gemm_ffn2" if last[0] == "gemm_ffn1" else "gemm_out"
             elif epi == 1 and bm == 128:
