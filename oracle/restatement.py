@@ -182,7 +182,6 @@ def layer_forward(sd, p: str, h, merged, H: int, half_w: int, eps: float):
     return y
 
 
-@torch.no_grad()
 def model_forward(sd: Dict[str, Tensor], cfg, input_ids, attention_mask=None, global_attention_mask=None,
                   token_type_ids=None, item_position_ids=None, prefix: str = "",
                   return_all_layers: bool = False):

@@ -74,3 +74,38 @@ def gather_rows(local: torch.Tensor, total: int) -> torch.Tensor:
         ra, rb = shard_range(total, r, ws)
         out.append(parts[r][: rb - ra])
     return torch.cat(out, 0)
+
+
+def allreduce_grads(params, bucket_bytes: int = 64 << 20, average: bool = True) -> int:
+    """Bucketed all-reduce of the parameter gradients over the default group (RCCL over xGMI
+    with the nccl backend; gloo on CPU) — the data-parallel exchange of a training step
+    (SURVEY.md §8e). Gradients are flattened per dtype into buckets of <= bucket_bytes, reduced
+    with one collective each, and copied back; returns the number of collectives issued.
+    (torch DistributedDataParallel over these modules does the same, overlapped with backward.)"""
+    rank, ws = world()
+    if ws == 1:
+        return 0
+    grads = [p.grad for p in params if p.grad is not None]
+    n = 0
+    by_dtype = {}
+    for g in grads:
+        by_dtype.setdefault((g.dtype, g.device), []).append(g)
+    for (_, _), gs in by_dtype.items():
+        bucket, size = [], 0
+        for g in gs + [None]:
+            if g is not None and (not bucket or size + g.numel() * g.element_size() <= bucket_bytes):
+                bucket.append(g)
+                size += g.numel() * g.element_size()
+                continue
+            if bucket:
+                flat = torch.cat([b.reshape(-1) for b in bucket])
+                dist.all_reduce(flat)
+                if average:
+                    flat /= ws
+                off = 0
+                for b in bucket:
+                    b.copy_(flat[off:off + b.numel()].view_as(b))
+                    off += b.numel()
+                n += 1
+            bucket, size = ([g], g.numel() * g.element_size()) if g is not None else ([], 0)
+    return n

@@ -18,6 +18,7 @@ from typing import Any, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import ops
 from .config import RecformerConfig
@@ -197,6 +198,21 @@ def _init_weights(module: nn.Module, std: float) -> None:
 
 
 # ----------------------------------------------------------------------------------
+def _needs_grad(module: nn.Module) -> bool:
+    """Autograd path when gradients are enabled and some parameter requires them."""
+    return torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters())
+
+
+def _cos_train(z: torch.Tensor, items: torch.Tensor, temp: float) -> torch.Tensor:
+    """Differentiable Similarity (models.py:358-369): cos(z_b, items_n) / temp in fp32 (autocast
+    computes cosine_similarity in fp32), as normalise + matmul instead of the (B,N,d) broadcast."""
+    zn = z.float() / z.float().norm(dim=-1, keepdim=True).clamp_min(1e-8)
+    it = items.float()
+    itn = it / it.norm(dim=-1, keepdim=True).clamp_min(1e-8)
+    with torch.autocast("cuda", enabled=False):
+        return (zn @ itn.t()) / temp
+
+
 def _compute_dtype(param_dtype: torch.dtype) -> torch.dtype:
     if torch.is_autocast_enabled("cuda"):
         return torch.bfloat16
@@ -327,12 +343,16 @@ class RecformerModel(nn.Module):
             raise NotImplementedError("recformer_amd: head_mask is not supported (callers pass None)")
         if output_attentions:
             raise NotImplementedError("recformer_amd: output_attentions is not supported on the HIP path")
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("recformer_amd: training forward/backward is not built yet")
-
-        last, hidden_all = self._encode(input_ids, attention_mask, global_attention_mask,
-                                        token_type_ids, position_ids, item_position_ids,
-                                        output_hidden_states)
+        if _needs_grad(self):
+            # autograd path (recformer_amd/train.py): same kernels, explicit backward
+            from .train import encode_train
+            last, hidden_all = encode_train(self, input_ids, attention_mask, global_attention_mask,
+                                            token_type_ids, position_ids, item_position_ids,
+                                            output_hidden_states)
+        else:
+            last, hidden_all = self._encode(input_ids, attention_mask, global_attention_mask,
+                                            token_type_ids, position_ids, item_position_ids,
+                                            output_hidden_states)
         pooled = self.pooler(attention_mask, last)
         if not return_dict:
             out = (last, pooled)
@@ -487,6 +507,24 @@ class RecformerForSeqRec(nn.Module):
                                   output_attentions=output_attentions,
                                   output_hidden_states=output_hidden_states, return_dict=True)
         pooler_output = outputs.pooler_output
+        if _needs_grad(self):
+            # training head: differentiable cosine scores + CrossEntropy (models.py:583-599);
+            # the item table is frozen (from_pretrained(freeze=True), models.py:536)
+            table = self.item_embedding.weight
+            if labels is None:
+                items = table if candidates is None else table[candidates]
+                return (_cos_train(pooler_output, items, self.config.temp) if candidates is None else
+                        torch.einsum("bd,bcd->bc", F.normalize(pooler_output.float(), dim=-1, eps=1e-8),
+                                     F.normalize(items.float(), dim=-1, eps=1e-8)) / self.config.temp)
+            if self.config.finetune_negative_sample_size <= 0:
+                return F.cross_entropy(_cos_train(pooler_output, table, self.config.temp), labels)
+            candidates = torch.cat((labels.unsqueeze(-1), torch.randint(
+                0, self.config.item_num, size=(batch_size, self.config.finetune_negative_sample_size)
+            ).to(labels.device)), dim=-1)
+            items = table[candidates].float()
+            zn = F.normalize(pooler_output.float(), dim=-1, eps=1e-8)
+            logits = torch.einsum("bd,bcd->bc", zn, F.normalize(items, dim=-1, eps=1e-8)) / self.config.temp
+            return F.cross_entropy(logits, torch.zeros_like(labels))
         if labels is None:
             return self.similarity_score(pooler_output, candidates)
         if self.config.finetune_negative_sample_size <= 0:
@@ -505,9 +543,10 @@ class RecformerForPretraining(nn.Module):
     """models.py:370-520: two-view contrastive loss (cos(z_a, z_b) / temp, CrossEntropy against
     arange, cl_correct_num) plus mlm_weight x the masked-LM losses of LongformerLMHead
     (TF:1265-1285: dense -> exact GELU -> LayerNorm -> decoder) on the MLM-input encodings.
-    Every encoder pass, the head's GEMMs / LayerNorm and both cross entropies run on the HIP
-    kernels. The distributed all_gather of z (models.py:474-490) applies in training only;
-    training needs the backward path, which is not built yet."""
+    Inference: every encoder pass, the head's GEMMs / LayerNorm and both cross entropies run on
+    the HIP kernels. Training (gradients enabled): the encoder runs through recformer_amd/train.py
+    and the heads are differentiable torch ops; under torch.distributed the z vectors are
+    all-gathered across ranks with the local slot keeping its graph (models.py:474-490)."""
 
     def __init__(self, config: RecformerConfig):
         super().__init__()
@@ -562,8 +601,9 @@ class RecformerForPretraining(nn.Module):
                              item_position_ids_b) if mlm_input_ids_b is not None else None)
 
         z1, z2 = outputs_a.pooler_output, outputs_b.pooler_output
-        if torch.distributed.is_available() and torch.distributed.is_initialized() and self.training:
-            raise NotImplementedError("recformer_amd: distributed pretraining needs the backward path")
+        if _needs_grad(self):
+            return self._train_losses(z1, z2, outputs_a, mlm_outputs_a, mlm_labels_a, mlm_outputs_b,
+                                      mlm_labels_b, batch_size)
         dt = _compute_dtype(self.longformer.dtype)
         z1c, z2c = z1.to(dt).contiguous(), z2.to(dt).contiguous()
         cos_sim = ops.cos_scores(z1c, z2c, 1.0 / self.config.temp)  # Similarity(z1[:,None], z2[None])
@@ -578,6 +618,41 @@ class RecformerForPretraining(nn.Module):
                                           cl_total_num=batch_size, hidden_states=outputs_a.hidden_states,
                                           attentions=outputs_a.attentions,
                                           global_attentions=outputs_a.global_attentions)
+
+
+def _pretrain_train_losses(self, z1, z2, outputs_a, mlm_a, lab_a, mlm_b, lab_b, batch_size):
+    """Differentiable losses of models.py:472-510 (training): all_gather of z across ranks (the
+    local slot keeps its graph, models.py:474-490), contrastive CE, LM head + masked-LM CE."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and self.training:
+        ws, rk = dist.get_world_size(), dist.get_rank()
+        z1_list = [torch.zeros_like(z1) for _ in range(ws)]
+        z2_list = [torch.zeros_like(z2) for _ in range(ws)]
+        dist.all_gather(z1_list, z1.contiguous())
+        dist.all_gather(z2_list, z2.contiguous())
+        z1_list[rk] = z1
+        z2_list[rk] = z2
+        z1 = torch.cat(z1_list, 0)
+        z2 = torch.cat(z2_list, 0)
+    cos_sim = _cos_train(z1, z2, self.config.temp)
+    labels = torch.arange(cos_sim.size(0), device=cos_sim.device)
+    loss = F.cross_entropy(cos_sim, labels)
+    correct_num = (torch.argmax(cos_sim, 1) == labels).sum()
+    head = self.lm_head
+    for mo, ml in ((mlm_a, lab_a), (mlm_b, lab_b)):
+        if mo is not None and ml is not None:
+            x = F.gelu(F.linear(mo.last_hidden_state, head.dense.weight, head.dense.bias))
+            x = F.layer_norm(x, (x.shape[-1],), head.layer_norm.weight, head.layer_norm.bias,
+                             self.config.layer_norm_eps)
+            scores = F.linear(x, head.decoder.weight, head.bias)
+            loss = loss + self.config.mlm_weight * F.cross_entropy(scores.reshape(-1, self.config.vocab_size),
+                                                                   ml.reshape(-1))
+    return RecformerPretrainingOutput(loss=loss, logits=cos_sim, cl_correct_num=correct_num,
+                                      cl_total_num=batch_size, hidden_states=outputs_a.hidden_states,
+                                      attentions=outputs_a.attentions, global_attentions=outputs_a.global_attentions)
+
+
+RecformerForPretraining._train_losses = _pretrain_train_losses
 
 
 class _LMHead(nn.Module):

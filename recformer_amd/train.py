@@ -1,0 +1,282 @@
+"""Training path (autograd) for the Recformer encoder (SURVEY.md §8a A9/A10 with gradients).
+
+Forward runs the same HIP kernels as inference; each is wrapped in a torch.autograd.Function
+whose backward is written out explicitly:
+
+  _Gemm        C = A.W^T + b (optional q-scale on the first columns)      TF:504-514, 1064-1130
+               backward: dA = dC.W, dW = dC^T.A (hipBLASLt through torch.matmul: plain
+               library GEMMs), db = colsum(dC)
+  _LayerNorm   y = LN(x) from the HIP kernel (row stats saved)             TF:1071, 1130
+               backward: the standard closed form in fp32
+  _EmbedLN     LN(Ew[id] + Ep[pos] + Et[tt] + Ei[ip])                       models.py:108-138
+               backward: LN backward, then index_add into the four tables (no gradient at
+               padding_idx rows of the word / position tables, as nn.Embedding)
+  _Attention   sliding-window local + global attention (band kernel + global fold)
+               TF:482-1057; backward: the attention is recomputed in fp32 (block-window form,
+               plus the reference's key_global / value_global over all tokens) under autograd.
+
+Mixed precision follows the reference's autocast run (finetune.py:106-110): GEMM operands in
+bf16, LayerNorm outputs / residual stream / losses in fp32, parameters fp32 (the bf16 weight
+copies are autograd-tracked casts, so gradients reach the fp32 masters).
+
+Dropout: hidden dropout (embeddings, attention output, FFN output; TF:1069, 1128, models.py:137)
+is applied with torch's RNG. Attention-probability dropout (TF:581) is not implemented: training
+with attention_probs_dropout_prob > 0 raises.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import ops
+
+__all__ = ["encode_train"]
+
+
+# ------------------------------------------------------------------------------------------
+class _Gemm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, w, b, scale_cols: int, col_scale: float):
+        ctx.save_for_backward(a, w)
+        ctx.sc = (scale_cols, col_scale)
+        return ops.gemm(a.contiguous(), w, b, ops.RF_EPI_BIAS, scale_cols=scale_cols, col_scale=col_scale)
+
+    @staticmethod
+    def backward(ctx, dc):
+        a, w = ctx.saved_tensors
+        sc, s = ctx.sc
+        dc = dc.to(a.dtype)
+        if sc > 0 and s != 1.0:
+            dc = dc.clone()
+            dc[:, :sc] *= s
+        da = dc @ w if ctx.needs_input_grad[0] else None
+        dw = dc.t() @ a if ctx.needs_input_grad[1] else None
+        db = dc.float().sum(0) if ctx.needs_input_grad[2] else None
+        return da, dw, db, None, None
+
+
+def _ln_backward(dy, x, mean, rstd, w):
+    xhat = (x.float() - mean[:, None]) * rstd[:, None]
+    g = dy.float() * w[None, :]
+    dx = rstd[:, None] * (g - g.mean(-1, keepdim=True) - xhat * (g * xhat).mean(-1, keepdim=True))
+    dw = (dy.float() * xhat).sum(0)
+    db = dy.float().sum(0)
+    return dx, dw, db
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps: float, out_dtype):
+        y, mean, rstd = ops.layernorm(x.contiguous(), w, b, eps, out_dtype=out_dtype, stats=True)
+        ctx.save_for_backward(x, mean, rstd, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, w = ctx.saved_tensors
+        dx, dw, db = _ln_backward(dy, x, mean, rstd, w)
+        return dx.to(x.dtype), dw, db, None, None
+
+
+class _EmbedLN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, pos, tt, ip, word, pe, te, ie, ln_w, ln_b, eps: float, pad_id: int):
+        h, mean, rstd = None, None, None
+        out = ops.embed_ln(ids, pos, tt, ip, word, pe, te, ie, ln_w, ln_b, eps, out_dtype=torch.float32)
+        h = out[0] if isinstance(out, tuple) else out
+        ctx.save_for_backward(ids, pos, tt, ip, word, pe, te, ie, ln_w)
+        ctx.eps, ctx.pad = eps, pad_id
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        ids, pos, tt, ip, word, pe, te, ie, ln_w = ctx.saved_tensors
+        i, p, t, q = (x.reshape(-1).long() for x in (ids, pos, tt, ip))
+        x = word[i] + pe[p] + te[t] + ie[q]  # recompute the pre-LN sum (fp32)
+        mean = x.mean(-1)
+        rstd = torch.rsqrt(x.var(-1, unbiased=False) + ctx.eps)
+        dx, dw, db = _ln_backward(dh.reshape(x.shape), x, mean, rstd, ln_w)
+        grads = []
+        for table, idx, pad in ((word, i, ctx.pad), (pe, p, ctx.pad), (te, t, None), (ie, q, None)):
+            g = torch.zeros_like(table).index_add_(0, idx, dx)
+            if pad is not None:
+                g[pad] = 0
+            grads.append(g)
+        return (None, None, None, None, *grads, dw, db, None, None)
+
+
+# ------------------------------------------------------------------------------------------
+def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, half_w: int):
+    """fp32 recompute of the attention block (same contract as the HIP kernels; used under
+    autograd by _Attention.backward). q, k, v (B*Lp, D) pre-scaled q; qg (B*gmax, D) pre-scaled;
+    h (B*Lp, D) the layer input; flags (B, Lp) {0 pad, 1 local, 2 global}; gidx (B, gmax)."""
+    D = q.shape[1]
+    hd = D // H
+    f = flags.long()
+    valid = f != 0
+    local = f == 1
+    qh = q.float().view(B, Lp, H, hd)
+    kh = k.float().view(B, Lp, H, hd)
+    vh = v.float().view(B, Lp, H, hd)
+    W = 2 * half_w
+    nb = Lp // W
+    # window keys for query block c: rows [cW - half_w, cW + W + half_w)
+    kp = F.pad(kh, (0, 0, 0, 0, half_w, half_w))
+    vp = F.pad(vh, (0, 0, 0, 0, half_w, half_w))
+    lp = F.pad(local, (half_w, half_w))
+    kw = kp.unfold(1, 2 * W, W)[:, :nb]        # (B, nb, H, hd, 2W)
+    vw = vp.unfold(1, 2 * W, W)[:, :nb]
+    lw = lp.unfold(1, 2 * W, W)[:, :nb]        # (B, nb, 2W)
+    qb = qh.view(B, nb, W, H, hd)
+    s = torch.einsum("bcihd,bchdj->bchij", qb, kw)   # (B, nb, H, W, 2W)
+    ii = torch.arange(W, device=q.device)[:, None] + half_w
+    jj = torch.arange(2 * W, device=q.device)[None, :]
+    band = (ii - jj).abs() <= half_w
+    ok = band[None, None, None] & lw[:, :, None, None, :]
+    s = s.masked_fill(~ok, float("-inf"))
+    gmax = gidx.shape[1]
+    if gmax > 0:
+        gv = gidx >= 0
+        gi = gidx.clamp(min=0).long()
+        kg_loc = torch.gather(kh, 1, gi[:, :, None, None].expand(B, gmax, H, hd))  # local K at globals
+        vg_loc = torch.gather(vh, 1, gi[:, :, None, None].expand(B, gmax, H, hd))
+        sg = torch.einsum("bcihd,bghd->bchig", qb, kg_loc)   # (B, nb, H, W, G)
+        sg = sg.masked_fill(~gv[:, None, None, None, :], float("-inf"))
+        s = torch.cat([s, sg], -1)
+    m = s.amax(-1, keepdim=True)
+    m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+    p = torch.exp(s - m)
+    p = p / p.sum(-1, keepdim=True).clamp_min(1e-30)
+    o = torch.einsum("bchij,bchdj->bcihd", p[..., :2 * W], vw)
+    if gmax > 0:
+        o = o + torch.einsum("bchig,bghd->bcihd", p[..., 2 * W:], vg_loc)
+    o = o.reshape(B, Lp, H, hd) * valid[:, :, None, None]
+    o = o.reshape(B * Lp, D)
+    if gmax > 0:
+        # global query rows: key_global / value_global over all tokens (TF:964-1057), overwrite
+        hf = h.float()
+        kgl = (hf @ wkg.float().t() + bkg).view(B, Lp, H, hd)
+        vgl = (hf @ wvg.float().t() + bvg).view(B, Lp, H, hd)
+        qgh = qg.float().view(B, gmax, H, hd)
+        sgg = torch.einsum("bghd,blhd->bhgl", qgh, kgl).masked_fill(~valid[:, None, None, :], float("-inf"))
+        pg = torch.softmax(sgg, -1)
+        og = torch.einsum("bhgl,blhd->bghd", pg, vgl).reshape(B, gmax, D)
+        rows = (torch.arange(B, device=q.device)[:, None] * Lp + gidx.clamp(min=0)).reshape(-1)
+        keep = gv.reshape(-1)
+        o = o.index_put((rows[keep],), og.reshape(-1, D)[keep])
+    return o
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold):
+        out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w)
+        if gidx.shape[1] > 0:
+            if fold:
+                ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg,
+                                          wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out)
+            else:
+                kg = ops.gemm(h.contiguous(), wkg.contiguous(), bkg, ops.RF_EPI_BIAS)
+                vg = ops.gemm(h.contiguous(), wvg.contiguous(), bvg, ops.RF_EPI_BIAS)
+                ops.global_attention(qg.contiguous(), kg, vg, flags, gidx, B, Lp, H, out)
+        ctx.save_for_backward(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx)
+        ctx.dims = (B, Lp, H, half_w)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx = ctx.saved_tensors
+        B, Lp, H, half_w = ctx.dims
+        inputs = [t.detach().requires_grad_(need) for t, need in
+                  zip((q, k, v, qg, h, wkg, bkg, wvg, bvg), ctx.needs_input_grad[:9])]
+        with torch.enable_grad(), torch.autocast("cuda", enabled=False):
+            o = _attention_torch(*inputs, flags, gidx, B, Lp, H, half_w)
+            want = [t for t in inputs if t.requires_grad]
+            grads = torch.autograd.grad(o, want, dout.float(), allow_unused=True) if want else []
+        it = iter(grads)
+        res = []
+        for t in inputs:
+            if t.requires_grad:
+                g = next(it)
+                res.append(None if g is None else g.to(t.dtype))
+            else:
+                res.append(None)
+        return (*res, None, None, None, None, None, None, None)
+
+
+# ------------------------------------------------------------------------------------------
+def encode_train(model, input_ids, attention_mask, global_attention_mask, token_type_ids,
+                 position_ids, item_position_ids, output_hidden_states: bool
+                 ) -> Tuple[torch.Tensor, Optional[tuple]]:
+    """Autograd forward of RecformerModel (same outputs as RecformerModel._encode)."""
+    from .models import _compute_dtype
+    cfg = model.config
+    if model.training and cfg.attention_probs_dropout_prob > 0:
+        raise NotImplementedError(
+            "recformer_amd: attention-probability dropout is not implemented on the training path; "
+            "set config.attention_probs_dropout_prob = 0")
+    B, L = input_ids.shape
+    Wn = model._window()
+    Lp = L + (Wn - L % Wn) % Wn
+    D, H = cfg.hidden_size, cfg.num_attention_heads
+    hd = D // H
+    dt = _compute_dtype(model.dtype)
+    eps = cfg.layer_norm_eps
+    p_hid = cfg.hidden_dropout_prob if model.training else 0.0
+    if global_attention_mask is not None:
+        gm = global_attention_mask != 0
+        if attention_mask is not None:
+            gm = gm & (attention_mask > 0)
+        gmax = int(gm.sum(1).max().item()) if B > 0 else 0
+    else:
+        gmax = 0
+    ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
+        input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
+        position_ids, Lp, cfg.pad_token_id, gmax)
+    emb = model.embeddings
+    h32 = _EmbedLN.apply(ids, pos, tt, ip, emb.word_embeddings.weight.float(),
+                         emb.position_embeddings.weight.float(), emb.token_type_embeddings.weight.float(),
+                         emb.item_position_embeddings.weight.float(), emb.LayerNorm.weight.float(),
+                         emb.LayerNorm.bias.float(), eps, cfg.pad_token_id)
+    h32 = F.dropout(h32, p_hid, model.training)
+    hidden_all = [h32] if output_hidden_states else None
+    scale = 1.0 / math.sqrt(hd)
+    windows = cfg.window_per_layer()
+    fold = getattr(cfg, "global_attention_fold", True)
+    rows = None
+    if gmax > 0:
+        rows = (torch.arange(B, device=input_ids.device)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
+        gvalid = (gidx >= 0).reshape(-1, 1)
+    for li, lyr in enumerate(model.encoder.layer):
+        sa = lyr.attention.self
+        h = h32.to(dt)
+        w_qkv = torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0).to(dt)
+        b_qkv = torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0).float()
+        qkv = _Gemm.apply(h, w_qkv, b_qkv, D, scale)
+        qg = None
+        if gmax > 0:
+            hg = h[rows] * gvalid.to(h.dtype)
+            qg = _Gemm.apply(hg, sa.query_global.weight.to(dt), sa.query_global.bias.float(), D, scale)
+        ctx = _Attention.apply(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], qg, h,
+                               sa.key_global.weight.to(dt), sa.key_global.bias.float(),
+                               sa.value_global.weight.to(dt), sa.value_global.bias.float(),
+                               flags, gidx, B, Lp, H, windows[li] // 2, fold)
+        ao = lyr.attention.output
+        t = _Gemm.apply(ctx, ao.dense.weight.to(dt), ao.dense.bias.float(), 0, 1.0)
+        x1 = F.dropout(t.float(), p_hid, model.training) + h32
+        a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
+        z = _Gemm.apply(a32.to(dt), lyr.intermediate.dense.weight.to(dt), lyr.intermediate.dense.bias.float(), 0, 1.0)
+        u = F.gelu(z)
+        fo = lyr.output
+        t2 = _Gemm.apply(u, fo.dense.weight.to(dt), fo.dense.bias.float(), 0, 1.0)
+        x2 = F.dropout(t2.float(), p_hid, model.training) + a32
+        h32 = _LayerNorm.apply(x2, fo.LayerNorm.weight.float(), fo.LayerNorm.bias.float(), eps, torch.float32)
+        if output_hidden_states:
+            hidden_all.append(h32)
+    last = h32.view(B, Lp, D)[:, :L]
+    if output_hidden_states:
+        hidden_all = tuple(x.view(B, Lp, D)[:, :L] for x in hidden_all)
+    return last, hidden_all

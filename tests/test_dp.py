@@ -89,3 +89,40 @@ def test_dp_gloo_world2_matches_single_process(B):
     # rows are computed independently; only BLAS blocking over the batch differs
     assert torch.allclose(gathered, ref, atol=1e-5, rtol=0)
     assert tmax == 2.0
+
+
+def _grad_worker(rank, ws, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.GELU(), torch.nn.Linear(32, 4))
+        x = torch.randn(8, 16)[rank * 4:(rank + 1) * 4]  # this rank's shard of one global batch
+        loss = net(x).pow(2).mean()
+        loss.backward()
+        n = dp.allreduce_grads(list(net.parameters()), bucket_bytes=1024)
+        if rank == 0:
+            out_q.put(([p.grad.clone() for p in net.parameters()], n))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_grads_matches_full_batch():
+    """world-2 data parallel: the averaged per-shard gradients equal the full-batch gradient."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    grads, n = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.GELU(), torch.nn.Linear(32, 4))
+    x = torch.randn(8, 16)
+    net(x).pow(2).mean().backward()
+    for g, p in zip(grads, net.parameters()):
+        assert torch.allclose(g, p.grad, atol=1e-6)
+    assert n >= 2  # 1 KiB buckets force more than one collective
