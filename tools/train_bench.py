@@ -1,0 +1,64 @@
+"""C3 finetune-step throughput (BASELINE configs[2]): RecformerForSeqRec forward + backward +
+AdamW step under bf16 autocast, 12L/768d, B sequences x L=1024 per step, 10k-item catalog,
+full softmax (finetune.sh) or sampled (--negatives k). Dropout on hidden layers (0.1) and off
+on attention probabilities (not implemented on the training path).
+
+    python tools/train_bench.py [--batch 16] [--steps 5] [--negatives 0]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from recformer_amd import RecformerConfig, RecformerForSeqRec  # noqa: E402
+from recformer_amd.synth import BASE, synth_batch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--negatives", type=int, default=0)
+    ap.add_argument("--catalog", type=int, default=10000)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    cfg = RecformerConfig(**dict(BASE, item_num=a.catalog, attention_probs_dropout_prob=0.0,
+                                 finetune_negative_sample_size=a.negatives))
+    torch.manual_seed(0)
+    model = RecformerForSeqRec(cfg)
+    model.init_item_embedding(torch.randn(a.catalog, cfg.hidden_size) * 0.5)
+    model = model.to(dev).train()
+    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=5e-5)
+    batch = {k: v.to(dev) for k, v in synth_batch(a.batch, 1024, cfg.vocab_size, seed=7, item_len=21).items()}
+    labels = torch.randint(0, a.catalog, (a.batch,), device=dev)
+
+    def step():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = model(**batch, labels=labels)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"workload": "C3 finetune step (fwd+bwd+AdamW), 12L/768d, L=1024, bf16 autocast",
+                      "batch": a.batch, "negatives": a.negatives, "catalog": a.catalog,
+                      "ms_per_step": round(1e3 * dt / a.steps, 2), "seq_per_s": round(a.batch * a.steps / dt, 2),
+                      "loss": float(loss.detach()),
+                      "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}))
+
+
+if __name__ == "__main__":
+    main()
