@@ -125,6 +125,16 @@ int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, const void* 
                             const int32_t* gidx, int gmax, void* workspace, void* out,
                             int ld_out, rf_stream_t stream);
 
+/* The same, starting from the layer input: qg_h = (Wqg_h h_g + bqg_h) * q_scale for each global
+ * row's hidden vector h_g (query_global, TF:972-982, rounded to dtype like a GEMM output), then
+ * the fold as above — one entry point for the whole global path of a layer (no separate gather
+ * and qg GEMM). D <= 1024. */
+int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
+                              const void* wqg, const float* bqg, float q_scale, const void* wkg,
+                              const float* bkg, const void* wvg, const float* bvg, const uint8_t* flags,
+                              const int32_t* gidx, int gmax, void* workspace, void* out, int ld_out,
+                              rf_stream_t stream);
+
 /* Row gather: out[r] = x[b*Lp + gidx[b, g]] for r = b*gmax + g (zero rows for -1). Feeds
  * the query_global projection of the global rows (TF:972-982). */
 int rf_gather_global_rows(int dtype, int B, int Lp, int D, int gmax, const void* x, int ldx,

@@ -115,6 +115,74 @@ __global__ void __launch_bounds__(256) k_gfold_u(int D, int H, int R, const T* _
   }
 }
 
+// ---- qg_h and u_h straight from the layer input ----------------------------------------------
+// grid (16 heads, R): qg_h = (Wqg_h h_g + bqg_h) * q_scale for the global row's hidden vector h_g
+// (rounded to the compute dtype, as the qg GEMM would store it), then u_h = Wkg_h^T qg_h as in
+// k_gfold_u. Replaces gather + qg GEMM + u (three launches) for the fold path.
+template <typename T>
+__global__ void __launch_bounds__(256) k_gfold_qu(int Lp, int D, int H, int gmax, const T* __restrict__ hs,
+                                                   int ldh, const T* __restrict__ wqg,
+                                                   const float* __restrict__ bqg, float q_scale,
+                                                   const T* __restrict__ wkg, const int32_t* __restrict__ gidx,
+                                                   GfoldWs ws, bool out_bf16) {
+  __shared__ float hrow[1024];
+  __shared__ float qs[64];
+  const int h = blockIdx.x, r = blockIdx.y;
+  const int pos = gidx[r];
+  if (pos < 0) return;
+  const int b = r / gmax;
+  const int t = threadIdx.x;
+  if (h < H) {
+    const T* hr = hs + ((int64_t)b * Lp + pos) * ldh;
+    for (int k = t; k < D; k += blockDim.x) hrow[k] = to_f32(hr[k]);
+    __syncthreads();
+    {
+      const int d = t >> 2, part = t & 3;  // 4 threads per output of qg_h (64 outputs)
+      const T* wr = wqg + (int64_t)(h * 64 + d) * D;
+      float a = 0.f;
+      for (int k = 8 * part; k < D; k += 32) {
+        float x[8];
+        load4(wr + k, x);
+        load4(wr + k + 4, x + 4);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a = fmaf(x[i], hrow[k + i], a);
+      }
+      a += __shfl_xor(a, 1, 64);
+      a += __shfl_xor(a, 2, 64);
+      if (part == 0) qs[d] = to_f32(from_f32<T>((a + bqg[h * 64 + d]) * q_scale));
+    }
+  }
+  __syncthreads();
+  for (int k = 4 * t; k < D; k += 4 * blockDim.x) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (h < H) {
+      const T* wp = wkg + (int64_t)(h * 64) * D + k;
+#pragma unroll 16
+      for (int d = 0; d < 64; ++d) {
+        float x[4];
+        load4(wp + (int64_t)d * D, x);
+        const float qd = qs[d];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = fmaf(qd, x[i], a[i]);
+      }
+    }
+    if (out_bf16) {
+      bf16* hi = ws.u16 + ((int64_t)r * 2 * GF_HP + h) * D + k;
+      bf16* lo = hi + (int64_t)GF_HP * D;
+      bf16x4 vh, vl;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        vh[i] = (bf16)a[i];
+        vl[i] = (bf16)(a[i] - (float)vh[i]);
+      }
+      *reinterpret_cast<bf16x4*>(hi) = vh;
+      *reinterpret_cast<bf16x4*>(lo) = vl;
+    } else if (h < H) {
+      *reinterpret_cast<float4*>(ws.u32 + ((int64_t)r * H + h) * (D + 4) + k) = make_float4(a[0], a[1], a[2], a[3]);
+    }
+  }
+}
+
 // ---- bf16 partial: MFMA over a 64-row chunk -----------------------------------------------
 // LDS image of the chunk: segment-major [D/64][64 rows][128 B] with the 16-B slot XOR
 // (row & 7) inside each 128-B segment (lane-linear DMA pieces of 8 rows x 128 B).
@@ -400,6 +468,42 @@ extern "C" size_t rf_global_fold_workspace(int B, int Lp, int D, int H, int gmax
   return gfold_bytes(B * gmax, nch, H, D);
 }
 
+// partial + out stages shared by both entry points (u already in the workspace)
+static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
+                            const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax,
+                            GfoldWs ws, int nch, void* out, int ld_out, hipStream_t s) {
+  const int R = B * gmax;
+  const size_t lds_o = (size_t)(D + nch) * sizeof(float);
+  if (dtype == RF_BF16) {
+    const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + 160 * sizeof(float);
+    RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
+#define GP_(DD)                                                                               \
+  case DD:                                                                                    \
+    (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<DD>,                          \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
+    k_gfold_partial_bf16<DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const bf16*)h, ldh,  \
+                                                              flags, gidx, ws, H);            \
+    break;
+    switch (D) {
+      GP_(64) GP_(128) GP_(192) GP_(256) GP_(384) GP_(512) GP_(768) GP_(1024)
+      default:
+        RF_REQUIRE(false, "rf_global_attn_fold(bf16): unsupported hidden size %d", D);
+    }
+#undef GP_
+    k_gfold_out<bf16><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const bf16*)wvg, bvg, gidx, ws,
+                                                      (bf16*)out, ld_out);
+  } else {
+    const size_t lds_p = (size_t)(H * (D + 4) + H * GF_CHF) * sizeof(float);
+    RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
+    (void)hipFuncSetAttribute((const void*)k_gfold_partial_f32,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);
+    k_gfold_partial_f32<<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const float*)h, ldh, flags, gidx, ws);
+    k_gfold_out<float><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const float*)wvg, bvg, gidx, ws,
+                                                       (float*)out, ld_out);
+  }
+  return RF_OK;
+}
+
 extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, const void* qg,
                                        int ld_qg, const void* h, int ldh, const void* wkg,
                                        const float* bkg, const void* wvg, const float* bvg,
@@ -411,48 +515,52 @@ extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, c
   RF_REQUIRE(D == H * 64, "rf_global_attn_fold_fwd: D=%d must be H*64", D);
   RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_fwd: at most %d heads", GF_HP);
   RF_REQUIRE(ldh >= D && ld_qg >= D && ld_out >= D, "rf_global_attn_fold_fwd: dims");
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F32, "rf_global_attn_fold_fwd: bad dtype %d", dtype);
   if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
   RF_REQUIRE(workspace && gidx && flags, "rf_global_attn_fold_fwd: null workspace/gidx/flags");
+  RF_REQUIRE(dtype != RF_BF16 || ldh % 8 == 0, "rf_global_attn_fold_fwd(bf16): ldh must be a multiple of 8");
+  RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_fwd(f32): ldh must be a multiple of 4");
   const int R = B * gmax;
-  const int chunk = dtype == RF_BF16 ? GF_CH : GF_CHF;
-  const int nch = (Lp + chunk - 1) / chunk;
+  const int nch = (Lp + (dtype == RF_BF16 ? GF_CH : GF_CHF) - 1) / (dtype == RF_BF16 ? GF_CH : GF_CHF);
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
-  const size_t lds_o = (size_t)(D + nch) * sizeof(float);
-  if (dtype == RF_BF16) {
-    RF_REQUIRE(ldh % 8 == 0, "rf_global_attn_fold_fwd(bf16): ldh must be a multiple of 8");
-    const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + 160 * sizeof(float);
-    RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold_fwd: D too large for LDS");
+  if (dtype == RF_BF16)
     k_gfold_u<bf16><<<dim3(GF_HP, R), 192, 0, s>>>(D, H, R, (const bf16*)qg, ld_qg, (const bf16*)wkg, gidx,
                                                     ws, true);
-#define GP_(DD)                                                                               \
-  case DD:                                                                                    \
-    (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<DD>,                          \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
-    k_gfold_partial_bf16<DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const bf16*)h, ldh,  \
-                                                              flags, gidx, ws, H);            \
-    break;
-    switch (D) {
-      GP_(64) GP_(128) GP_(192) GP_(256) GP_(384) GP_(512) GP_(768) GP_(1024)
-      default:
-        RF_REQUIRE(false, "rf_global_attn_fold_fwd(bf16): unsupported hidden size %d", D);
-    }
-#undef GP_
-    k_gfold_out<bf16><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const bf16*)wvg, bvg, gidx, ws,
-                                                      (bf16*)out, ld_out);
-  } else if (dtype == RF_F32) {
-    RF_REQUIRE(ldh % 4 == 0, "rf_global_attn_fold_fwd(f32): ldh must be a multiple of 4");
-    const size_t lds_p = (size_t)(H * (D + 4) + H * GF_CHF) * sizeof(float);
-    RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold_fwd: D too large for LDS");
-    (void)hipFuncSetAttribute((const void*)k_gfold_partial_f32,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);
+  else
     k_gfold_u<float><<<dim3(H, R), 192, 0, s>>>(D, H, R, (const float*)qg, ld_qg, (const float*)wkg, gidx,
                                                  ws, false);
-    k_gfold_partial_f32<<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const float*)h, ldh, flags, gidx, ws);
-    k_gfold_out<float><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const float*)wvg, bvg, gidx, ws,
-                                                       (float*)out, ld_out);
-  } else {
-    RF_REQUIRE(false, "rf_global_attn_fold_fwd: bad dtype %d", dtype);
-  }
+  const int rc = fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s);
+  if (rc != RF_OK) return rc;
   RF_LAUNCH_CHECK("rf_global_attn_fold_fwd");
+}
+
+extern "C" int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
+                                         const void* wqg, const float* bqg, float q_scale, const void* wkg,
+                                         const float* bkg, const void* wvg, const float* bvg,
+                                         const uint8_t* flags, const int32_t* gidx, int gmax,
+                                         void* workspace, void* out, int ld_out, rf_stream_t stream) {
+  (void)bkg;
+  RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0, "rf_global_attn_fold_h_fwd: bad shape");
+  RF_REQUIRE(D == H * 64 && D <= 1024, "rf_global_attn_fold_h_fwd: D=%d must be H*64 <= 1024", D);
+  RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_h_fwd: at most %d heads", GF_HP);
+  RF_REQUIRE(ldh >= D && ld_out >= D, "rf_global_attn_fold_h_fwd: dims");
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F32, "rf_global_attn_fold_h_fwd: bad dtype %d", dtype);
+  if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
+  RF_REQUIRE(workspace && gidx && flags && wqg && bqg, "rf_global_attn_fold_h_fwd: null pointer");
+  RF_REQUIRE(dtype != RF_BF16 || ldh % 8 == 0, "rf_global_attn_fold_h_fwd(bf16): ldh must be a multiple of 8");
+  RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_h_fwd(f32): ldh must be a multiple of 4");
+  const int R = B * gmax;
+  const int nch = (Lp + (dtype == RF_BF16 ? GF_CH : GF_CHF) - 1) / (dtype == RF_BF16 ? GF_CH : GF_CHF);
+  GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16)
+    k_gfold_qu<bf16><<<dim3(GF_HP, R), 256, 0, s>>>(Lp, D, H, gmax, (const bf16*)h, ldh, (const bf16*)wqg, bqg,
+                                                     q_scale, (const bf16*)wkg, gidx, ws, true);
+  else
+    k_gfold_qu<float><<<dim3(H, R), 256, 0, s>>>(Lp, D, H, gmax, (const float*)h, ldh, (const float*)wqg, bqg,
+                                                  q_scale, (const float*)wkg, gidx, ws, false);
+  const int rc = fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s);
+  if (rc != RF_OK) return rc;
+  RF_LAUNCH_CHECK("rf_global_attn_fold_h_fwd");
 }

@@ -408,13 +408,14 @@ class RecformerModel(nn.Module):
             ctx = ops.band_attention(qkv[:, 0:D], qkv[:, D:2 * D], qkv[:, 2 * D:3 * D], flags,
                                      gidx, B, Lp, H, half_w, tag="band_attn")
             if gmax > 0:
-                hg = ops.gather_global_rows(h, gidx, B, Lp)
-                qg = ops.gemm(hg, lw["w_qg"], lw["b_qg"], ops.RF_EPI_BIAS, scale_cols=D, col_scale=scale)
                 if fold:
-                    ops.global_attention_fold(qg, h, lw["w_qkv"][3 * D:4 * D], lw["b_qkv"][3 * D:4 * D],
-                                              lw["w_qkv"][4 * D:5 * D], lw["b_qkv"][4 * D:5 * D],
-                                              flags, gidx, B, Lp, H, ctx, tag="global_attn")
+                    ops.global_attention_fold_h(h, lw["w_qg"], lw["b_qg"], scale, lw["w_qkv"][3 * D:4 * D],
+                                                lw["b_qkv"][3 * D:4 * D], lw["w_qkv"][4 * D:5 * D],
+                                                lw["b_qkv"][4 * D:5 * D], flags, gidx, B, Lp, H, ctx,
+                                                tag="global_attn")
                 else:
+                    hg = ops.gather_global_rows(h, gidx, B, Lp)
+                    qg = ops.gemm(hg, lw["w_qg"], lw["b_qg"], ops.RF_EPI_BIAS, scale_cols=D, col_scale=scale)
                     ops.global_attention(qg, qkv[:, 3 * D:4 * D], qkv[:, 4 * D:5 * D], flags, gidx,
                                          B, Lp, H, ctx, tag="global_attn")
             if not mixed:

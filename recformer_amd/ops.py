@@ -293,6 +293,31 @@ def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: in
     return out
 
 
+def global_attention_fold_h(h, wqg, bqg, q_scale: float, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int,
+                            H: int, out: torch.Tensor, tag: Optional[str] = None):
+    """Whole global path of a layer from its input h (rf_global_attn_fold_h_fwd): query_global
+    projection of the global rows, then the key/value-projection fold; overwrites ctx rows at
+    the global positions."""
+    lib = _lib.load()
+    gmax = gidx.shape[1]
+    if gmax == 0:
+        return out
+    _dev(h, wqg, wkg, wvg, flags)
+    D = h.shape[1]
+    for t in (wqg, wkg, wvg):
+        if not t.is_contiguous() or t.dtype != h.dtype:
+            raise ValueError("global_attention_fold_h: weights must be contiguous in the compute dtype")
+    ws_bytes = lib.rf_global_fold_workspace(B, Lp, D, H, gmax)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=h.device)
+    with _region(tag):
+        rc = lib.rf_global_attn_fold_h_fwd(dtype_code(h.dtype), B, Lp, D, H, _p(h), _rowmajor(h, "h"), _p(wqg),
+                                           _p(bqg), float(q_scale), _p(wkg), _p(bkg), _p(wvg), _p(bvg),
+                                           _p(flags), _p(gidx.contiguous()), gmax, _p(ws), _p(out),
+                                           _rowmajor(out, "out"), _stream(out))
+    check(rc, "rf_global_attn_fold_h_fwd")
+    return out
+
+
 def gather_global_rows(x, gidx, B: int, Lp: int):
     lib = _lib.load()
     gmax = gidx.shape[1]

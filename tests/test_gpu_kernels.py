@@ -267,3 +267,33 @@ def test_cross_entropy(dev, dt, N):
     xp = torch.zeros(M, N + 5, device=dev, dtype=dt)
     xp[:, :N] = x
     assert abs(float(ops.cross_entropy(xp[:, :N], lab)) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [
+    dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
+    dict(B=2, Lp=1024, H=12, lens=[1024, 333], globals_=((0, 0), (1, 0))),
+])
+def test_global_attention_fold_from_h(dev, dt, case):
+    """rf_global_attn_fold_h_fwd (query_global projection of the gathered rows + fold in one
+    entry point) against gather + qg GEMM + rf_global_attn_fold_fwd on the same inputs."""
+    B, Lp, H = case["B"], case["Lp"], case["H"]
+    D = H * 64
+    _, merged, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, case["lens"], case["globals_"], 3)
+    h = _rand((B * Lp, D), dev, dt, 1.0, seed=50)
+    wqg = _rand((D, D), dev, dt, 0.05, seed=51)
+    wkg = _rand((D, D), dev, dt, 0.05, seed=52)
+    wvg = _rand((D, D), dev, dt, 0.05, seed=53)
+    bqg = _rand((D,), dev, torch.float32, 0.1, seed=54)
+    bkg = _rand((D,), dev, torch.float32, 0.1, seed=55)
+    bvg = _rand((D,), dev, torch.float32, 0.1, seed=56)
+    scale = 0.125
+    ctx_a = torch.zeros(B * Lp, D, dtype=dt, device=dev)
+    ops.global_attention_fold_h(h, wqg, bqg, scale, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, ctx_a)
+    hg = ops.gather_global_rows(h, gidx, B, Lp)
+    qg = ops.gemm(hg, wqg, bqg, ops.RF_EPI_BIAS, scale_cols=D, col_scale=scale)
+    ctx_b = torch.zeros(B * Lp, D, dtype=dt, device=dev)
+    ops.global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, ctx_b)
+    err = (ctx_a.float() - ctx_b.float()).abs().max().item()
+    assert err <= (1e-4 if dt == torch.float32 else 2e-2), err
+    assert ctx_a.abs().sum().item() > 0
