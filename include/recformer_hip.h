@@ -157,6 +157,14 @@ int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, co
 int rf_cross_entropy_fwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,
                          int64_t ignore_index, float* loss, int32_t* argmax, rf_stream_t stream);
 
+/* Ranker (utils.py:76-108) counts over a block of fp32 scores (M rows x N columns, ld):
+ * gt[m] += #{n: s[m,n] > s_label[m]} (the strict rank), valid[m] += #{n: s[m,n] > -max_val}
+ * (valid_length), and, if sexp != NULL, sexp[m] += sum_n exp(s[m,n] - shift) (log-sum-exp of
+ * cosine/temp rows with |s| <= shift, for the CE without a row max). Accumulates with atomics,
+ * so a catalog can be scored in column blocks (never the whole (B, N) matrix) — §8f row 1. */
+int rf_rank_accum(int M, int N, const float* scores, int64_t ld, const float* s_label, float max_val,
+                  float shift, int32_t* gt, int32_t* valid, float* sexp, rf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

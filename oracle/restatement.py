@@ -248,3 +248,20 @@ def pretrain_forward(sd_lf: Dict[str, Tensor], sd_head: Dict[str, Tensor], cfg, 
         scores = lm_head_forward(sd_head, h, cfg.layer_norm_eps)
         loss = loss + cfg.mlm_weight * F.cross_entropy(scores.reshape(-1, scores.shape[-1]), lab.reshape(-1))
     return loss, cos_sim, correct
+
+
+def ranker_metrics(scores: Tensor, labels: Tensor, ks, max_val: float = 1e4):
+    """utils.py:76-108 (Ranker.forward): [ndcg@k, hr@k]... + [MRR, AUC, CE loss]."""
+    labels = labels.squeeze()
+    loss = F.cross_entropy(scores, labels).item()
+    predicts = scores[torch.arange(scores.size(0)), labels].unsqueeze(-1)
+    valid_length = (scores > -max_val).sum(-1).float()
+    rank = (predicts < scores).sum(-1).float()
+    res = []
+    for k in ks:
+        indicator = (rank < k).float()
+        res.append(((1 / torch.log2(rank + 2)) * indicator).mean().item())
+        res.append(indicator.mean().item())
+    res.append((1 / (rank + 1)).mean().item())
+    res.append((1 - (rank / valid_length)).mean().item())
+    return res + [loss]

@@ -4,6 +4,7 @@ Drop-in for the reference package `recformer` (recformer/__init__.py:1-3): the s
 names and forward() signatures, backed by hand-written HIP kernels in librecformer_hip.so.
 """
 from .config import RecformerConfig
+from .ranker import Ranker
 from .models import (RecformerEmbeddings, RecformerForPretraining, RecformerForSeqRec,
                      RecformerModel, RecformerModelOutput, RecformerPooler,
                      RecformerPretrainingOutput, Similarity, create_position_ids_from_input_ids)
@@ -11,5 +12,5 @@ from .models import (RecformerEmbeddings, RecformerForPretraining, RecformerForS
 __all__ = [
     "RecformerConfig", "RecformerModel", "RecformerForSeqRec", "RecformerForPretraining",
     "RecformerPretrainingOutput", "RecformerModelOutput", "RecformerEmbeddings", "RecformerPooler",
-    "Similarity", "create_position_ids_from_input_ids",
+    "Similarity", "create_position_ids_from_input_ids", "Ranker",
 ]

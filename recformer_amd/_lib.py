@@ -45,6 +45,7 @@ SIGNATURES = {
     "rf_row_inv_norm": (c_int, [c_int, c_int, c_int, P, c_int, c_float, P, P]),
     "rf_cos_score_cand": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P,
                                   c_float, P, P]),
+    "rf_rank_accum": (c_int, [c_int, c_int, P, ctypes.c_int64, P, c_float, c_float, P, P, P, P]),
     "rf_cross_entropy_fwd": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, ctypes.c_int64, P, P, P]),
 }
 

@@ -377,6 +377,46 @@ __global__ void __launch_bounds__(256) k_cross_entropy(int N, const T* __restric
   }
 }
 
+// Ranker counts (utils.py:76-108) over a block of fp32 scores: per row b,
+//   gt[b]    += #{n : s[b,n] > s_label[b]}   (rank, strict — predicts < scores)
+//   valid[b] += #{n : s[b,n] > -max_val}     (valid_length)
+//   sexp[b]  += sum_n exp(s[b,n] - shift)   (optional: bounded log-sum-exp for the CE of a
+//                                             cosine / temp score row, |s| <= shift = 1/temp)
+// grid (rows, column splits); integer atomics, so the counts are exact for any split.
+__global__ void __launch_bounds__(256) k_rank_accum(int N, const float* __restrict__ sc, int64_t ld,
+                                                     const float* __restrict__ slab, float max_val, float shift,
+                                                     int32_t* __restrict__ gt, int32_t* __restrict__ valid,
+                                                     float* __restrict__ sexp) {
+  __shared__ int sg[4], sv[4];
+  __shared__ float se[4];
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int per = (N + gridDim.y - 1) / gridDim.y;
+  const int c0 = blockIdx.y * per, c1 = min(N, c0 + per);
+  const float* sr = sc + (int64_t)row * ld;
+  const float lab = slab[row];
+  int cg = 0, cv = 0;
+  float e = 0.f;
+  for (int c = c0 + t; c < c1; c += 256) {
+    const float v = sr[c];
+    cg += v > lab;
+    cv += v > -max_val;
+    if (sexp) e += __expf(v - shift);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cg += __shfl_xor(cg, o, 64);
+    cv += __shfl_xor(cv, o, 64);
+    e += __shfl_xor(e, o, 64);
+  }
+  if (lane == 0) { sg[wave] = cg; sv[wave] = cv; se[wave] = e; }
+  __syncthreads();
+  if (t == 0) {
+    atomicAdd(gt + row, sg[0] + sg[1] + sg[2] + sg[3]);
+    atomicAdd(valid + row, sv[0] + sv[1] + sv[2] + sv[3]);
+    if (sexp) atomicAdd(sexp + row, se[0] + se[1] + se[2] + se[3]);
+  }
+}
+
 template <typename TT, typename T>
 static int launch_embed(int M, int D, const int32_t* ids, const int32_t* pos, const int32_t* tt,
                         const int32_t* ip, const void* we, const void* pe, const void* te,
@@ -529,6 +569,17 @@ int rf_cross_entropy_fwd(int dtype, int M, int N, const void* logits, int64_t ld
   else
     RF_REQUIRE(false, "rf_cross_entropy_fwd: bad dtype %d", dtype);
   RF_LAUNCH_CHECK("rf_cross_entropy_fwd");
+}
+
+int rf_rank_accum(int M, int N, const float* scores, int64_t ld, const float* s_label, float max_val,
+                  float shift, int32_t* gt, int32_t* valid, float* sexp, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && N >= 0 && ld >= N, "rf_rank_accum: bad shape");
+  RF_REQUIRE(scores && s_label && gt && valid, "rf_rank_accum: null pointer");
+  if (M == 0 || N == 0) return RF_OK;
+  const int splits = min(64, (N + 8191) / 8192);
+  k_rank_accum<<<dim3(M, splits), 256, 0, as_stream(stream)>>>(N, scores, ld, s_label, max_val, shift, gt, valid,
+                                                              sexp);
+  RF_LAUNCH_CHECK("rf_rank_accum");
 }
 
 }  // extern "C"

@@ -297,3 +297,24 @@ def test_global_attention_fold_from_h(dev, dt, case):
     err = (ctx_a.float() - ctx_b.float()).abs().max().item()
     assert err <= (1e-4 if dt == torch.float32 else 2e-2), err
     assert ctx_a.abs().sum().item() > 0
+
+
+@pytest.mark.parametrize("N", [7, 1000, 100003])
+def test_ranker_matches_reference_formula(dev, N):
+    """Ranker (rf_rank_accum + rf_cross_entropy_fwd) vs utils.py:76-108 restated (oracle), with
+    ties, masked (-MAX_VAL) columns and labels at the extremes."""
+    from recformer_amd import Ranker
+    torch.manual_seed(N)
+    B = 33
+    s = torch.randn(B, N) * 4
+    s[:, ::7] = torch.round(s[:, ::7])  # ties
+    s[3, : N // 2] = -2e4                # masked part of a row (valid_length < N)
+    labels = torch.randint(0, N, (B,))
+    labels[0], labels[1] = 0, N - 1
+    s[5, labels[5]] = s[5].max()        # rank 0
+    ref = R.ranker_metrics(s.clone(), labels.clone(), [1, 10, 50])
+    got = Ranker([1, 10, 50])(s.to(dev), labels.to(dev))
+    assert len(got) == len(ref)
+    for g, r in zip(got[:-1], ref[:-1]):
+        assert abs(g - r) <= 1e-6, (got, ref)
+    assert abs(got[-1] - ref[-1]) <= 1e-5 * max(1.0, abs(ref[-1]))
