@@ -327,51 +327,48 @@ __global__ void __launch_bounds__(256) k_cos_cand(int B, int C, int D, const T* 
 // Cross entropy of one logits row against an integer label (torch CrossEntropyLoss with
 // ignore_index, the losses of models.py:494-510 and :589-597): loss = logsumexp(x) - x[label],
 // 0 for ignored rows; also the row's argmax (first max, as torch.argmax) for cl_correct_num.
-// One block per row: streaming max/sum-exp in registers, online rescale, 16-B loads.
+// One block per row, two passes over the row (max + first argmax, then sum of exp(x - max)):
+// branch-free, ~4 VALU ops per element.
 template <typename T>
 __global__ void __launch_bounds__(256) k_cross_entropy(int N, const T* __restrict__ x, int64_t ldx,
                                                         const int64_t* __restrict__ labels, int64_t ignore,
                                                         float* __restrict__ loss, int32_t* __restrict__ amax) {
-  __shared__ float sm[8], ss[8];
-  __shared__ int si[8];
+  __shared__ float sm[4];
+  __shared__ int si[4];
+  __shared__ float ss[4];
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const T* xr = x + (int64_t)row * ldx;
-  float m = -__builtin_inff(), l = 0.f;
+  float m = -__builtin_inff();
   int im = 0x7fffffff;
   for (int c = t; c < N; c += 256) {
     const float v = to_f32(xr[c]);
-    if (v > m) {
-      l = l * __expf(m - v) + 1.f;
-      m = v;
-      im = c;
-    } else {
-      l += __expf(v - m);
-    }
+    if (v > m) { m = v; im = c; }  // per thread columns ascend: keeps the first maximum
   }
-  // wave merge (max, argmax first index, rescaled sum)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(l, o, 64);
+    const float m2 = __shfl_xor(m, o, 64);
     const int i2 = __shfl_xor(im, o, 64);
-    const float mn = fmaxf(m, m2);
-    l = (m == -__builtin_inff() ? 0.f : l * __expf(m - mn)) + (m2 == -__builtin_inff() ? 0.f : l2 * __expf(m2 - mn));
-    im = (m2 > m || (m2 == m && i2 < im)) ? i2 : im;
-    m = mn;
+    if (m2 > m || (m2 == m && i2 < im)) { m = m2; im = i2; }
   }
-  if (lane == 0) { sm[wave] = m; ss[wave] = l; si[wave] = im; }
+  if (lane == 0) { sm[wave] = m; si[wave] = im; }
+  __syncthreads();
+  float M = sm[0];
+  int I = si[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w)
+    if (sm[w] > M || (sm[w] == M && si[w] < I)) { M = sm[w]; I = si[w]; }
+  const float mu = M == -__builtin_inff() ? 0.f : M;
+  float l = 0.f;
+  for (int c = t; c < N; c += 256) l += __expf(to_f32(xr[c]) - mu);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+  if (lane == 0) ss[wave] = l;
   __syncthreads();
   if (t == 0) {
-    float M = sm[0], Lq = ss[0];
-    int I = si[0];
-    for (int w = 1; w < 4; ++w) {
-      const float mn = fmaxf(M, sm[w]);
-      Lq = (M == -__builtin_inff() ? 0.f : Lq * __expf(M - mn)) + (sm[w] == -__builtin_inff() ? 0.f : ss[w] * __expf(sm[w] - mn));
-      I = (sm[w] > M || (sm[w] == M && si[w] < I)) ? si[w] : I;
-      M = mn;
-    }
+    const float Lq = ss[0] + ss[1] + ss[2] + ss[3];
     const int64_t lab = labels[row];
     float out = 0.f;
-    if (lab != ignore) out = (M + __logf(Lq)) - to_f32(xr[lab]);
+    if (lab != ignore) out = (mu + __logf(Lq)) - to_f32(xr[lab]);
     loss[row] = out;
     if (amax) amax[row] = I;
   }
