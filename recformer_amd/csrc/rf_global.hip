@@ -190,6 +190,204 @@ __device__ __forceinline__ int gimg(int row, int col) {
   return (((col >> 6) * 64 + row) << 7) + ((((col >> 3) & 7) ^ (row & 7)) << 4) + ((col & 7) << 1);
 }
 
+// ---- bf16 qg_h and u_h on MFMA, 64 global rows per block -------------------------------------
+// grid (H, ceil(R/64)), 4 waves x 16 global rows. The head's 64 x D slice of Wqg, then of Wkg,
+// is DMA'd once into an LDS image shared by the block's 64 rows (the GEMV kernels above read it
+// once per row: L2-bound when R is large, e.g. a catalog of short item sequences).
+//   qg[row][d] = bf16((h_g[row] . Wqg[h*64+d] + bqg) * q_scale)   (A: h rows from HBM, B: LDS)
+//   u[row][c]  = sum_d qg[row][d] Wkg[h*64+d][c]                    (A: Wkg^T via ds_read_tr,
+//                                                                    B: qg^T via ds_read_tr)
+// u is written as the hi + lo bf16 planes k_gfold_partial_bf16 reads; heads >= H are not
+// written (the partial kernel does not load them).
+template <int D>
+__global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, const bf16* __restrict__ hs,
+                                                        int ldh, const bf16* __restrict__ wqg,
+                                                        const float* __restrict__ bqg, float q_scale,
+                                                        const bf16* __restrict__ wkg,
+                                                        const int32_t* __restrict__ gidx, GfoldWs ws) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NK = D / 32;
+  constexpr int nseg = D >> 6;
+  const int h = blockIdx.x, r0 = blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int q4 = li >> 2, p4 = li & 3;
+  char* pimg = smem + nseg * 64 * 128 + wave * 2048;  // this wave's qg^T [64 d][16 rows] bf16
+  const int r = r0 + 16 * wave + li;
+  const int pos = r < R ? gidx[r] : -1;
+
+  bf16x8 a[NK];
+  if (pos >= 0) {
+    const bf16* hr = hs + ((int64_t)(r / gmax) * Lp + pos) * ldh + 8 * g;
+#pragma unroll
+    for (int s = 0; s < NK; ++s) a[s] = *reinterpret_cast<const bf16x8*>(hr + 32 * s);
+  } else {
+#pragma unroll
+    for (int s = 0; s < NK; ++s) a[s] = bf16x8{};
+  }
+  auto dma_head = [&](const bf16* w) {
+    for (int p = wave; p < nseg * 8; p += 4) {
+      const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
+      const int chk = (lane & 7) ^ (row & 7);
+      glds16(w + (int64_t)(h * 64 + row) * D + seg * 64 + chk * 8, smem + (seg * 64 + (p & 7) * 8) * 128);
+    }
+  };
+  dma_head(wqg);
+  wait_vmcnt0();
+  __syncthreads();
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NK; ++s)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(smem + gimg(16 * nt + li, 32 * s + 8 * g));
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[nt], 0, 0, 0);
+      }
+    // C[row 4g+i][d 16nt+li] -> qg^T image [d][row]
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int d = 16 * nt + li;
+      const float bb = bqg[h * 64 + d];
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (bf16)((acc[nt][i] + bb) * q_scale);
+      *reinterpret_cast<bf16x4*>(pimg + (d * 16 + 4 * g) * 2) = v;
+    }
+  }
+  __syncthreads();  // every wave is done with the Wqg image
+#if defined(RF_GF_DIAG) && (RF_GF_DIAG & 2)
+  return;
+#endif
+  dma_head(wkg);
+  wait_vmcnt0();
+  __syncthreads();
+  bf16x8 pb[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int rb = 32 * s + 8 * g + q4;
+    const bf16x4 v0 = tr_read_g(pimg + (rb * 16 + 4 * p4) * 2);
+    const bf16x4 v1 = tr_read_g(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
+    pb[s] = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  }
+  const int rw = r0 + 16 * wave + li;  // C column n = li -> this wave's row li
+  const bool wr = rw < R && gidx[rw] >= 0;
+  bf16* hi = ws.u16 + ((int64_t)rw * 2 * GF_HP + h) * D + 4 * g;
+  bf16* lo = hi + (int64_t)GF_HP * D;
+#pragma unroll 4
+  for (int ct = 0; ct < D / 16; ++ct) {
+    const int c0 = 16 * ct;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int rb = 32 * s + 8 * g + q4;
+      const bf16x4 v0 = tr_read_g(smem + gimg(rb, c0 + 4 * p4));
+      const bf16x4 v1 = tr_read_g(smem + gimg(rb + 4, c0 + 4 * p4));
+      const bf16x8 wa = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, pb[s], acc, 0, 0, 0);
+    }
+    // C[col c0+4g+i][row li]
+#if defined(RF_GF_DIAG) && (RF_GF_DIAG & 1)
+    if (acc[0] == 1234.5f) {
+#else
+    if (wr) {
+#endif
+      bf16x4 vh, vl;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        vh[i] = (bf16)acc[i];
+        vl[i] = (bf16)(acc[i] - (float)vh[i]);
+      }
+      *reinterpret_cast<bf16x4*>(hi + c0) = vh;
+      *reinterpret_cast<bf16x4*>(lo + c0) = vl;
+    }
+  }
+}
+
+// ---- bf16 merge + out on MFMA, 64 global rows per block ----------------------------------------
+// grid (H, ceil(R/64)). w_h[row] = sum_c exp(m_c - M) w_c / sum_c exp(m_c - M) l_c is formed in
+// registers from the fp32 chunk partials and split into hi + lo bf16 (MFMA B operand);
+// out[row][h*64+d] = Wvg[h*64+d] . w_h[row] + bvg, with the head's Wvg slice in LDS.
+template <int D>
+__global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax, int nch,
+                                                         const bf16* __restrict__ wvg,
+                                                         const float* __restrict__ bvg,
+                                                         const int32_t* __restrict__ gidx, GfoldWs ws,
+                                                         bf16* __restrict__ out, int ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NK = D / 32;
+  constexpr int nseg = D >> 6;
+  const int h = blockIdx.x, r0 = blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  for (int p = wave; p < nseg * 8; p += 4) {
+    const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
+    const int chk = (lane & 7) ^ (row & 7);
+    glds16(wvg + (int64_t)(h * 64 + row) * D + seg * 64 + chk * 8, smem + (seg * 64 + (p & 7) * 8) * 128);
+  }
+  const int r = r0 + 16 * wave + li;
+  const int pos = r < R ? gidx[r] : -1;
+  const int rr = pos >= 0 ? r : 0;  // rows without a global token read row 0's partials, unused
+  float mx = GF_NEG_INF;
+  for (int c = 0; c < nch; ++c) mx = fmaxf(mx, ws.m[((int64_t)rr * nch + c) * GF_HP + h]);
+  float lsum = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    const float mc = ws.m[((int64_t)rr * nch + c) * GF_HP + h];
+    lsum += (mc == GF_NEG_INF ? 0.f : __expf(mc - mx)) * ws.l[((int64_t)rr * nch + c) * GF_HP + h];
+  }
+  const float inv = lsum > 0.f ? 1.0f / lsum : 0.f;
+  wait_vmcnt0();
+  __syncthreads();
+  f32x4 acc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* wbase = ws.w + ((int64_t)rr * nch * GF_HP + h) * D + 8 * g;
+#pragma unroll 2
+  for (int s = 0; s < NK; ++s) {
+    float w8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nch; ++c) {
+      const float mc = ws.m[((int64_t)rr * nch + c) * GF_HP + h];
+      const float sc = (mc == GF_NEG_INF ? 0.f : __expf(mc - mx)) * inv;
+      const float* wp = wbase + (int64_t)c * GF_HP * D + 32 * s;
+#if defined(RF_GF_DIAG) && (RF_GF_DIAG & 4)
+      const float4 x0 = make_float4(sc, sc, sc, (float)s), x1 = x0; (void)wp;
+#else
+      const float4 x0 = *reinterpret_cast<const float4*>(wp);
+      const float4 x1 = *reinterpret_cast<const float4*>(wp + 4);
+#endif
+      w8[0] = fmaf(sc, x0.x, w8[0]); w8[1] = fmaf(sc, x0.y, w8[1]);
+      w8[2] = fmaf(sc, x0.z, w8[2]); w8[3] = fmaf(sc, x0.w, w8[3]);
+      w8[4] = fmaf(sc, x1.x, w8[4]); w8[5] = fmaf(sc, x1.y, w8[5]);
+      w8[6] = fmaf(sc, x1.z, w8[6]); w8[7] = fmaf(sc, x1.w, w8[7]);
+    }
+    bf16x8 bh, bl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bh[i] = (bf16)w8[i];
+      bl[i] = (bf16)(w8[i] - (float)bh[i]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const bf16x8 wa = *reinterpret_cast<const bf16x8*>(smem + gimg(16 * nt + li, 32 * s + 8 * g));
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bh, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bl, acc[nt], 0, 0, 0);
+    }
+  }
+  // C[d 16nt+4g+i][row li]
+  if (pos >= 0) {
+    bf16* o = out + ((int64_t)(r / gmax) * Lp + pos) * ldo + h * 64 + 4 * g;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (bf16)(acc[nt][i] + bvg[h * 64 + 16 * nt + 4 * g + i]);
+      *reinterpret_cast<bf16x4*>(o + 16 * nt) = v;
+    }
+  }
+}
+
 template <int D>
 __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
                                                              const bf16* __restrict__ hs, int ldh,
@@ -212,9 +410,9 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     const bf16* uhi = ws.u16 + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
     const bf16* ulo = uhi + (int64_t)GF_HP * D;
 #pragma unroll
-    for (int s = 0; s < NK; ++s) {
-      uh[s] = *reinterpret_cast<const bf16x8*>(uhi + 32 * s);
-      ul[s] = *reinterpret_cast<const bf16x8*>(ulo + 32 * s);
+    for (int s = 0; s < NK; ++s) {  // heads >= H: zero scores (their u rows are not written)
+      uh[s] = li < H ? *reinterpret_cast<const bf16x8*>(uhi + 32 * s) : bf16x8{};
+      ul[s] = li < H ? *reinterpret_cast<const bf16x8*>(ulo + 32 * s) : bf16x8{};
     }
   }
   char* pimg = smem + nseg * 64 * 128;                         // P [64 rows][16 heads] bf16
@@ -468,6 +666,17 @@ extern "C" size_t rf_global_fold_workspace(int B, int Lp, int D, int H, int gmax
   return gfold_bytes(B * gmax, nch, H, D);
 }
 
+// The 64-row MFMA kernels for qg/u and out amortise each head's weight slice over 64 global rows
+// but launch only H * R/64 blocks; below a few hundred global rows (one CLS row per 1024-token
+// sequence, C2) the per-row GEMV kernels fill the chip better (tools/gfold_bench.py: C2 R=64
+// 28 vs 66 us; catalog R=4096 970 vs 155 us). RF_GFOLD_PATH=gemv|mfma forces one.
+static bool gfold_use_mfma(int R) {
+  const char* e = getenv("RF_GFOLD_PATH");
+  if (e && e[0] == 'g') return false;
+  if (e && e[0] == 'm') return true;
+  return R >= 256;
+}
+
 // partial + out stages shared by both entry points (u already in the workspace)
 static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
                             const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax,
@@ -490,8 +699,21 @@ static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* 
         RF_REQUIRE(false, "rf_global_attn_fold(bf16): unsupported hidden size %d", D);
     }
 #undef GP_
-    k_gfold_out<bf16><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const bf16*)wvg, bvg, gidx, ws,
-                                                      (bf16*)out, ld_out);
+    if (ld_out % 4 == 0 && gfold_use_mfma(R)) {
+      const size_t lds_w = (size_t)D * 128;
+#define GO_(DD)                                                                                 \
+  case DD:                                                                                      \
+    (void)hipFuncSetAttribute((const void*)k_gfold_out_mfma<DD>,                                \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w);          \
+    k_gfold_out_mfma<DD><<<dim3(H, (R + 63) / 64), 256, lds_w, s>>>(Lp, R, gmax, nch, (const bf16*)wvg, \
+                                                                   bvg, gidx, ws, (bf16*)out, ld_out); \
+    break;
+      switch (D) { GO_(64) GO_(128) GO_(192) GO_(256) GO_(384) GO_(512) GO_(768) GO_(1024) }
+#undef GO_
+    } else {
+      k_gfold_out<bf16><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const bf16*)wvg, bvg, gidx, ws,
+                                                        (bf16*)out, ld_out);
+    }
   } else {
     const size_t lds_p = (size_t)(H * (D + 4) + H * GF_CHF) * sizeof(float);
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
@@ -554,7 +776,20 @@ extern "C" int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H,
   const int nch = (Lp + (dtype == RF_BF16 ? GF_CH : GF_CHF) - 1) / (dtype == RF_BF16 ? GF_CH : GF_CHF);
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
-  if (dtype == RF_BF16)
+  if (dtype == RF_BF16 && gfold_use_mfma(R)) {
+    RF_REQUIRE(D % 64 == 0 && D <= 1024, "rf_global_attn_fold_h_fwd: D=%d", D);
+    const size_t lds_q = (size_t)D * 128 + 4 * 2048;
+#define GQ_(DD)                                                                                   \
+  case DD:                                                                                        \
+    (void)hipFuncSetAttribute((const void*)k_gfold_qu_mfma<DD>,                                   \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q);            \
+    k_gfold_qu_mfma<DD><<<dim3(H, (R + 63) / 64), 256, lds_q, s>>>(Lp, R, gmax, (const bf16*)h, ldh, \
+                                                                  (const bf16*)wqg, bqg, q_scale,  \
+                                                                  (const bf16*)wkg, gidx, ws);     \
+    break;
+    switch (D) { GQ_(64) GQ_(128) GQ_(192) GQ_(256) GQ_(384) GQ_(512) GQ_(768) GQ_(1024) default: break; }
+#undef GQ_
+  } else if (dtype == RF_BF16)
     k_gfold_qu<bf16><<<dim3(GF_HP, R), 256, 0, s>>>(Lp, D, H, gmax, (const bf16*)h, ldh, (const bf16*)wqg, bqg,
                                                      q_scale, (const bf16*)wkg, gidx, ws, true);
   else

@@ -299,6 +299,36 @@ def test_global_attention_fold_from_h(dev, dt, case):
     assert ctx_a.abs().sum().item() > 0
 
 
+@pytest.mark.parametrize("B,Lp,H", [(300, 64, 12), (70, 192, 3), (5, 1024, 12)])
+def test_global_fold_mfma_matches_gemv(dev, monkeypatch, B, Lp, H):
+    """The 64-row MFMA qg/u and out kernels (chosen for >= 256 global rows, e.g. a catalog of
+    short item sequences) against the per-row GEMV kernels (pinned to the torch reference by
+    test_band_and_global_attention) on the same inputs: ragged lengths, sequences without a
+    global token (gidx -1), several globals per sequence and a partial last 64-row tile."""
+    dt = torch.bfloat16
+    D = H * 64
+    g = torch.Generator().manual_seed(B)
+    lens = [int(x) for x in torch.randint(1, Lp + 1, (B,), generator=g)]
+    lens[0] = Lp
+    globals_ = [(b, 0) for b in range(B) if b % 7 != 3] + [(b, lens[b] - 1) for b in range(0, B, 5)]
+    _, _, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, lens, globals_, 3)
+    h = _rand((B * Lp, D), dev, dt, 1.0, seed=60)
+    w = [_rand((D, D), dev, dt, 0.05, seed=61 + i) for i in range(3)]
+    bias = [_rand((D,), dev, torch.float32, 0.1, seed=64 + i) for i in range(3)]
+    outs = {}
+    for path in ("gemv", "mfma"):
+        monkeypatch.setenv("RF_GFOLD_PATH", path)
+        ctx = torch.zeros(B * Lp, D, dtype=dt, device=dev)
+        ops.global_attention_fold_h(h, w[0], bias[0], 0.125, w[1], bias[1], w[2], bias[2], flags, gidx, B, Lp, H,
+                                    ctx)
+        torch.cuda.synchronize()
+        outs[path] = ctx.float()
+    err = (outs["gemv"] - outs["mfma"]).abs().max().item()
+    assert err <= 2e-2, err
+    written = outs["mfma"].abs().sum(1) > 0
+    assert int(written.sum()) == int((gidx >= 0).sum())  # exactly the global rows are overwritten
+
+
 @pytest.mark.parametrize("N", [7, 1000, 100003])
 def test_ranker_matches_reference_formula(dev, N):
     """Ranker (rf_rank_accum + rf_cross_entropy_fwd) vs utils.py:76-108 restated (oracle), with
