@@ -94,6 +94,14 @@ int rf_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, int 
                      const float* w, const float* b, float eps, void* y, int ldy, float* y32,
                      float* mean, float* rstd, rf_stream_t stream);
 
+/* Residual add + LayerNorm, the reference's LayerNorm(dense(h) + input_tensor) (TF:1064-1071
+ * LongformerSelfOutput, TF:1123-1130 LongformerOutput): y = LN(x + res) with x the dense
+ * output (x_dtype, the bf16 GEMM output under autocast) and res the fp32 residual stream
+ * (M x D, contiguous). y32 (fp32 copy, M x D) may alias res: the stream is updated in place. */
+int rf_add_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, int ldx, const float* res,
+                         const float* w, const float* b, float eps, void* y, int ldy, float* y32,
+                         float* mean, float* rstd, rf_stream_t stream);
+
 /* A5 — LongformerSelfAttention local branch (TF:482-604 with _sliding_chunks_* 759-867,
  * _mask_invalid_locations 743-757, _concat_with_global_key_attn_probs 898-926,
  * _compute_attn_output_with_global_indices 928-962). q (pre-scaled), k, v are

@@ -32,6 +32,8 @@ SIGNATURES = {
                                  P, P, P, c_int, P]),
     "rf_layernorm_fwd":(c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_float, P, c_int, P,
                                  P, P, P]),
+    "rf_add_layernorm_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_float, P, c_int, P,
+                                     P, P, P]),
     "rf_band_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
                                  c_int, P, c_int, P]),
     "rf_global_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P,

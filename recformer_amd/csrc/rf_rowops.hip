@@ -212,12 +212,17 @@ __global__ void __launch_bounds__(256) k_embed_ln(
   }
 }
 
+// LayerNorm of one row per wave; with `res` (fp32, row stride D) the row is x + res first:
+// the reference's LayerNorm(dense(h) + input_tensor) (TF:1064-1071, 1123-1130) where, under
+// autocast, dense() returns bf16 and the residual input is fp32. y32 may alias res (the fp32
+// residual stream updated in place: every lane reads its whole row before the first store).
 template <typename TX, typename T, int VEC, int NCH>
 __global__ void __launch_bounds__(256) k_layernorm(int M, const TX* __restrict__ x, int ldx,
+                                                    const float* res,
                                                     const float* __restrict__ lw,
                                                     const float* __restrict__ lb, float eps,
                                                     T* __restrict__ y, int ldy,
-                                                    float* __restrict__ y32,
+                                                    float* y32,
                                                     float* __restrict__ mean_out,
                                                     float* __restrict__ rstd_out) {
   constexpr int D = 64 * VEC * NCH;
@@ -229,6 +234,12 @@ __global__ void __launch_bounds__(256) k_layernorm(int M, const TX* __restrict__
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     Vec<TX, VEC>::load(x + (int64_t)row * ldx + c * 64 * VEC + lane * VEC, xv[c]);
+    if (res) {
+      float rv[VEC];
+      Vec<float, VEC>::load(res + (int64_t)row * D + c * 64 * VEC + lane * VEC, rv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) xv[c][j] += rv[j];
+    }
 #pragma unroll
     for (int j = 0; j < VEC; ++j) s += xv[c][j];
   }
@@ -430,12 +441,12 @@ static int launch_embed(int M, int D, const int32_t* ids, const int32_t* pos, co
 }
 
 template <typename TX, typename T>
-static int launch_ln(int M, int D, const void* x, int ldx, const float* w, const float* b,
+static int launch_ln(int M, int D, const void* x, int ldx, const float* res, const float* w, const float* b,
                      float eps, void* y, int ldy, float* y32, float* mean, float* rstd,
                      hipStream_t s) {
   dim3 grid((M + 3) / 4);
 #define L_(V, N) \
-  k_layernorm<TX, T, V, N><<<grid, 256, 0, s>>>(M, (const TX*)x, ldx, w, b, eps, (T*)y, ldy, y32, mean, rstd)
+  k_layernorm<TX, T, V, N><<<grid, 256, 0, s>>>(M, (const TX*)x, ldx, res, w, b, eps, (T*)y, ldy, y32, mean, rstd)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
   RF_LAUNCH_CHECK("rf_layernorm_fwd");
@@ -487,17 +498,24 @@ int rf_embed_ln_fwd(int table_dtype, int out_dtype, int M, int D, const int32_t*
 int rf_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, int ldx,
                      const float* w, const float* b, float eps, void* y, int ldy, float* y32,
                      float* mean, float* rstd, rf_stream_t stream) {
+  return rf_add_layernorm_fwd(x_dtype, y_dtype, M, D, x, ldx, nullptr, w, b, eps, y, ldy, y32, mean, rstd,
+                              stream);
+}
+
+int rf_add_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, int ldx, const float* res,
+                         const float* w, const float* b, float eps, void* y, int ldy, float* y32,
+                         float* mean, float* rstd, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && ldx >= D && ldy >= D, "rf_layernorm_fwd: bad shape");
   if (M == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
   if (x_dtype == RF_BF16 && y_dtype == RF_BF16)
-    return launch_ln<bf16, bf16>(M, D, x, ldx, w, b, eps, y, ldy, y32, mean, rstd, s);
+    return launch_ln<bf16, bf16>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
   if (x_dtype == RF_F32 && y_dtype == RF_BF16)
-    return launch_ln<float, bf16>(M, D, x, ldx, w, b, eps, y, ldy, y32, mean, rstd, s);
+    return launch_ln<float, bf16>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
   if (x_dtype == RF_F32 && y_dtype == RF_F32)
-    return launch_ln<float, float>(M, D, x, ldx, w, b, eps, y, ldy, y32, mean, rstd, s);
+    return launch_ln<float, float>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
   if (x_dtype == RF_BF16 && y_dtype == RF_F32)
-    return launch_ln<bf16, float>(M, D, x, ldx, w, b, eps, y, ldy, y32, mean, rstd, s);
+    return launch_ln<bf16, float>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
   RF_REQUIRE(false, "rf_layernorm_fwd: bad dtypes %d/%d", x_dtype, y_dtype);
 }
 

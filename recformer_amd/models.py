@@ -398,8 +398,6 @@ class RecformerModel(nn.Module):
         # = False` keeps the reference's structure (k_g/v_g projected over all tokens).
         fold = getattr(cfg, "global_attention_fold", True)
         eps = cfg.layer_norm_eps
-        nl = len(pk["layers"])
-        res = None  # (pre-LN rows, mean, rstd, gamma, beta) of the residual, bf16 path
         for li, lw in enumerate(pk["layers"]):
             half_w = windows[li] // 2
             nq = 5 * D if (gmax > 0 and not fold) else 3 * D
@@ -426,27 +424,17 @@ class RecformerModel(nn.Module):
                 t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a, tag="gemm_ffn2")
                 h = h32 = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out=t2, tag="layernorm")
             else:
-                # bf16 path: the residual stream stays fp32 (the reference's autocast LayerNorm
-                # outputs fp32). It is never materialised: the residual-add GEMMs recompute
-                # LN(x) = (x - mean) * rstd * gamma + beta from the fp32 pre-LN rows x and the
-                # row stats the LayerNorm kernel wrote; LayerNorm itself only emits bf16.
-                if res is None:
-                    t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h32,
-                                 out_f32=True, tag="gemm_out")
-                else:
-                    t = ops.gemm_resid_ln(ctx, lw["w_o"], lw["b_o"], *res, tag="gemm_out")
-                a, m1, r1 = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], eps, out_dtype=dt, stats=True,
-                                          tag="layernorm")
+                # bf16 path, the reference under autocast: each dense output is bf16 (the GEMM
+                # epilogue rounds it, as autocast's Linear does), the residual stream and the
+                # LayerNorm are fp32 (TF:1064-1071, 1123-1130): LN(bf16 dense + fp32 stream) ->
+                # bf16 GEMM operand + fp32 stream, updated in place unless hidden states are kept.
+                t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
+                a, a32 = ops.add_layernorm(t, h32, lw["ln1_w"], lw["ln1_b"], eps, out_dtype=dt,
+                                           res_out=None if output_hidden_states else h32, tag="layernorm")
                 f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
-                t2 = ops.gemm_resid_ln(f, lw["w_2"], lw["b_2"], t, m1, r1, lw["ln1_w"], lw["ln1_b"],
-                                       tag="gemm_ffn2")
-                if li == nl - 1 or output_hidden_states:
-                    h, h32, m2, r2 = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out_dtype=dt,
-                                                   stats=True, want_f32=True, tag="layernorm")
-                else:
-                    h, m2, r2 = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out_dtype=dt,
-                                              stats=True, tag="layernorm")
-                res = (t2, m2, r2, lw["ln2_w"], lw["ln2_b"])
+                t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS, tag="gemm_ffn2")
+                h, h32 = ops.add_layernorm(t2, a32, lw["ln2_w"], lw["ln2_b"], eps, out_dtype=dt, res_out=a32,
+                                           tag="layernorm")
             if output_hidden_states:
                 hidden_all.append(h32)
         last = h32.view(B, Lp, D)[:, :L]

@@ -16,7 +16,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF
                    RF_EPI_NONE, RF_F32, check)
 
 __all__ = [
-    "dtype_code", "prepare_inputs", "embed_ln", "gemm", "layernorm", "band_attention",
+    "dtype_code", "prepare_inputs", "embed_ln", "gemm", "layernorm", "add_layernorm", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -229,6 +229,30 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
     if want_f32:
         return out, y32
     return out
+
+
+def add_layernorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
+                  out_dtype: Optional[torch.dtype] = None, res_out: Optional[torch.Tensor] = None,
+                  tag: Optional[str] = None):
+    """y = LN(x + res) (rf_add_layernorm_fwd): x the dense output (bf16 under autocast, as the
+    reference's Linear returns it), res the fp32 residual stream (M, D) contiguous. Returns
+    (y in out_dtype, y32 fp32); y32 is `res_out` when given, which may be `res` itself (the
+    stream updated in place)."""
+    lib = _lib.load()
+    _dev(x, res)
+    M, D = x.shape
+    if res.dtype != torch.float32 or not res.is_contiguous() or tuple(res.shape) != (M, D):
+        raise ValueError("add_layernorm: res must be a contiguous fp32 (M, D) tensor")
+    y = torch.empty(M, D, dtype=out_dtype or x.dtype, device=x.device)
+    y32 = res_out if res_out is not None else torch.empty(M, D, dtype=torch.float32, device=x.device)
+    if y32.dtype != torch.float32 or not y32.is_contiguous() or tuple(y32.shape) != (M, D):
+        raise ValueError("add_layernorm: res_out must be a contiguous fp32 (M, D) tensor")
+    with _region(tag):
+        rc = lib.rf_add_layernorm_fwd(dtype_code(x.dtype), dtype_code(y.dtype), M, D, _p(x), _rowmajor(x, "x"),
+                                      _p(res), _p(w), _p(b), float(eps), _p(y), _rowmajor(y, "y"), _p(y32),
+                                      None, None, _stream(x))
+    check(rc, "rf_add_layernorm_fwd")
+    return y, y32
 
 
 def band_attention(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int,

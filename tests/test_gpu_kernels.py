@@ -111,6 +111,22 @@ def test_layernorm(dev, dt, D):
     assert torch.allclose(mean, x.float().mean(1), atol=1e-4)
 
 
+@pytest.mark.parametrize("D", [128, 768])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_add_layernorm(dev, D, inplace):
+    """LN(bf16 dense + fp32 residual) -> bf16 + fp32 stream (TF:1064-1071 under autocast)."""
+    M = 333
+    x = _rand((M, D), dev, torch.bfloat16, 3.0, seed=17)
+    res = _rand((M, D), dev, torch.float32, 2.0, seed=18) + 0.5
+    w = _rand((D,), dev, torch.float32, seed=19)
+    b = _rand((D,), dev, torch.float32, seed=20)
+    ref = F.layer_norm(x.float() + res, (D,), w, b, 1e-5)
+    y, y32 = ops.add_layernorm(x, res, w, b, 1e-5, res_out=res if inplace else None)
+    assert (y32 - ref).abs().max().item() <= 1e-4
+    assert (y.float() - ref).abs().max().item() <= 2 ** -8 * ref.abs().max().item()
+    assert y.dtype == torch.bfloat16 and (y32.data_ptr() == res.data_ptr()) == inplace
+
+
 @pytest.mark.parametrize("tdt,dt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
                                      (torch.bfloat16, torch.bfloat16)])
 def test_embed_ln_and_prepare(dev, tdt, dt):
