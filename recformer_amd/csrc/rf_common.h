@@ -73,6 +73,20 @@ __device__ __forceinline__ float gelu_bf16out(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * p));
 }
 
+// gelu_bf16out on a pair (the same operations, so bit-identical): the multiplies, adds and
+// FMAs issue as v_pk_*_f32, one instruction per pair.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu2_bf16out(f32x2 x) {
+  const f32x2 x2 = __builtin_elementwise_min(x * x, (f32x2){64.0f, 64.0f});
+  const f32x2 p = __builtin_elementwise_fma(
+      __builtin_elementwise_fma((f32x2){0.0010142630552196598f, 0.0010142630552196598f}, x2,
+                                (f32x2){-0.1067757240026454f, -0.1067757240026454f}),
+      x2, (f32x2){-2.3011213394567367f, -2.3011213394567367f});
+  const f32x2 t = x * p;
+  const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.0f;
+  return x * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
 // Bijective XCD-aware remap of a 1-D block id (guide §5 T1): the hardware deals block ids
 // round-robin over the 8 XCDs; the returned index is contiguous per XCD, so blocks that share
 // data (neighbouring tiles, windows) run on one XCD's L2.

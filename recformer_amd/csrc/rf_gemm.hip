@@ -19,6 +19,8 @@
 // fp32 path: exact-f32 v_mfma_f32_16x16x4_f32, 64x64x16 tiles, register staging.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "rf_common.h"
 
 namespace rf {
@@ -493,17 +495,19 @@ __device__ __forceinline__ int wperm(int rho) {
 
 // n (4 or 8) consecutive columns [c0, c0 + n) of one output row; bv/gm/bt = bias / LN gamma /
 // LN beta for those columns (hoisted by the caller). Mirrors epi_row16 / epi_store.
-template <int EPI, bool CF32, bool RF32, int NV>
+// CHECK = false: interior tile (no bounds tests, EPI_COS row norm `rsc` from LDS), so the
+// epilogue holds no global load and hipcc places no vmcnt wait between its stores.
+template <int EPI, bool CF32, bool RF32, int NV, bool CHECK = true>
 __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float* v, const float* bv,
-                                        const float* gm, const float* bt) {
-  if (row >= e.M) return;
-  if (c0 + NV > e.N) {
+                                        const float* gm, const float* bt, float rsc = 0.f) {
+  if (CHECK && row >= e.M) return;
+  if (CHECK && c0 + NV > e.N) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) epi_store<bf16, EPI, CF32, RF32>(e, row, c0 + k, v[k]);
     return;
   }
   if (EPI == RF_EPI_COS) {
-    const float sc = e.ra[row] * e.col_scale;
+    const float sc = (CHECK ? e.ra[row] : rsc) * e.col_scale;
     float* out = reinterpret_cast<float*>(e.C) + (int64_t)row * e.ldc + c0;
 #pragma unroll
     for (int q = 0; q < NV / 4; ++q)
@@ -521,8 +525,17 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
     for (int k = 0; k < NV; ++k) v[k] *= e.col_scale;
   }
   if (EPI == RF_EPI_BIAS_GELU) {
+    if (CF32) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = CF32 ? gelu_erf(v[k]) : gelu_bf16out(v[k]);
+      for (int k = 0; k < NV; ++k) v[k] = gelu_erf(v[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; k += 2) {
+        const f32x2 y = gelu2_bf16out((f32x2){v[k], v[k + 1]});
+        v[k] = y.x;
+        v[k + 1] = y.y;
+      }
+    }
   }
   if (EPI == RF_EPI_BIAS_RESID) {
     if (RF32) {
@@ -593,6 +606,27 @@ __device__ __forceinline__ void load_cols(const EpiArgs& e, int c0, float* bv, f
     bv[4 * q] = b.x; bv[4 * q + 1] = b.y; bv[4 * q + 2] = b.z; bv[4 * q + 3] = b.w;
     gm[4 * q] = g.x; gm[4 * q + 1] = g.y; gm[4 * q + 2] = g.z; gm[4 * q + 3] = g.w;
     bt[4 * q] = t.x; bt[4 * q + 1] = t.y; bt[4 * q + 2] = t.z; bt[4 * q + 3] = t.w;
+  }
+}
+
+constexpr int CV_OFF = 8 * PP_HALF + 1024;  // LDS: ring, stamp area, then 2 x 3 column vectors
+
+template <int EPI, int NV>
+__device__ __forceinline__ void lds_cols(const float* cb, int co, float* bv, float* gm, float* bt) {
+#pragma unroll
+  for (int q = 0; q < NV / 4; ++q) {
+    const f32x4 b = *reinterpret_cast<const f32x4*>(cb + co + 4 * q);
+    f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f}, t = g;
+    if (EPI == RF_EPI_BIAS_RESID_LN) {
+      g = *reinterpret_cast<const f32x4*>(cb + 256 + co + 4 * q);
+      t = *reinterpret_cast<const f32x4*>(cb + 512 + co + 4 * q);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bv[4 * q + k] = b[k];
+      gm[4 * q + k] = g[k];
+      bt[4 * q + k] = t[k];
+    }
   }
 }
 
@@ -677,6 +711,24 @@ __global__ void __launch_bounds__(512, 1)
     glds16(base + (min(ra, lim) * ld + kt * 64 + pch), dst);
     glds16(base + (min(rb, lim) * ld + kt * 64 + pch), dst + 1024);
   };
+  // Epilogue column vectors of a tile (bias or EPI_COS item norms; LN gamma, beta) as one
+  // 1-KiB DMA per wave into LDS slot [parity][vector]: wave w loads vector w % 3 (vectors an
+  // epilogue does not have repeat the bias), so every wave issues exactly one DMA and the
+  // counted waits stay uniform. Source columns are clamped into [0, N): the ragged last
+  // column tile's out-of-range segments take the scalar epi_store path, never these values.
+  auto dma_cols = [&](int tm0, int tn0, int par) {
+    if (EPI == RF_EPI_NONE) return;
+    const int vec = wave % 3;
+    const float* src = EPI == RF_EPI_COS ? e.rw : e.bias;
+    int idx = min(tn0 + 4 * lane, e.N - 4);
+    if (EPI == RF_EPI_BIAS_RESID_LN && vec == 1) src = e.lgamma;
+    if (EPI == RF_EPI_BIAS_RESID_LN && vec == 2) src = e.lbeta;
+    if (EPI == RF_EPI_COS && vec == 1) {  // EPI_COS: the tile's 256 row norms
+      src = e.ra;
+      idx = min(tm0 + 4 * lane, e.M - 4);
+    }
+    glds16(src + idx, smem + CV_OFF + (par * 3 + vec) * 1024);
+  };
   auto prologue_dma = [&]() {  // K-tiles 0 and 1 complete
     dma(0, 0); dma(0, 1); dma(0, 2); dma(0, 3);
     dma(1, 0); dma(1, 1); dma(1, 2); dma(1, 3);
@@ -747,6 +799,7 @@ __global__ void __launch_bounds__(512, 1)
     }
   };
   set_tile(v);
+  dma_cols(m0, n0, 0);
   prologue_dma();
   int relax = 0;  // S stores of the previous (interior) tile may still be outstanding
   for (;;) {
@@ -801,38 +854,51 @@ __global__ void __launch_bounds__(512, 1)
     // [8c, 8c+8) (bf16) or [4c, 4c+4) u [64+4c, 64+4c+4) (fp32) of the wave's 128 (wperm)
     const int erow = em0 + wr * 64 + 4 * (el >> 4);
     const int ecol = en0 + wc * 128 + (OUT32 ? 4 : 8) * (el & 15);
-    float bv[8], gm[8], bt[8];  // column vectors, loaded before the next tile's DMAs
-    if (OUT32) {
-      load_cols<EPI, 4>(e, ecol, bv, gm, bt);
-      load_cols<EPI, 4>(e, ecol + 64, bv + 4, gm + 4, bt + 4);
-    } else {
-      load_cols<EPI, 8>(e, ecol, bv, gm, bt);
+    // column vectors of this tile: DMA'd into LDS with its prologue (retired by the K-loop's
+    // counted waits, published by its barriers), so the epilogue issues no global load
+    float bv[8], gm[8], bt[8];
+    const float* cb = reinterpret_cast<const float*>(smem + CV_OFF + (tix & 1) * 3 * 1024);
+    {
+      const int co = ecol - en0;
+      if (OUT32) {
+        lds_cols<EPI, 4>(cb, co, bv, gm, bt);
+        lds_cols<EPI, 4>(cb, co + 64, bv + 4, gm + 4, bt + 4);
+      } else {
+        lds_cols<EPI, 8>(cb, co, bv, gm, bt);
+      }
     }
     v += gridDim.x;
     if (has_next) {
       set_tile(v);
       launder();
+      dma_cols(m0, n0, (tix + 1) & 1);  // before the prologue DMAs: the first counted waits cover it
       if (pf) dma(1, 3);  // the rest of the next tile's K-tiles 0, 1 went out in the last iteration
       else prologue_dma();
     }
     asm volatile("" ::: "memory");
     stamp(4);
-    // Epilogue straight from the accumulators: whole-line vector stores, no LDS
+    // Epilogue straight from the accumulators: whole-line vector stores
+    auto epilogue = [&](auto check) {
+      constexpr bool CK = decltype(check)::value;
 #pragma unroll
-    for (int mf = 0; mf < 4; ++mf)
+      for (int mf = 0; mf < 4; ++mf)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float vv[8];
+        for (int r = 0; r < 4; ++r) {
+          float vv[8];
 #pragma unroll
-        for (int f = 0; f < 8; ++f) vv[f] = acc[mf][f][r];
-        const int row = erow + mf * 16 + r;
-        if (OUT32) {
-          epi_seg<EPI, CF32, RF32, 4>(e, row, ecol, vv, bv, gm, bt);
-          epi_seg<EPI, CF32, RF32, 4>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4);
-        } else {
-          epi_seg<EPI, CF32, RF32, 8>(e, row, ecol, vv, bv, gm, bt);
+          for (int f = 0; f < 8; ++f) vv[f] = acc[mf][f][r];
+          const int row = erow + mf * 16 + r;
+          const float rsc = EPI == RF_EPI_COS ? cb[256 + row - em0] : 0.f;
+          if (OUT32) {
+            epi_seg<EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+            epi_seg<EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
+          } else {
+            epi_seg<EPI, CF32, RF32, 8, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+          }
         }
-      }
+    };
+    if (interior) epilogue(std::false_type{});
+    else epilogue(std::true_type{});
     asm volatile("" ::: "memory");
     stamp(5);
     ++tix;
@@ -862,7 +928,7 @@ static int num_cus() {
 template <int EPI, bool CF32, bool RF32>
 static void launch_pp(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
                       hipStream_t s) {
-  constexpr size_t lds = 8 * PP_HALF + 1024;  // ring + diagnostic stamp area
+  constexpr size_t lds = CV_OFF + 6 * 1024;  // ring + diagnostic stamp area + column vectors
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)k_gemm_pp<EPI, CF32, RF32>,
@@ -905,6 +971,14 @@ static int gemm_variant() {
 }
 
 
+// The ping-pong kernel DMAs its epilogue column vectors (and EPI_COS row norms) as 16-B
+// pieces: they must be 16-B aligned with N (M for the row norms) a multiple of 4.
+static bool pp_cols_ok(int M, int N, const EpiArgs& e) {
+  auto al16 = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return N >= 4 && N % 4 == 0 && al16(e.bias) && al16(e.rw) && al16(e.lgamma) && al16(e.lbeta) &&
+         (e.ra == nullptr || (M >= 4 && M % 4 == 0 && al16(e.ra)));
+}
+
 template <int EPI, bool CF32, bool RF32>
 static void dispatch_tile(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                           const EpiArgs& e, hipStream_t s) {
@@ -916,7 +990,13 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
       case 2: launch_bf16<256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 3: launch_bf16<128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 4: launch_bf16<256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
-      case 5: launch_pp<EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 5:
+        if (pp_cols_ok(M, N, e)) {
+          launch_pp<EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+          break;
+        }
+        launch_bf16<256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+        break;
       default: launch_bf16<256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
     }
   } else {

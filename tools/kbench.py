@@ -30,8 +30,9 @@ def gemm_bench():
     dev = torch.device("cuda")
     M = 65536
     cases = [("qkv3", 2304, 768, ops.RF_EPI_BIAS, False), ("qkv5", 3840, 768, ops.RF_EPI_BIAS, False),
-             ("out", 768, 768, ops.RF_EPI_BIAS_RESID, True), ("ffn1", 3072, 768, ops.RF_EPI_BIAS_GELU, False),
-             ("ffn2", 768, 3072, ops.RF_EPI_BIAS_RESID, True), ("ffn1_nogelu", 3072, 768, ops.RF_EPI_BIAS, False)]
+             ("out", 768, 768, ops.RF_EPI_BIAS, False), ("ffn1", 3072, 768, ops.RF_EPI_BIAS_GELU, False),
+             ("ffn2", 768, 3072, ops.RF_EPI_BIAS, False), ("ffn1_nogelu", 3072, 768, ops.RF_EPI_BIAS, False),
+             ("ffn2_resid32", 768, 3072, ops.RF_EPI_BIAS_RESID, True)]
     for name, N, K, epi, f32 in cases:
         a = (torch.randn(M, K, device=dev) * 0.5).bfloat16()
         w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
