@@ -18,7 +18,7 @@ import re
 import sys
 
 EPI_TAG = {1: "gemm_qkv", 2: "gemm_ffn1", 3: "gemm_out", 4: "gemm_cos"}
-SIMPLE = ("k_band_attn", "k_gfold_partial", "k_gfold_u", "k_gfold_out", "k_layernorm",
+SIMPLE = ("k_band_attn", "k_gfold_partial", "k_gfold_qu", "k_gfold_u", "k_gfold_out", "k_layernorm",
           "k_embed_ln", "k_prepare", "k_gather_rows", "k_row_inv_norm", "k_cos_cand",
           "k_global_attn", "k_gemm_f32")
 
@@ -31,10 +31,12 @@ def tagger():
         mp = re.search(r"k_gemm_pp<(\d+),", name)
         if m or mp:
             bm, epi = (int(m.group(1)), int(m.group(3))) if m else (256, int(mp.group(1)))
-            if epi == 5:
+            if epi == 5:  # residual + LN recompute epilogue (training / older runs)
                 t = "gemm_ffn2" if last[0] == "gemm_ffn1" else "gemm_out"
             elif epi == 1 and bm == 128:
                 t = "gemm_qg"
+            elif epi == 1:  # bias epilogue: qkv, out-proj and FFN2 by their order in a layer
+                t = {"gemm_ffn1": "gemm_ffn2", "gemm_qkv": "gemm_out"}.get(last[0], "gemm_qkv")
             else:
                 t = EPI_TAG.get(epi, f"gemm_epi{epi}")
             last[0] = t
