@@ -361,13 +361,18 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe(int Lp, int H, int qpb, 
   const int ks = min(16 * wave, 32);  // first window row of the wave's 96-key span
   const int myw = 32 + 16 * wave + li;  // this lane's query row inside the 128-row window
   for (int x = x0; x < x1; ++x) {
-    wait_vm_small((x + 2 <= x1 ? 4 : 0) + (x + 1 < x1 ? 2 : 0) + (x > x0 ? 4 : 0));
+    wait_vm_small((x + 2 <= x1 ? 4 : 0) + (x + 1 < x1 ? 2 : 0) + (x > x0 ? 2 : 0));
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int i0 = 64 * x;
-    const int myq = i0 + 16 * wave + li;
     const unsigned long long ml0 = mk[2 * (x - x0)], ml1 = mk[2 * (x - x0) + 2];
     const unsigned long long mv0 = mk[2 * (x - x0) + 1], mv1 = mk[2 * (x - x0) + 3];
+#if defined(RF_BAND_DIAG) && (RF_BAND_DIAG & 1)
+    float lsum = 1.f;
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#else
     const char* qs = smem + AP_Q + (x & 1) * 8192;
     bf16x8 qf[2];
 #pragma unroll
@@ -509,26 +514,337 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe(int Lp, int H, int qpb, 
       }
     }
 
+#endif
     lsum += __shfl_xor(lsum, 16, 64);
     lsum += __shfl_xor(lsum, 32, 64);
     const unsigned long long qmw = (myw >> 6) ? mv1 : mv0;
     const bool qvalid = (qmw >> (myw & 63)) & 1ull;
     const float inv = (qvalid && lsum > 0.f) ? 1.0f / lsum : 0.f;
 
-    // every wave is done with chunk slot x%3 and Q slot x&1: refill them two blocks ahead
+    // every wave is done with chunk slot x%3 and Q slot x&1: refill them two blocks ahead.
+    // First the slot's K rows 16w..16w+15 (exactly what this wave's chunk DMA will overwrite)
+    // stage the wave's 16 x 64 O tile, so it leaves as whole 128-B lines (8 rows x 128 B per
+    // store instruction) instead of 16 rows x 32 B partial lines.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (x + 3 <= x1) dma_chunk(x + 3);
-    if (x + 2 < x1) dma_q(x + 2);
-
-    bf16* orow = out + (rb + myq) * ldo + hoff + 4 * g;
+    char* ostg = smem + AP_KV + (x % 3) * 16384 + wave * 2048;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x4 w;
 #pragma unroll
       for (int r = 0; r < 4; ++r) w[r] = (bf16)(qvalid ? o[dt][r] * inv : 0.f);
-      *reinterpret_cast<bf16x4*>(orow + 16 * dt) = w;
+      *reinterpret_cast<bf16x4*>(ostg + li * 128 + (((2 * dt + (g >> 1)) ^ (li & 7)) << 4) + (g & 1) * 8) = w;
+    }
+    bf16x8 ov[2];
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2) {
+      const int orow = 8 * p2 + (lane >> 3);
+      ov[p2] = *reinterpret_cast<const bf16x8*>(ostg + orow * 128 + (((lane & 7) ^ (orow & 7)) << 4));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staged O read back before the DMA lands
+    if (x + 3 <= x1) dma_chunk(x + 3);
+    if (x + 2 < x1) dma_q(x + 2);
+#if !(defined(RF_BAND_DIAG) && (RF_BAND_DIAG & 2))
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2) {
+      const int orow = 8 * p2 + (lane >> 3);
+      *reinterpret_cast<bf16x8*>(out + (rb + i0 + 16 * wave + orow) * ldo + hoff + (lane & 7) * 8) = ov[p2];
+    }
+#else
+    if (ov[0][0] == (bf16)1234.5f && inv == 3.f) out[rb] = (bf16)1.f;
+#endif
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ------------------------------------------------------------------------------------
+// k_band_attn_pipe2: the pipelined kernel above with its per-block instruction count cut
+// (it is issue-bound at two waves per SIMD, not HBM-bound):
+//  - each wave scores exactly its band: keys [16w-32, 16w+48) of the block = 5 key tiles
+//    (was 6), the PV tail step pairs tile 4 with zero probabilities;
+//  - global keys are scored in the same pass (one max / exp / sum over local + global, no
+//    online rescale of O); their K fragments and V^T fragments are loop-invariant registers;
+//  - masks: one bit-extract + bit-select per score; ring-slot and DMA offsets are wave-uniform
+//    or 24-bit products precomputed per lane; V^T reads are batched 8 per wait.
+__device__ __forceinline__ void tr_read8(const uint32_t* a, bf16x4* v) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8\n\t"
+      "ds_read_b64_tr_b16 %1, %9\n\t"
+      "ds_read_b64_tr_b16 %2, %10\n\t"
+      "ds_read_b64_tr_b16 %3, %11\n\t"
+      "ds_read_b64_tr_b16 %4, %12\n\t"
+      "ds_read_b64_tr_b16 %5, %13\n\t"
+      "ds_read_b64_tr_b16 %6, %14\n\t"
+      "ds_read_b64_tr_b16 %7, %15\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7])
+      : "memory");
+}
+
+__device__ __forceinline__ float mask_score(unsigned int bits, int bit, float sv) {
+  const int m = (int)(bits << (31 - bit)) >> 31;  // 0 or -1 (v_bfe_i32)
+  return __int_as_float((m & __float_as_int(sv)) | (~m & (int)0xff800000u));  // v_bfi_b32
+}
+
+__global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb, const bf16* __restrict__ q,
+                                                          const bf16* __restrict__ k,
+                                                          const bf16* __restrict__ v, int ld,
+                                                          const uint8_t* __restrict__ flags,
+                                                          const int32_t* __restrict__ gidx, int gmax,
+                                                          bf16* __restrict__ out, int ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nqb = Lp >> 6;
+  const int nparts = (nqb + qpb - 1) / qpb;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int part = wg % nparts, bh = wg / nparts;
+  const int h = bh % H, b = bh / H;
+  const int x0 = part * qpb, x1 = min(nqb, x0 + qpb);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t rb = (int64_t)b * Lp;
+  const bf16* kb = k + rb * ld + h * 64;
+  const bf16* vb = v + rb * ld + h * 64;
+  const bf16* qb = q + rb * ld + h * 64;
+  bf16* ob = out + rb * ldo + h * 64;
+  int* gp = reinterpret_cast<int*>(smem + AP_GP);
+  unsigned long long* mk = reinterpret_cast<unsigned long long*>(smem + AP_MK);
+  const int gt = gmax > 16 ? 2 : (gmax > 0 ? 1 : 0);  // 16-key tiles of global keys
+
+  // ---- prologue: chunk masks, global keys ----
+  for (int c = x0 + wave; c <= x1; c += 4) {
+    const int row = 64 * c - 32 + lane;
+    const int f = (row >= 0 && row < Lp) ? flags[rb + row] : 0;
+    const unsigned long long ml = __ballot(f == 1), mv = __ballot(f != 0);
+    if (lane == 0) {
+      mk[2 * (c - x0)] = ml;
+      mk[2 * (c - x0) + 1] = mv;
+    }
+  }
+  if (gmax > 0) {
+    const int row = wave * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ (row & 7);
+    const int p = row < gmax ? gidx[(int64_t)b * gmax + row] : -1;
+    const uint32_t off = __umul24(p >= 0 ? p : 0, ld) + ch * 8;
+    glds16(kb + off, smem + AP_KG + wave * 1024);
+    glds16(vb + off, smem + AP_VG + wave * 1024);
+    if (threadIdx.x < 32) gp[threadIdx.x] = (int)threadIdx.x < gmax ? gidx[(int64_t)b * gmax + threadIdx.x] : -1;
+  }
+  const int prow = 16 * wave + (lane >> 3);  // DMA piece rows prow, prow + 8 (pieces 2w, 2w+1)
+  const int pch = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
+  auto dma_chunk = [&](int c) {
+    char* base = smem + AP_KV + (c % 3) * 16384 + wave * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kp = min(max(64 * c - 32 + prow + 8 * j, 0), Lp - 1);
+      const uint32_t off = __umul24(kp, ld) + pch;
+      glds16(kb + off, base + j * 1024);
+      glds16(vb + off, base + 8192 + j * 1024);
+    }
+  };
+  auto dma_q = [&](int x) {
+    char* base = smem + AP_Q + (x & 1) * 8192 + wave * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(qb + __umul24(64 * x + prow + 8 * j, ld) + pch, base + j * 1024);
+  };
+  dma_q(x0);
+  dma_chunk(x0);
+  dma_chunk(x0 + 1);  // x0 + 1 <= x1 always
+  if (x0 + 1 < x1) dma_q(x0 + 1);
+  if (x0 + 2 <= x1) dma_chunk(x0 + 2);
+
+  // per-lane LDS offsets: fragment reads of 16-row tiles (row li, 16-B chunk 4 s2 + g) and the
+  // transposed V reads (rows rr, rr + 16 of a 32-row key step; columns 16 dt + 4 (li & 3))
+  const int rr = 4 * g + (li >> 2);
+  int koff[2], voff[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) koff[s2] = li * 128 + (((4 * s2 + g) ^ (li & 7)) << 4);
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) voff[dt] = swz_el(rr, 16 * dt + 4 * (li & 3));
+  const uint32_t lds0 = lds_addr(smem);
+  const int myw = 32 + 16 * wave + li;  // this lane's query row in the 128-row window
+  // band bits of the wave's 80-key span [16w, 16w + 80): relative rows [li, li + 64]
+  const unsigned int band0 = ~0u << li, band2 = (2u << li) - 1u;
+
+  bf16x8 kgf[2][2], vgf[4];
+  unsigned int gbits = 0;
+  for (int x = x0; x < x1; ++x) {
+    // retire chunks x, x+1 and Q(x); still in flight (issue order, newest last): the O stores of
+    // block x-2, chunk x+2, Q(x+1), the O stores of block x-1
+    wait_vm_small((x - 2 >= x0 ? 2 : 0) + (x + 2 <= x1 ? 4 : 0) + (x + 1 < x1 ? 2 : 0) + (x > x0 ? 2 : 0));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (x == x0 && gt > 0) {  // loop-invariant global-key operands (DMA'd first, so landed)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          kgf[t][s2] = *reinterpret_cast<const bf16x8*>(smem + AP_KG + t * 2048 + koff[s2]);
+      uint32_t a[8];
+      bf16x4 vv[8];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        a[2 * dt] = lds0 + AP_VG + voff[dt];
+        a[2 * dt + 1] = lds0 + AP_VG + 16 * 128 + voff[dt];
+      }
+      tr_read8(a, vv);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        vgf[dt] = bf16x8{vv[2 * dt][0], vv[2 * dt][1], vv[2 * dt][2], vv[2 * dt][3],
+                         vv[2 * dt + 1][0], vv[2 * dt + 1][1], vv[2 * dt + 1][2], vv[2 * dt + 1][3]};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gbits |= (gp[16 * t + 4 * g + r] >= 0 ? 1u : 0u) << (4 * t + r);
+    }
+    const int i0 = 64 * x;
+    const int sb0 = AP_KV + (x % 3) * 16384, sb1 = AP_KV + ((x + 1) % 3) * 16384;
+    const unsigned long long ml0 = mk[2 * (x - x0)], ml1 = mk[2 * (x - x0) + 2];
+    const unsigned long long mv0 = mk[2 * (x - x0) + 1], mv1 = mk[2 * (x - x0) + 3];
+    bf16x8 qf[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      qf[s2] = *reinterpret_cast<const bf16x8*>(smem + AP_Q + (x & 1) * 8192 + 16 * wave * 128 + koff[s2]);
+
+    // ---- scores: 5 local key tiles (window rows 16w + 16t) + gt global tiles ----
+    f32x4 st[5], sg[2];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int rt = 16 * wave + 16 * t;
+      const char* kt = smem + (rt >= 64 ? sb1 : sb0) + (rt & 63) * 128;
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(kt + koff[s2]), qf[s2],
+                                                        st[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sg[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < gt) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          sg[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kgf[t][s2], qf[s2], sg[t], 0, 0, 0);
+      }
+    }
+    // allowed local keys: valid & local (chunk ballots) & band, as 3 words over the span,
+    // shifted right by 4g so score (t, r) is bit 16 (t & 1) + r of word t >> 1
+    unsigned int aw[3];
+    {
+      const int ks = 16 * wave;
+      const unsigned long long lo = ks ? ((ml0 >> ks) | (ml1 << (64 - ks))) : ml0;
+      const unsigned long long hi = ml1 >> ks;
+      aw[0] = ((unsigned int)lo & band0) >> (4 * g);
+      aw[1] = (unsigned int)(lo >> 32) >> (4 * g);
+      aw[2] = ((unsigned int)hi & band2) >> (4 * g);
+    }
+    float mx = RF_NEG_INF;
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[t][r] = mask_score(aw[t >> 1], 16 * (t & 1) + r, st[t][r]);
+        mx = fmaxf(mx, st[t][r]);
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sg[t][r] = t < gt ? mask_score(gbits, 4 * t + r, sg[t][r]) : RF_NEG_INF;
+        mx = fmaxf(mx, sg[t][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float nmu = (mx == RF_NEG_INF) ? 0.f : -mx * LOG2E;
+    float lsum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[t][r] = __builtin_amdgcn_exp2f(fmaf(st[t][r], LOG2E, nmu));
+        lsum += st[t][r];
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sg[t][r] = __builtin_amdgcn_exp2f(fmaf(sg[t][r], LOG2E, nmu));
+        lsum += sg[t][r];
+      }
+
+    // ---- O = P V: 3 key steps of 32 (the last pairs tile 4 with p = 0) + the global step ----
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = 2 * s2 + (j >> 2);
+        pf[j] = (bf16)(t < 5 ? st[t < 5 ? t : 4][j & 3] : 0.f);
+      }
+      const int ga = 16 * wave + 32 * s2, gb = s2 < 2 ? ga + 16 : ga;  // finite rows for p = 0
+      const uint32_t va = lds0 + (ga >= 64 ? sb1 : sb0) + 8192 + (ga & 63) * 128;
+      const uint32_t vb2 = lds0 + (gb >= 64 ? sb1 : sb0) + 8192 + (gb & 63) * 128;
+      uint32_t a[8];
+      bf16x4 vv[8];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        a[2 * dt] = va + voff[dt];
+        a[2 * dt + 1] = vb2 + voff[dt];
+      }
+      tr_read8(a, vv);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 vf = bf16x8{vv[2 * dt][0], vv[2 * dt][1], vv[2 * dt][2], vv[2 * dt][3],
+                                 vv[2 * dt + 1][0], vv[2 * dt + 1][1], vv[2 * dt + 1][2], vv[2 * dt + 1][3]};
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+      }
+    }
+    if (gt > 0) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[j] = (bf16)sg[j >> 2][j & 3];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vgf[dt], pf, o[dt], 0, 0, 0);
+    }
+
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    const unsigned long long qmw = (myw >> 6) ? mv1 : mv0;
+    const bool qvalid = (qmw >> (myw & 63)) & 1ull;
+    const float inv = (qvalid && lsum > 0.f) ? 1.0f / lsum : 0.f;
+
+    // every wave is done with chunk slot x%3 and Q slot x&1: stage O in the slot's K rows
+    // 16w..16w+15 (what this wave's chunk DMA overwrites next), then refill two blocks ahead
+    // and store O as whole 128-B lines
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    char* ostg = smem + sb0 + wave * 2048;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv);
+      *reinterpret_cast<bf16x4*>(ostg + li * 128 + (((2 * dt + (g >> 1)) ^ (li & 7)) << 4) + (g & 1) * 8) = w;
+    }
+    bf16x8 ov[2];
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2) {
+      const int orow = 8 * p2 + (lane >> 3);
+      ov[p2] = *reinterpret_cast<const bf16x8*>(ostg + orow * 128 + (((lane & 7) ^ (orow & 7)) << 4));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (x + 3 <= x1) dma_chunk(x + 3);
+    if (x + 2 < x1) dma_q(x + 2);
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2) {
+      const int orow = 8 * p2 + (lane >> 3);
+      *reinterpret_cast<bf16x8*>(ob + __umul24(i0 + 16 * wave + orow, ldo) + (lane & 7) * 8) = ov[p2];
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -689,7 +1005,8 @@ extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int hal
     if (gmax <= 32 && !getenv("RF_BAND_ONESHOT")) {
       // pipelined: runs of qpb query blocks per workgroup, >= ~3 workgroups per CU slot
       const int nqb = Lp / 64;
-      const int qpb = nqb >= 16 ? (nqb + 1) / 2 : nqb;
+      int qpb = nqb >= 16 ? (nqb + 1) / 2 : nqb;
+      if (const char* e = getenv("RF_BAND_QPB")) qpb = max(1, min(nqb, atoi(e)));  // A/B tools
       const int nparts = (nqb + qpb - 1) / qpb;
       const size_t lds = AP_MK + (size_t)(qpb + 1) * 16;
       static bool attr = false;
@@ -698,9 +1015,21 @@ extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int hal
         attr = true;
       }
       RF_REQUIRE(lds <= 80000, "rf_band_attn_fwd(bf16): Lp=%d too long for the pipelined kernel", Lp);
-      k_band_attn_pipe<<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
-                                                         (const bf16*)v, ld_qkv, flags, gidx, gmax,
-                                                         (bf16*)out, ld_out);
+      if (getenv("RF_BAND_V1")) {
+        k_band_attn_pipe<<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
+                                                           (const bf16*)v, ld_qkv, flags, gidx, gmax,
+                                                           (bf16*)out, ld_out);
+      } else {
+        static bool attr2 = false;
+        if (!attr2) {
+          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    80000);
+          attr2 = true;
+        }
+        k_band_attn_pipe2<<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
+                                                            (const bf16*)v, ld_qkv, flags, gidx, gmax,
+                                                            (bf16*)out, ld_out);
+      }
     } else {
       k_band_attn_bf16<<<(Lp / 64) * H * B, 256, 0, s>>>(Lp, (const bf16*)q, (const bf16*)k, (const bf16*)v,
                                                          ld_qkv, flags, gidx, gmax, (bf16*)out, ld_out, H);
