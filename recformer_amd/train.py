@@ -156,14 +156,18 @@ def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp
     o = o.reshape(B, Lp, H, hd) * valid[:, :, None, None]
     o = o.reshape(B * Lp, D)
     if gmax > 0:
-        # global query rows: key_global / value_global over all tokens (TF:964-1057), overwrite
-        hf = h.float()
-        kgl = (hf @ wkg.float().t() + bkg).view(B, Lp, H, hd)
-        vgl = (hf @ wvg.float().t() + bvg).view(B, Lp, H, hd)
+        # global query rows (TF:964-1057), overwrite; key_global / value_global over all tokens
+        # through the fold (rf_global.hip): s = (Wkg_h^T qg_h) . h_l + qg_h . bkg_h and
+        # out = Wvg_h (sum_l p_l h_l) + bvg_h, so no (B*Lp, D) projection is materialised and
+        # autograd differentiates the same algebra.
+        hf = h.float().view(B, Lp, D)
         qgh = qg.float().view(B, gmax, H, hd)
-        sgg = torch.einsum("bghd,blhd->bhgl", qgh, kgl).masked_fill(~valid[:, None, None, :], float("-inf"))
+        u = torch.einsum("bghd,hdk->bghk", qgh, wkg.float().view(H, hd, D))
+        sgg = torch.einsum("bghk,blk->bhgl", u, hf) + torch.einsum("bghd,hd->bhg", qgh, bkg.float().view(H, hd))[..., None]
+        sgg = sgg.masked_fill(~valid[:, None, None, :], float("-inf"))
         pg = torch.softmax(sgg, -1)
-        og = torch.einsum("bhgl,blhd->bghd", pg, vgl).reshape(B, gmax, D)
+        w = torch.einsum("bhgl,blk->bghk", pg, hf)
+        og = (torch.einsum("bghk,hdk->bghd", w, wvg.float().view(H, hd, D)) + bvg.float().view(H, hd)).reshape(B, gmax, D)
         rows = (torch.arange(B, device=q.device)[:, None] * Lp + gidx.clamp(min=0)).reshape(-1)
         keep = gv.reshape(-1)
         o = o.index_put((rows[keep],), og.reshape(-1, D)[keep])
