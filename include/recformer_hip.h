@@ -111,6 +111,20 @@ int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int half_w, const 
                      const void* k, const void* v, int ld_qkv, const uint8_t* flags,
                      const int32_t* gidx, int gmax, void* out, int ld_out, rf_stream_t stream);
 
+
+
+/* Backward of the local branch (A5/A9: gradient of LongformerSelfAttention's sliding-window
+ * attention TF:482-604 incl. its global-key columns TF:898-962), bf16 q/k/v/o/dout (q
+ * pre-scaled, as the forward), fp32 gradients (B*Lp, ld_grad) dq, dk, dv. Workspace outputs:
+ * lse2, delta (B*H*Lp fp32: row log2-sum-exp and dO.O), gds, gpr (B*H*Lp*gmax fp32: dS and P
+ * of the global-key columns; the caller reduces them into dk/dv at the global positions).
+ * Query rows with flag != 1 (padding, or global rows whose local output is overwritten) carry
+ * no gradient. Window 64 (half 32), head_dim 64, gmax <= 32. */
+int rf_band_attn_bwd(int B, int Lp, int H, int hd, int half_w, const void* q, const void* k,
+                     const void* v, int ld_qkv, const void* o, int ld_o, const void* dout, int ld_do,
+                     const uint8_t* flags, const int32_t* gidx, int gmax, float* dq, float* dk,
+                     float* dv, int ld_grad, float* lse2, float* delta, float* gds, float* gpr,
+                     rf_stream_t stream);
 /* A6 — global query rows, _compute_global_attn_output_from_hidden TF:964-1057 + the
  * overwrite TF:612-629: for every (b, g < count_b): ctx[gidx[b,g], h] =
  * softmax(qg[b*gmax+g, h] . kg[b, :, h]^T over valid keys) . vg[b, :, h]. */

@@ -16,7 +16,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF
                    RF_EPI_NONE, RF_F32, check)
 
 __all__ = [
-    "dtype_code", "prepare_inputs", "embed_ln", "gemm", "layernorm", "add_layernorm", "band_attention",
+    "dtype_code", "prepare_inputs", "embed_ln", "gemm", "layernorm", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -229,6 +229,34 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
     if want_f32:
         return out, y32
     return out
+
+
+def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, tag: Optional[str] = None):
+    """Gradient of the local branch (rf_band_attn_bwd): q/k/v (pre-scaled q) and o, dout bf16
+    (B*Lp, >=H*64) views; returns fp32 (dq, dk, dv) of shape (B*Lp, H*64) plus, when there are
+    global keys, gds / gpr (B, H, Lp, gmax): dS and P of the global-key columns."""
+    lib = _lib.load()
+    _dev(q, k, v, o, dout, flags)
+    ld = _rowmajor(q, "q")
+    if _rowmajor(k, "k") != ld or _rowmajor(v, "v") != ld:
+        raise ValueError("band_attention_bwd: q/k/v must share a leading dimension")
+    D = H * 64
+    gmax = gidx.shape[1]
+    dev = q.device
+    dq = torch.empty(B * Lp, D, dtype=torch.float32, device=dev)
+    dk = torch.empty_like(dq)
+    dv = torch.empty_like(dq)
+    lse2 = torch.empty(B * H * Lp, dtype=torch.float32, device=dev)
+    delta = torch.empty_like(lse2)
+    gds = torch.empty(B, H, Lp, max(gmax, 1), dtype=torch.float32, device=dev) if gmax else None
+    gpr = torch.empty_like(gds) if gmax else None
+    with _region(tag):
+        rc = lib.rf_band_attn_bwd(B, Lp, H, 64, 32, _p(q), _p(k), _p(v), ld, _p(o), _rowmajor(o, "o"), _p(dout),
+                                  _rowmajor(dout, "dout"), _p(flags), _p(gidx.contiguous()) if gmax else None,
+                                  gmax, _p(dq), _p(dk), _p(dv), D, _p(lse2), _p(delta), _p(gds), _p(gpr),
+                                  _stream(q))
+    check(rc, "rf_band_attn_bwd")
+    return dq, dk, dv, gds, gpr
 
 
 def add_layernorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,

@@ -12,8 +12,9 @@ whose backward is written out explicitly:
                backward: LN backward, then index_add into the four tables (no gradient at
                padding_idx rows of the word / position tables, as nn.Embedding)
   _Attention   sliding-window local + global attention (band kernel + global fold)
-               TF:482-1057; backward: the attention is recomputed in fp32 (block-window form,
-               plus the reference's key_global / value_global over all tokens) under autograd.
+               TF:482-1057; backward (bf16): the local branch on the HIP backward kernels
+               (rf_attn_bwd.hip; global-key columns reduced per sequence here), the global
+               rows by autograd over the fold algebra; fp32 mode: an fp32 recompute of both.
 
 Mixed precision follows the reference's autocast run (finetune.py:106-110): GEMM operands in
 bf16, LayerNorm outputs / residual stream / losses in fp32, parameters fp32 (the bf16 weight
@@ -109,10 +110,11 @@ class _EmbedLN(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------------
-def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, half_w: int):
-    """fp32 recompute of the attention block (same contract as the HIP kernels; used under
-    autograd by _Attention.backward). q, k, v (B*Lp, D) pre-scaled q; qg (B*gmax, D) pre-scaled;
-    h (B*Lp, D) the layer input; flags (B, Lp) {0 pad, 1 local, 2 global}; gidx (B, gmax)."""
+def _local_torch(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int):
+    """fp32 recompute of the local branch (band keys + the local K/V rows at the global
+    positions); padded query rows 0. q, k, v (B*Lp, D), q pre-scaled; flags (B, Lp)
+    {0 pad, 1 local, 2 global}; gidx (B, gmax). The global query rows' values are replaced by
+    the global branch in _attention_torch."""
     D = q.shape[1]
     hd = D // H
     f = flags.long()
@@ -154,23 +156,41 @@ def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp
     if gmax > 0:
         o = o + torch.einsum("bchig,bghd->bcihd", p[..., 2 * W:], vg_loc)
     o = o.reshape(B, Lp, H, hd) * valid[:, :, None, None]
-    o = o.reshape(B * Lp, D)
-    if gmax > 0:
-        # global query rows (TF:964-1057), overwrite; key_global / value_global over all tokens
-        # through the fold (rf_global.hip): s = (Wkg_h^T qg_h) . h_l + qg_h . bkg_h and
-        # out = Wvg_h (sum_l p_l h_l) + bvg_h, so no (B*Lp, D) projection is materialised and
-        # autograd differentiates the same algebra.
-        hf = h.float().view(B, Lp, D)
-        qgh = qg.float().view(B, gmax, H, hd)
-        u = torch.einsum("bghd,hdk->bghk", qgh, wkg.float().view(H, hd, D))
-        sgg = torch.einsum("bghk,blk->bhgl", u, hf) + torch.einsum("bghd,hd->bhg", qgh, bkg.float().view(H, hd))[..., None]
-        sgg = sgg.masked_fill(~valid[:, None, None, :], float("-inf"))
-        pg = torch.softmax(sgg, -1)
-        w = torch.einsum("bhgl,blk->bghk", pg, hf)
-        og = (torch.einsum("bghk,hdk->bghd", w, wvg.float().view(H, hd, D)) + bvg.float().view(H, hd)).reshape(B, gmax, D)
-        rows = (torch.arange(B, device=q.device)[:, None] * Lp + gidx.clamp(min=0)).reshape(-1)
-        keep = gv.reshape(-1)
-        o = o.index_put((rows[keep],), og.reshape(-1, D)[keep])
+    return o.reshape(B * Lp, D)
+
+
+def _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B: int, Lp: int, H: int):
+    """Global query rows (TF:964-1057), (B*gmax, D): key_global / value_global over all tokens
+    through the fold (rf_global.hip): s = (Wkg_h^T qg_h) . h_l + qg_h . bkg_h and
+    out = Wvg_h (sum_l p_l h_l) + bvg_h, so no (B*Lp, D) projection is materialised and autograd
+    differentiates the same algebra."""
+    D = h.shape[1]
+    hd = D // H
+    gmax = qg.shape[0] // B
+    valid = flags.long() != 0
+    hf = h.float().view(B, Lp, D)
+    qgh = qg.float().view(B, gmax, H, hd)
+    u = torch.einsum("bghd,hdk->bghk", qgh, wkg.float().view(H, hd, D))
+    sgg = torch.einsum("bghk,blk->bhgl", u, hf) + torch.einsum("bghd,hd->bhg", qgh, bkg.float().view(H, hd))[..., None]
+    sgg = sgg.masked_fill(~valid[:, None, None, :], float("-inf"))
+    pg = torch.softmax(sgg, -1)
+    w = torch.einsum("bhgl,blk->bghk", pg, hf)
+    og = torch.einsum("bghk,hdk->bghd", w, wvg.float().view(H, hd, D)) + bvg.float().view(H, hd)
+    return og.reshape(B * gmax, D)
+
+
+def _global_rows(gidx, B: int, Lp: int):
+    rows = (torch.arange(B, device=gidx.device)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
+    return rows, (gidx >= 0).reshape(-1)
+
+
+def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, half_w: int):
+    """fp32 recompute of the whole attention block (same contract as the HIP kernels)."""
+    o = _local_torch(q, k, v, flags, gidx, B, Lp, H, half_w)
+    if gidx.shape[1] > 0:
+        og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H)
+        rows, keep = _global_rows(gidx, B, Lp)
+        o = o.index_put((rows[keep],), og[keep])
     return o
 
 
@@ -186,13 +206,56 @@ class _Attention(torch.autograd.Function):
                 kg = ops.gemm(h.contiguous(), wkg.contiguous(), bkg, ops.RF_EPI_BIAS)
                 vg = ops.gemm(h.contiguous(), wvg.contiguous(), bvg, ops.RF_EPI_BIAS)
                 ops.global_attention(qg.contiguous(), kg, vg, flags, gidx, B, Lp, H, out)
-        ctx.save_for_backward(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx)
+        ctx.save_for_backward(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out)
         ctx.dims = (B, Lp, H, half_w)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx = ctx.saved_tensors
+        q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out = ctx.saved_tensors
+        B, Lp, H, half_w = ctx.dims
+        gmax = gidx.shape[1]
+        hip_local = q.dtype == torch.bfloat16 and half_w == 32 and q.shape[1] == 64 * H and gmax <= 32
+        if not hip_local:
+            return _Attention._backward_torch(ctx, dout)
+        # local branch on the HIP backward kernels (rf_attn_bwd.hip); global rows of dout belong
+        # to the global branch only (their local output was overwritten)
+        d16 = dout.to(torch.bfloat16).contiguous()
+        dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H)
+        D = q.shape[1]
+        res = [None] * 9
+        if gmax > 0:
+            rows, keep = _global_rows(gidx, B, Lp)
+            # gradients of the global-key columns, reduced over every query of the sequence
+            qh = q.float().view(B, Lp, H, 64)
+            dh = d16.float().view(B, Lp, H, 64)
+            dkg = torch.einsum("bhig,bihd->bghd", gds[..., :gmax], qh).reshape(B * gmax, D)
+            dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :gmax], dh).reshape(B * gmax, D)
+            dk.index_add_(0, rows[keep], dkg[keep])
+            dv.index_add_(0, rows[keep], dvg[keep])
+            # global branch through autograd over the fold algebra
+            gin = [t.detach().requires_grad_(need) for t, need in
+                   zip((qg, h, wkg, bkg, wvg, bvg), ctx.needs_input_grad[3:9])]
+            if any(t.requires_grad for t in gin):
+                with torch.enable_grad(), torch.autocast("cuda", enabled=False):
+                    og = _global_torch(*gin, flags, B, Lp, H)
+                    gout = torch.zeros_like(og)
+                    gout[keep] = dout[rows[keep]].float()
+                    want = [t for t in gin if t.requires_grad]
+                    grads = torch.autograd.grad(og, want, gout, allow_unused=True)
+                it = iter(grads)
+                for n, t in enumerate(gin):
+                    if t.requires_grad:
+                        g = next(it)
+                        res[3 + n] = None if g is None else g.to(t.dtype)
+        for n, (t, g) in enumerate(zip((q, k, v), (dq, dk, dv))):
+            if ctx.needs_input_grad[n]:
+                res[n] = g.to(t.dtype)
+        return (*res, None, None, None, None, None, None, None)
+
+    @staticmethod
+    def _backward_torch(ctx, dout):
+        q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, _ = ctx.saved_tensors
         B, Lp, H, half_w = ctx.dims
         inputs = [t.detach().requires_grad_(need) for t, need in
                   zip((q, k, v, qg, h, wkg, bkg, wvg, bvg), ctx.needs_input_grad[:9])]

@@ -82,3 +82,41 @@ def test_pretrain_training_step(dev):
     opt.step()
     out2 = m(**kw)
     assert torch.isfinite(out2.loss)
+
+
+@pytest.mark.parametrize("case", [
+    dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
+    dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
+    dict(B=1, Lp=128, H=1, lens=[128], globals_=()),
+    dict(B=2, Lp=1024, H=12, lens=[1024, 700], globals_=((0, 0), (1, 0), (1, 5))),
+])
+def test_band_attention_bwd_matches_autograd(dev, case):
+    """rf_band_attn_bwd (+ the per-sequence reduction of the global-key columns, as
+    train._Attention.backward does it) against autograd through the fp32 recompute of the local
+    branch (train._local_torch) on the same bf16 inputs; rows with flag != 1 get no gradient.
+    Tolerance: max-abs error <= 2e-2 x max |g| (P and dS enter the MFMAs as bf16)."""
+    from recformer_amd import ops
+    from recformer_amd.train import _global_rows, _local_torch
+    from tests.test_gpu_kernels import _attn_case
+    B, Lp, H = case["B"], case["Lp"], case["H"]
+    D = H * 64
+    qkv, merged, flags, gidx, G = _attn_case(dev, torch.bfloat16, B, Lp, H, case["lens"], case["globals_"], 11)
+    qkv[:, :D] = (qkv[:, :D].float() * 0.125).to(torch.bfloat16)  # pre-scaled, like the QKV GEMM output
+    q, k, v = (qkv[:, i * D:(i + 1) * D] for i in range(3))
+    out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, 32)
+    torch.manual_seed(1)
+    dout = torch.randn(B * Lp, D, device=dev).to(torch.bfloat16)
+    dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, dout, flags, gidx, B, Lp, H)
+    if G > 0:
+        rows, keep = _global_rows(gidx, B, Lp)
+        dkg = torch.einsum("bhig,bihd->bghd", gds[..., :G], q.float().view(B, Lp, H, 64)).reshape(B * G, D)
+        dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :G], dout.float().view(B, Lp, H, 64)).reshape(B * G, D)
+        dk.index_add_(0, rows[keep], dkg[keep])
+        dv.index_add_(0, rows[keep], dvg[keep])
+    qr, kr, vr = (t.float().detach().requires_grad_(True) for t in (q, k, v))
+    o = _local_torch(qr, kr, vr, flags, gidx, B, Lp, H, 32)
+    dmask = (flags.reshape(-1) == 1).float()[:, None]
+    ref = torch.autograd.grad(o, (qr, kr, vr), dout.float() * dmask)
+    for name, got, r in zip("qkv", (dq, dk, dv), ref):
+        err = float((got - r).abs().max())
+        assert err <= 2e-2 * max(float(r.abs().max()), 1e-6), (name, err, float(r.abs().max()))
