@@ -276,8 +276,10 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
   const bool wr = rw < R && gidx[rw] >= 0;
   bf16* hi = ws.u16 + ((int64_t)rw * 2 * GF_HP + h) * D + 4 * g;
   bf16* lo = hi + (int64_t)GF_HP * D;
+  // column split (gridDim.z): this block writes u columns [z D / nz, (z + 1) D / nz)
+  const int nct = D / 16 / gridDim.z, ct0 = blockIdx.z * nct;
 #pragma unroll 4
-  for (int ct = 0; ct < D / 16; ++ct) {
+  for (int ct = ct0; ct < ct0 + nct; ++ct) {
     const int c0 = 16 * ct;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -667,14 +669,15 @@ extern "C" size_t rf_global_fold_workspace(int B, int Lp, int D, int H, int gmax
 }
 
 // The 64-row MFMA kernels for qg/u and out amortise each head's weight slice over 64 global rows
-// but launch only H * R/64 blocks; below a few hundred global rows (one CLS row per 1024-token
-// sequence, C2) the per-row GEMV kernels fill the chip better (tools/gfold_bench.py: C2 R=64
-// 28 vs 66 us; catalog R=4096 970 vs 155 us). RF_GFOLD_PATH=gemv|mfma forces one.
-static bool gfold_use_mfma(int R) {
+// but launch only H * R/64 blocks; qg/u splits u's columns over up to 4 blocks and wins at any
+// R, while for out below a few hundred global rows (one CLS row per 1024-token sequence, C2)
+// the per-row GEMV kernel fills the chip better (tools/gfold_bench.py: C2 R=64 out 14.5 vs
+// 45 us; catalog R=4096 qu+out 970 vs 155 us). RF_GFOLD_PATH=gemv|mfma forces one.
+static bool gfold_use_mfma(int R, bool qu) {
   const char* e = getenv("RF_GFOLD_PATH");
   if (e && e[0] == 'g') return false;
   if (e && e[0] == 'm') return true;
-  return R >= 256;
+  return qu || R >= 256;  // qg/u: MFMA with a column split wins at any R (C2: 20 -> 12.5 us)
 }
 
 // partial + out stages shared by both entry points (u already in the workspace)
@@ -699,7 +702,7 @@ static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* 
         RF_REQUIRE(false, "rf_global_attn_fold(bf16): unsupported hidden size %d", D);
     }
 #undef GP_
-    if (ld_out % 4 == 0 && gfold_use_mfma(R)) {
+    if (ld_out % 4 == 0 && gfold_use_mfma(R, false)) {
       const size_t lds_w = (size_t)D * 128;
 #define GO_(DD)                                                                                 \
   case DD:                                                                                      \
@@ -776,14 +779,17 @@ extern "C" int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H,
   const int nch = (Lp + (dtype == RF_BF16 ? GF_CH : GF_CHF) - 1) / (dtype == RF_BF16 ? GF_CH : GF_CHF);
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
-  if (dtype == RF_BF16 && gfold_use_mfma(R)) {
+  if (dtype == RF_BF16 && gfold_use_mfma(R, true)) {
     RF_REQUIRE(D % 64 == 0 && D <= 1024, "rf_global_attn_fold_h_fwd: D=%d", D);
     const size_t lds_q = (size_t)D * 128 + 4 * 2048;
+    // few row tiles: split u's columns over more blocks (each recomputes its tile's qg)
+    int qsplit = 1;
+    while (qsplit < 4 && H * ((R + 63) / 64) * qsplit < 128 && (D / 16) % (2 * qsplit) == 0) qsplit *= 2;
 #define GQ_(DD)                                                                                   \
   case DD:                                                                                        \
     (void)hipFuncSetAttribute((const void*)k_gfold_qu_mfma<DD>,                                   \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q);            \
-    k_gfold_qu_mfma<DD><<<dim3(H, (R + 63) / 64), 256, lds_q, s>>>(Lp, R, gmax, (const bf16*)h, ldh, \
+    k_gfold_qu_mfma<DD><<<dim3(H, (R + 63) / 64, qsplit), 256, lds_q, s>>>(Lp, R, gmax, (const bf16*)h, ldh, \
                                                                   (const bf16*)wqg, bqg, q_scale,  \
                                                                   (const bf16*)wkg, gidx, ws);     \
     break;
