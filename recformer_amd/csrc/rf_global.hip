@@ -68,6 +68,11 @@ __device__ __forceinline__ bf16x4 tr_read_g(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_g*)p);
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // ---- u = Wkg_h^T qg_h ------------------------------------------------------------------
 // grid (16 heads, R): one block per (head, global row); thread t owns columns 4t..4t+3 of
 // Wkg_h (64 rows x D), reads them with 8-B vector loads (L2-resident weights) and dots them
@@ -278,7 +283,6 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
   bf16* lo = hi + (int64_t)GF_HP * D;
   // column split (gridDim.z): this block writes u columns [z D / nz, (z + 1) D / nz)
   const int nct = D / 16 / gridDim.z, ct0 = blockIdx.z * nct;
-#pragma unroll 4
   for (int ct = ct0; ct < ct0 + nct; ++ct) {
     const int c0 = 16 * ct;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -390,8 +394,194 @@ __global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax,
   }
 }
 
+// The chunk image is filled in two column halves (segments [0, D/128) and [D/128, D/64)),
+// each 12 (D=768) DMA pieces per wave: the scores' k-steps over half A run while half B lands,
+// and the next sub-chunk's half A / half B are issued as soon as every wave's P.H products
+// over that half are done — so the h stream overlaps the MFMA work instead of alternating
+// with it. Row validity comes from per-sub-chunk ballots taken in the prologue (no global
+// load inside the loop, whose hipcc wait would drain the DMA queue).
 template <int D>
 __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
+                                                             const bf16* __restrict__ hs, int ldh,
+                                                             const uint8_t* __restrict__ flags,
+                                                             const int32_t* __restrict__ gidx,
+                                                             GfoldWs ws, int H) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NK = D / 32;
+  constexpr int nseg = D >> 6;
+  constexpr int hseg = nseg / 2;        // segments per half
+  constexpr int nmt = D >> 6;            // 16-column tiles of W per wave (D/16 over 4 waves)
+  constexpr int hmt = nmt / 2;           // ... per half
+  constexpr int PPW = hseg * 8 / 4;      // DMA pieces per wave per half
+  if constexpr (nseg % 2 != 0) return;  // D not a multiple of 128: k_gfold_partial_bf16_1 instead
+  const int ch = blockIdx.x, r = blockIdx.y, nch = gridDim.x;
+  if (gidx[r] < 0) return;
+  const int b = r / gmax;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int q4 = li >> 2, p4 = li & 3;
+  char* pimg = smem + nseg * 64 * 128;                         // P [64 rows][16 heads] bf16
+  float* red = reinterpret_cast<float*>(pimg + 64 * 16 * 2);    // [max 4x16][sum 4x16][m 16][alpha 16]
+  float* m_run = red + 128;
+  float* alpha_s = red + 144;
+  unsigned long long* vmask = reinterpret_cast<unsigned long long*>(red + 160);  // per sub-chunk
+  const bf16* hb = hs + (int64_t)b * Lp * ldh;
+  const int row_begin = ch * GF_CH;
+  const int row_end = min(row_begin + GF_CH, Lp);
+  const int nsub = (row_end - row_begin + 63) >> 6;
+
+  auto dma_half = [&](int j0, int half) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wave * PPW + i;                     // piece within the half
+      const int seg = half * hseg + (p >> 3), row = (p & 7) * 8 + (lane >> 3);
+      const int chk = (lane & 7) ^ (row & 7);
+      const int jr = min(j0 + row, Lp - 1);
+      glds16(hb + (int64_t)jr * ldh + seg * 64 + chk * 8, smem + (seg * 64 + (p & 7) * 8) * 128);
+    }
+  };
+  // u fragments (B operand of S^T = H.U^T): hi and lo planes; heads >= H score 0
+  bf16x8 uh[NK], ul[NK];
+  {
+    const bf16* uhi = ws.u16 + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
+    const bf16* ulo = uhi + (int64_t)GF_HP * D;
+#pragma unroll
+    for (int s2 = 0; s2 < NK; ++s2) {
+      uh[s2] = li < H ? *reinterpret_cast<const bf16x8*>(uhi + 32 * s2) : bf16x8{};
+      ul[s2] = li < H ? *reinterpret_cast<const bf16x8*>(ulo + 32 * s2) : bf16x8{};
+    }
+  }
+  if (wave < nsub) {  // validity ballots of the (up to 4) 64-row sub-chunks
+    const int jr = row_begin + 64 * wave + lane;
+    const bool ok = jr < Lp && flags[(int64_t)b * Lp + jr] != 0;
+    const unsigned long long m = __ballot(ok);
+    if (lane == 0) vmask[wave] = m;
+  }
+  if (threadIdx.x < 16) m_run[threadIdx.x] = GF_NEG_INF;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // u fragments and flags, before the DMA stream
+  dma_half(row_begin, 0);
+  dma_half(row_begin, 1);
+  float l_run = 0.f;  // per head li (valid in wave 0, g == 0)
+  f32x4 acc[nmt];
+#pragma unroll
+  for (int i = 0; i < nmt; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int sub = 0; sub < nsub; ++sub) {
+    const int j0 = row_begin + 64 * sub;
+    const bool more = sub + 1 < nsub;
+    // S^T[j = 16*wave + 4g + q][head = li]: k-steps over half A, then half B
+    f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int arow = 16 * wave + li;
+    wait_vm_n<PPW>();  // half A landed (half B's PPW pieces may still fly)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int s2 = 0; s2 < NK / 2; ++s2) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + gimg(arow, 32 * s2 + 8 * g));
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, uh[s2], st, 0, 0, 0);
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ul[s2], st, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // half B landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int s2 = NK / 2; s2 < NK; ++s2) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + gimg(arow, 32 * s2 + 8 * g));
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, uh[s2], st, 0, 0, 0);
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ul[s2], st, 0, 0, 0);
+    }
+    const unsigned long long vm = vmask[sub];
+    float mx = GF_NEG_INF;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int jj = 16 * wave + 4 * g + q;
+      const bool ok = (vm >> jj) & 1ull;
+      st[q] = ok ? st[q] : GF_NEG_INF;
+      mx = fmaxf(mx, st[q]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (g == 0) red[wave * 16 + li] = mx;
+    __syncthreads();
+    const float m_old = m_run[li];
+    const float m_new = fmaxf(m_old, fmaxf(fmaxf(red[li], red[16 + li]), fmaxf(red[32 + li], red[48 + li])));
+    const float mu = (m_new == GF_NEG_INF) ? 0.f : m_new;
+    float ls = 0.f;
+    bf16* pt = reinterpret_cast<bf16*>(pimg);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float p = __expf(st[q] - mu);
+      ls += p;
+      pt[(16 * wave + 4 * g + q) * 16 + li] = (bf16)p;
+    }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    if (g == 0) red[64 + wave * 16 + li] = ls;
+    __syncthreads();  // P, sums and every wave's read of m_run are done
+    if (wave == 0 && g == 0) {
+      const float a = __expf(m_old - mu);  // 0 when m_old = -inf
+      l_run = l_run * a + red[64 + li] + red[80 + li] + red[96 + li] + red[112 + li];
+      alpha_s[li] = a;
+      m_run[li] = m_new;
+    }
+    __syncthreads();
+    // rescale W rows (head 4g + q) by alpha, then W[head][c] += sum_j p[j][head] h[j][c]
+    float al[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) al[q] = alpha_s[4 * g + q];
+    bf16x8 pa[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int rb = 32 * s2 + 8 * g + q4;
+      const bf16x4 v0 = tr_read_g(pimg + (rb * 16 + 4 * p4) * 2);
+      const bf16x4 v1 = tr_read_g(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
+      pa[s2] = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int ii = 0; ii < hmt; ++ii) {
+        const int i = half * hmt + ii;
+        const int col = (half * (nmt * 2) + wave * hmt + ii) * 16 + 4 * p4;  // column tile of this half
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][q] *= al[q];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int rb = 32 * s2 + 8 * g + q4;
+          const bf16x4 v0 = tr_read_g(smem + gimg(rb, col));
+          const bf16x4 v1 = tr_read_g(smem + gimg(rb + 4, col));
+          const bf16x8 hb8 = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[s2], hb8, acc[i], 0, 0, 0);
+        }
+      }
+      // every wave is done reading this half of the image: refill it with the next sub-chunk
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (more) dma_half(j0 + 64, half);
+    }
+  }
+  if (wave == 0 && g == 0) {
+    ws.m[((int64_t)r * nch + ch) * GF_HP + li] = m_run[li];
+    ws.l[((int64_t)r * nch + ch) * GF_HP + li] = l_run;
+  }
+  float* wout = ws.w + ((int64_t)r * nch + ch) * GF_HP * D;
+#pragma unroll
+  for (int half = 0; half < 2; ++half)
+#pragma unroll
+    for (int ii = 0; ii < hmt; ++ii) {
+      const int i = half * hmt + ii;
+      const int c0 = (half * (nmt * 2) + wave * hmt + ii) * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * g + q < H) wout[(int64_t)(4 * g + q) * D + c0 + li] = acc[i][q];
+    }
+}
+
+// Single-buffered form for D not a multiple of 128 (one 64-row DMA, then compute).
+template <int D>
+__global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
                                                              const bf16* __restrict__ hs, int ldh,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
@@ -687,14 +877,21 @@ static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* 
   const int R = B * gmax;
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
   if (dtype == RF_BF16) {
-    const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + 160 * sizeof(float);
+    const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + 160 * sizeof(float) + 4 * 8;
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
-#define GP_(DD)                                                                               \
-  case DD:                                                                                    \
-    (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<DD>,                          \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
-    k_gfold_partial_bf16<DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const bf16*)h, ldh,  \
-                                                              flags, gidx, ws, H);            \
+#define GP_(DD)                                                                                 \
+  case DD:                                                                                      \
+    if (DD % 128 == 0) {                                                                        \
+      (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<DD>,                          \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
+      k_gfold_partial_bf16<DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const bf16*)h, ldh,  \
+                                                                flags, gidx, ws, H);            \
+    } else {                                                                                    \
+      (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16_1<DD>,                        \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
+      k_gfold_partial_bf16_1<DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const bf16*)h, ldh, \
+                                                                  flags, gidx, ws, H);          \
+    }                                                                                           \
     break;
     switch (D) {
       GP_(64) GP_(128) GP_(192) GP_(256) GP_(384) GP_(512) GP_(768) GP_(1024)
