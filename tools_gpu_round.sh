@@ -2,7 +2,7 @@
 # One GPU session: tests -> smoke -> bench -> rocprof kernel-trace summary.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest.log 2>&1
 echo "pytest rc=$?" >> gpurun_out/pytest.log
 grep -E "passed|failed|FAILED" gpurun_out/pytest.log | tail -20
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
