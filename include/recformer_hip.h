@@ -102,6 +102,21 @@ int rf_add_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, 
                          const float* w, const float* b, float eps, void* y, int ldy, float* y32,
                          float* mean, float* rstd, rf_stream_t stream);
 
+/* The bf16 path's fp32 residual stream, stored split: plane hi (bf16, M x D) =
+ * the top half of each fp32 value rounded half-up — also the next GEMM's bf16 operand — and
+ * plane lo (uint16, M x D) = its low 16 bits; together they decode to the fp32 value exactly.
+ * rf_embed_ln_split_fwd: rf_embed_ln_fwd writing the stream as planes (models.py:108-138).
+ * rf_add_layernorm_split_fwd: rf_add_layernorm_fwd on planes: y = LN(x + join(res_hi, res_lo))
+ * (TF:1064-1071, 1123-1130) with x bf16; writes planes (y_hi, y_lo; may alias res_hi, res_lo)
+ * and/or an fp32 copy y32 (M x D). res planes NULL = plain LayerNorm of x. */
+int rf_embed_ln_split_fwd(int table_dtype, int M, int D, const int32_t* ids, const int32_t* pos,
+                          const int32_t* tt, const int32_t* ip, const void* word_emb, const void* pos_emb,
+                          const void* type_emb, const void* ipos_emb, const float* ln_w, const float* ln_b,
+                          float eps, uint16_t* out_hi, uint16_t* out_lo, rf_stream_t stream);
+int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint16_t* res_hi,
+                               const uint16_t* res_lo, const float* w, const float* b, float eps,
+                               uint16_t* y_hi, uint16_t* y_lo, float* y32, rf_stream_t stream);
+
 /* A5 — LongformerSelfAttention local branch (TF:482-604 with _sliding_chunks_* 759-867,
  * _mask_invalid_locations 743-757, _concat_with_global_key_attn_probs 898-926,
  * _compute_attn_output_with_global_indices 928-962). q (pre-scaled), k, v are

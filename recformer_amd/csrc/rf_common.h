@@ -87,6 +87,20 @@ __device__ __forceinline__ f32x2 gelu2_bf16out(f32x2 x) {
   return x * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
+// ---- split fp32 residual stream ------------------------------------------------
+// An fp32 value v is stored as two 16-bit planes: hi = the top half of bits(v) rounded half-up
+// (a bf16 within half an ulp of v: the GEMM operand), lo = the low 16 bits of bits(v). The
+// pair decodes to bits(v) exactly: hi was rounded up iff bit 15 of lo is set. Rounding half-up
+// differs from the round-to-nearest-even bf16 cast only on exact ties (by one bf16 ulp).
+__device__ __forceinline__ void split_f32(float v, uint16_t& hi, uint16_t& lo) {
+  const uint32_t u = __float_as_uint(v);
+  hi = (uint16_t)((u + 0x8000u) >> 16);
+  lo = (uint16_t)(u & 0xFFFFu);
+}
+__device__ __forceinline__ float join_f32(uint32_t hi, uint32_t lo) {
+  return __uint_as_float(((hi - (lo >> 15)) << 16) | lo);
+}
+
 // Bijective XCD-aware remap of a 1-D block id (guide §5 T1): the hardware deals block ids
 // round-robin over the 8 XCDs; the returned index is contiguous per XCD, so blocks that share
 // data (neighbouring tiles, windows) run on one XCD's L2.

@@ -71,6 +71,30 @@ template <> struct Vec<bf16, 1> {
   static __device__ __forceinline__ void store(bf16* p, const float* o) { *p = (bf16)o[0]; }
 };
 
+// VEC consecutive elements of the split fp32 stream (rf_common.h split_f32 / join_f32)
+template <int VEC>
+__device__ __forceinline__ void load_split(const uint16_t* hi, const uint16_t* lo, float* o) {
+  typedef __attribute__((ext_vector_type(VEC))) uint16_t u16v;
+  const u16v h = *reinterpret_cast<const u16v*>(hi);
+  const u16v l = *reinterpret_cast<const u16v*>(lo);
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) o[j] = join_f32(h[j], l[j]);
+}
+template <int VEC>
+__device__ __forceinline__ void store_split(uint16_t* hi, uint16_t* lo, const float* o) {
+  typedef __attribute__((ext_vector_type(VEC))) uint16_t u16v;
+  u16v h, l;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    uint16_t a, b;
+    split_f32(o[j], a, b);
+    h[j] = a;
+    l[j] = b;
+  }
+  *reinterpret_cast<u16v*>(hi) = h;
+  *reinterpret_cast<u16v*>(lo) = l;
+}
+
 // ------------------------------------------------------------------------------------
 // 256-thread block exclusive scan of one int per thread.
 __device__ __forceinline__ int block_excl_scan256(int v, int* lds /*[8]*/, int* total) {
@@ -165,7 +189,7 @@ __global__ void __launch_bounds__(256) k_embed_ln(
     const int32_t* __restrict__ tt, const int32_t* __restrict__ ip, const TT* __restrict__ we,
     const TT* __restrict__ pe, const TT* __restrict__ te, const TT* __restrict__ ie,
     const float* __restrict__ lw, const float* __restrict__ lb, float eps, T* __restrict__ out,
-    float* __restrict__ out32) {
+    float* __restrict__ out32, uint16_t* __restrict__ out_lo) {
   constexpr int D = 64 * VEC * NCH;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -207,7 +231,11 @@ __global__ void __launch_bounds__(256) k_embed_ln(
     Vec<float, VEC>::load(lb + e, bb);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) y[j] = (x[c][j] - mean) * rstd * w[j] + bb[j];
-    Vec<T, VEC>::store(out + (int64_t)row * D + e, y);
+    if (out_lo) {  // split fp32 stream: out holds the hi plane (T is bf16 here)
+      store_split<VEC>(reinterpret_cast<uint16_t*>(out) + (int64_t)row * D + e, out_lo + (int64_t)row * D + e, y);
+    } else {
+      Vec<T, VEC>::store(out + (int64_t)row * D + e, y);
+    }
     if (out32) Vec<float, VEC>::store(out32 + (int64_t)row * D + e, y);
   }
 }
@@ -266,6 +294,61 @@ __global__ void __launch_bounds__(256) k_layernorm(int M, const TX* __restrict__
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o[j] = (xv[c][j] - mean) * rstd * w[j] + bb[j];
     Vec<T, VEC>::store(y + (int64_t)row * ldy + e, o);
+    if (y32) Vec<float, VEC>::store(y32 + (int64_t)row * D + e, o);
+  }
+}
+
+// The residual-add LayerNorm on the split fp32 stream (split_f32 / join_f32): y = LN(x + r)
+// with x the bf16 dense output and r = join(r_hi, r_lo) exactly the fp32 stream of the
+// reference's autocast run (TF:1064-1071, 1123-1130). Outputs: the new stream as planes
+// (y_hi is also the next GEMM's bf16 operand) and/or an fp32 copy y32. Planes may alias the
+// inputs (in-place update: every lane reads its whole row before its first store).
+// Traffic per row: 2 B (x) + 4 B (r) in, 4 B out per element, vs 2 + 4 in, 4 + 2 out with a
+// separate fp32 stream and bf16 operand.
+template <int VEC, int NCH>
+__global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restrict__ x, int ldx,
+                                                       const uint16_t* r_hi, const uint16_t* r_lo,
+                                                       const float* __restrict__ lw,
+                                                       const float* __restrict__ lb, float eps,
+                                                       uint16_t* y_hi, uint16_t* y_lo, float* y32) {
+  constexpr int D = 64 * VEC * NCH;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float xv[NCH][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = c * 64 * VEC + lane * VEC;
+    Vec<bf16, VEC>::load(x + (int64_t)row * ldx + e, xv[c]);
+    if (r_hi) {
+      float rv[VEC];
+      load_split<VEC>(r_hi + (int64_t)row * D + e, r_lo + (int64_t)row * D + e, rv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) xv[c][j] += rv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) s += xv[c][j];
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float v = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float d = xv[c][j] - mean;
+      v += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(v) * (1.0f / D) + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = c * 64 * VEC + lane * VEC;
+    float w[VEC], bb[VEC], o[VEC];
+    Vec<float, VEC>::load(lw + e, w);
+    Vec<float, VEC>::load(lb + e, bb);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (xv[c][j] - mean) * rstd * w[j] + bb[j];
+    if (y_hi) store_split<VEC>(y_hi + (int64_t)row * D + e, y_lo + (int64_t)row * D + e, o);
     if (y32) Vec<float, VEC>::store(y32 + (int64_t)row * D + e, o);
   }
 }
@@ -429,12 +512,12 @@ template <typename TT, typename T>
 static int launch_embed(int M, int D, const int32_t* ids, const int32_t* pos, const int32_t* tt,
                         const int32_t* ip, const void* we, const void* pe, const void* te,
                         const void* ie, const float* lw, const float* lb, float eps, void* out,
-                        float* out32, hipStream_t s) {
+                        float* out32, uint16_t* out_lo, hipStream_t s) {
   dim3 grid((M + 3) / 4);
 #define L_(V, N)                                                                                 \
   k_embed_ln<TT, T, V, N><<<grid, 256, 0, s>>>(M, ids, pos, tt, ip, (const TT*)we, (const TT*)pe, \
                                                (const TT*)te, (const TT*)ie, lw, lb, eps, (T*)out, \
-                                               out32)
+                                               out32, out_lo)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
   RF_LAUNCH_CHECK("rf_embed_ln_fwd");
@@ -487,11 +570,11 @@ int rf_embed_ln_fwd(int table_dtype, int out_dtype, int M, int D, const int32_t*
   if (M == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
   if (table_dtype == RF_F32 && out_dtype == RF_F32)
-    return launch_embed<float, float>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, s);
+    return launch_embed<float, float>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, nullptr, s);
   if (table_dtype == RF_F32 && out_dtype == RF_BF16)
-    return launch_embed<float, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, s);
+    return launch_embed<float, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, nullptr, s);
   if (table_dtype == RF_BF16 && out_dtype == RF_BF16)
-    return launch_embed<bf16, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, s);
+    return launch_embed<bf16, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, nullptr, s);
   RF_REQUIRE(false, "rf_embed_ln_fwd: unsupported dtypes table=%d out=%d", table_dtype, out_dtype);
 }
 
@@ -517,6 +600,40 @@ int rf_add_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, 
   if (x_dtype == RF_BF16 && y_dtype == RF_F32)
     return launch_ln<bf16, float>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
   RF_REQUIRE(false, "rf_layernorm_fwd: bad dtypes %d/%d", x_dtype, y_dtype);
+}
+
+int rf_embed_ln_split_fwd(int table_dtype, int M, int D, const int32_t* ids, const int32_t* pos,
+                          const int32_t* tt, const int32_t* ip, const void* word_emb, const void* pos_emb,
+                          const void* type_emb, const void* ipos_emb, const float* ln_w, const float* ln_b,
+                          float eps, uint16_t* out_hi, uint16_t* out_lo, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0, "rf_embed_ln_split_fwd: bad M");
+  if (M == 0) return RF_OK;
+  RF_REQUIRE(out_hi && out_lo, "rf_embed_ln_split_fwd: null output plane");
+  hipStream_t s = as_stream(stream);
+  if (table_dtype == RF_F32)
+    return launch_embed<float, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b,
+                                     eps, out_hi, nullptr, out_lo, s);
+  if (table_dtype == RF_BF16)
+    return launch_embed<bf16, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b,
+                                    eps, out_hi, nullptr, out_lo, s);
+  RF_REQUIRE(false, "rf_embed_ln_split_fwd: unsupported table dtype %d", table_dtype);
+}
+
+int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint16_t* res_hi,
+                               const uint16_t* res_lo, const float* w, const float* b, float eps,
+                               uint16_t* y_hi, uint16_t* y_lo, float* y32, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && ldx >= D, "rf_add_layernorm_split_fwd: bad shape");
+  RF_REQUIRE((res_hi == nullptr) == (res_lo == nullptr) && (y_hi == nullptr) == (y_lo == nullptr),
+             "rf_add_layernorm_split_fwd: planes come in (hi, lo) pairs");
+  RF_REQUIRE(y_hi || y32, "rf_add_layernorm_split_fwd: no output");
+  if (M == 0) return RF_OK;
+  hipStream_t s = as_stream(stream);
+  dim3 grid((M + 3) / 4);
+#define L_(V, N)                                                                                       \
+  k_add_ln_split<V, N><<<grid, 256, 0, s>>>(M, (const bf16*)x, ldx, res_hi, res_lo, w, b, eps, y_hi, y_lo, y32)
+  RF_ROW_DISPATCH(D, L_);
+#undef L_
+  RF_LAUNCH_CHECK("rf_add_layernorm_split_fwd");
 }
 
 int rf_row_inv_norm(int dtype, int M, int D, const void* x, int ldx, float eps, float* out,

@@ -213,6 +213,11 @@ def _cos_train(z: torch.Tensor, items: torch.Tensor, temp: float) -> torch.Tenso
         return (zn @ itn.t()) / temp
 
 
+# bf16 path: keep the fp32 residual stream as split (hi, lo) 16-bit planes;
+# False = a plain fp32 tensor plus a separate bf16 GEMM operand (A/B tools, tests).
+SPLIT_STREAM = True
+
+
 def _compute_dtype(param_dtype: torch.dtype) -> torch.dtype:
     if torch.is_autocast_enabled("cuda"):
         return torch.bfloat16
@@ -385,12 +390,20 @@ class RecformerModel(nn.Module):
             input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
             position_ids, Lp, cfg.pad_token_id, gmax)
         # bf16 path: GEMM operands in bf16, residual stream / LN outputs in fp32 (as the
-        # reference's autocast run); fp32 path: everything fp32 (h32 is h).
+        # reference's autocast run), the fp32 stream held split as (hi, lo) 16-bit planes whose
+        # hi plane is the bf16 GEMM operand (ops.add_layernorm_split); fp32 path: everything fp32.
         mixed = dt != torch.float32
-        h, h32 = ops.embed_ln(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
-                              pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps, out_dtype=dt, want_f32=mixed)
-        if not mixed:
-            h32 = h
+        split = mixed and SPLIT_STREAM
+        nl = len(pk["layers"])
+        if split:
+            h, h_lo = ops.embed_ln_split(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
+                                         pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps)
+            h32 = ops.join_split(h, h_lo) if (output_hidden_states or nl == 0) else None
+        else:
+            h, h32 = ops.embed_ln(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
+                                  pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps, out_dtype=dt, want_f32=mixed)
+            if not mixed:
+                h32 = h
         hidden_all = [h32] if output_hidden_states else None
         scale = 1.0 / math.sqrt(hd)
         windows = cfg.window_per_layer()
@@ -423,11 +436,23 @@ class RecformerModel(nn.Module):
                 f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
                 t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a, tag="gemm_ffn2")
                 h = h32 = ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out=t2, tag="layernorm")
-            else:
+            elif split:
                 # bf16 path, the reference under autocast: each dense output is bf16 (the GEMM
                 # epilogue rounds it, as autocast's Linear does), the residual stream and the
-                # LayerNorm are fp32 (TF:1064-1071, 1123-1130): LN(bf16 dense + fp32 stream) ->
-                # bf16 GEMM operand + fp32 stream, updated in place unless hidden states are kept.
+                # LayerNorm are fp32 (TF:1064-1071, 1123-1130): LN(bf16 dense + fp32 stream),
+                # the stream updated in place as planes (h = its hi plane); the last layer (and
+                # every layer when hidden states are returned) also writes the fp32 output.
+                last_layer = li == nl - 1
+                t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
+                ops.add_layernorm_split(t, h, h_lo, lw["ln1_w"], lw["ln1_b"], eps, tag="layernorm")
+                f = ops.gemm(h, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
+                t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS, tag="gemm_ffn2")
+                _, _, h32 = ops.add_layernorm_split(t2, h, h_lo, lw["ln2_w"], lw["ln2_b"], eps,
+                                                    planes=not last_layer,
+                                                    want_f32=last_layer or output_hidden_states,
+                                                    tag="layernorm")
+            else:
+                # the same with the fp32 stream as a plain fp32 tensor (SPLIT_STREAM = False)
                 t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
                 a, a32 = ops.add_layernorm(t, h32, lw["ln1_w"], lw["ln1_b"], eps, out_dtype=dt,
                                            res_out=None if output_hidden_states else h32, tag="layernorm")

@@ -16,7 +16,8 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF
                    RF_EPI_NONE, RF_F32, check)
 
 __all__ = [
-    "dtype_code", "prepare_inputs", "embed_ln", "gemm", "layernorm", "add_layernorm", "band_attention_bwd", "band_attention",
+    "dtype_code", "prepare_inputs", "embed_ln", "embed_ln_split", "add_layernorm_split", "join_split",
+    "gemm", "layernorm", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -136,6 +137,58 @@ def embed_ln(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, ln_b, eps: 
                               _p(ln_w.float().contiguous()), _p(ln_b.float().contiguous()),
                               float(eps), _p(out), _p(out32), _stream(out)), "rf_embed_ln_fwd")
     return out, out32
+
+
+def embed_ln_split(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, ln_b, eps: float):
+    """The embedding LayerNorm output as the split fp32 stream: (hi bf16, lo int16) planes
+    (rf_embed_ln_split_fwd; hi is the first layer's GEMM operand)."""
+    lib = _lib.load()
+    _dev(ids, word)
+    M = ids.numel()
+    D = word.shape[1]
+    for t in (word, posemb, typeemb, iposemb):
+        if not t.is_contiguous() or t.dtype != word.dtype or t.shape[1] != D:
+            raise ValueError("embedding tables must be contiguous, same dtype and width")
+    hi = torch.empty(M, D, dtype=torch.bfloat16, device=word.device)
+    lo = torch.empty(M, D, dtype=torch.int16, device=word.device)
+    check(lib.rf_embed_ln_split_fwd(dtype_code(word.dtype), M, D, _p(ids), _p(pos), _p(tt), _p(ip),
+                                    _p(word), _p(posemb), _p(typeemb), _p(iposemb),
+                                    _p(ln_w.float().contiguous()), _p(ln_b.float().contiguous()),
+                                    float(eps), _p(hi), _p(lo), _stream(hi)), "rf_embed_ln_split_fwd")
+    return hi, lo
+
+
+def add_layernorm_split(x: torch.Tensor, res_hi: torch.Tensor, res_lo: torch.Tensor, w: torch.Tensor,
+                        b: torch.Tensor, eps: float, planes: bool = True, want_f32: bool = False,
+                        tag: Optional[str] = None):
+    """y = LN(x + r) on the split fp32 stream (rf_add_layernorm_split_fwd): x the bf16 dense output,
+    r = join(res_hi, res_lo). With `planes` the new stream overwrites (res_hi, res_lo) in place;
+    `want_f32` also returns an fp32 copy. Returns (hi, lo, y32) (entries None when not written)."""
+    lib = _lib.load()
+    _dev(x, res_hi, res_lo)
+    M, D = x.shape
+    if x.dtype != torch.bfloat16:
+        raise TypeError("add_layernorm_split: x must be bf16")
+    for t, dt in ((res_hi, torch.bfloat16), (res_lo, torch.int16)):
+        if t.dtype != dt or not t.is_contiguous() or tuple(t.shape) != (M, D):
+            raise ValueError("add_layernorm_split: residual planes must be contiguous (M, D) bf16 / int16")
+    if not (planes or want_f32):
+        raise ValueError("add_layernorm_split: no output requested")
+    y32 = torch.empty(M, D, dtype=torch.float32, device=x.device) if want_f32 else None
+    yh, yl = (res_hi, res_lo) if planes else (None, None)
+    with _region(tag):
+        rc = lib.rf_add_layernorm_split_fwd(M, D, _p(x), _rowmajor(x, "x"), _p(res_hi), _p(res_lo),
+                                            _p(w), _p(b), float(eps), _p(yh), _p(yl), _p(y32), _stream(x))
+    check(rc, "rf_add_layernorm_split_fwd")
+    return yh, yl, y32
+
+
+def join_split(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
+    """fp32 values of split-stream rows (host-side torch integer ops; used on a few rows only,
+    e.g. the pooled CLS rows)."""
+    h = hi.view(torch.int16).to(torch.int32) & 0xFFFF
+    l = lo.to(torch.int32) & 0xFFFF
+    return (((h - (l >> 15)) << 16) | l).view(torch.float32)
 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,

@@ -127,6 +127,68 @@ def test_add_layernorm(dev, D, inplace):
     assert y.dtype == torch.bfloat16 and (y32.data_ptr() == res.data_ptr()) == inplace
 
 
+def _split_ref(v):
+    """Host restatement of rf_common.h split_f32: hi = top half of the fp32 bits rounded
+    half-up, lo = the low 16 bits."""
+    u = v.float().contiguous().view(torch.int32).long() & 0xFFFFFFFF
+    return (((u + 0x8000) >> 16) & 0xFFFF), u & 0xFFFF
+
+
+@pytest.mark.parametrize("D", [128, 768])
+@pytest.mark.parametrize("mode", ["planes", "f32", "both", "nores"])
+def test_add_layernorm_split(dev, D, mode):
+    """LN(bf16 dense + fp32 stream) on the split stream: the fp32 result is bit-identical to the
+    fp32-stream kernel (same arithmetic), the planes decode to it exactly, and the hi plane is
+    the bf16 rounding of it (half-up: within half a bf16 ulp)."""
+    M = 333
+    x = _rand((M, D), dev, torch.bfloat16, 3.0, seed=17)
+    res = _rand((M, D), dev, torch.float32, 2.0, seed=18) + 0.5
+    w = _rand((D,), dev, torch.float32, seed=19)
+    b = _rand((D,), dev, torch.float32, seed=20)
+    hi_r, lo_r = _split_ref(res)
+    hi = (hi_r.to(torch.int32).to(torch.int16)).view(torch.bfloat16).clone()
+    lo = lo_r.to(torch.int32).to(torch.int16).clone()
+    assert torch.equal(ops.join_split(hi, lo), res)  # host decode of the host encode
+    if mode == "nores":
+        _, y32 = ops.add_layernorm(x, torch.zeros_like(res), w, b, 1e-5)
+        ref32 = y32.clone()
+        lib = ops._lib.load()
+        hh, ll = torch.empty_like(hi), torch.empty_like(lo)
+        ops.check(lib.rf_add_layernorm_split_fwd(M, D, x.data_ptr(), D, None, None, w.data_ptr(), b.data_ptr(),
+                                                 1e-5, hh.data_ptr(), ll.data_ptr(), None,
+                                                 torch.cuda.current_stream().cuda_stream), "split")
+        assert torch.equal(ops.join_split(hh, ll), ref32)
+        return
+    _, ref32 = ops.add_layernorm(x, res, w, b, 1e-5)  # fp32-stream kernel, same arithmetic
+    yh, yl, y32 = ops.add_layernorm_split(x, hi, lo, w, b, 1e-5, planes=mode != "f32",
+                                          want_f32=mode != "planes")
+    if mode != "planes":
+        assert torch.equal(y32, ref32)
+    if mode != "f32":
+        assert yh.data_ptr() == hi.data_ptr() and yl.data_ptr() == lo.data_ptr()  # in place
+        assert torch.equal(ops.join_split(yh, yl), ref32)
+        eh, el = _split_ref(ref32)
+        assert torch.equal(yh.view(torch.int16).long() & 0xFFFF, eh)
+        assert torch.equal(yl.long() & 0xFFFF, el)
+        ulp = 2.0 ** (torch.floor(torch.log2(ref32.abs().clamp_min(1e-30))) - 7)
+        assert ((yh.float() - ref32).abs() <= 0.5 * ulp + 1e-30).all()
+
+
+def test_embed_ln_split(dev):
+    from recformer_amd.synth import synth_batch
+    B, L, D, V = 2, 128, 768, 500
+    bt = {k: v.to(dev) for k, v in synth_batch(B, L, V, seed=5, lens=[128, 77]).items()}
+    ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
+        bt["input_ids"], bt["attention_mask"], bt["global_attention_mask"], bt["token_type_ids"],
+        bt["item_position_ids"], None, L, 1, 1)
+    tabs = [_rand((n, D), dev, torch.float32, 0.02, seed=30 + i) for i, n in enumerate((V, 300, 4, 51))]
+    lw = _rand((D,), dev, torch.float32, seed=40)
+    lb = _rand((D,), dev, torch.float32, seed=41)
+    _, out32 = ops.embed_ln(ids, pos, tt, ip, *tabs, lw, lb, 1e-5, out_dtype=torch.bfloat16, want_f32=True)
+    hi, lo = ops.embed_ln_split(ids, pos, tt, ip, *tabs, lw, lb, 1e-5)
+    assert torch.equal(ops.join_split(hi, lo), out32)
+
+
 @pytest.mark.parametrize("tdt,dt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
                                      (torch.bfloat16, torch.bfloat16)])
 def test_embed_ln_and_prepare(dev, tdt, dt):

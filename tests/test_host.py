@@ -72,3 +72,27 @@ def test_product_path_has_no_cpu_fallback():
     ids = torch.zeros(1, 64, dtype=torch.long)
     with pytest.raises(_lib.RecformerHipError):
         m(input_ids=ids, item_position_ids=ids)
+
+
+def test_split_stream_encoding_is_exact():
+    """The bf16 path's fp32 residual stream is stored as (hi, lo) 16-bit planes
+    (rf_common.h split_f32 / join_f32): restated on the host, every fp32 value - ties,
+    negatives, subnormals, exponent carries - decodes exactly, and hi is a bf16 within half an
+    ulp of the value (round half-up: differs from round-to-nearest-even only on exact ties)."""
+    import torch
+
+    from recformer_amd.ops import join_split
+    g = torch.Generator().manual_seed(0)
+    v = torch.cat([torch.randn(100000, generator=g) * 10.0 ** torch.randint(-30, 30, (100000,), generator=g),
+                   torch.tensor([0.0, -0.0, 1.0, -1.0, 1.00390625, 1.0 + 2 ** -9, -(1.0 + 2 ** -9),
+                                 1.9999999, -1.9999999, 1e-40, -1e-40, 3.0e38])])
+    u = v.view(torch.int32).long() & 0xFFFFFFFF
+    hi = ((u + 0x8000) >> 16) & 0xFFFF
+    lo = u & 0xFFFF
+    hi_t = hi.to(torch.int32).to(torch.int16).view(torch.bfloat16)
+    lo_t = lo.to(torch.int32).to(torch.int16)
+    back = join_split(hi_t, lo_t)
+    assert torch.equal(back.view(torch.int32), v.view(torch.int32))
+    rne = v.to(torch.bfloat16)
+    differ = hi_t.view(torch.int16) != rne.view(torch.int16)
+    assert (lo[differ] == 0x8000).all()  # only exact ties may round differently
