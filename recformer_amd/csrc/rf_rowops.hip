@@ -305,22 +305,33 @@ __global__ void __launch_bounds__(256) k_layernorm(int M, const TX* __restrict__
 // inputs (in-place update: every lane reads its whole row before its first store).
 // Traffic per row: 2 B (x) + 4 B (r) in, 4 B out per element, vs 2 + 4 in, 4 + 2 out with a
 // separate fp32 stream and bf16 operand.
-template <int VEC, int NCH>
+// LPR lanes per row (a group of 8..64 lanes), 8 elements (16-B loads of each plane) per lane
+// and chunk: D = LPR * 8 * NCH; 256 / LPR rows per block (D = 768: half a wave per row).
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int LPR, int NCH>
 __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restrict__ x, int ldx,
                                                        const uint16_t* r_hi, const uint16_t* r_lo,
                                                        const float* __restrict__ lw,
                                                        const float* __restrict__ lb, float eps,
                                                        uint16_t* y_hi, uint16_t* y_lo, float* y32) {
-  constexpr int D = 64 * VEC * NCH;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+  constexpr int VEC = 8, D = LPR * VEC * NCH;
+  const int gl = threadIdx.x % LPR;
+  const int row = blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+  if (row >= M) return;  // whole lane groups exit together: the shuffles below stay in-group
   float xv[NCH][VEC];
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int e = c * 64 * VEC + lane * VEC;
-    Vec<bf16, VEC>::load(x + (int64_t)row * ldx + e, xv[c]);
+    const int e = c * LPR * VEC + gl * VEC;
+    const bf16x8 xb = *reinterpret_cast<const bf16x8*>(x + (int64_t)row * ldx + e);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) xv[c][j] = (float)xb[j];
     if (r_hi) {
       float rv[VEC];
       load_split<VEC>(r_hi + (int64_t)row * D + e, r_lo + (int64_t)row * D + e, rv);
@@ -330,7 +341,7 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
 #pragma unroll
     for (int j = 0; j < VEC; ++j) s += xv[c][j];
   }
-  const float mean = wave_sum(s) * (1.0f / D);
+  const float mean = group_sum<LPR>(s) * (1.0f / D);
   float v = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
@@ -339,17 +350,22 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
       float d = xv[c][j] - mean;
       v += d * d;
     }
-  const float rstd = rsqrtf(wave_sum(v) * (1.0f / D) + eps);
+  const float rstd = rsqrtf(group_sum<LPR>(v) * (1.0f / D) + eps);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int e = c * 64 * VEC + lane * VEC;
+    const int e = c * LPR * VEC + gl * VEC;
     float w[VEC], bb[VEC], o[VEC];
-    Vec<float, VEC>::load(lw + e, w);
-    Vec<float, VEC>::load(lb + e, bb);
+    Vec<float, 4>::load(lw + e, w);
+    Vec<float, 4>::load(lw + e + 4, w + 4);
+    Vec<float, 4>::load(lb + e, bb);
+    Vec<float, 4>::load(lb + e + 4, bb + 4);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o[j] = (xv[c][j] - mean) * rstd * w[j] + bb[j];
     if (y_hi) store_split<VEC>(y_hi + (int64_t)row * D + e, y_lo + (int64_t)row * D + e, o);
-    if (y32) Vec<float, VEC>::store(y32 + (int64_t)row * D + e, o);
+    if (y32) {
+      Vec<float, 4>::store(y32 + (int64_t)row * D + e, o);
+      Vec<float, 4>::store(y32 + (int64_t)row * D + e + 4, o + 4);
+    }
   }
 }
 
@@ -628,11 +644,20 @@ int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint1
   RF_REQUIRE(y_hi || y32, "rf_add_layernorm_split_fwd: no output");
   if (M == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
-  dim3 grid((M + 3) / 4);
-#define L_(V, N)                                                                                       \
-  k_add_ln_split<V, N><<<grid, 256, 0, s>>>(M, (const bf16*)x, ldx, res_hi, res_lo, w, b, eps, y_hi, y_lo, y32)
-  RF_ROW_DISPATCH(D, L_);
-#undef L_
+  RF_REQUIRE(ldx % 8 == 0, "rf_add_layernorm_split_fwd: ldx must be a multiple of 8");
+#define LS_(LPR, NCH) k_add_ln_split<LPR, NCH><<<(M + 256 / LPR - 1) / (256 / LPR), 256, 0, s>>>( \
+      M, (const bf16*)x, ldx, res_hi, res_lo, w, b, eps, y_hi, y_lo, y32)
+  switch (D) {
+    case 64: LS_(8, 1); break;
+    case 128: LS_(16, 1); break;
+    case 256: LS_(32, 1); break;
+    case 384: LS_(16, 3); break;
+    case 512: LS_(64, 1); break;
+    case 768: LS_(32, 3); break;
+    case 1024: LS_(32, 4); break;
+    default: RF_REQUIRE(false, "rf_add_layernorm_split_fwd: unsupported width D=%d", D);
+  }
+#undef LS_
   RF_LAUNCH_CHECK("rf_add_layernorm_split_fwd");
 }
 

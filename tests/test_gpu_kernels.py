@@ -137,9 +137,9 @@ def _split_ref(v):
 @pytest.mark.parametrize("D", [128, 768])
 @pytest.mark.parametrize("mode", ["planes", "f32", "both", "nores"])
 def test_add_layernorm_split(dev, D, mode):
-    """LN(bf16 dense + fp32 stream) on the split stream: the fp32 result is bit-identical to the
-    fp32-stream kernel (same arithmetic), the planes decode to it exactly, and the hi plane is
-    the bf16 rounding of it (half-up: within half a bf16 ulp)."""
+    """LN(bf16 dense + fp32 stream) on the split stream, vs the fp32 torch LayerNorm of the
+    decoded stream: the planes decode exactly to the fp32 output (when both are written) and
+    the hi plane is that value rounded half-up to bf16 (within half a bf16 ulp); in place."""
     M = 333
     x = _rand((M, D), dev, torch.bfloat16, 3.0, seed=17)
     res = _rand((M, D), dev, torch.float32, 2.0, seed=18) + 0.5
@@ -150,28 +150,29 @@ def test_add_layernorm_split(dev, D, mode):
     lo = lo_r.to(torch.int32).to(torch.int16).clone()
     assert torch.equal(ops.join_split(hi, lo), res)  # host decode of the host encode
     if mode == "nores":
-        _, y32 = ops.add_layernorm(x, torch.zeros_like(res), w, b, 1e-5)
-        ref32 = y32.clone()
+        ref = F.layer_norm(x.float(), (D,), w, b, 1e-5)
         lib = ops._lib.load()
         hh, ll = torch.empty_like(hi), torch.empty_like(lo)
         ops.check(lib.rf_add_layernorm_split_fwd(M, D, x.data_ptr(), D, None, None, w.data_ptr(), b.data_ptr(),
                                                  1e-5, hh.data_ptr(), ll.data_ptr(), None,
                                                  torch.cuda.current_stream().cuda_stream), "split")
-        assert torch.equal(ops.join_split(hh, ll), ref32)
+        assert (ops.join_split(hh, ll) - ref).abs().max().item() <= 1e-4
         return
-    _, ref32 = ops.add_layernorm(x, res, w, b, 1e-5)  # fp32-stream kernel, same arithmetic
+    ref = F.layer_norm(x.float() + res, (D,), w, b, 1e-5)
     yh, yl, y32 = ops.add_layernorm_split(x, hi, lo, w, b, 1e-5, planes=mode != "f32",
                                           want_f32=mode != "planes")
     if mode != "planes":
-        assert torch.equal(y32, ref32)
+        assert (y32 - ref).abs().max().item() <= 1e-4
     if mode != "f32":
         assert yh.data_ptr() == hi.data_ptr() and yl.data_ptr() == lo.data_ptr()  # in place
-        assert torch.equal(ops.join_split(yh, yl), ref32)
-        eh, el = _split_ref(ref32)
+        joined = ops.join_split(yh, yl)
+        assert (joined - ref).abs().max().item() <= 1e-4
+        if mode == "both":
+            assert torch.equal(joined, y32)
+        eh, el = _split_ref(joined)
         assert torch.equal(yh.view(torch.int16).long() & 0xFFFF, eh)
-        assert torch.equal(yl.long() & 0xFFFF, el)
-        ulp = 2.0 ** (torch.floor(torch.log2(ref32.abs().clamp_min(1e-30))) - 7)
-        assert ((yh.float() - ref32).abs() <= 0.5 * ulp + 1e-30).all()
+        ulp = 2.0 ** (torch.floor(torch.log2(joined.abs().clamp_min(1e-30))) - 7)
+        assert ((yh.float() - joined).abs() <= 0.5 * ulp + 1e-30).all()
 
 
 def test_embed_ln_split(dev):
