@@ -9,8 +9,20 @@ from .models import (RecformerEmbeddings, RecformerForPretraining, RecformerForS
                      RecformerModel, RecformerModelOutput, RecformerPooler,
                      RecformerPretrainingOutput, Similarity, create_position_ids_from_input_ids)
 
+_LAZY = {"RecformerTokenizer": "data", "FinetuneDataCollatorWithPadding": "data",
+         "EvalDataCollatorWithPadding": "data", "LitWrapper": "lit"}
+
+
+def __getattr__(name):  # host-side pieces load transformers / the host library on first use
+    if name in _LAZY:
+        import importlib
+        return getattr(importlib.import_module(f".{_LAZY[name]}", __name__), name)
+    raise AttributeError(name)
+
+
 __all__ = [
     "RecformerConfig", "RecformerModel", "RecformerForSeqRec", "RecformerForPretraining",
     "RecformerPretrainingOutput", "RecformerModelOutput", "RecformerEmbeddings", "RecformerPooler",
-    "Similarity", "create_position_ids_from_input_ids", "Ranker",
+    "Similarity", "create_position_ids_from_input_ids", "Ranker", "RecformerTokenizer",
+    "FinetuneDataCollatorWithPadding", "EvalDataCollatorWithPadding", "LitWrapper",
 ]

@@ -96,3 +96,44 @@ def test_split_stream_encoding_is_exact():
     rne = v.to(torch.bfloat16)
     differ = hi_t.view(torch.int16) != rne.view(torch.int16)
     assert (lo[differ] == 0x8000).all()  # only exact ties may round differently
+
+
+def test_host_library_exports_every_header_symbol():
+    from recformer_amd import data
+    with open(os.path.join(ROOT, "include", "recformer_host.h")) as f:
+        txt = f.read()
+    names = sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(rf_\w+)\s*\(", txt, re.M)))
+    assert names == ["rf_collate_fill", "rf_collate_lengths", "rf_host_last_error"]
+    lib = data.load_host()
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_litwrapper_contract():
+    """recformer_amd.LitWrapper mirrors litmodels.py: training_step returns outputs.loss,
+    validation accuracy = cl_correct_num / cl_total_num, AdamW groups without decay for biases
+    and LayerNorm weights, linear warmup schedule stepped per step."""
+    from types import SimpleNamespace
+
+    import recformer_amd
+
+    class Tiny(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.dense = torch.nn.Linear(4, 4)
+            self.LayerNorm = torch.nn.LayerNorm(4)
+
+        def forward(self, x):
+            loss = self.LayerNorm(self.dense(x)).pow(2).mean()
+            return SimpleNamespace(loss=loss, cl_correct_num=3, cl_total_num=4)
+
+    lit = recformer_amd.LitWrapper(Tiny(), learning_rate=1e-3, warmup_steps=2, weight_decay=0.1, num_training_steps=10)
+    loss = lit.training_step({"x": torch.ones(2, 4)}, 0)
+    assert loss.requires_grad
+    m = lit.validation_step({"x": torch.ones(2, 4)}, 0)
+    assert m["accuracy"] == 0.75
+    (opt,), (sch,) = lit.configure_optimizers()
+    decay, no_decay = opt.param_groups
+    assert decay["weight_decay"] == 0.1 and no_decay["weight_decay"] == 0.0
+    assert len(decay["params"]) == 1 and len(no_decay["params"]) == 3  # dense.weight | biases, LN.weight
+    assert sch["interval"] == "step" and opt.param_groups[0]["lr"] == 0.0  # warmup starts at 0

@@ -18,6 +18,7 @@ import re
 import sys
 
 EPI_TAG = {1: "gemm_qkv", 2: "gemm_ffn1", 3: "gemm_out", 4: "gemm_cos"}
+RENAME = {"k_add_ln_split": "layernorm"}  # split-stream residual LayerNorm = bench tag "layernorm"
 SIMPLE = ("k_band_attn", "k_gfold_partial", "k_gfold_qu", "k_gfold_u", "k_gfold_out", "k_layernorm",
           "k_embed_ln", "k_prepare", "k_gather_rows", "k_row_inv_norm", "k_cos_cand",
           "k_global_attn", "k_gemm_f32")
@@ -41,6 +42,9 @@ def tagger():
                 t = EPI_TAG.get(epi, f"gemm_epi{epi}")
             last[0] = t
             return t
+        for k, t in RENAME.items():
+            if k in name:
+                return t
         for k in SIMPLE:
             if k in name:
                 return k[2:]
