@@ -708,8 +708,10 @@ __global__ void __launch_bounds__(512, 1)
     const int lim = (isA ? e.M : e.N) - 1;
     const int r0 = (isA ? bm0 : bn0) + (half & 1) * 128;
     const int ra = r0 + (isA ? xa : xw0), rb = r0 + (isA ? xa + 8 : xw1);
+#if !(defined(RF_GEMM_DIAG) && (RF_GEMM_DIAG & 2))  // diagnostic: no operand DMA
     glds16(base + (min(ra, lim) * ld + kt * 64 + pch), dst);
     glds16(base + (min(rb, lim) * ld + kt * 64 + pch), dst + 1024);
+#endif
   };
   // Epilogue column vectors of a tile (bias or EPI_COS item norms; LN gamma, beta) as one
   // 1-KiB DMA per wave into LDS slot [parity][vector]: wave w loads vector w % 3 (vectors an
@@ -746,6 +748,10 @@ __global__ void __launch_bounds__(512, 1)
   f32x4 acc[4][8];
 
   auto read_a = [&](int buf, int qm) {
+#if defined(RF_GEMM_DIAG) && (RF_GEMM_DIAG & 1)  // timing diagnostic: no LDS operand reads
+    for (int i = 0; i < 2; ++i) asm volatile("" : "=v"(a[qm][i][0]), "=v"(a[qm][i][1]));
+    return;
+#endif
     const char* base = smem + buf * 4 * PP_HALF + aBase + qm * 32 * 128;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -754,6 +760,10 @@ __global__ void __launch_bounds__(512, 1)
     }
   };
   auto read_b = [&](int buf, int qn) {
+#if defined(RF_GEMM_DIAG) && (RF_GEMM_DIAG & 1)
+    for (int j = 0; j < 4; ++j) asm volatile("" : "=v"(b[qn][j][0]), "=v"(b[qn][j][1]));
+    return;
+#endif
     const char* base = smem + buf * 4 * PP_HALF + bBase + qn * 64 * 128;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -777,6 +787,16 @@ __global__ void __launch_bounds__(512, 1)
   };
   // the MFMA half of a phase: barrier, retire this phase's LDS reads, MFMAs at raised priority
   auto compute = [&](int qm, int qn, bool live) {
+#if defined(RF_GEMM_DIAG) && (RF_GEMM_DIAG & 4)  // diagnostic: no barriers around the MFMAs
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (live) {
+      __builtin_amdgcn_s_setprio(1);
+      mma(qm, qn);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    return;
+#endif
     bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (live) {
