@@ -117,6 +117,15 @@ int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint1
                                const uint16_t* res_lo, const float* w, const float* b, float eps,
                                uint16_t* y_hi, uint16_t* y_lo, float* y32, rf_stream_t stream);
 
+/* LayerNorm backward for the training path (autograd of TF:1071, 1130 / models.py:136):
+ * dy, x (the fp32 LayerNorm input rows, leading dim ldx), the forward's row mean / rstd and
+ * gamma w -> dx (M x D fp32), dw = sum_rows dy * xhat, db = sum_rows dy (fp32 [D]); column sums
+ * are reduced deterministically through rf_layernorm_bwd_workspace(M, D) bytes of workspace. */
+size_t rf_layernorm_bwd_workspace(int M, int D);
+int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
+                     const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
+                     rf_stream_t stream);
+
 /* A5 — LongformerSelfAttention local branch (TF:482-604 with _sliding_chunks_* 759-867,
  * _mask_invalid_locations 743-757, _concat_with_global_key_attn_probs 898-926,
  * _compute_attn_output_with_global_indices 928-962). q (pre-scaled), k, v are

@@ -36,6 +36,8 @@ SIGNATURES = {
                                      P, P, P]),
     "rf_embed_ln_split_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_float, P, P, P]),
     "rf_add_layernorm_split_fwd": (c_int, [c_int, c_int, P, c_int, P, P, P, P, c_float, P, P, P, P]),
+    "rf_layernorm_bwd_workspace": (ctypes.c_size_t, [c_int, c_int]),
+    "rf_layernorm_bwd": (c_int, [c_int, c_int, P, P, c_int, P, P, P, P, P, P, P, P]),
     "rf_band_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
                                  c_int, P, c_int, P]),
     "rf_band_attn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, c_int, P, c_int,

@@ -369,6 +369,88 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
   }
 }
 
+// LayerNorm backward (training path; TF:1071, 1130 under autograd): per row, with
+// xhat = (x - mean) * rstd and g = dy * w,
+//   dx = rstd * (g - mean(g) - xhat * mean(g * xhat))
+// and per-column partial sums of dy * xhat (dw) and dy (db) over this block's rows, written to
+// part[blockIdx][2][D] and reduced by k_colsum2 (deterministic; no float atomics).
+// One wave per row, LNB_ROWS rows per 256-thread block.
+constexpr int LNB_ROWS = 32;
+
+template <int VEC, int NCH>
+__global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __restrict__ dy,
+                                                        const float* __restrict__ x, int ldx,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd,
+                                                        const float* __restrict__ w, float* __restrict__ dx,
+                                                        float* __restrict__ part) {
+  constexpr int D = 64 * VEC * NCH;
+  __shared__ float red[4][2][D];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float pw[NCH][VEC], pb[NCH][VEC], wr[NCH][VEC];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    Vec<float, VEC>::load(w + c * 64 * VEC + lane * VEC, wr[c]);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) pw[c][j] = pb[c][j] = 0.f;
+  }
+  const int r0 = blockIdx.x * LNB_ROWS;
+  for (int rr = wv; rr < LNB_ROWS; rr += 4) {
+    const int row = r0 + rr;
+    if (row >= M) break;
+    const float mu = mean[row], rs = rstd[row];
+    float g[NCH][VEC], xh[NCH][VEC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = c * 64 * VEC + lane * VEC;
+      float d[VEC], xv[VEC];
+      Vec<float, VEC>::load(dy + (int64_t)row * D + e, d);
+      Vec<float, VEC>::load(x + (int64_t)row * ldx + e, xv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        xh[c][j] = (xv[j] - mu) * rs;
+        g[c][j] = d[j] * wr[c][j];
+        s1 += g[c][j];
+        s2 += g[c][j] * xh[c][j];
+        pw[c][j] += d[j] * xh[c][j];
+        pb[c][j] += d[j];
+      }
+    }
+    const float c1 = wave_sum(s1) * (1.0f / D), c2 = wave_sum(s2) * (1.0f / D);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      float o[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = rs * (g[c][j] - c1 - xh[c][j] * c2);
+      Vec<float, VEC>::store(dx + (int64_t)row * D + c * 64 * VEC + lane * VEC, o);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      red[wv][0][c * 64 * VEC + lane * VEC + j] = pw[c][j];
+      red[wv][1][c * 64 * VEC + lane * VEC + j] = pb[c][j];
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * D; i += 256) {
+    const int k = i / D, col = i - k * D;
+    part[((int64_t)blockIdx.x * 2 + k) * D + col] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
+  }
+}
+
+// out[k][col] = sum_b part[b][k][col] for k in {0, 1} (dw, db)
+__global__ void __launch_bounds__(256) k_colsum2(int nb, int D, const float* __restrict__ part,
+                                                  float* __restrict__ dw, float* __restrict__ db) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * D) return;
+  const int k = i / D, col = i - k * D;
+  float acc = 0.f;
+  for (int b = 0; b < nb; ++b) acc += part[((int64_t)b * 2 + k) * D + col];
+  (k == 0 ? dw : db)[col] = acc;
+}
+
 template <typename T, int VEC, int NCH>
 __global__ void __launch_bounds__(256) k_row_inv_norm(int M, const T* __restrict__ x, int ldx,
                                                        float eps, float* __restrict__ out) {
@@ -659,6 +741,28 @@ int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint1
   }
 #undef LS_
   RF_LAUNCH_CHECK("rf_add_layernorm_split_fwd");
+}
+
+size_t rf_layernorm_bwd_workspace(int M, int D) {
+  if (M <= 0 || D <= 0) return 0;
+  return (size_t)((M + LNB_ROWS - 1) / LNB_ROWS) * 2 * D * sizeof(float);
+}
+
+int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
+                     const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
+                     rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && ldx >= D, "rf_layernorm_bwd: bad shape");
+  if (M == 0) return RF_OK;
+  RF_REQUIRE(dy && x && mean && rstd && w && dx && dw && db && workspace, "rf_layernorm_bwd: null pointer");
+  RF_REQUIRE(ldx % 4 == 0, "rf_layernorm_bwd: ldx must be a multiple of 4");
+  hipStream_t s = as_stream(stream);
+  const int nb = (M + LNB_ROWS - 1) / LNB_ROWS;
+  float* part = reinterpret_cast<float*>(workspace);
+#define L_(V, N) k_layernorm_bwd<V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part)
+  RF_ROW_DISPATCH(D, L_);
+#undef L_
+  k_colsum2<<<(2 * D + 255) / 256, 256, 0, s>>>(nb, D, part, dw, db);
+  RF_LAUNCH_CHECK("rf_layernorm_bwd");
 }
 
 int rf_row_inv_norm(int dtype, int M, int D, const void* x, int ldx, float eps, float* out,

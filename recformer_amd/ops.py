@@ -17,7 +17,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF
 
 __all__ = [
     "dtype_code", "prepare_inputs", "embed_ln", "embed_ln_split", "add_layernorm_split", "join_split",
-    "gemm", "layernorm", "add_layernorm", "band_attention_bwd", "band_attention",
+    "gemm", "layernorm", "layernorm_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -282,6 +282,27 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
     if want_f32:
         return out, y32
     return out
+
+
+def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, w: torch.Tensor,
+                  tag: Optional[str] = None):
+    """rf_layernorm_bwd: (dx, dw, db) of y = LN(x) for fp32 dy (contiguous) and x (row-major)."""
+    lib = _lib.load()
+    _dev(dy, x, mean, rstd, w)
+    M, D = x.shape
+    if dy.dtype != torch.float32 or x.dtype != torch.float32:
+        raise TypeError("layernorm_bwd: dy and x must be fp32")
+    dy = dy.contiguous()
+    wf = w.float().contiguous()
+    dx = torch.empty(M, D, dtype=torch.float32, device=x.device)
+    dw = torch.empty(D, dtype=torch.float32, device=x.device)
+    db = torch.empty(D, dtype=torch.float32, device=x.device)
+    ws = torch.empty(max(lib.rf_layernorm_bwd_workspace(M, D), 4), dtype=torch.uint8, device=x.device)
+    with _region(tag):
+        rc = lib.rf_layernorm_bwd(M, D, _p(dy), _p(x), _rowmajor(x, "x"), _p(mean), _p(rstd), _p(wf), _p(dx),
+                                  _p(dw), _p(db), _p(ws), _stream(x))
+    check(rc, "rf_layernorm_bwd")
+    return dx, dw, db
 
 
 def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, tag: Optional[str] = None):

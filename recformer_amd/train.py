@@ -7,7 +7,8 @@ whose backward is written out explicitly:
                backward: dA = dC.W, dW = dC^T.A (hipBLASLt through torch.matmul: plain
                library GEMMs), db = colsum(dC)
   _LayerNorm   y = LN(x) from the HIP kernel (row stats saved)             TF:1071, 1130
-               backward: the standard closed form in fp32
+               backward: the standard closed form in fp32, one HIP pass (rf_layernorm_bwd:
+               dx per row, dgamma / dbeta as deterministic column sums)
   _EmbedLN     LN(Ew[id] + Ep[pos] + Et[tt] + Ei[ip])                       models.py:108-138
                backward: LN backward, then index_add into the four tables (no gradient at
                padding_idx rows of the word / position tables, as nn.Embedding)
@@ -60,6 +61,8 @@ class _Gemm(torch.autograd.Function):
 
 
 def _ln_backward(dy, x, mean, rstd, w):
+    if x.dtype == torch.float32 and x.is_cuda:  # one HIP pass (rf_layernorm_bwd)
+        return ops.layernorm_bwd(dy.float(), x, mean, rstd, w)
     xhat = (x.float() - mean[:, None]) * rstd[:, None]
     g = dy.float() * w[None, :]
     dx = rstd[:, None] * (g - g.mean(-1, keepdim=True) - xhat * (g * xhat).mean(-1, keepdim=True))

@@ -427,3 +427,20 @@ def test_ranker_matches_reference_formula(dev, N):
     for g, r in zip(got[:-1], ref[:-1]):
         assert abs(g - r) <= 1e-6, (got, ref)
     assert abs(got[-1] - ref[-1]) <= 1e-5 * max(1.0, abs(ref[-1]))
+
+
+@pytest.mark.parametrize("M,D", [(333, 768), (64, 128), (1000, 1024)])
+def test_layernorm_bwd_matches_autograd(dev, M, D):
+    """rf_layernorm_bwd vs torch autograd of F.layer_norm in fp32 (training path, TF:1071)."""
+    x = _rand((M, D), dev, torch.float32, 2.0, seed=31) + 0.3
+    w = _rand((D,), dev, torch.float32, seed=32)
+    b = _rand((D,), dev, torch.float32, seed=33)
+    dy = _rand((M, D), dev, torch.float32, seed=34)
+    xr = x.clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.layer_norm(xr, (D,), wr, br, 1e-5).backward(dy)
+    _, mean, rstd = ops.layernorm(x, w, b, 1e-5, stats=True)
+    dx, dw, db = ops.layernorm_bwd(dy, x, mean, rstd, w)
+    assert (dx - xr.grad).abs().max().item() <= 1e-4 * xr.grad.abs().max().item() + 1e-5
+    assert (dw - wr.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item() + 1e-4
+    assert (db - br.grad).abs().max().item() <= 1e-4 * br.grad.abs().max().item() + 1e-4
