@@ -122,6 +122,11 @@ int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint1
  * gamma w -> dx (M x D fp32), dw = sum_rows dy * xhat, db = sum_rows dy (fp32 [D]); column sums
  * are reduced deterministically through rf_layernorm_bwd_workspace(M, D) bytes of workspace. */
 size_t rf_layernorm_bwd_workspace(int M, int D);
+/* Column sums out[n] = sum_m x[m][n] (fp32 out; x in dtype, row-major, leading dim ldx), two
+ * deterministic stages through rf_colsum_workspace(M, N) bytes — the bias gradient of the
+ * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias). */
+size_t rf_colsum_workspace(int M, int N);
+int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, void* workspace, rf_stream_t stream);
 int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                      const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                      rf_stream_t stream);

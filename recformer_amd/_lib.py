@@ -37,6 +37,8 @@ SIGNATURES = {
     "rf_embed_ln_split_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_float, P, P, P]),
     "rf_add_layernorm_split_fwd": (c_int, [c_int, c_int, P, c_int, P, P, P, P, c_float, P, P, P, P]),
     "rf_layernorm_bwd_workspace": (ctypes.c_size_t, [c_int, c_int]),
+    "rf_colsum_workspace": (ctypes.c_size_t, [c_int, c_int]),
+    "rf_colsum": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, P, P]),
     "rf_layernorm_bwd": (c_int, [c_int, c_int, P, P, c_int, P, P, P, P, P, P, P, P]),
     "rf_band_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
                                  c_int, P, c_int, P]),

@@ -440,15 +440,68 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
   }
 }
 
-// out[k][col] = sum_b part[b][k][col] for k in {0, 1} (dw, db)
-__global__ void __launch_bounds__(256) k_colsum2(int nb, int D, const float* __restrict__ part,
-                                                  float* __restrict__ dw, float* __restrict__ db) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= 2 * D) return;
-  const int k = i / D, col = i - k * D;
-  float acc = 0.f;
-  for (int b = 0; b < nb; ++b) acc += part[((int64_t)b * 2 + k) * D + col];
-  (k == 0 ? dw : db)[col] = acc;
+// Deterministic column sums of an (M, N) row-major matrix (T = fp32 or bf16) in two stages:
+// k_colsum_part: block (column group of 64, row slice z) -> part[z][N] (4 row phases per block
+// combined in LDS); k_colsum_fin: out[n] = sum_z part[z][n]. Used for LayerNorm dgamma / dbeta
+// (over k_layernorm_bwd's per-block partials) and for bias gradients (column sums of dC).
+constexpr int CS_SLICES = 64;  // k_colsum_fin reduces at most 64 slices
+
+template <typename T, bool VECOK>
+__global__ void __launch_bounds__(256) k_colsum_part(int M, int N, const T* __restrict__ x, int64_t ldx,
+                                                      float* __restrict__ part) {
+  // 64 lanes x 4 consecutive columns = 256 columns per block; 4 row phases (waves) combined in LDS
+  __shared__ float red[4][256];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + 4 * lane;
+  const int per = (M + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(M, r0 + per);
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (VECOK && c + 4 <= N) {  // 4-element vector loads (aligned rows), 8 rows in flight
+#pragma unroll 8
+    for (int r = r0 + ph; r < r1; r += 4) {
+      float v[4];
+      Vec<T, 4>::load(x + (int64_t)r * ldx + c, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += v[k];
+    }
+  } else {
+    for (int r = r0 + ph; r < r1; r += 4)
+      for (int k = 0; k < 4 && c + k < N; ++k) a[k] += to_f32(x[(int64_t)r * ldx + c + k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[ph][4 * lane + k] = a[k];
+  __syncthreads();
+  const int cc = blockIdx.x * 256 + threadIdx.x;
+  if (cc < N)
+    part[(int64_t)blockIdx.y * N + cc] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// out[n] = sum_z part[z][n]: 64 slices x 4 columns per block, tree-reduced in LDS (fixed order)
+__global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* __restrict__ part, float* __restrict__ out,
+                                                     float* __restrict__ out2, int split) {
+  __shared__ float red[64][5];
+  const int z = threadIdx.x >> 2, k = threadIdx.x & 3;
+  const int c = blockIdx.x * 4 + k;
+  red[z][k] = (c < N && z < S) ? part[(int64_t)z * N + c] : 0.f;
+  __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    if (z < o) red[z][k] += red[z + o][k];
+    __syncthreads();
+  }
+  if (z == 0 && c < N) {
+    if (out2 && c >= split) out2[c - split] = red[0][k];
+    else out[c] = red[0][k];
+  }
+}
+
+template <typename T>
+static void colsum(int M, int N, const T* x, int64_t ldx, float* part, float* out, float* out2, int split,
+                   hipStream_t s) {
+  const int S = max(1, min(CS_SLICES, (M + 63) / 64));
+  const bool vec = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(T))) == 0;
+  if (vec) k_colsum_part<T, true><<<dim3((N + 255) / 256, S), 256, 0, s>>>(M, N, x, ldx, part);
+  else k_colsum_part<T, false><<<dim3((N + 255) / 256, S), 256, 0, s>>>(M, N, x, ldx, part);
+  k_colsum_fin<<<(N + 3) / 4, 256, 0, s>>>(S, N, part, out, out2, split);
 }
 
 template <typename T, int VEC, int NCH>
@@ -745,7 +798,23 @@ int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint1
 
 size_t rf_layernorm_bwd_workspace(int M, int D) {
   if (M <= 0 || D <= 0) return 0;
-  return (size_t)((M + LNB_ROWS - 1) / LNB_ROWS) * 2 * D * sizeof(float);
+  return ((size_t)((M + LNB_ROWS - 1) / LNB_ROWS) + CS_SLICES) * 2 * D * sizeof(float);
+}
+
+size_t rf_colsum_workspace(int M, int N) { return (size_t)CS_SLICES * (N > 0 ? N : 0) * sizeof(float); }
+
+int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, void* workspace, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && N > 0 && ldx >= N, "rf_colsum: bad shape");
+  RF_REQUIRE(out && workspace && (M == 0 || x), "rf_colsum: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    (void)hipMemsetAsync(out, 0, (size_t)N * sizeof(float), s);
+    RF_LAUNCH_CHECK("rf_colsum");
+  }
+  if (dtype == RF_BF16) colsum<bf16>(M, N, (const bf16*)x, ldx, (float*)workspace, out, nullptr, N, s);
+  else if (dtype == RF_F32) colsum<float>(M, N, (const float*)x, ldx, (float*)workspace, out, nullptr, N, s);
+  else RF_REQUIRE(false, "rf_colsum: bad dtype %d", dtype);
+  RF_LAUNCH_CHECK("rf_colsum");
 }
 
 int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
@@ -761,7 +830,7 @@ int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, con
 #define L_(V, N) k_layernorm_bwd<V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
-  k_colsum2<<<(2 * D + 255) / 256, 256, 0, s>>>(nb, D, part, dw, db);
+  colsum<float>(nb, 2 * D, part, 2 * D, part + (size_t)nb * 2 * D, dw, db, D, s);  // [dw | db] columns
   RF_LAUNCH_CHECK("rf_layernorm_bwd");
 }
 

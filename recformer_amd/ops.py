@@ -17,7 +17,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF
 
 __all__ = [
     "dtype_code", "prepare_inputs", "embed_ln", "embed_ln_split", "add_layernorm_split", "join_split",
-    "gemm", "layernorm", "layernorm_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
+    "gemm", "colsum", "layernorm", "layernorm_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -303,6 +303,19 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
                                   _p(dw), _p(db), _p(ws), _stream(x))
     check(rc, "rf_layernorm_bwd")
     return dx, dw, db
+
+
+def colsum(x: torch.Tensor, tag: Optional[str] = None) -> torch.Tensor:
+    """rf_colsum: fp32 column sums of a row-major (M, N) bf16 / fp32 matrix (bias gradients)."""
+    lib = _lib.load()
+    _dev(x)
+    M, N = x.shape
+    out = torch.empty(N, dtype=torch.float32, device=x.device)
+    ws = torch.empty(max(lib.rf_colsum_workspace(M, N), 4), dtype=torch.uint8, device=x.device)
+    with _region(tag):
+        rc = lib.rf_colsum(dtype_code(x.dtype), M, N, _p(x), _rowmajor(x, "x"), _p(out), _p(ws), _stream(x))
+    check(rc, "rf_colsum")
+    return out
 
 
 def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, tag: Optional[str] = None):

@@ -56,7 +56,7 @@ class _Gemm(torch.autograd.Function):
             dc[:, :sc] *= s
         da = dc @ w if ctx.needs_input_grad[0] else None
         dw = dc.t() @ a if ctx.needs_input_grad[1] else None
-        db = dc.float().sum(0) if ctx.needs_input_grad[2] else None
+        db = ops.colsum(dc) if ctx.needs_input_grad[2] else None  # deterministic HIP column sums
         return da, dw, db, None, None
 
 

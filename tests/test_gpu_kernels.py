@@ -444,3 +444,12 @@ def test_layernorm_bwd_matches_autograd(dev, M, D):
     assert (dx - xr.grad).abs().max().item() <= 1e-4 * xr.grad.abs().max().item() + 1e-5
     assert (dw - wr.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item() + 1e-4
     assert (db - br.grad).abs().max().item() <= 1e-4 * br.grad.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N", [(1, 5), (333, 768), (16384, 2304), (70, 3072), (65, 6)])
+def test_colsum(dev, dt, M, N):
+    for x in (_rand((M, N + 8), dev, dt, seed=41)[:, :N], _rand((M, N + 3), dev, dt, seed=42)[:, :N]):
+        ref = x.float().sum(0)  # strided rows: vector path (ld % 4 == 0) and scalar path
+        out = ops.colsum(x)
+        assert (out - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item()) + 1e-3
