@@ -122,6 +122,18 @@ int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint1
  * gamma w -> dx (M x D fp32), dw = sum_rows dy * xhat, db = sum_rows dy (fp32 [D]); column sums
  * are reduced deterministically through rf_layernorm_bwd_workspace(M, D) bytes of workspace. */
 size_t rf_layernorm_bwd_workspace(int M, int D);
+/* Training path, hidden dropout + residual + LayerNorm (TF:1068-1071, 1127-1130 with
+ * nn.Dropout(hidden_dropout_prob)): x = dropout_p(t) + res (t bf16 dense output, ld ldt; res fp32
+ * M x D), y = LN(x); writes x (fp32, the backward's input), y (fp32) and the row stats. The keep
+ * mask is a counter hash of (seed, row * D + col), regenerated by rf_drop_add_ln_bwd, which
+ * writes dres = dx (fp32), dt = dx * mask / (1 - p) (bf16) and dw / db (workspace as
+ * rf_layernorm_bwd). p = 0: plain residual add. */
+int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
+                       const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,
+                       rf_stream_t stream);
+int rf_drop_add_ln_bwd(int M, int D, const float* dy, const float* x, const float* mean, const float* rstd,
+                       const float* w, float p, uint64_t seed, float* dres, void* dt, float* dw, float* db,
+                       void* workspace, rf_stream_t stream);
 /* Column sums out[n] = sum_m x[m][n] (fp32 out; x in dtype, row-major, leading dim ldx), two
  * deterministic stages through rf_colsum_workspace(M, N) bytes — the bias gradient of the
  * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias). */

@@ -369,6 +369,74 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
   }
 }
 
+// ---- training path: hidden dropout + residual add + LayerNorm (TF:1068-1071, 1127-1130) ----
+// Forward: x = dropout(t) + res, y = LN(x) in one pass (t the bf16 dense output, res the fp32
+// stream); x (the backward's input) and the row stats are written. The keep mask is a counter
+// hash of (seed, element index) — regenerated by the backward, never stored.
+__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  uint32_t h = (uint32_t)idx * 0x9E3779B1u ^ (uint32_t)(idx >> 32) * 0x85EBCA77u ^ (uint32_t)seed;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= (uint32_t)(seed >> 32);
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h >= thresh;  // P(keep) = 1 - thresh / 2^32
+}
+
+template <int VEC, int NCH>
+__global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const bf16* __restrict__ t, int ldt,
+                                                          const float* __restrict__ res, uint32_t thresh,
+                                                          float keep_scale, uint64_t seed,
+                                                          const float* __restrict__ lw, const float* __restrict__ lb,
+                                                          float eps, float* __restrict__ xo, float* __restrict__ y,
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int D = 64 * VEC * NCH;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float xv[NCH][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = c * 64 * VEC + lane * VEC;
+    float tv[VEC], rv[VEC];
+    Vec<bf16, VEC>::load(t + (int64_t)row * ldt + e, tv);
+    Vec<float, VEC>::load(res + (int64_t)row * D + e, rv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const bool keep = thresh == 0 || drop_keep(seed, (uint64_t)row * D + e + j, thresh);
+      xv[c][j] = (keep ? tv[j] * keep_scale : 0.f) + rv[j];
+      s += xv[c][j];
+    }
+    Vec<float, VEC>::store(xo + (int64_t)row * D + e, xv[c]);
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float v = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float d = xv[c][j] - mean;
+      v += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(v) * (1.0f / D) + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = c * 64 * VEC + lane * VEC;
+    float w[VEC], bb[VEC], o[VEC];
+    Vec<float, VEC>::load(lw + e, w);
+    Vec<float, VEC>::load(lb + e, bb);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (xv[c][j] - mean) * rstd * w[j] + bb[j];
+    Vec<float, VEC>::store(y + (int64_t)row * D + e, o);
+  }
+}
+
 // LayerNorm backward (training path; TF:1071, 1130 under autograd): per row, with
 // xhat = (x - mean) * rstd and g = dy * w,
 //   dx = rstd * (g - mean(g) - xhat * mean(g * xhat))
@@ -377,13 +445,16 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
 // One wave per row, LNB_ROWS rows per 256-thread block.
 constexpr int LNB_ROWS = 32;
 
+// With dt != null (the dropout + residual form above) it also writes the dense branch's
+// gradient dt = dx * keep * keep_scale in bf16 (the mask regenerated from the seed).
 template <int VEC, int NCH>
 __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __restrict__ dy,
                                                         const float* __restrict__ x, int ldx,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ rstd,
                                                         const float* __restrict__ w, float* __restrict__ dx,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, bf16* __restrict__ dt,
+                                                        uint32_t thresh, float keep_scale, uint64_t seed) {
   constexpr int D = 64 * VEC * NCH;
   __shared__ float red[4][2][D];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -423,7 +494,15 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
       float o[VEC];
 #pragma unroll
       for (int j = 0; j < VEC; ++j) o[j] = rs * (g[c][j] - c1 - xh[c][j] * c2);
-      Vec<float, VEC>::store(dx + (int64_t)row * D + c * 64 * VEC + lane * VEC, o);
+      const int e = c * 64 * VEC + lane * VEC;
+      Vec<float, VEC>::store(dx + (int64_t)row * D + e, o);
+      if (dt) {
+        float od[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+          od[j] = (thresh == 0 || drop_keep(seed, (uint64_t)row * D + e + j, thresh)) ? o[j] * keep_scale : 0.f;
+        Vec<bf16, VEC>::store(dt + (int64_t)row * D + e, od);
+      }
     }
   }
 #pragma unroll
@@ -817,9 +896,51 @@ int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, v
   RF_LAUNCH_CHECK("rf_colsum");
 }
 
+static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
+                       const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
+                       bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream);
+
+static uint32_t drop_thresh(float p) {
+  return p <= 0.f ? 0u : (p >= 1.f ? 0xFFFFFFFFu : (uint32_t)((double)p * 4294967296.0));
+}
+
+int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
+                       const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,
+                       rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && ldt >= D && p >= 0.f && p < 1.f, "rf_drop_add_ln_fwd: bad arguments");
+  if (M == 0) return RF_OK;
+  RF_REQUIRE(t && res && w && b && x && y && mean && rstd, "rf_drop_add_ln_fwd: null pointer");
+  RF_REQUIRE(ldt % 4 == 0, "rf_drop_add_ln_fwd: ldt must be a multiple of 4");
+  hipStream_t s = as_stream(stream);
+  const uint32_t th = drop_thresh(p);
+  const float ks = 1.0f / (1.0f - p);
+  dim3 grid((M + 3) / 4);
+#define L_(V, N)                                                                                   \
+  k_drop_add_ln_fwd<V, N><<<grid, 256, 0, s>>>(M, (const bf16*)t, ldt, res, th, ks, seed, w, b, eps, x, y, \
+                                               mean, rstd)
+  RF_ROW_DISPATCH(D, L_);
+#undef L_
+  RF_LAUNCH_CHECK("rf_drop_add_ln_fwd");
+}
+
+int rf_drop_add_ln_bwd(int M, int D, const float* dy, const float* x, const float* mean, const float* rstd,
+                       const float* w, float p, uint64_t seed, float* dres, void* dt, float* dw, float* db,
+                       void* workspace, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && p >= 0.f && p < 1.f, "rf_drop_add_ln_bwd: bad arguments");
+  RF_REQUIRE(M == 0 || dt, "rf_drop_add_ln_bwd: null dt");
+  return ln_bwd_impl(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (bf16*)dt, drop_thresh(p),
+                     1.0f / (1.0f - p), seed, stream);
+}
+
 int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                      const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                      rf_stream_t stream) {
+  return ln_bwd_impl(M, D, dy, x, ldx, mean, rstd, w, dx, dw, db, workspace, nullptr, 0u, 1.f, 0ull, stream);
+}
+
+static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
+                       const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
+                       bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && ldx >= D, "rf_layernorm_bwd: bad shape");
   if (M == 0) return RF_OK;
   RF_REQUIRE(dy && x && mean && rstd && w && dx && dw && db && workspace, "rf_layernorm_bwd: null pointer");
@@ -827,7 +948,7 @@ int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, con
   hipStream_t s = as_stream(stream);
   const int nb = (M + LNB_ROWS - 1) / LNB_ROWS;
   float* part = reinterpret_cast<float*>(workspace);
-#define L_(V, N) k_layernorm_bwd<V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part)
+#define L_(V, N) k_layernorm_bwd<V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
   colsum<float>(nb, 2 * D, part, 2 * D, part + (size_t)nb * 2 * D, dw, db, D, s);  // [dw | db] columns

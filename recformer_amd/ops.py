@@ -17,7 +17,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF
 
 __all__ = [
     "dtype_code", "prepare_inputs", "embed_ln", "embed_ln_split", "add_layernorm_split", "join_split",
-    "gemm", "colsum", "layernorm", "layernorm_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
+    "gemm", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -316,6 +316,40 @@ def colsum(x: torch.Tensor, tag: Optional[str] = None) -> torch.Tensor:
         rc = lib.rf_colsum(dtype_code(x.dtype), M, N, _p(x), _rowmajor(x, "x"), _p(out), _p(ws), _stream(x))
     check(rc, "rf_colsum")
     return out
+
+
+def drop_add_ln_fwd(t: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float, p: float,
+                    seed: int):
+    """rf_drop_add_ln_fwd: (x, y, mean, rstd) with x = dropout_p(t) + res, y = LN(x), all fp32."""
+    lib = _lib.load()
+    _dev(t, res, w, b)
+    M, D = t.shape
+    if t.dtype != torch.bfloat16 or res.dtype != torch.float32 or not res.is_contiguous():
+        raise TypeError("drop_add_ln_fwd: t bf16 (row-major), res contiguous fp32")
+    x = torch.empty(M, D, dtype=torch.float32, device=t.device)
+    y = torch.empty_like(x)
+    mean = torch.empty(M, dtype=torch.float32, device=t.device)
+    rstd = torch.empty_like(mean)
+    check(lib.rf_drop_add_ln_fwd(M, D, _p(t), _rowmajor(t, "t"), _p(res), float(p), seed, _p(w.float().contiguous()),
+                                 _p(b.float().contiguous()), float(eps), _p(x), _p(y), _p(mean), _p(rstd),
+                                 _stream(t)), "rf_drop_add_ln_fwd")
+    return x, y, mean, rstd
+
+
+def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int):
+    """rf_drop_add_ln_bwd: (dres fp32, dt bf16, dw, db)."""
+    lib = _lib.load()
+    _dev(dy, x, mean, rstd, w)
+    M, D = x.shape
+    dy = dy.float().contiguous()
+    dres = torch.empty(M, D, dtype=torch.float32, device=x.device)
+    dt = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
+    dw = torch.empty(D, dtype=torch.float32, device=x.device)
+    db = torch.empty_like(dw)
+    ws = torch.empty(max(lib.rf_layernorm_bwd_workspace(M, D), 4), dtype=torch.uint8, device=x.device)
+    check(lib.rf_drop_add_ln_bwd(M, D, _p(dy), _p(x), _p(mean), _p(rstd), _p(w.float().contiguous()), float(p), seed,
+                                 _p(dres), _p(dt), _p(dw), _p(db), _p(ws), _stream(x)), "rf_drop_add_ln_bwd")
+    return dres, dt, dw, db
 
 
 def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, tag: Optional[str] = None):

@@ -22,7 +22,8 @@ bf16, LayerNorm outputs / residual stream / losses in fp32, parameters fp32 (the
 copies are autograd-tracked casts, so gradients reach the fp32 masters).
 
 Dropout: hidden dropout (embeddings, attention output, FFN output; TF:1069, 1128, models.py:137)
-is applied with torch's RNG. Attention-probability dropout (TF:581) is not implemented: training
+is applied with torch's RNG, except in the bf16 path's fused dropout + residual + LayerNorm
+(_DropAddLN), whose keep mask is a counter hash of a seed drawn from torch's RNG. Attention-probability dropout (TF:581) is not implemented: training
 with attention_probs_dropout_prob > 0 raises.
 """
 from __future__ import annotations
@@ -83,6 +84,26 @@ class _LayerNorm(torch.autograd.Function):
         x, mean, rstd, w = ctx.saved_tensors
         dx, dw, db = _ln_backward(dy, x, mean, rstd, w)
         return dx.to(x.dtype), dw, db, None, None
+
+
+class _DropAddLN(torch.autograd.Function):
+    """y = LN(dropout_p(t) + res) (TF:1068-1071, 1127-1130): t the bf16 dense output, res the fp32
+    residual stream; one HIP pass each way (rf_drop_add_ln_fwd / _bwd), the dropout mask a
+    counter hash of a seed drawn from torch's RNG."""
+
+    @staticmethod
+    def forward(ctx, t, res, w, b, eps: float, p: float):
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        x, y, mean, rstd = ops.drop_add_ln_fwd(t, res.contiguous(), w, b, eps, p, seed)
+        ctx.save_for_backward(x, mean, rstd, w)
+        ctx.p, ctx.seed = p, seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, w = ctx.saved_tensors
+        dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed)
+        return dt, dres, dw, db, None, None
 
 
 class _EmbedLN(torch.autograd.Function):
@@ -320,6 +341,8 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     if gmax > 0:
         rows = (torch.arange(B, device=input_ids.device)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
         gvalid = (gidx >= 0).reshape(-1, 1)
+    # bf16 path: dropout + residual + LayerNorm as one HIP pass each way (_DropAddLN)
+    fused = dt == torch.bfloat16 and D in (64, 128, 256, 384, 512, 768, 1024)
     for li, lyr in enumerate(model.encoder.layer):
         sa = lyr.attention.self
         h = h32.to(dt)
@@ -336,14 +359,20 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
                                flags, gidx, B, Lp, H, windows[li] // 2, fold)
         ao = lyr.attention.output
         t = _Gemm.apply(ctx, ao.dense.weight.to(dt), ao.dense.bias.float(), 0, 1.0)
-        x1 = F.dropout(t.float(), p_hid, model.training) + h32
-        a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
+        if fused:
+            a32 = _DropAddLN.apply(t, h32, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid)
+        else:
+            x1 = F.dropout(t.float(), p_hid, model.training) + h32
+            a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
         z = _Gemm.apply(a32.to(dt), lyr.intermediate.dense.weight.to(dt), lyr.intermediate.dense.bias.float(), 0, 1.0)
         u = F.gelu(z)
         fo = lyr.output
         t2 = _Gemm.apply(u, fo.dense.weight.to(dt), fo.dense.bias.float(), 0, 1.0)
-        x2 = F.dropout(t2.float(), p_hid, model.training) + a32
-        h32 = _LayerNorm.apply(x2, fo.LayerNorm.weight.float(), fo.LayerNorm.bias.float(), eps, torch.float32)
+        if fused:
+            h32 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid)
+        else:
+            x2 = F.dropout(t2.float(), p_hid, model.training) + a32
+            h32 = _LayerNorm.apply(x2, fo.LayerNorm.weight.float(), fo.LayerNorm.bias.float(), eps, torch.float32)
         if output_hidden_states:
             hidden_all.append(h32)
     last = h32.view(B, Lp, D)[:, :L]

@@ -453,3 +453,37 @@ def test_colsum(dev, dt, M, N):
         ref = x.float().sum(0)  # strided rows: vector path (ld % 4 == 0) and scalar path
         out = ops.colsum(x)
         assert (out - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item()) + 1e-3
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_drop_add_ln_matches_torch(dev, p):
+    """Fused dropout + residual + LayerNorm (training path): with the keep mask recovered from the
+    saved pre-LN rows, forward and every gradient match torch autograd of the same composition;
+    the keep fraction is 1 - p."""
+    M, D = 512, 768
+    t = _rand((M, D), dev, torch.bfloat16, 1.0, seed=51)
+    res = _rand((M, D), dev, torch.float32, 1.0, seed=52)
+    w = _rand((D,), dev, torch.float32, seed=53)
+    b = _rand((D,), dev, torch.float32, seed=54)
+    dy = _rand((M, D), dev, torch.float32, seed=55)
+    x, y, mean, rstd = ops.drop_add_ln_fwd(t, res, w, b, 1e-5, p, 12345)
+    scaled = t.float() / (1 - p)
+    keep = ((x - res) - scaled).abs() <= 1e-5 * scaled.abs() + 1e-6
+    zero = (x - res).abs() <= 1e-6
+    assert bool((keep | zero).all())
+    if p > 0:
+        frac = keep.float().mean().item()
+        assert abs(frac - (1 - p)) < 0.01, frac
+    else:
+        assert bool(keep.all())
+    mask = keep.float()
+    tr, rr = t.float().clone().requires_grad_(True), res.clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.layer_norm(tr * mask / (1 - p) + rr, (D,), wr, br, 1e-5)
+    yr.backward(dy)
+    assert (y - yr).abs().max().item() <= 1e-4
+    dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, p, 12345)
+    assert (dres - rr.grad).abs().max().item() <= 1e-4 * rr.grad.abs().max().item() + 1e-5
+    assert (dt.float() - tr.grad).abs().max().item() <= 2 ** -7 * tr.grad.abs().max().item()
+    assert (dw - wr.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item() + 1e-4
+    assert (db - br.grad).abs().max().item() <= 1e-4 * br.grad.abs().max().item() + 1e-4
