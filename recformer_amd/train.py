@@ -219,8 +219,13 @@ def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp
 
 
 class _Attention(torch.autograd.Function):
+    """Takes the fused (B*Lp, 3D) q|k|v projection and returns its gradient as one tensor (no
+    per-slice zero-fill + accumulate in autograd)."""
+
     @staticmethod
-    def forward(ctx, q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold):
+    def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold):
+        D = qkv.shape[1] // 3
+        q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w)
         if gidx.shape[1] > 0:
             if fold:
@@ -230,24 +235,26 @@ class _Attention(torch.autograd.Function):
                 kg = ops.gemm(h.contiguous(), wkg.contiguous(), bkg, ops.RF_EPI_BIAS)
                 vg = ops.gemm(h.contiguous(), wvg.contiguous(), bvg, ops.RF_EPI_BIAS)
                 ops.global_attention(qg.contiguous(), kg, vg, flags, gidx, B, Lp, H, out)
-        ctx.save_for_backward(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out)
+        ctx.save_for_backward(qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out)
         ctx.dims = (B, Lp, H, half_w)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out = ctx.saved_tensors
+        qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out = ctx.saved_tensors
         B, Lp, H, half_w = ctx.dims
+        D = qkv.shape[1] // 3
+        q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         gmax = gidx.shape[1]
-        hip_local = q.dtype == torch.bfloat16 and half_w == 32 and q.shape[1] == 64 * H and gmax <= 32
+        hip_local = q.dtype == torch.bfloat16 and half_w == 32 and D == 64 * H and gmax <= 32
         if not hip_local:
             return _Attention._backward_torch(ctx, dout)
         # local branch on the HIP backward kernels (rf_attn_bwd.hip); global rows of dout belong
         # to the global branch only (their local output was overwritten)
         d16 = dout.to(torch.bfloat16).contiguous()
-        dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H)
-        D = q.shape[1]
-        res = [None] * 9
+        dqkv = torch.empty(B * Lp, 3 * D, dtype=torch.float32, device=q.device)
+        dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H, dqkv=dqkv)
+        res = [None] * 7
         if gmax > 0:
             rows, keep = _global_rows(gidx, B, Lp)
             # gradients of the global-key columns, reduced over every query of the sequence
@@ -259,7 +266,7 @@ class _Attention(torch.autograd.Function):
             dv.index_add_(0, rows[keep], dvg[keep])
             # global branch through autograd over the fold algebra
             gin = [t.detach().requires_grad_(need) for t, need in
-                   zip((qg, h, wkg, bkg, wvg, bvg), ctx.needs_input_grad[3:9])]
+                   zip((qg, h, wkg, bkg, wvg, bvg), ctx.needs_input_grad[1:7])]
             if any(t.requires_grad for t in gin):
                 with torch.enable_grad(), torch.autocast("cuda", enabled=False):
                     og = _global_torch(*gin, flags, B, Lp, H)
@@ -271,18 +278,20 @@ class _Attention(torch.autograd.Function):
                 for n, t in enumerate(gin):
                     if t.requires_grad:
                         g = next(it)
-                        res[3 + n] = None if g is None else g.to(t.dtype)
-        for n, (t, g) in enumerate(zip((q, k, v), (dq, dk, dv))):
-            if ctx.needs_input_grad[n]:
-                res[n] = g.to(t.dtype)
+                        res[1 + n] = None if g is None else g.to(t.dtype)
+        if ctx.needs_input_grad[0]:
+            res[0] = dqkv.to(qkv.dtype)
         return (*res, None, None, None, None, None, None, None)
 
     @staticmethod
     def _backward_torch(ctx, dout):
-        q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, _ = ctx.saved_tensors
+        qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, _ = ctx.saved_tensors
         B, Lp, H, half_w = ctx.dims
-        inputs = [t.detach().requires_grad_(need) for t, need in
-                  zip((q, k, v, qg, h, wkg, bkg, wvg, bvg), ctx.needs_input_grad[:9])]
+        D = qkv.shape[1] // 3
+        need = ctx.needs_input_grad
+        inputs = [t.detach().requires_grad_(nd) for t, nd in
+                  zip((qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], qg, h, wkg, bkg, wvg, bvg),
+                      (need[0],) * 3 + tuple(need[1:7]))]
         with torch.enable_grad(), torch.autocast("cuda", enabled=False):
             o = _attention_torch(*inputs, flags, gidx, B, Lp, H, half_w)
             want = [t for t in inputs if t.requires_grad]
@@ -295,6 +304,11 @@ class _Attention(torch.autograd.Function):
                 res.append(None if g is None else g.to(t.dtype))
             else:
                 res.append(None)
+        if need[0]:
+            z = [g if g is not None else torch.zeros_like(qkv[:, :D]) for g in res[:3]]
+            res = [torch.cat(z, 1)] + res[3:]
+        else:
+            res = [None] + res[3:]
         return (*res, None, None, None, None, None, None, None)
 
 
@@ -353,7 +367,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         if gmax > 0:
             hg = h[rows] * gvalid.to(h.dtype)
             qg = _Gemm.apply(hg, sa.query_global.weight.to(dt), sa.query_global.bias.float(), D, scale)
-        ctx = _Attention.apply(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], qg, h,
+        ctx = _Attention.apply(qkv, qg, h,
                                sa.key_global.weight.to(dt), sa.key_global.bias.float(),
                                sa.value_global.weight.to(dt), sa.value_global.bias.float(),
                                flags, gidx, B, Lp, H, windows[li] // 2, fold)
