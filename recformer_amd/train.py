@@ -214,7 +214,10 @@ def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp
     if gidx.shape[1] > 0:
         og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H)
         rows, keep = _global_rows(gidx, B, Lp)
-        o = o.index_put((rows[keep],), og[keep])
+        # overwrite the valid global rows (TF:621-629) without boolean-mask indexing (a host
+        # sync): padded slots point at row 0 of their sequence and add exactly zero
+        kf = keep[:, None].to(o.dtype)
+        o = o.index_add(0, rows, (og - o[rows]) * kf)
     return o
 
 
@@ -262,16 +265,17 @@ class _Attention(torch.autograd.Function):
             dh = d16.float().view(B, Lp, H, 64)
             dkg = torch.einsum("bhig,bihd->bghd", gds[..., :gmax], qh).reshape(B * gmax, D)
             dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :gmax], dh).reshape(B * gmax, D)
-            dk.index_add_(0, rows[keep], dkg[keep])
-            dv.index_add_(0, rows[keep], dvg[keep])
+            # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
+            kf = keep[:, None].to(dkg.dtype)
+            dk.index_add_(0, rows, dkg * kf)
+            dv.index_add_(0, rows, dvg * kf)
             # global branch through autograd over the fold algebra
             gin = [t.detach().requires_grad_(need) for t, need in
                    zip((qg, h, wkg, bkg, wvg, bvg), ctx.needs_input_grad[1:7])]
             if any(t.requires_grad for t in gin):
                 with torch.enable_grad(), torch.autocast("cuda", enabled=False):
                     og = _global_torch(*gin, flags, B, Lp, H)
-                    gout = torch.zeros_like(og)
-                    gout[keep] = dout[rows[keep]].float()
+                    gout = dout[rows].float() * keep[:, None].to(torch.float32)
                     want = [t for t in gin if t.requires_grad]
                     grads = torch.autograd.grad(og, want, gout, allow_unused=True)
                 it = iter(grads)

@@ -2,7 +2,7 @@
 # rocprofv3 kernel-trace summary of the C3 training step (tools/train_bench.py)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 rm -rf gpurun_out/trainprof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trainprof -o tr -- python3 tools/train_bench.py --steps 3 --warmup 1 > gpurun_out/trainprof.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trainprof -o tr -- python3 ${TRAIN_TOOL:-tools/train_bench.py} --steps 3 --warmup 1 > gpurun_out/trainprof.log 2>&1 || exit 1
 python3 - <<'PY'
 import csv, glob
 f = glob.glob('gpurun_out/trainprof/**/*kernel_stats.csv', recursive=True)[0]
