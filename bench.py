@@ -115,10 +115,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank control flow on a one-GPU box (tools/gpu/dist_rehearsal.sh): every
+    # rank on cuda:0 with gloo collectives on host tensors. Production runs use nccl (RCCL).
+    rehearsal = os.environ.get("RF_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    coll_dev = None if rehearsal else dev
 
     from recformer_amd import RecformerConfig, RecformerForSeqRec, dp, ops
     from recformer_amd.synth import BASE, synth_batch
@@ -171,7 +180,7 @@ def main():
             ops.enable_timing(False)
     assert scores.shape == (B, args.catalog)
 
-    tmax = dp.max_over_ranks(elapsed, device=dev)
+    tmax = dp.max_over_ranks(elapsed, device=coll_dev)
     total_seqs = B * world * args.steps
     value = total_seqs / tmax
 
