@@ -198,6 +198,17 @@ int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H, const void
                               const int32_t* gidx, int gmax, void* workspace, void* out, int ld_out,
                               rf_stream_t stream);
 
+/* rf_global_attn_fold_h_fwd in two halves on one workspace: stage 1 = the query_global
+ * projection + the partial softmax over h (reads h, writes only the workspace), stage 2 = the
+ * merge + value fold (reads only the workspace, writes the global rows of out); 3 = both. Lets
+ * the caller read h while it is still cache-resident (right after the LayerNorm that wrote it)
+ * and write out after the local attention has filled the other rows. */
+int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
+                                const void* wqg, const float* bqg, float q_scale, const void* wkg,
+                                const float* bkg, const void* wvg, const float* bvg, const uint8_t* flags,
+                                const int32_t* gidx, int gmax, void* workspace, void* out, int ld_out,
+                                rf_stream_t stream);
+
 /* Row gather: out[r] = x[b*Lp + gidx[b, g]] for r = b*gmax + g (zero rows for -1). Feeds
  * the query_global projection of the global rows (TF:972-982). */
 int rf_gather_global_rows(int dtype, int B, int Lp, int D, int gmax, const void* x, int ldx,

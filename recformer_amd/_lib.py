@@ -54,6 +54,8 @@ SIGNATURES = {
                                         P, P, P, P, c_int, P, P, c_int, P]),
     "rf_global_attn_fold_h_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_float, P, P, P,
                                           P, P, P, c_int, P, P, c_int, P]),
+    "rf_global_attn_fold_h_stage": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_float, P,
+                                            P, P, P, P, P, c_int, P, P, c_int, P]),
     "rf_gather_global_rows":(c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
     "rf_row_inv_norm": (c_int, [c_int, c_int, c_int, P, c_int, c_float, P, P]),
     "rf_cos_score_cand": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P,

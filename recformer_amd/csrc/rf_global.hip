@@ -873,7 +873,8 @@ static bool gfold_use_mfma(int R, bool qu) {
 // partial + out stages shared by both entry points (u already in the workspace)
 static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
                             const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax,
-                            GfoldWs ws, int nch, void* out, int ld_out, hipStream_t s) {
+                            GfoldWs ws, int nch, void* out, int ld_out, hipStream_t s, bool do_partial = true,
+                            bool do_out = true) {
   const int R = B * gmax;
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
   if (dtype == RF_BF16) {
@@ -893,13 +894,14 @@ static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* 
                                                                   flags, gidx, ws, H);          \
     }                                                                                           \
     break;
-    switch (D) {
+    if (do_partial) switch (D) {
       GP_(64) GP_(128) GP_(192) GP_(256) GP_(384) GP_(512) GP_(768) GP_(1024)
       default:
         RF_REQUIRE(false, "rf_global_attn_fold(bf16): unsupported hidden size %d", D);
     }
 #undef GP_
-    if (ld_out % 4 == 0 && gfold_use_mfma(R, false)) {
+    if (!do_out) {
+    } else if (ld_out % 4 == 0 && gfold_use_mfma(R, false)) {
       const size_t lds_w = (size_t)D * 128;
 #define GO_(DD)                                                                                 \
   case DD:                                                                                      \
@@ -919,8 +921,10 @@ static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* 
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
     (void)hipFuncSetAttribute((const void*)k_gfold_partial_f32,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);
-    k_gfold_partial_f32<<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const float*)h, ldh, flags, gidx, ws);
-    k_gfold_out<float><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const float*)wvg, bvg, gidx, ws,
+    if (do_partial)
+      k_gfold_partial_f32<<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const float*)h, ldh, flags, gidx, ws);
+    if (do_out)
+      k_gfold_out<float><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const float*)wvg, bvg, gidx, ws,
                                                        (float*)out, ld_out);
   }
   return RF_OK;
@@ -957,27 +961,29 @@ extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, c
   RF_LAUNCH_CHECK("rf_global_attn_fold_fwd");
 }
 
-extern "C" int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
-                                         const void* wqg, const float* bqg, float q_scale, const void* wkg,
-                                         const float* bkg, const void* wvg, const float* bvg,
-                                         const uint8_t* flags, const int32_t* gidx, int gmax,
-                                         void* workspace, void* out, int ld_out, rf_stream_t stream) {
+extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, int D, int H, const void* h,
+                                           int ldh, const void* wqg, const float* bqg, float q_scale,
+                                           const void* wkg, const float* bkg, const void* wvg, const float* bvg,
+                                           const uint8_t* flags, const int32_t* gidx, int gmax,
+                                           void* workspace, void* out, int ld_out, rf_stream_t stream) {
   (void)bkg;
-  RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0, "rf_global_attn_fold_h_fwd: bad shape");
-  RF_REQUIRE(D == H * 64 && D <= 1024, "rf_global_attn_fold_h_fwd: D=%d must be H*64 <= 1024", D);
-  RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_h_fwd: at most %d heads", GF_HP);
-  RF_REQUIRE(ldh >= D && ld_out >= D, "rf_global_attn_fold_h_fwd: dims");
-  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F32, "rf_global_attn_fold_h_fwd: bad dtype %d", dtype);
+  RF_REQUIRE(stage >= 1 && stage <= 3, "rf_global_attn_fold_h_stage: stage %d not in 1..3", stage);
+  RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0, "rf_global_attn_fold_h: bad shape");
+  RF_REQUIRE(D == H * 64 && D <= 1024, "rf_global_attn_fold_h: D=%d must be H*64 <= 1024", D);
+  RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_h: at most %d heads", GF_HP);
+  RF_REQUIRE(ldh >= D && ld_out >= D, "rf_global_attn_fold_h: dims");
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F32, "rf_global_attn_fold_h: bad dtype %d", dtype);
   if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
-  RF_REQUIRE(workspace && gidx && flags && wqg && bqg, "rf_global_attn_fold_h_fwd: null pointer");
-  RF_REQUIRE(dtype != RF_BF16 || ldh % 8 == 0, "rf_global_attn_fold_h_fwd(bf16): ldh must be a multiple of 8");
-  RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_h_fwd(f32): ldh must be a multiple of 4");
+  RF_REQUIRE(workspace && gidx && flags && wqg && bqg, "rf_global_attn_fold_h: null pointer");
+  RF_REQUIRE(dtype != RF_BF16 || ldh % 8 == 0, "rf_global_attn_fold_h(bf16): ldh must be a multiple of 8");
+  RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_h(f32): ldh must be a multiple of 4");
   const int R = B * gmax;
   const int nch = (Lp + (dtype == RF_BF16 ? GF_CH : GF_CHF) - 1) / (dtype == RF_BF16 ? GF_CH : GF_CHF);
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
-  if (dtype == RF_BF16 && gfold_use_mfma(R, true)) {
-    RF_REQUIRE(D % 64 == 0 && D <= 1024, "rf_global_attn_fold_h_fwd: D=%d", D);
+  if (!(stage & 1)) {
+  } else if (dtype == RF_BF16 && gfold_use_mfma(R, true)) {
+    RF_REQUIRE(D % 64 == 0 && D <= 1024, "rf_global_attn_fold_h: D=%d", D);
     const size_t lds_q = (size_t)D * 128 + 4 * 2048;
     // few row tiles: split u's columns over more blocks (each recomputes its tile's qg)
     int qsplit = 1;
@@ -998,7 +1004,17 @@ extern "C" int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H,
   else
     k_gfold_qu<float><<<dim3(H, R), 256, 0, s>>>(Lp, D, H, gmax, (const float*)h, ldh, (const float*)wqg, bqg,
                                                   q_scale, (const float*)wkg, gidx, ws, false);
-  const int rc = fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s);
+  const int rc = fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s,
+                                  (stage & 1) != 0, (stage & 2) != 0);
   if (rc != RF_OK) return rc;
-  RF_LAUNCH_CHECK("rf_global_attn_fold_h_fwd");
+  RF_LAUNCH_CHECK("rf_global_attn_fold_h_stage");
+}
+
+extern "C" int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
+                                         const void* wqg, const float* bqg, float q_scale, const void* wkg,
+                                         const float* bkg, const void* wvg, const float* bvg,
+                                         const uint8_t* flags, const int32_t* gidx, int gmax,
+                                         void* workspace, void* out, int ld_out, rf_stream_t stream) {
+  return rf_global_attn_fold_h_stage(3, dtype, B, Lp, D, H, h, ldh, wqg, bqg, q_scale, wkg, bkg, wvg, bvg, flags,
+                                     gidx, gmax, workspace, out, ld_out, stream);
 }

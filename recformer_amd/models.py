@@ -216,6 +216,8 @@ def _cos_train(z: torch.Tensor, items: torch.Tensor, temp: float) -> torch.Tenso
 # bf16 path: keep the fp32 residual stream as split (hi, lo) 16-bit planes;
 # False = a plain fp32 tensor plus a separate bf16 GEMM operand (A/B tools, tests).
 SPLIT_STREAM = True
+# run the global fold's pass over h before the qkv GEMM (rf_global_attn_fold_h_stage)
+FOLD_EARLY = True
 
 
 def _compute_dtype(param_dtype: torch.dtype) -> torch.dtype:
@@ -411,14 +413,26 @@ class RecformerModel(nn.Module):
         # = False` keeps the reference's structure (k_g/v_g projected over all tokens).
         fold = getattr(cfg, "global_attention_fold", True)
         eps = cfg.layer_norm_eps
+        gws = None
         for li, lw in enumerate(pk["layers"]):
             half_w = windows[li] // 2
             nq = 5 * D if (gmax > 0 and not fold) else 3 * D
+            gargs = (h, lw["w_qg"], lw["b_qg"], scale, lw["w_qkv"][3 * D:4 * D], lw["b_qkv"][3 * D:4 * D],
+                     lw["w_qkv"][4 * D:5 * D], lw["b_qkv"][4 * D:5 * D], flags, gidx, B, Lp, H)
+            early = gmax > 0 and fold and FOLD_EARLY
+            if early:
+                # the fold's pass over h while h is still cache-resident from the LayerNorm
+                # that wrote it; its last stage runs after the local attention has written ctx
+                if gws is None:
+                    gws = ops.global_fold_workspace(h, B, Lp, H, gmax)
+                ops.global_attention_fold_h_stage(1, gws, *gargs, tag="global_attn")
             qkv = ops.gemm(h, lw["w_qkv"][:nq], lw["b_qkv"][:nq], ops.RF_EPI_BIAS,
                            scale_cols=D, col_scale=scale, tag="gemm_qkv")
             ctx = ops.band_attention(qkv[:, 0:D], qkv[:, D:2 * D], qkv[:, 2 * D:3 * D], flags,
                                      gidx, B, Lp, H, half_w, tag="band_attn")
-            if gmax > 0:
+            if early:
+                ops.global_attention_fold_h_stage(2, gws, *gargs, out=ctx, tag="global_attn")
+            elif gmax > 0:
                 if fold:
                     ops.global_attention_fold_h(h, lw["w_qg"], lw["b_qg"], scale, lw["w_qkv"][3 * D:4 * D],
                                                 lw["b_qkv"][3 * D:4 * D], lw["w_qkv"][4 * D:5 * D],

@@ -499,6 +499,38 @@ def global_attention_fold_h(h, wqg, bqg, q_scale: float, wkg, bkg, wvg, bvg, fla
     return out
 
 
+def global_fold_workspace(h, B: int, Lp: int, H: int, gmax: int) -> torch.Tensor:
+    ws_bytes = _lib.load().rf_global_fold_workspace(B, Lp, h.shape[1], H, gmax)
+    return torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=h.device)
+
+
+def global_attention_fold_h_stage(stage: int, ws: torch.Tensor, h, wqg, bqg, q_scale: float, wkg, bkg, wvg, bvg,
+                                  flags, gidx, B: int, Lp: int, H: int, out: Optional[torch.Tensor] = None,
+                                  tag: Optional[str] = None):
+    """rf_global_attn_fold_h_stage: stage 1 (query_global projection + partial softmax over h,
+    into `ws`), stage 2 (merge + value fold from `ws` into the global rows of `out`)."""
+    lib = _lib.load()
+    gmax = gidx.shape[1]
+    if gmax == 0:
+        return out
+    if stage & 2 and out is None:
+        raise ValueError("global_attention_fold_h_stage: stage 2 writes `out`")
+    _dev(h, wqg, wkg, wvg, flags, ws)
+    D = h.shape[1]
+    for t in (wqg, wkg, wvg):
+        if not t.is_contiguous() or t.dtype != h.dtype:
+            raise ValueError("global_attention_fold_h_stage: weights must be contiguous in the compute dtype")
+    if ws.numel() < lib.rf_global_fold_workspace(B, Lp, D, H, gmax):
+        raise ValueError("global_attention_fold_h_stage: workspace too small")
+    with _region(tag):
+        rc = lib.rf_global_attn_fold_h_stage(int(stage), dtype_code(h.dtype), B, Lp, D, H, _p(h), _rowmajor(h, "h"),
+                                             _p(wqg), _p(bqg), float(q_scale), _p(wkg), _p(bkg), _p(wvg), _p(bvg),
+                                             _p(flags), _p(gidx.contiguous()), gmax, _p(ws), _p(out),
+                                             D if out is None else _rowmajor(out, "out"), _stream(h))
+    check(rc, "rf_global_attn_fold_h_stage")
+    return out
+
+
 def gather_global_rows(x, gidx, B: int, Lp: int):
     lib = _lib.load()
     gmax = gidx.shape[1]

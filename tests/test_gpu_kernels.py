@@ -378,6 +378,36 @@ def test_global_attention_fold_from_h(dev, dt, case):
     assert ctx_a.abs().sum().item() > 0
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,Lp,H", [(3, 192, 3), (4, 1024, 12), (300, 64, 12)])
+def test_global_fold_h_stages_match_one_call(dev, dt, B, Lp, H):
+    """rf_global_attn_fold_h_stage(1) then (2) — as the encoder runs it, with h overwritten in
+    between (stage 2 must read only the workspace) and out untouched by stage 1 — is bit-identical
+    to the one-call rf_global_attn_fold_h_fwd."""
+    D = H * 64
+    g = torch.Generator().manual_seed(B + Lp)
+    lens = [int(x) for x in torch.randint(1, Lp + 1, (B,), generator=g)]
+    lens[0] = Lp
+    globals_ = [(b, 0) for b in range(B) if b % 5 != 2] + [(b, lens[b] - 1) for b in range(0, B, 3)]
+    _, _, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, lens, globals_, 3)
+    h = _rand((B * Lp, D), dev, dt, 1.0, seed=70)
+    w = [_rand((D, D), dev, dt, 0.05, seed=71 + i) for i in range(3)]
+    bias = [_rand((D,), dev, torch.float32, 0.1, seed=74 + i) for i in range(3)]
+    args = (w[0], bias[0], 0.125, w[1], bias[1], w[2], bias[2], flags, gidx, B, Lp, H)
+    ref = torch.full((B * Lp, D), 3.0, dtype=dt, device=dev)
+    ops.global_attention_fold_h(h, *args, ref)
+    ws = ops.global_fold_workspace(h, B, Lp, H, gidx.shape[1])
+    out = torch.full((B * Lp, D), 3.0, dtype=dt, device=dev)
+    ops.global_attention_fold_h_stage(1, ws, h, *args)
+    h_keep = h.clone()
+    h.normal_()
+    ops.global_attention_fold_h_stage(2, ws, h, *args, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    with pytest.raises(ValueError):
+        ops.global_attention_fold_h_stage(2, ws, h_keep, *args)
+
+
 @pytest.mark.parametrize("B,Lp,H", [(300, 64, 12), (70, 192, 3), (5, 1024, 12)])
 def test_global_fold_mfma_matches_gemv(dev, monkeypatch, B, Lp, H):
     """The 64-row MFMA qg/u and out kernels (chosen for >= 256 global rows, e.g. a catalog of
