@@ -12,6 +12,7 @@ fp32 otherwise (exact-fp32 MFMA GEMMs).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from dataclasses import dataclass
 from typing import Any, List, Optional, Tuple
@@ -218,6 +219,8 @@ def _cos_train(z: torch.Tensor, items: torch.Tensor, temp: float) -> torch.Tenso
 SPLIT_STREAM = True
 # run the global fold's pass over h before the qkv GEMM (rf_global_attn_fold_h_stage)
 FOLD_EARLY = True
+# training: RecformerForPretraining's four encoder passes share one autograd cast per weight
+SHARE_TRAIN_CASTS = True
 
 
 def _compute_dtype(param_dtype: torch.dtype) -> torch.dtype:
@@ -621,12 +624,20 @@ class RecformerForPretraining(nn.Module):
                                    inputs_embeds=inputs_embeds, output_attentions=output_attentions,
                                    output_hidden_states=output_hidden_states, return_dict=True)
 
-        outputs_a = enc(input_ids_a, attention_mask_a, global_attention_mask_a, token_type_ids_a, item_position_ids_a)
-        outputs_b = enc(input_ids_b, attention_mask_b, global_attention_mask_b, token_type_ids_b, item_position_ids_b)
-        mlm_outputs_a = (enc(mlm_input_ids_a, attention_mask_a, global_attention_mask_a, token_type_ids_a,
-                             item_position_ids_a) if mlm_input_ids_a is not None else None)
-        mlm_outputs_b = (enc(mlm_input_ids_b, attention_mask_b, global_attention_mask_b, token_type_ids_b,
-                             item_position_ids_b) if mlm_input_ids_b is not None else None)
+        # training: the four passes share one autograd cast per weight (train.shared_casts)
+        share = contextlib.nullcontext()
+        if _needs_grad(self) and SHARE_TRAIN_CASTS:
+            from .train import shared_casts
+            share = shared_casts()
+        with share:
+            outputs_a = enc(input_ids_a, attention_mask_a, global_attention_mask_a, token_type_ids_a,
+                            item_position_ids_a)
+            outputs_b = enc(input_ids_b, attention_mask_b, global_attention_mask_b, token_type_ids_b,
+                            item_position_ids_b)
+            mlm_outputs_a = (enc(mlm_input_ids_a, attention_mask_a, global_attention_mask_a, token_type_ids_a,
+                                 item_position_ids_a) if mlm_input_ids_a is not None else None)
+            mlm_outputs_b = (enc(mlm_input_ids_b, attention_mask_b, global_attention_mask_b, token_type_ids_b,
+                                 item_position_ids_b) if mlm_input_ids_b is not None else None)
 
         z1, z2 = outputs_a.pooler_output, outputs_b.pooler_output
         if _needs_grad(self):

@@ -317,6 +317,54 @@ class _Attention(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------------
+# Per-forward cache of the autograd-tracked weight casts (bf16 copies, the fused q|k|v weight):
+# RecformerForPretraining runs four encoder passes over the same parameters, and one cast node
+# per parameter shared by all four (gradients accumulate through it) replaces four.
+_CASTS: Optional[dict] = None
+
+
+class shared_casts:
+    """Context manager: within it, encode_train reuses each weight cast it has made."""
+
+    def __enter__(self):
+        global _CASTS
+        self._outer = _CASTS
+        if _CASTS is None:
+            _CASTS = {}
+        return self
+
+    def __exit__(self, *exc):
+        global _CASTS
+        _CASTS = self._outer
+        return False
+
+
+def _cast(key, make):
+    if _CASTS is None:
+        return make()
+    t = _CASTS.get(key)
+    if t is None:
+        t = _CASTS[key] = make()
+    return t
+
+
+def _layer_weights(li: int, lyr, dt: torch.dtype) -> dict:
+    """The layer's weights as the forward consumes them (cached under shared_casts)."""
+    def make():
+        sa, ao, fo = lyr.attention.self, lyr.attention.output, lyr.output
+        return {
+            "w_qkv": torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0).to(dt),
+            "b_qkv": torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0).float(),
+            "w_qg": sa.query_global.weight.to(dt), "b_qg": sa.query_global.bias.float(),
+            "w_kg": sa.key_global.weight.to(dt), "b_kg": sa.key_global.bias.float(),
+            "w_vg": sa.value_global.weight.to(dt), "b_vg": sa.value_global.bias.float(),
+            "w_o": ao.dense.weight.to(dt), "b_o": ao.dense.bias.float(),
+            "w_1": lyr.intermediate.dense.weight.to(dt), "b_1": lyr.intermediate.dense.bias.float(),
+            "w_2": fo.dense.weight.to(dt), "b_2": fo.dense.bias.float(),
+        }
+    return _cast((id(lyr), li, dt), make)
+
+
 def encode_train(model, input_ids, attention_mask, global_attention_mask, token_type_ids,
                  position_ids, item_position_ids, output_hidden_states: bool
                  ) -> Tuple[torch.Tensor, Optional[tuple]]:
@@ -362,30 +410,26 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     # bf16 path: dropout + residual + LayerNorm as one HIP pass each way (_DropAddLN)
     fused = dt == torch.bfloat16 and D in (64, 128, 256, 384, 512, 768, 1024)
     for li, lyr in enumerate(model.encoder.layer):
-        sa = lyr.attention.self
+        lw = _layer_weights(li, lyr, dt)
         h = h32.to(dt)
-        w_qkv = torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0).to(dt)
-        b_qkv = torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0).float()
-        qkv = _Gemm.apply(h, w_qkv, b_qkv, D, scale)
+        qkv = _Gemm.apply(h, lw["w_qkv"], lw["b_qkv"], D, scale)
         qg = None
         if gmax > 0:
             hg = h[rows] * gvalid.to(h.dtype)
-            qg = _Gemm.apply(hg, sa.query_global.weight.to(dt), sa.query_global.bias.float(), D, scale)
-        ctx = _Attention.apply(qkv, qg, h,
-                               sa.key_global.weight.to(dt), sa.key_global.bias.float(),
-                               sa.value_global.weight.to(dt), sa.value_global.bias.float(),
+            qg = _Gemm.apply(hg, lw["w_qg"], lw["b_qg"], D, scale)
+        ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
                                flags, gidx, B, Lp, H, windows[li] // 2, fold)
         ao = lyr.attention.output
-        t = _Gemm.apply(ctx, ao.dense.weight.to(dt), ao.dense.bias.float(), 0, 1.0)
+        t = _Gemm.apply(ctx, lw["w_o"], lw["b_o"], 0, 1.0)
         if fused:
             a32 = _DropAddLN.apply(t, h32, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid)
         else:
             x1 = F.dropout(t.float(), p_hid, model.training) + h32
             a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
-        z = _Gemm.apply(a32.to(dt), lyr.intermediate.dense.weight.to(dt), lyr.intermediate.dense.bias.float(), 0, 1.0)
+        z = _Gemm.apply(a32.to(dt), lw["w_1"], lw["b_1"], 0, 1.0)
         u = F.gelu(z)
         fo = lyr.output
-        t2 = _Gemm.apply(u, fo.dense.weight.to(dt), fo.dense.bias.float(), 0, 1.0)
+        t2 = _Gemm.apply(u, lw["w_2"], lw["b_2"], 0, 1.0)
         if fused:
             h32 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid)
         else:

@@ -84,6 +84,35 @@ def test_pretrain_training_step(dev):
     assert torch.isfinite(out2.loss)
 
 
+@pytest.mark.parametrize("autocast", [False, True])
+def test_pretrain_shared_casts_same_grads(dev, monkeypatch, autocast):
+    """The four pretraining passes sharing one autograd cast per weight (models.SHARE_TRAIN_CASTS)
+    give the loss and parameter gradients of per-pass casts (dropout off, so both runs are
+    deterministic up to the order in which the four passes' gradients are summed)."""
+    from recformer_amd import models
+    from tests.common import hashed_pretrain, pretrain_inputs
+    g = load_golden("c1_pretrain")
+    m = hashed_pretrain(CFG).to(dev).train()
+    kw = {k: v.to(dev) for k, v in pretrain_inputs(g).items()}
+    res = {}
+    for share in (False, True):
+        monkeypatch.setattr(models, "SHARE_TRAIN_CASTS", share)
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            out = m(**kw)
+        out.loss.backward()
+        res[share] = (float(out.loss), {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+    assert res[True][0] == pytest.approx(res[False][0], rel=1e-6, abs=1e-6)
+    assert res[True][1].keys() == res[False][1].keys()
+    for k, ga in res[False][1].items():
+        gb = res[True][1][k]
+        # under autocast the shared bf16 cast sums the four passes' bf16 weight gradients in
+        # bf16 before the fp32 master (as torch autocast's own per-region cast cache does for the
+        # reference), per-pass casts sum them in fp32: bf16 rounding of the sum apart
+        tol = 1e-5 if not autocast else 1e-2
+        assert float((ga - gb).abs().max()) <= tol * max(float(ga.abs().max()), 1e-6), k
+
+
 @pytest.mark.parametrize("case", [
     dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
     dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),

@@ -12,7 +12,7 @@ def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "pretrain"
     B = sys.argv[2] if len(sys.argv) > 2 else "4"
     mod = __import__(f"tools.{'pretrain_bench' if which == 'pretrain' else 'train_bench'}", fromlist=["main"])
-    sys.argv = [sys.argv[0], "--batch", B, "--steps", "2", "--warmup", "1"]
+    sys.argv = [sys.argv[0], "--batch", B, "--steps", os.environ.get("HP_STEPS", "2"), "--warmup", "1"]
     pr = cProfile.Profile()
     pr.enable()
     mod.main()
