@@ -38,6 +38,9 @@ from . import ops
 
 __all__ = ["encode_train"]
 
+# the global rows' backward in closed form (_global_bwd); False: autograd over _global_torch
+GLOBAL_BWD_CLOSED_FORM = True
+
 
 # ------------------------------------------------------------------------------------------
 class _Gemm(torch.autograd.Function):
@@ -203,6 +206,42 @@ def _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B: int, Lp: int, H: int):
     return og.reshape(B * gmax, D)
 
 
+def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout):
+    """Closed-form gradient of _global_torch (the fold algebra, TF:964-1057) for the output
+    gradient gout (B*gmax, D) — batched matmuls instead of autograd over einsums (a third of the
+    ops, no nested graph). Returns fp32 (dqg, dh, dwkg, dbkg, dwvg, dbvg); dbkg is exactly zero:
+    the key bias adds q.bkg to every score of a row, which the softmax cancels."""
+    D = h.shape[1]
+    hd = D // H
+    G = qg.shape[0] // B
+    HG = H * G
+    hf = h.float().view(B, Lp, D)
+    wk = wkg.float().view(H, hd, D)
+    wv = wvg.float().view(H, hd, D)
+    qH = qg.float().view(B * G, H, hd).transpose(0, 1)                       # (H, BG, hd)
+    uH = torch.bmm(qH, wk)                                                   # (H, BG, D)
+    u = uH.view(H, B, G, D).transpose(0, 1).reshape(B, HG, D)                # (B, HG, D)
+    s = torch.bmm(u, hf.transpose(1, 2))                                     # (B, HG, Lp)
+    s.masked_fill_((flags == 0).view(B, 1, Lp), float("-inf"))
+    p = torch.softmax(s, -1)
+    w = torch.bmm(p, hf)                                                     # (B, HG, D)
+    wH = w.view(B, H, G, D).transpose(0, 1).reshape(H, B * G, D)             # (H, BG, D)
+    doH = gout.float().view(B * G, H, hd).transpose(0, 1)                    # (H, BG, hd)
+    dbvg = doH.sum(1).reshape(D)
+    dwvg = torch.bmm(doH.transpose(1, 2), wH).reshape(D, D)                  # (H, hd, D)
+    dwH = torch.bmm(doH, wv)                                                 # (H, BG, D)
+    dw = dwH.view(H, B, G, D).transpose(0, 1).reshape(B, HG, D)
+    dp = torch.bmm(dw, hf.transpose(1, 2))                                   # (B, HG, Lp)
+    ds = p * (dp - (p * dp).sum(-1, keepdim=True))
+    dh = torch.bmm(p.transpose(1, 2), dw).add_(torch.bmm(ds.transpose(1, 2), u))  # (B, Lp, D)
+    du = torch.bmm(ds, hf)                                                   # (B, HG, D)
+    duH = du.view(B, H, G, D).transpose(0, 1).reshape(H, B * G, D)
+    dq = torch.bmm(duH, wk.transpose(1, 2)).transpose(0, 1).reshape(B * G, D)
+    dwkg = torch.bmm(qH.transpose(1, 2), duH).reshape(D, D)
+    dbkg = torch.zeros(D, dtype=torch.float32, device=h.device)
+    return dq, dh.view(B * Lp, D), dwkg, dbkg, dwvg, dbvg
+
+
 def _global_rows(gidx, B: int, Lp: int):
     rows = (torch.arange(B, device=gidx.device)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
     return rows, (gidx >= 0).reshape(-1)
@@ -269,19 +308,20 @@ class _Attention(torch.autograd.Function):
             kf = keep[:, None].to(dkg.dtype)
             dk.index_add_(0, rows, dkg * kf)
             dv.index_add_(0, rows, dvg * kf)
-            # global branch through autograd over the fold algebra
-            gin = [t.detach().requires_grad_(need) for t, need in
-                   zip((qg, h, wkg, bkg, wvg, bvg), ctx.needs_input_grad[1:7])]
-            if any(t.requires_grad for t in gin):
-                with torch.enable_grad(), torch.autocast("cuda", enabled=False):
-                    og = _global_torch(*gin, flags, B, Lp, H)
-                    gout = dout[rows].float() * keep[:, None].to(torch.float32)
-                    want = [t for t in gin if t.requires_grad]
-                    grads = torch.autograd.grad(og, want, gout, allow_unused=True)
-                it = iter(grads)
-                for n, t in enumerate(gin):
-                    if t.requires_grad:
-                        g = next(it)
+            # global branch: closed-form gradient of the fold algebra
+            if any(ctx.needs_input_grad[1:7]):
+                gout = dout[rows].float() * keep[:, None].to(torch.float32)
+                if GLOBAL_BWD_CLOSED_FORM:
+                    with torch.autocast("cuda", enabled=False):
+                        grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout)
+                else:
+                    gin = [t.detach().requires_grad_(True) for t in (qg, h, wkg, bkg, wvg, bvg)]
+                    with torch.enable_grad(), torch.autocast("cuda", enabled=False):
+                        og = _global_torch(*gin, flags, B, Lp, H)
+                        grads = torch.autograd.grad(og, gin, gout, allow_unused=True)
+                for n, t in enumerate((qg, h, wkg, bkg, wvg, bvg)):
+                    if ctx.needs_input_grad[1 + n]:
+                        g = grads[n]
                         res[1 + n] = None if g is None else g.to(t.dtype)
         if ctx.needs_input_grad[0]:
             res[0] = dqkv.to(qkv.dtype)

@@ -1,0 +1,42 @@
+"""Host-side (CPU) checks of the training path's torch algebra (no GPU needed)."""
+import pytest
+import torch
+
+from recformer_amd import train
+
+
+@pytest.mark.parametrize("B,Lp,H,G", [(2, 64, 2, 1), (3, 128, 3, 2), (1, 192, 12, 3)])
+def test_global_bwd_closed_form_matches_autograd(B, Lp, H, G):
+    """train._global_bwd (closed-form gradient of the global rows' fold algebra, TF:964-1057)
+    against autograd through train._global_torch on the same inputs: ragged valid lengths,
+    several global slots, one empty slot (zero query row and zero output gradient)."""
+    g = torch.Generator().manual_seed(B * 100 + Lp + H + G)
+    D = 64 * H
+    qg = torch.randn(B * G, D, generator=g, dtype=torch.float64)
+    h = torch.randn(B * Lp, D, generator=g, dtype=torch.float64)
+    wkg = torch.randn(D, D, generator=g, dtype=torch.float64) * 0.05
+    bkg = torch.randn(D, generator=g, dtype=torch.float64) * 0.1
+    wvg = torch.randn(D, D, generator=g, dtype=torch.float64) * 0.05
+    bvg = torch.randn(D, generator=g, dtype=torch.float64) * 0.1
+    flags = torch.ones(B, Lp, dtype=torch.uint8)
+    for b in range(B):
+        n = Lp - 17 * b
+        flags[b, n:] = 0
+    gout = torch.randn(B * G, D, generator=g, dtype=torch.float64)
+    if G > 1:
+        qg[G - 1] = 0  # an empty slot of sequence 0
+        gout[G - 1] = 0
+    ins = [t.clone().requires_grad_(True) for t in (qg, h, wkg, bkg, wvg, bvg)]
+    og = train._global_torch(*ins, flags, B, Lp, H)
+    ref = torch.autograd.grad(og, ins, gout.float(), allow_unused=True)
+    got = train._global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout)
+    names = ("dqg", "dh", "dwkg", "dbkg", "dwvg", "dbvg")
+    # the key bias only shifts each softmax row: its gradient is zero (autograd: rounding noise)
+    assert torch.count_nonzero(got[3]) == 0
+    assert ref[3] is None or float(ref[3].abs().max()) <= 1e-4 * float(ref[0].abs().max())
+    for name, r, x in zip(names, ref, got):
+        if name == "dbkg":
+            continue
+        r = torch.zeros_like(x) if r is None else r.float()
+        scale = max(float(r.abs().max()), 1e-3)
+        assert float((x.float() - r).abs().max()) <= 1e-4 * scale, name

@@ -39,10 +39,14 @@ def main():
     ap.add_argument("--len-a", type=int, default=1024)
     ap.add_argument("--len-b", type=int, default=128)
     ap.add_argument("--no-share-casts", action="store_true", help="A/B: per-pass weight casts")
+    ap.add_argument("--autograd-global-bwd", action="store_true", help="A/B: global rows' backward by autograd")
     a = ap.parse_args()
     if a.no_share_casts:
         from recformer_amd import models
         models.SHARE_TRAIN_CASTS = False
+    if a.autograd_global_bwd:
+        from recformer_amd import train
+        train.GLOBAL_BWD_CLOSED_FORM = False
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
