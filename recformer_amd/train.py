@@ -15,7 +15,7 @@ whose backward is written out explicitly:
   _Attention   sliding-window local + global attention (band kernel + global fold)
                TF:482-1057; backward (bf16): the local branch on the HIP backward kernels
                (rf_attn_bwd.hip; global-key columns reduced per sequence here), the global
-               rows by autograd over the fold algebra; fp32 mode: an fp32 recompute of both.
+               rows in closed form (_global_bwd); fp32 mode: an fp32 recompute of both.
 
 Mixed precision follows the reference's autocast run (finetune.py:106-110): GEMM operands in
 bf16, LayerNorm outputs / residual stream / losses in fp32, parameters fp32 (the bf16 weight
@@ -55,12 +55,21 @@ class _Gemm(torch.autograd.Function):
         a, w = ctx.saved_tensors
         sc, s = ctx.sc
         dc = dc.to(a.dtype)
-        if sc > 0 and s != 1.0:
-            dc = dc.clone()
-            dc[:, :sc] *= s
-        da = dc @ w if ctx.needs_input_grad[0] else None
+        scaled = sc > 0 and s != 1.0
+        # the column scale of the first sc outputs goes on the small operands (W rows, dW rows,
+        # db) instead of a scaled copy of dC
+        wa = w
+        if scaled and ctx.needs_input_grad[0]:
+            wa = w.clone()
+            wa[:sc] *= s
+        da = dc @ wa if ctx.needs_input_grad[0] else None
         dw = dc.t() @ a if ctx.needs_input_grad[1] else None
         db = ops.colsum(dc) if ctx.needs_input_grad[2] else None  # deterministic HIP column sums
+        if scaled:
+            if dw is not None:
+                dw[:sc] *= s
+            if db is not None:
+                db[:sc] *= s
         return da, dw, db, None, None
 
 
@@ -265,7 +274,7 @@ class _Attention(torch.autograd.Function):
     per-slice zero-fill + accumulate in autograd)."""
 
     @staticmethod
-    def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold):
+    def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold, grows=None):
         D = qkv.shape[1] // 3
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w)
@@ -279,6 +288,7 @@ class _Attention(torch.autograd.Function):
                 ops.global_attention(qg.contiguous(), kg, vg, flags, gidx, B, Lp, H, out)
         ctx.save_for_backward(qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out)
         ctx.dims = (B, Lp, H, half_w)
+        ctx.grows = grows  # (rows, keep) of the pass, shared by its layers
         return out
 
     @staticmethod
@@ -298,7 +308,7 @@ class _Attention(torch.autograd.Function):
         dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H, dqkv=dqkv)
         res = [None] * 7
         if gmax > 0:
-            rows, keep = _global_rows(gidx, B, Lp)
+            rows, keep = ctx.grows if ctx.grows is not None else _global_rows(gidx, B, Lp)
             # gradients of the global-key columns, reduced over every query of the sequence
             qh = q.float().view(B, Lp, H, 64)
             dh = d16.float().view(B, Lp, H, 64)
@@ -325,7 +335,7 @@ class _Attention(torch.autograd.Function):
                         res[1 + n] = None if g is None else g.to(t.dtype)
         if ctx.needs_input_grad[0]:
             res[0] = dqkv.to(qkv.dtype)
-        return (*res, None, None, None, None, None, None, None)
+        return (*res, None, None, None, None, None, None, None, None)
 
     @staticmethod
     def _backward_torch(ctx, dout):
@@ -353,7 +363,7 @@ class _Attention(torch.autograd.Function):
             res = [torch.cat(z, 1)] + res[3:]
         else:
             res = [None] + res[3:]
-        return (*res, None, None, None, None, None, None, None)
+        return (*res, None, None, None, None, None, None, None, None)
 
 
 # ------------------------------------------------------------------------------------------
@@ -443,10 +453,11 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     scale = 1.0 / math.sqrt(hd)
     windows = cfg.window_per_layer()
     fold = getattr(cfg, "global_attention_fold", True)
-    rows = None
+    rows = grows = None
     if gmax > 0:
         rows = (torch.arange(B, device=input_ids.device)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
         gvalid = (gidx >= 0).reshape(-1, 1)
+        grows = (rows, gvalid.view(-1))
     # bf16 path: dropout + residual + LayerNorm as one HIP pass each way (_DropAddLN)
     fused = dt == torch.bfloat16 and D in (64, 128, 256, 384, 512, 768, 1024)
     for li, lyr in enumerate(model.encoder.layer):
@@ -458,7 +469,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
             hg = h[rows] * gvalid.to(h.dtype)
             qg = _Gemm.apply(hg, lw["w_qg"], lw["b_qg"], D, scale)
         ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
-                               flags, gidx, B, Lp, H, windows[li] // 2, fold)
+                               flags, gidx, B, Lp, H, windows[li] // 2, fold, grows)
         ao = lyr.attention.output
         t = _Gemm.apply(ctx, lw["w_o"], lw["b_o"], 0, 1.0)
         if fused:
