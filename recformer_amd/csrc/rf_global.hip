@@ -203,13 +203,17 @@ __device__ __forceinline__ int gimg(int row, int col) {
 //   u[row][c]  = sum_d qg[row][d] Wkg[h*64+d][c]                    (A: Wkg^T via ds_read_tr,
 //                                                                    B: qg^T via ds_read_tr)
 // u is written as the hi + lo bf16 planes k_gfold_partial_bf16 reads; heads >= H are not
-// written (the partial kernel does not load them).
+// written (the partial kernel does not load them). Column split (gridDim.z): a block stages only
+// the 64-column segments of Wkg its u columns need; with `sep` that slice has its own LDS region
+// and its DMA goes out with Wqg's at the start (one wait), else it reuses the Wqg region after
+// the qg phase.
 template <int D>
 __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, const bf16* __restrict__ hs,
                                                         int ldh, const bf16* __restrict__ wqg,
                                                         const float* __restrict__ bqg, float q_scale,
                                                         const bf16* __restrict__ wkg,
-                                                        const int32_t* __restrict__ gidx, GfoldWs ws) {
+                                                        const int32_t* __restrict__ gidx, GfoldWs ws,
+                                                        int sep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NK = D / 32;
   constexpr int nseg = D >> 6;
@@ -217,7 +221,11 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int q4 = li >> 2, p4 = li & 3;
-  char* pimg = smem + nseg * 64 * 128 + wave * 2048;  // this wave's qg^T [64 d][16 rows] bf16
+  // u columns of this block and the Wkg segments they span
+  const int nct = D / 16 / gridDim.z, ct0 = blockIdx.z * nct;
+  const int sg0 = (16 * ct0) >> 6, sg1 = (16 * (ct0 + nct) + 63) >> 6;
+  char* kimg = sep ? smem + nseg * 64 * 128 : smem;                  // Wkg slice image
+  char* pimg = smem + (nseg + (sep ? sg1 - sg0 : 0)) * 64 * 128 + wave * 2048;  // qg^T [64 d][16 rows]
   const int r = r0 + 16 * wave + li;
   const int pos = r < R ? gidx[r] : -1;
 
@@ -230,14 +238,16 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
 #pragma unroll
     for (int s = 0; s < NK; ++s) a[s] = bf16x8{};
   }
-  auto dma_head = [&](const bf16* w) {
-    for (int p = wave; p < nseg * 8; p += 4) {
+  // segments [s0, s1) of the head's 64-row weight slice into image `dst` (segment s at s - s0)
+  auto dma_head = [&](const bf16* w, char* dst, int s0, int s1) {
+    for (int p = wave + 8 * s0; p < s1 * 8; p += 4) {
       const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
       const int chk = (lane & 7) ^ (row & 7);
-      glds16(w + (int64_t)(h * 64 + row) * D + seg * 64 + chk * 8, smem + (seg * 64 + (p & 7) * 8) * 128);
+      glds16(w + (int64_t)(h * 64 + row) * D + seg * 64 + chk * 8, dst + ((seg - s0) * 64 + (p & 7) * 8) * 128);
     }
   };
-  dma_head(wqg);
+  dma_head(wqg, smem, 0, nseg);
+  if (sep) dma_head(wkg, kimg, sg0, sg1);
   wait_vmcnt0();
   __syncthreads();
   {
@@ -266,8 +276,10 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
 #if defined(RF_GF_DIAG) && (RF_GF_DIAG & 2)
   return;
 #endif
-  dma_head(wkg);
-  wait_vmcnt0();
+  if (!sep) {
+    dma_head(wkg, kimg, sg0, sg1);
+    wait_vmcnt0();
+  }
   __syncthreads();
   bf16x8 pb[2];
 #pragma unroll
@@ -282,15 +294,14 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
   bf16* hi = ws.u16 + ((int64_t)rw * 2 * GF_HP + h) * D + 4 * g;
   bf16* lo = hi + (int64_t)GF_HP * D;
   // column split (gridDim.z): this block writes u columns [z D / nz, (z + 1) D / nz)
-  const int nct = D / 16 / gridDim.z, ct0 = blockIdx.z * nct;
   for (int ct = ct0; ct < ct0 + nct; ++ct) {
-    const int c0 = 16 * ct;
+    const int c0 = 16 * ct, cl = c0 - 64 * sg0;  // column within the staged slice
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int rb = 32 * s + 8 * g + q4;
-      const bf16x4 v0 = tr_read_g(smem + gimg(rb, c0 + 4 * p4));
-      const bf16x4 v1 = tr_read_g(smem + gimg(rb + 4, c0 + 4 * p4));
+      const bf16x4 v0 = tr_read_g(kimg + gimg(rb, cl + 4 * p4));
+      const bf16x4 v1 = tr_read_g(kimg + gimg(rb + 4, cl + 4 * p4));
       const bf16x8 wa = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, pb[s], acc, 0, 0, 0);
     }
@@ -984,17 +995,20 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
   if (!(stage & 1)) {
   } else if (dtype == RF_BF16 && gfold_use_mfma(R, true)) {
     RF_REQUIRE(D % 64 == 0 && D <= 1024, "rf_global_attn_fold_h: D=%d", D);
-    const size_t lds_q = (size_t)D * 128 + 4 * 2048;
     // few row tiles: split u's columns over more blocks (each recomputes its tile's qg)
     int qsplit = 1;
     while (qsplit < 4 && H * ((R + 63) / 64) * qsplit < 128 && (D / 16) % (2 * qsplit) == 0) qsplit *= 2;
+    // Wkg slice: at most ceil(cols / 64) + 1 segments of 8 KiB; its own region when it fits
+    const int nslice = std::min(D / 64, (D / qsplit + 63) / 64 + 1);
+    const int sep = (size_t)D * 128 + (size_t)nslice * 8192 + 4 * 2048 <= 160 * 1024 ? 1 : 0;
+    const size_t lds_q = (size_t)D * 128 + (sep ? (size_t)nslice * 8192 : 0) + 4 * 2048;
 #define GQ_(DD)                                                                                   \
   case DD:                                                                                        \
     (void)hipFuncSetAttribute((const void*)k_gfold_qu_mfma<DD>,                                   \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q);            \
     k_gfold_qu_mfma<DD><<<dim3(H, (R + 63) / 64, qsplit), 256, lds_q, s>>>(Lp, R, gmax, (const bf16*)h, ldh, \
                                                                   (const bf16*)wqg, bqg, q_scale,  \
-                                                                  (const bf16*)wkg, gidx, ws);     \
+                                                                  (const bf16*)wkg, gidx, ws, sep); \
     break;
     switch (D) { GQ_(64) GQ_(128) GQ_(192) GQ_(256) GQ_(384) GQ_(512) GQ_(768) GQ_(1024) default: break; }
 #undef GQ_
