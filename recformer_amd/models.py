@@ -221,6 +221,8 @@ SPLIT_STREAM = True
 FOLD_EARLY = True
 # training: RecformerForPretraining's four encoder passes share one autograd cast per weight
 SHARE_TRAIN_CASTS = True
+# pretraining: the LM head runs on the masked (labelled) rows only (_mlm_rows)
+LM_HEAD_MASKED_ONLY = True
 
 
 def _compute_dtype(param_dtype: torch.dtype) -> torch.dtype:
@@ -651,12 +653,28 @@ class RecformerForPretraining(nn.Module):
         correct_num = (amax == cl_labels).sum()
         for mo, ml in ((mlm_outputs_a, mlm_labels_a), (mlm_outputs_b, mlm_labels_b)):
             if mo is not None and ml is not None:
-                scores = self.lm_logits(mo.last_hidden_state)
-                loss = loss + self.config.mlm_weight * ops.cross_entropy(scores, ml.reshape(-1))
+                hid, lab = _mlm_rows(mo.last_hidden_state, ml)
+                scores = self.lm_logits(hid)
+                loss = loss + self.config.mlm_weight * ops.cross_entropy(scores, lab)
         return RecformerPretrainingOutput(loss=loss, logits=cos_sim, cl_correct_num=correct_num,
                                           cl_total_num=batch_size, hidden_states=outputs_a.hidden_states,
                                           attentions=outputs_a.attentions,
                                           global_attentions=outputs_a.global_attentions)
+
+
+def _mlm_rows(hidden: torch.Tensor, labels: torch.Tensor):
+    """The rows the masked-LM loss reads: CrossEntropyLoss ignores label -100
+    (models.py:499-510), so the LM head over only the labelled rows gives the same loss as over
+    every token, at ~15% of the head's GEMM work and logits memory. One host read (the row count)
+    per call. LM_HEAD_MASKED_ONLY = False (or no labelled row) keeps every row."""
+    h = hidden.reshape(-1, hidden.shape[-1])
+    lab = labels.reshape(-1)
+    if not LM_HEAD_MASKED_ONLY:
+        return h, lab
+    sel = (lab != -100).nonzero().squeeze(1)
+    if sel.numel() == 0:
+        return h, lab
+    return h.index_select(0, sel), lab.index_select(0, sel)
 
 
 def _pretrain_train_losses(self, z1, z2, outputs_a, mlm_a, lab_a, mlm_b, lab_b, batch_size):
@@ -680,12 +698,12 @@ def _pretrain_train_losses(self, z1, z2, outputs_a, mlm_a, lab_a, mlm_b, lab_b, 
     head = self.lm_head
     for mo, ml in ((mlm_a, lab_a), (mlm_b, lab_b)):
         if mo is not None and ml is not None:
-            x = F.gelu(F.linear(mo.last_hidden_state, head.dense.weight, head.dense.bias))
+            hid, lab = _mlm_rows(mo.last_hidden_state, ml)
+            x = F.gelu(F.linear(hid, head.dense.weight, head.dense.bias))
             x = F.layer_norm(x, (x.shape[-1],), head.layer_norm.weight, head.layer_norm.bias,
                              self.config.layer_norm_eps)
             scores = F.linear(x, head.decoder.weight, head.bias)
-            loss = loss + self.config.mlm_weight * F.cross_entropy(scores.reshape(-1, self.config.vocab_size),
-                                                                   ml.reshape(-1))
+            loss = loss + self.config.mlm_weight * F.cross_entropy(scores.reshape(-1, self.config.vocab_size), lab)
     return RecformerPretrainingOutput(loss=loss, logits=cos_sim, cl_correct_num=correct_num,
                                       cl_total_num=batch_size, hidden_states=outputs_a.hidden_states,
                                       attentions=outputs_a.attentions, global_attentions=outputs_a.global_attentions)

@@ -113,6 +113,33 @@ def test_pretrain_shared_casts_same_grads(dev, monkeypatch, autocast):
         assert float((ga - gb).abs().max()) <= tol * max(float(ga.abs().max()), 1e-6), k
 
 
+@pytest.mark.parametrize("train", [False, True])
+def test_pretrain_lm_head_masked_rows_only(dev, monkeypatch, train):
+    """The LM head over the labelled rows only (models.LM_HEAD_MASKED_ONLY)
+    gives the loss (and, training, the gradients) of the head over every token: the masked-LM
+    cross entropy ignores label -100 (models.py:499-510)."""
+    from recformer_amd import models
+    from tests.common import hashed_pretrain, pretrain_inputs
+    g = load_golden("c1_pretrain")
+    m = hashed_pretrain(CFG).to(dev).train(train)
+    kw = {k: v.to(dev) for k, v in pretrain_inputs(g).items()}
+    assert int((kw["mlm_labels_a"] != -100).sum()) > 0
+    res = {}
+    for masked in (False, True):
+        monkeypatch.setattr(models, "LM_HEAD_MASKED_ONLY", masked)
+        m.zero_grad(set_to_none=True)
+        with torch.set_grad_enabled(train):
+            out = m(**kw)
+        if train:
+            out.loss.backward()
+        res[masked] = (float(out.loss), {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+    assert res[True][0] == pytest.approx(res[False][0], rel=1e-5, abs=1e-6)
+    assert abs(res[True][0] - float(g["loss"])) <= 1e-4
+    for k, ga in res[False][1].items():
+        gb = res[True][1][k]
+        assert float((ga - gb).abs().max()) <= 1e-4 * max(float(ga.abs().max()), 1e-6), k
+
+
 @pytest.mark.parametrize("case", [
     dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
     dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),

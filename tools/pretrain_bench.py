@@ -40,7 +40,11 @@ def main():
     ap.add_argument("--len-b", type=int, default=128)
     ap.add_argument("--no-share-casts", action="store_true", help="A/B: per-pass weight casts")
     ap.add_argument("--autograd-global-bwd", action="store_true", help="A/B: global rows' backward by autograd")
+    ap.add_argument("--full-lm-head", action="store_true", help="A/B: LM head over every token")
     a = ap.parse_args()
+    if a.full_lm_head:
+        from recformer_amd import models
+        models.LM_HEAD_MASKED_ONLY = False
     if a.no_share_casts:
         from recformer_amd import models
         models.SHARE_TRAIN_CASTS = False
