@@ -310,10 +310,11 @@ class _Attention(torch.autograd.Function):
         if gmax > 0:
             rows, keep = ctx.grows if ctx.grows is not None else _global_rows(gidx, B, Lp)
             # gradients of the global-key columns, reduced over every query of the sequence
-            qh = q.float().view(B, Lp, H, 64)
-            dh = d16.float().view(B, Lp, H, 64)
-            dkg = torch.einsum("bhig,bihd->bghd", gds[..., :gmax], qh).reshape(B * gmax, D)
-            dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :gmax], dh).reshape(B * gmax, D)
+            # bf16 operands, fp32 accumulation (no fp32 copies of the (B*Lp, D) q and dout)
+            qh = q.reshape(B, Lp, H, 64)
+            dh = d16.view(B, Lp, H, 64)
+            dkg = torch.einsum("bhig,bihd->bghd", gds[..., :gmax].to(q.dtype), qh).reshape(B * gmax, D).float()
+            dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :gmax].to(q.dtype), dh).reshape(B * gmax, D).float()
             # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
             kf = keep[:, None].to(dkg.dtype)
             dk.index_add_(0, rows, dkg * kf)
