@@ -166,6 +166,13 @@ int rf_band_attn_bwd(int B, int Lp, int H, int hd, int half_w, const void* q, co
                      const uint8_t* flags, const int32_t* gidx, int gmax, float* dq, float* dk,
                      float* dv, int ld_grad, float* lse2, float* delta, float* gds, float* gpr,
                      rf_stream_t stream);
+/* The same with the gradients dq, dk, dv written in grad_dtype (RF_F32 or RF_BF16: what the
+ * bf16 q|k|v projection's backward consumes, as under the reference's autocast). */
+int rf_band_attn_bwd_dt(int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
+                        const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
+                        const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx,
+                        int gmax, void* dq, void* dk, void* dv, int ld_grad, float* lse2,
+                        float* delta, float* gds, float* gpr, rf_stream_t stream);
 /* A6 — global query rows, _compute_global_attn_output_from_hidden TF:964-1057 + the
  * overwrite TF:612-629: for every (b, g < count_b): ctx[gidx[b,g], h] =
  * softmax(qg[b*gmax+g, h] . kg[b, :, h]^T over valid keys) . vg[b, :, h]. */

@@ -57,13 +57,20 @@ constexpr int BQ_GP = 57344;   // 32 int
 constexpr int BQ_MK = 57472;   // 2 x uint64 window ballots (valid & local)
 constexpr int BQ_LDS = 57488;
 
+// 4 consecutive gradient values: fp32 (16 B) or bf16 (8 B) output
+__device__ __forceinline__ void store_g4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void store_g4(bf16* p, f32x4 v) {
+  *reinterpret_cast<bf16x4*>(p) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+}
+
+template <typename GT>
 __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* __restrict__ q,
                                                      const bf16* __restrict__ k, const bf16* __restrict__ v,
                                                      int ld, const bf16* __restrict__ o, int ldo,
                                                      const bf16* __restrict__ dout, int ldd,
                                                      const uint8_t* __restrict__ flags,
                                                      const int32_t* __restrict__ gidx, int gmax,
-                                                     float* __restrict__ dq, int lddq, float* __restrict__ lse2,
+                                                     GT* __restrict__ dq, int lddq, float* __restrict__ lse2,
                                                      float* __restrict__ delta, float* __restrict__ gds,
                                                      float* __restrict__ gpr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -261,10 +268,9 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* _
       acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, pf, acc[dt], 0, 0, 0);
     }
   }
-  float* dqr = dq + (rb + myq) * lddq + h * 64 + 4 * g;
+  GT* dqr = dq + (rb + myq) * lddq + h * 64 + 4 * g;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-    *reinterpret_cast<f32x4*>(dqr + 16 * dt) = live ? acc[dt] : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int dt = 0; dt < 4; ++dt) store_g4(dqr + 16 * dt, live ? acc[dt] : f32x4{0.f, 0.f, 0.f, 0.f});
   const int64_t ri = ((int64_t)b * H + h) * Lp + myq;
   if (g == 0) {
     lse2[ri] = live ? -nmu + __log2f(l) : __builtin_inff();
@@ -291,13 +297,14 @@ constexpr int BK_L = 49152;    // 128 float lse2
 constexpr int BK_D = 49664;    // 128 float delta
 constexpr int BK_LDS = 50176;
 
+template <typename GT>
 __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* __restrict__ q,
                                                       const bf16* __restrict__ k, const bf16* __restrict__ v,
                                                       int ld, const bf16* __restrict__ dout, int ldd,
                                                       const uint8_t* __restrict__ flags,
                                                       const float* __restrict__ lse2,
-                                                      const float* __restrict__ delta, float* __restrict__ dk,
-                                                      float* __restrict__ dv, int lddkv) {
+                                                      const float* __restrict__ delta, GT* __restrict__ dk,
+                                                      GT* __restrict__ dv, int lddkv) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -399,12 +406,12 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
       ak[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf, sf, ak[dt], 0, 0, 0);
     }
   }
-  float* dkr = dk + (rb + myk) * lddkv + h * 64 + 4 * g;
-  float* dvr = dv + (rb + myk) * lddkv + h * 64 + 4 * g;
+  GT* dkr = dk + (rb + myk) * lddkv + h * 64 + 4 * g;
+  GT* dvr = dv + (rb + myk) * lddkv + h * 64 + 4 * g;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    *reinterpret_cast<f32x4*>(dkr + 16 * dt) = ak[dt];
-    *reinterpret_cast<f32x4*>(dvr + 16 * dt) = av[dt];
+    store_g4(dkr + 16 * dt, ak[dt]);
+    store_g4(dvr + 16 * dt, av[dt]);
   }
 }
 
@@ -412,11 +419,31 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
 
 using namespace rf;
 
-extern "C" int rf_band_attn_bwd(int B, int Lp, int H, int hd, int half_w, const void* q, const void* k,
-                                const void* v, int ld_qkv, const void* o, int ld_o, const void* dout, int ld_do,
-                                const uint8_t* flags, const int32_t* gidx, int gmax, float* dq, float* dk,
-                                float* dv, int ld_grad, float* lse2, float* delta, float* gds, float* gpr,
-                                rf_stream_t stream) {
+template <typename GT>
+static void launch_band_bwd(int B, int Lp, int H, const void* q, const void* k, const void* v, int ld_qkv,
+                            const void* o, int ld_o, const void* dout, int ld_do, const uint8_t* flags,
+                            const int32_t* gidx, int gmax, GT* dq, GT* dk, GT* dv, int ld_grad, float* lse2,
+                            float* delta, float* gds, float* gpr, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_band_bwd_q<GT>, hipFuncAttributeMaxDynamicSharedMemorySize, BQ_LDS);
+    (void)hipFuncSetAttribute((const void*)k_band_bwd_kv<GT>, hipFuncAttributeMaxDynamicSharedMemorySize, BK_LDS);
+    attr = true;
+  }
+  const int nblk = (Lp / 64) * H * B;
+  k_band_bwd_q<GT><<<nblk, 256, BQ_LDS, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
+                                             (const bf16*)o, ld_o, (const bf16*)dout, ld_do, flags, gidx, gmax, dq,
+                                             ld_grad, lse2, delta, gds, gpr);
+  k_band_bwd_kv<GT><<<nblk, 256, BK_LDS, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
+                                              (const bf16*)dout, ld_do, flags, lse2, delta, dk, dv, ld_grad);
+}
+
+extern "C" int rf_band_attn_bwd_dt(int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
+                                   const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
+                                   const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx, int gmax,
+                                   void* dq, void* dk, void* dv, int ld_grad, float* lse2, float* delta, float* gds,
+                                   float* gpr, rf_stream_t stream) {
+  RF_REQUIRE(grad_dtype == RF_F32 || grad_dtype == RF_BF16, "rf_band_attn_bwd: bad gradient dtype %d", grad_dtype);
   RF_REQUIRE(hd == 64 && half_w == 32, "rf_band_attn_bwd: head_dim 64 and window 64 only (got %d, %d)", hd,
              2 * half_w);
   RF_REQUIRE(B >= 0 && H > 0 && Lp >= 0 && gmax >= 0 && gmax <= 32, "rf_band_attn_bwd: bad shape");
@@ -428,17 +455,20 @@ extern "C" int rf_band_attn_bwd(int B, int Lp, int H, int hd, int half_w, const 
   RF_REQUIRE(gmax == 0 || (gidx && gds && gpr), "rf_band_attn_bwd: gidx / global outputs required");
   if (B == 0 || Lp == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_band_bwd_q, hipFuncAttributeMaxDynamicSharedMemorySize, BQ_LDS);
-    (void)hipFuncSetAttribute((const void*)k_band_bwd_kv, hipFuncAttributeMaxDynamicSharedMemorySize, BK_LDS);
-    attr = true;
-  }
-  const int nblk = (Lp / 64) * H * B;
-  k_band_bwd_q<<<nblk, 256, BQ_LDS, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
-                                         (const bf16*)o, ld_o, (const bf16*)dout, ld_do, flags, gidx, gmax, dq,
-                                         ld_grad, lse2, delta, gds, gpr);
-  k_band_bwd_kv<<<nblk, 256, BK_LDS, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
-                                          (const bf16*)dout, ld_do, flags, lse2, delta, dk, dv, ld_grad);
+  if (grad_dtype == RF_BF16)
+    launch_band_bwd<bf16>(B, Lp, H, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx, gmax, (bf16*)dq, (bf16*)dk,
+                          (bf16*)dv, ld_grad, lse2, delta, gds, gpr, s);
+  else
+    launch_band_bwd<float>(B, Lp, H, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx, gmax, (float*)dq,
+                           (float*)dk, (float*)dv, ld_grad, lse2, delta, gds, gpr, s);
   RF_LAUNCH_CHECK("rf_band_attn_bwd");
+}
+
+extern "C" int rf_band_attn_bwd(int B, int Lp, int H, int hd, int half_w, const void* q, const void* k,
+                                const void* v, int ld_qkv, const void* o, int ld_o, const void* dout, int ld_do,
+                                const uint8_t* flags, const int32_t* gidx, int gmax, float* dq, float* dk,
+                                float* dv, int ld_grad, float* lse2, float* delta, float* gds, float* gpr,
+                                rf_stream_t stream) {
+  return rf_band_attn_bwd_dt(RF_F32, B, Lp, H, hd, half_w, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx, gmax,
+                             dq, dk, dv, ld_grad, lse2, delta, gds, gpr, stream);
 }

@@ -355,8 +355,8 @@ def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int):
 def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, tag: Optional[str] = None,
                        dqkv: Optional[torch.Tensor] = None):
     """Gradient of the local branch (rf_band_attn_bwd): q/k/v (pre-scaled q) and o, dout bf16
-    (B*Lp, >=H*64) views; returns fp32 (dq, dk, dv) of shape (B*Lp, H*64) — column views of
-    `dqkv` (B*Lp, 3*H*64) fp32 when given — plus, when there are global keys, gds / gpr
+    (B*Lp, >=H*64) views; returns (dq, dk, dv) of shape (B*Lp, H*64) — fp32, or column views of
+    `dqkv` (B*Lp, 3*H*64) in its dtype (fp32 or bf16) when given — plus, when there are global keys, gds / gpr
     (B, H, Lp, gmax): dS and P of the global-key columns."""
     lib = _lib.load()
     _dev(q, k, v, o, dout, flags)
@@ -367,8 +367,9 @@ def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, t
     gmax = gidx.shape[1]
     dev = q.device
     if dqkv is not None:
-        if dqkv.dtype != torch.float32 or not dqkv.is_contiguous() or tuple(dqkv.shape) != (B * Lp, 3 * D):
-            raise ValueError("band_attention_bwd: dqkv must be a contiguous fp32 (B*Lp, 3*D) tensor")
+        if (dqkv.dtype not in (torch.float32, torch.bfloat16) or not dqkv.is_contiguous()
+                or tuple(dqkv.shape) != (B * Lp, 3 * D)):
+            raise ValueError("band_attention_bwd: dqkv must be a contiguous fp32 or bf16 (B*Lp, 3*D) tensor")
         dq, dk, dv, ldg = dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], 3 * D
     else:
         dq = torch.empty(B * Lp, D, dtype=torch.float32, device=dev)
@@ -380,10 +381,10 @@ def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, t
     gds = torch.empty(B, H, Lp, max(gmax, 1), dtype=torch.float32, device=dev) if gmax else None
     gpr = torch.empty_like(gds) if gmax else None
     with _region(tag):
-        rc = lib.rf_band_attn_bwd(B, Lp, H, 64, 32, _p(q), _p(k), _p(v), ld, _p(o), _rowmajor(o, "o"), _p(dout),
-                                  _rowmajor(dout, "dout"), _p(flags), _p(gidx.contiguous()) if gmax else None,
-                                  gmax, _p(dq), _p(dk), _p(dv), ldg, _p(lse2), _p(delta), _p(gds), _p(gpr),
-                                  _stream(q))
+        rc = lib.rf_band_attn_bwd_dt(dtype_code(dq.dtype), B, Lp, H, 64, 32, _p(q), _p(k), _p(v), ld, _p(o),
+                                     _rowmajor(o, "o"), _p(dout), _rowmajor(dout, "dout"), _p(flags),
+                                     _p(gidx.contiguous()) if gmax else None, gmax, _p(dq), _p(dk), _p(dv), ldg,
+                                     _p(lse2), _p(delta), _p(gds), _p(gpr), _stream(q))
     check(rc, "rf_band_attn_bwd")
     return dq, dk, dv, gds, gpr
 

@@ -304,7 +304,8 @@ class _Attention(torch.autograd.Function):
         # local branch on the HIP backward kernels (rf_attn_bwd.hip); global rows of dout belong
         # to the global branch only (their local output was overwritten)
         d16 = dout.to(torch.bfloat16).contiguous()
-        dqkv = torch.empty(B * Lp, 3 * D, dtype=torch.float32, device=q.device)
+        # gradients written in the projection's dtype (bf16): no fp32 copy and cast per layer
+        dqkv = torch.empty(B * Lp, 3 * D, dtype=qkv.dtype, device=q.device)
         dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H, dqkv=dqkv)
         res = [None] * 7
         if gmax > 0:
@@ -313,12 +314,12 @@ class _Attention(torch.autograd.Function):
             # bf16 operands, fp32 accumulation (no fp32 copies of the (B*Lp, D) q and dout)
             qh = q.reshape(B, Lp, H, 64)
             dh = d16.view(B, Lp, H, 64)
-            dkg = torch.einsum("bhig,bihd->bghd", gds[..., :gmax].to(q.dtype), qh).reshape(B * gmax, D).float()
-            dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :gmax].to(q.dtype), dh).reshape(B * gmax, D).float()
+            dkg = torch.einsum("bhig,bihd->bghd", gds[..., :gmax].to(q.dtype), qh).reshape(B * gmax, D)
+            dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :gmax].to(q.dtype), dh).reshape(B * gmax, D)
             # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
             kf = keep[:, None].to(dkg.dtype)
-            dk.index_add_(0, rows, dkg * kf)
-            dv.index_add_(0, rows, dvg * kf)
+            dk.index_add_(0, rows, (dkg * kf).to(dk.dtype))  # bf16 throughout (dqkv is bf16)
+            dv.index_add_(0, rows, (dvg * kf).to(dv.dtype))
             # global branch: closed-form gradient of the fold algebra
             if any(ctx.needs_input_grad[1:7]):
                 gout = dout[rows].float() * keep[:, None].to(torch.float32)

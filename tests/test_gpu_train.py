@@ -176,3 +176,25 @@ def test_band_attention_bwd_matches_autograd(dev, case):
     for name, got, r in zip("qkv", (dq, dk, dv), ref):
         err = float((got - r).abs().max())
         assert err <= 2e-2 * max(float(r.abs().max()), 1e-6), (name, err, float(r.abs().max()))
+
+
+def test_band_attention_bwd_bf16_grads(dev):
+    """rf_band_attn_bwd_dt with bf16 gradients (the training path's dqkv) is the fp32 result
+    rounded to bf16, bit for bit; the workspace outputs are unchanged."""
+    from recformer_amd import ops
+    from tests.test_gpu_kernels import _attn_case
+    B, Lp, H = 2, 1024, 12
+    D = H * 64
+    qkv, _, flags, gidx, G = _attn_case(dev, torch.bfloat16, B, Lp, H, [1024, 700], ((0, 0), (1, 0), (1, 5)), 11)
+    q, k, v = (qkv[:, i * D:(i + 1) * D] for i in range(3))
+    out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, 32)
+    torch.manual_seed(2)
+    dout = torch.randn(B * Lp, D, device=dev).to(torch.bfloat16)
+    r32 = ops.band_attention_bwd(q, k, v, out, dout, flags, gidx, B, Lp, H,
+                                 dqkv=torch.empty(B * Lp, 3 * D, device=dev))
+    d16 = torch.empty(B * Lp, 3 * D, device=dev, dtype=torch.bfloat16)
+    r16 = ops.band_attention_bwd(q, k, v, out, dout, flags, gidx, B, Lp, H, dqkv=d16)
+    for a, b in zip(r32[:3], r16[:3]):
+        assert b.dtype == torch.bfloat16
+        assert torch.equal(a.to(torch.bfloat16), b)
+    assert torch.equal(r32[3], r16[3]) and torch.equal(r32[4], r16[4])
