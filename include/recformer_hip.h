@@ -134,6 +134,16 @@ int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, f
 int rf_drop_add_ln_bwd(int M, int D, const float* dy, const float* x, const float* mean, const float* rstd,
                        const float* w, float p, uint64_t seed, float* dres, void* dt, float* dw, float* db,
                        void* workspace, rf_stream_t stream);
+/* The same pair for an output with two consumers (training: the next residual add in fp32 and
+ * the next GEMM in bf16): _dual forward also writes y16 = bf16(y) (null: not written); _dual
+ * backward takes both consumers' gradients, dy (fp32) and dy16 (bf16), either may be null, and
+ * sums them in the kernel (dy + float(dy16), as autograd would). */
+int rf_drop_add_ln_fwd_dual(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
+                            const float* w, const float* b, float eps, float* x, float* y, float* mean,
+                            float* rstd, void* y16, rf_stream_t stream);
+int rf_drop_add_ln_bwd_dual(int M, int D, const float* dy, const void* dy16, const float* x, const float* mean,
+                            const float* rstd, const float* w, float p, uint64_t seed, float* dres, void* dt,
+                            float* dw, float* db, void* workspace, rf_stream_t stream);
 /* Column sums out[n] = sum_m x[m][n] (fp32 out; x in dtype, row-major, leading dim ldx), two
  * deterministic stages through rf_colsum_workspace(M, N) bytes — the bias gradient of the
  * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias). */

@@ -40,6 +40,10 @@ SIGNATURES = {
     "rf_drop_add_ln_fwd": (c_int, [c_int, c_int, P, c_int, P, c_float, ctypes.c_uint64, P, P, c_float, P, P, P, P,
                                    P]),
     "rf_drop_add_ln_bwd": (c_int, [c_int, c_int, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P, P]),
+    "rf_drop_add_ln_fwd_dual": (c_int, [c_int, c_int, P, c_int, P, c_float, ctypes.c_uint64, P, P, c_float, P, P, P,
+                                        P, P, P]),
+    "rf_drop_add_ln_bwd_dual": (c_int, [c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
+                                        P]),
     "rf_colsum_workspace": (ctypes.c_size_t, [c_int, c_int]),
     "rf_colsum": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, P, P]),
     "rf_layernorm_bwd": (c_int, [c_int, c_int, P, P, c_int, P, P, P, P, P, P, P, P]),

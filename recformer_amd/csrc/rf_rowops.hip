@@ -390,7 +390,8 @@ __global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const bf16* __re
                                                           float keep_scale, uint64_t seed,
                                                           const float* __restrict__ lw, const float* __restrict__ lb,
                                                           float eps, float* __restrict__ xo, float* __restrict__ y,
-                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                          bf16* __restrict__ y16) {
   constexpr int D = 64 * VEC * NCH;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -434,6 +435,7 @@ __global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const bf16* __re
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o[j] = (xv[c][j] - mean) * rstd * w[j] + bb[j];
     Vec<float, VEC>::store(y + (int64_t)row * D + e, o);
+    if (y16) Vec<bf16, VEC>::store(y16 + (int64_t)row * D + e, o);  // the next GEMM's operand
   }
 }
 
@@ -454,7 +456,8 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
                                                         const float* __restrict__ rstd,
                                                         const float* __restrict__ w, float* __restrict__ dx,
                                                         float* __restrict__ part, bf16* __restrict__ dt,
-                                                        uint32_t thresh, float keep_scale, uint64_t seed) {
+                                                        uint32_t thresh, float keep_scale, uint64_t seed,
+                                                        const bf16* __restrict__ dy2) {
   constexpr int D = 64 * VEC * NCH;
   __shared__ float red[4][2][D];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -476,7 +479,18 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
     for (int c = 0; c < NCH; ++c) {
       const int e = c * 64 * VEC + lane * VEC;
       float d[VEC], xv[VEC];
-      Vec<float, VEC>::load(dy + (int64_t)row * D + e, d);
+      if (dy) {
+        Vec<float, VEC>::load(dy + (int64_t)row * D + e, d);
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) d[j] = 0.f;
+      }
+      if (dy2) {  // second consumer's gradient (bf16), summed as autograd would
+        float d2[VEC];
+        Vec<bf16, VEC>::load(dy2 + (int64_t)row * D + e, d2);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) d[j] += d2[j];
+      }
       Vec<float, VEC>::load(x + (int64_t)row * ldx + e, xv);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
@@ -898,7 +912,8 @@ int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, v
 
 static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                        const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
-                       bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream);
+                       bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
+                       const bf16* dy2 = nullptr);
 
 static uint32_t drop_thresh(float p) {
   return p <= 0.f ? 0u : (p >= 1.f ? 0xFFFFFFFFu : (uint32_t)((double)p * 4294967296.0));
@@ -907,6 +922,12 @@ static uint32_t drop_thresh(float p) {
 int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
                        const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,
                        rf_stream_t stream) {
+  return rf_drop_add_ln_fwd_dual(M, D, t, ldt, res, p, seed, w, b, eps, x, y, mean, rstd, nullptr, stream);
+}
+
+int rf_drop_add_ln_fwd_dual(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
+                            const float* w, const float* b, float eps, float* x, float* y, float* mean,
+                            float* rstd, void* y16, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && ldt >= D && p >= 0.f && p < 1.f, "rf_drop_add_ln_fwd: bad arguments");
   if (M == 0) return RF_OK;
   RF_REQUIRE(t && res && w && b && x && y && mean && rstd, "rf_drop_add_ln_fwd: null pointer");
@@ -917,7 +938,7 @@ int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, f
   dim3 grid((M + 3) / 4);
 #define L_(V, N)                                                                                   \
   k_drop_add_ln_fwd<V, N><<<grid, 256, 0, s>>>(M, (const bf16*)t, ldt, res, th, ks, seed, w, b, eps, x, y, \
-                                               mean, rstd)
+                                               mean, rstd, (bf16*)y16)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
   RF_LAUNCH_CHECK("rf_drop_add_ln_fwd");
@@ -926,10 +947,17 @@ int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, f
 int rf_drop_add_ln_bwd(int M, int D, const float* dy, const float* x, const float* mean, const float* rstd,
                        const float* w, float p, uint64_t seed, float* dres, void* dt, float* dw, float* db,
                        void* workspace, rf_stream_t stream) {
+  RF_REQUIRE(M == 0 || dy, "rf_drop_add_ln_bwd: null dy");
+  return rf_drop_add_ln_bwd_dual(M, D, dy, nullptr, x, mean, rstd, w, p, seed, dres, dt, dw, db, workspace, stream);
+}
+
+int rf_drop_add_ln_bwd_dual(int M, int D, const float* dy, const void* dy16, const float* x, const float* mean,
+                            const float* rstd, const float* w, float p, uint64_t seed, float* dres, void* dt,
+                            float* dw, float* db, void* workspace, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && p >= 0.f && p < 1.f, "rf_drop_add_ln_bwd: bad arguments");
   RF_REQUIRE(M == 0 || dt, "rf_drop_add_ln_bwd: null dt");
   return ln_bwd_impl(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (bf16*)dt, drop_thresh(p),
-                     1.0f / (1.0f - p), seed, stream);
+                     1.0f / (1.0f - p), seed, stream, (const bf16*)dy16);
 }
 
 int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
@@ -940,15 +968,16 @@ int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, con
 
 static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                        const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
-                       bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream) {
+                       bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
+                       const bf16* dy2) {
   RF_REQUIRE(M >= 0 && ldx >= D, "rf_layernorm_bwd: bad shape");
   if (M == 0) return RF_OK;
-  RF_REQUIRE(dy && x && mean && rstd && w && dx && dw && db && workspace, "rf_layernorm_bwd: null pointer");
+  RF_REQUIRE((dy || dy2) && x && mean && rstd && w && dx && dw && db && workspace, "rf_layernorm_bwd: null pointer");
   RF_REQUIRE(ldx % 4 == 0, "rf_layernorm_bwd: ldx must be a multiple of 4");
   hipStream_t s = as_stream(stream);
   const int nb = (M + LNB_ROWS - 1) / LNB_ROWS;
   float* part = reinterpret_cast<float*>(workspace);
-#define L_(V, N) k_layernorm_bwd<V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed)
+#define L_(V, N) k_layernorm_bwd<V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, dy2)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
   colsum<float>(nb, 2 * D, part, 2 * D, part + (size_t)nb * 2 * D, dw, db, D, s);  // [dw | db] columns

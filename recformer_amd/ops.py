@@ -319,8 +319,9 @@ def colsum(x: torch.Tensor, tag: Optional[str] = None) -> torch.Tensor:
 
 
 def drop_add_ln_fwd(t: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float, p: float,
-                    seed: int):
-    """rf_drop_add_ln_fwd: (x, y, mean, rstd) with x = dropout_p(t) + res, y = LN(x), all fp32."""
+                    seed: int, want_bf16: bool = False):
+    """rf_drop_add_ln_fwd(_dual): (x, y, mean, rstd) with x = dropout_p(t) + res, y = LN(x), all
+    fp32; with want_bf16 also y16 = bf16(y) (rf_drop_add_ln_fwd_dual), appended."""
     lib = _lib.load()
     _dev(t, res, w, b)
     M, D = t.shape
@@ -330,25 +331,34 @@ def drop_add_ln_fwd(t: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torc
     y = torch.empty_like(x)
     mean = torch.empty(M, dtype=torch.float32, device=t.device)
     rstd = torch.empty_like(mean)
-    check(lib.rf_drop_add_ln_fwd(M, D, _p(t), _rowmajor(t, "t"), _p(res), float(p), seed, _p(w.float().contiguous()),
-                                 _p(b.float().contiguous()), float(eps), _p(x), _p(y), _p(mean), _p(rstd),
-                                 _stream(t)), "rf_drop_add_ln_fwd")
-    return x, y, mean, rstd
+    y16 = torch.empty(M, D, dtype=torch.bfloat16, device=t.device) if want_bf16 else None
+    check(lib.rf_drop_add_ln_fwd_dual(M, D, _p(t), _rowmajor(t, "t"), _p(res), float(p), seed,
+                                      _p(w.float().contiguous()), _p(b.float().contiguous()), float(eps), _p(x),
+                                      _p(y), _p(mean), _p(rstd), _p(y16), _stream(t)), "rf_drop_add_ln_fwd")
+    return (x, y, mean, rstd, y16) if want_bf16 else (x, y, mean, rstd)
 
 
-def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int):
-    """rf_drop_add_ln_bwd: (dres fp32, dt bf16, dw, db)."""
+def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[torch.Tensor] = None):
+    """rf_drop_add_ln_bwd(_dual): (dres fp32, dt bf16, dw, db) for the gradient dy (fp32) of y plus,
+    when given, dy16 (bf16) of its bf16 copy; either may be None (not both)."""
     lib = _lib.load()
-    _dev(dy, x, mean, rstd, w)
+    _dev(x, mean, rstd, w)
     M, D = x.shape
-    dy = dy.float().contiguous()
+    if dy is None and dy16 is None:
+        raise ValueError("drop_add_ln_bwd: no gradient")
+    dy = None if dy is None else dy.float().contiguous()
+    if dy16 is not None:
+        if dy16.dtype != torch.bfloat16 or tuple(dy16.shape) != (M, D):
+            raise TypeError("drop_add_ln_bwd: dy16 must be a bf16 (M, D) tensor")
+        dy16 = dy16.contiguous()
     dres = torch.empty(M, D, dtype=torch.float32, device=x.device)
     dt = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
     dw = torch.empty(D, dtype=torch.float32, device=x.device)
     db = torch.empty_like(dw)
     ws = torch.empty(max(lib.rf_layernorm_bwd_workspace(M, D), 4), dtype=torch.uint8, device=x.device)
-    check(lib.rf_drop_add_ln_bwd(M, D, _p(dy), _p(x), _p(mean), _p(rstd), _p(w.float().contiguous()), float(p), seed,
-                                 _p(dres), _p(dt), _p(dw), _p(db), _p(ws), _stream(x)), "rf_drop_add_ln_bwd")
+    check(lib.rf_drop_add_ln_bwd_dual(M, D, _p(dy), _p(dy16), _p(x), _p(mean), _p(rstd), _p(w.float().contiguous()),
+                                      float(p), seed, _p(dres), _p(dt), _p(dw), _p(db), _p(ws), _stream(x)),
+          "rf_drop_add_ln_bwd")
     return dres, dt, dw, db
 
 

@@ -101,21 +101,27 @@ class _LayerNorm(torch.autograd.Function):
 class _DropAddLN(torch.autograd.Function):
     """y = LN(dropout_p(t) + res) (TF:1068-1071, 1127-1130): t the bf16 dense output, res the fp32
     residual stream; one HIP pass each way (rf_drop_add_ln_fwd / _bwd), the dropout mask a
-    counter hash of a seed drawn from torch's RNG."""
+    counter hash of a seed drawn from torch's RNG. dual: also returns bf16(y), the next GEMM's
+    operand, from the same pass, and the backward sums both outputs' gradients in the kernel
+    (no separate cast, cast-backward and gradient add per LayerNorm)."""
 
     @staticmethod
-    def forward(ctx, t, res, w, b, eps: float, p: float):
+    def forward(ctx, t, res, w, b, eps: float, p: float, dual: bool = False):
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
-        x, y, mean, rstd = ops.drop_add_ln_fwd(t, res.contiguous(), w, b, eps, p, seed)
+        out = ops.drop_add_ln_fwd(t, res.contiguous(), w, b, eps, p, seed, want_bf16=dual)
+        x, y, mean, rstd = out[:4]
         ctx.save_for_backward(x, mean, rstd, w)
         ctx.p, ctx.seed = p, seed
-        return y
+        ctx.set_materialize_grads(False)
+        return (y, out[4]) if dual else y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dy16=None):
+        if dy is None and dy16 is None:
+            return None, None, None, None, None, None, None
         x, mean, rstd, w = ctx.saved_tensors
-        dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed)
-        return dt, dres, dw, db, None, None
+        dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16)
+        return dt, dres, dw, db, None, None, None
 
 
 class _EmbedLN(torch.autograd.Function):
@@ -462,9 +468,11 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         grows = (rows, gvalid.view(-1))
     # bf16 path: dropout + residual + LayerNorm as one HIP pass each way (_DropAddLN)
     fused = dt == torch.bfloat16 and D in (64, 128, 256, 384, 512, 768, 1024)
+    h16 = None  # bf16 copy of h32 written by the previous layer's LayerNorm (fused path)
+    nl = len(model.encoder.layer)
     for li, lyr in enumerate(model.encoder.layer):
         lw = _layer_weights(li, lyr, dt)
-        h = h32.to(dt)
+        h = h16 if h16 is not None else h32.to(dt)
         qkv = _Gemm.apply(h, lw["w_qkv"], lw["b_qkv"], D, scale)
         qg = None
         if gmax > 0:
@@ -475,15 +483,18 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         ao = lyr.attention.output
         t = _Gemm.apply(ctx, lw["w_o"], lw["b_o"], 0, 1.0)
         if fused:
-            a32 = _DropAddLN.apply(t, h32, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid)
+            a32, a16 = _DropAddLN.apply(t, h32, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid, True)
         else:
             x1 = F.dropout(t.float(), p_hid, model.training) + h32
             a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
-        z = _Gemm.apply(a32.to(dt), lw["w_1"], lw["b_1"], 0, 1.0)
+            a16 = a32.to(dt)
+        z = _Gemm.apply(a16, lw["w_1"], lw["b_1"], 0, 1.0)
         u = F.gelu(z)
         fo = lyr.output
         t2 = _Gemm.apply(u, lw["w_2"], lw["b_2"], 0, 1.0)
-        if fused:
+        if fused and li + 1 < nl:
+            h32, h16 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, True)
+        elif fused:
             h32 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid)
         else:
             x2 = F.dropout(t2.float(), p_hid, model.training) + a32

@@ -517,3 +517,28 @@ def test_drop_add_ln_matches_torch(dev, p):
     assert (dt.float() - tr.grad).abs().max().item() <= 2 ** -7 * tr.grad.abs().max().item()
     assert (dw - wr.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item() + 1e-4
     assert (db - br.grad).abs().max().item() <= 1e-4 * br.grad.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("D", [768, 256])
+def test_drop_add_ln_dual(dev, D):
+    """rf_drop_add_ln_fwd_dual / _bwd_dual (the training path's LayerNorm feeding both the next
+    residual add and the next GEMM): y16 is bf16(y) bit for bit, and the backward with the two
+    consumers' gradients (fp32 dy, bf16 dy16; either alone) equals the single-gradient backward
+    of dy + float(dy16)."""
+    M = 300
+    g = torch.Generator(device=dev).manual_seed(D)
+    t = torch.randn(M, D, device=dev, generator=g).to(torch.bfloat16)
+    res = torch.randn(M, D, device=dev, generator=g)
+    w = torch.rand(D, device=dev, generator=g) + 0.5
+    b = torch.randn(D, device=dev, generator=g) * 0.1
+    x, y, mean, rstd, y16 = ops.drop_add_ln_fwd(t, res, w, b, 1e-5, 0.1, 1234, want_bf16=True)
+    x1, y1, _, _ = ops.drop_add_ln_fwd(t, res, w, b, 1e-5, 0.1, 1234)
+    assert torch.equal(y16, y.to(torch.bfloat16)) and torch.equal(y, y1) and torch.equal(x, x1)
+    dy = torch.randn(M, D, device=dev, generator=g)
+    dy16 = torch.randn(M, D, device=dev, generator=g).to(torch.bfloat16)
+    cases = ((dy, dy16, dy + dy16.float()), (None, dy16, dy16.float()), (dy, None, dy))
+    for a, c, ref_dy in cases:
+        got = ops.drop_add_ln_bwd(a, x, mean, rstd, w, 0.1, 1234, dy16=c)
+        ref = ops.drop_add_ln_bwd(ref_dy, x, mean, rstd, w, 0.1, 1234)
+        for u, v in zip(got, ref):
+            assert torch.equal(u, v)
