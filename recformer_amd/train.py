@@ -40,9 +40,30 @@ __all__ = ["encode_train"]
 
 # the global rows' backward in closed form (_global_bwd); False: autograd over _global_torch
 GLOBAL_BWD_CLOSED_FORM = True
+# weight gradients of the layer GEMMs as a split-K batched GEMM (_weight_grad)
+DW_SPLIT_K = True
 
 
 # ------------------------------------------------------------------------------------------
+def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+    """dW = dC^T A (N, K), reduced over the M = B*Lp token rows. The layer weights are small
+    (N*K <= 3072*768: at most 36 tiles of 256^2) against a long reduction, so one GEMM leaves
+    most of the chip idle; with DW_SPLIT_K the rows are split into S chunks computed as one
+    batched GEMM (S times the tiles) and the S fp32 partials summed (bf16 result, as the single
+    GEMM's)."""
+    M, N = dc.shape
+    K = a.shape[1]
+    S = 1
+    if DW_SPLIT_K and M >= 8192 and N * K <= 4 * 1024 * 1024:
+        S = 8
+        while S > 1 and (M % S or M // S < 2048):
+            S //= 2
+    if S == 1:
+        return dc.t() @ a
+    part = torch.bmm(dc.reshape(S, M // S, N).transpose(1, 2), a.reshape(S, M // S, K))  # (S, N, K)
+    return part.sum(0, dtype=torch.float32).to(dc.dtype)
+
+
 class _Gemm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, w, b, scale_cols: int, col_scale: float):
@@ -63,7 +84,7 @@ class _Gemm(torch.autograd.Function):
             wa = w.clone()
             wa[:sc] *= s
         da = dc @ wa if ctx.needs_input_grad[0] else None
-        dw = dc.t() @ a if ctx.needs_input_grad[1] else None
+        dw = _weight_grad(dc, a) if ctx.needs_input_grad[1] else None
         db = ops.colsum(dc) if ctx.needs_input_grad[2] else None  # deterministic HIP column sums
         if scaled:
             if dw is not None:

@@ -25,7 +25,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--negatives", type=int, default=0)
     ap.add_argument("--catalog", type=int, default=10000)
+    ap.add_argument("--no-dw-split", action="store_true", help="A/B: weight gradients as one GEMM each")
     a = ap.parse_args()
+    if a.no_dw_split:
+        from recformer_amd import train
+        train.DW_SPLIT_K = False
     dev = torch.device("cuda")
     cfg = RecformerConfig(**dict(BASE, item_num=a.catalog, attention_probs_dropout_prob=0.0,
                                  finetune_negative_sample_size=a.negatives))
