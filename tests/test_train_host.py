@@ -40,3 +40,18 @@ def test_global_bwd_closed_form_matches_autograd(B, Lp, H, G):
         r = torch.zeros_like(x) if r is None else r.float()
         scale = max(float(r.abs().max()), 1e-3)
         assert float((x.float() - r).abs().max()) <= 1e-4 * scale, name
+
+
+def test_weight_grad_split_k_matches_single_gemm():
+    """train._weight_grad (split-K batched dW = dC^T A with fp32 partial sums) against the
+    single-GEMM product in fp64, within bf16 rounding."""
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 16384, 48, 40
+    dc = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    a = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    ref = dc.double().t() @ a.double()
+    got = train._weight_grad(dc, a)
+    assert got.dtype == torch.bfloat16 and got.shape == (N, K)
+    assert float((got.double() - ref).abs().max()) <= 2e-2 * float(ref.abs().max())
+    # a short reduction stays one GEMM
+    assert torch.equal(train._weight_grad(dc[:1024], a[:1024]), dc[:1024].t() @ a[:1024])
