@@ -149,6 +149,12 @@ int rf_drop_add_ln_bwd_dual(int M, int D, const float* dy, const void* dy16, con
  * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias). */
 size_t rf_colsum_workspace(int M, int N);
 int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, void* workspace, rf_stream_t stream);
+/* dst[rows[r]] += src[r] (r < R; rows[r] < 0 skipped) for one or two (src, dst) pairs of the
+ * same shape (src1 = dst1 = null: one); repeated rows add in row order. The training path's
+ * global-key gradient columns added into dk / dv at the global positions (the reduction of
+ * TF:898-926's gradient, train.py). */
+int rf_scatter_add_rows(int dtype, int R, int D, const int32_t* rows, const void* src0, const void* src1,
+                        int ld_src, void* dst0, void* dst1, int ld_dst, rf_stream_t stream);
 int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                      const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                      rf_stream_t stream);

@@ -45,6 +45,7 @@ SIGNATURES = {
     "rf_drop_add_ln_bwd_dual": (c_int, [c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
                                         P]),
     "rf_colsum_workspace": (ctypes.c_size_t, [c_int, c_int]),
+    "rf_scatter_add_rows": (c_int, [c_int, c_int, c_int, P, P, P, c_int, P, P, c_int, P]),
     "rf_colsum": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, P, P]),
     "rf_layernorm_bwd": (c_int, [c_int, c_int, P, P, c_int, P, P, P, P, P, P, P, P]),
     "rf_band_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,

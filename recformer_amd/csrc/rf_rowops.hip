@@ -537,6 +537,26 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
 // k_colsum_part: block (column group of 64, row slice z) -> part[z][N] (4 row phases per block
 // combined in LDS); k_colsum_fin: out[n] = sum_z part[z][n]. Used for LayerNorm dgamma / dbeta
 // (over k_layernorm_bwd's per-block partials) and for bias gradients (column sums of dC).
+// dst[rows[r]] += src[r] for r < R (rows[r] < 0: skipped), two (src, dst) pairs per launch; one
+// thread per column walks the rows in order, so repeated destination rows add up in a fixed
+// order (no atomics). The training path's global-key gradient columns (a few rows per sequence).
+template <typename T>
+__global__ void __launch_bounds__(256) k_scatter_add_rows(int R, int D, const int32_t* __restrict__ rows,
+                                                           const T* __restrict__ s0, const T* __restrict__ s1,
+                                                           int lds, T* __restrict__ d0, T* __restrict__ d1,
+                                                           int ldd) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= D) return;
+  const T* src = blockIdx.y ? s1 : s0;
+  T* dst = blockIdx.y ? d1 : d0;
+  for (int r = 0; r < R; ++r) {
+    const int row = rows[r];
+    if (row < 0) continue;
+    T* p = dst + (int64_t)row * ldd + col;
+    *p = from_f32<T>(to_f32(*p) + to_f32(src[(int64_t)r * lds + col]));
+  }
+}
+
 constexpr int CS_SLICES = 64;  // k_colsum_fin reduces at most 64 slices
 
 template <typename T, bool VECOK>
@@ -895,6 +915,24 @@ size_t rf_layernorm_bwd_workspace(int M, int D) {
 }
 
 size_t rf_colsum_workspace(int M, int N) { return (size_t)CS_SLICES * (N > 0 ? N : 0) * sizeof(float); }
+
+int rf_scatter_add_rows(int dtype, int R, int D, const int32_t* rows, const void* src0, const void* src1,
+                        int ld_src, void* dst0, void* dst1, int ld_dst, rf_stream_t stream) {
+  RF_REQUIRE(R >= 0 && D >= 0 && ld_src >= D && ld_dst >= D, "rf_scatter_add_rows: bad shape");
+  if (R == 0 || D == 0) return RF_OK;
+  RF_REQUIRE(rows && src0 && dst0 && (!src1 == !dst1), "rf_scatter_add_rows: null pointer");
+  hipStream_t s = as_stream(stream);
+  dim3 grid((D + 255) / 256, src1 ? 2 : 1);
+  if (dtype == RF_BF16)
+    k_scatter_add_rows<bf16><<<grid, 256, 0, s>>>(R, D, rows, (const bf16*)src0, (const bf16*)src1, ld_src,
+                                                  (bf16*)dst0, (bf16*)dst1, ld_dst);
+  else if (dtype == RF_F32)
+    k_scatter_add_rows<float><<<grid, 256, 0, s>>>(R, D, rows, (const float*)src0, (const float*)src1, ld_src,
+                                                   (float*)dst0, (float*)dst1, ld_dst);
+  else
+    RF_REQUIRE(false, "rf_scatter_add_rows: bad dtype %d", dtype);
+  RF_LAUNCH_CHECK("rf_scatter_add_rows");
+}
 
 int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, void* workspace, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && N > 0 && ldx >= N, "rf_colsum: bad shape");

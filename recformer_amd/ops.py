@@ -362,6 +362,25 @@ def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[to
     return dres, dt, dw, db
 
 
+def scatter_add_rows(rows: torch.Tensor, src0, dst0, src1=None, dst1=None):
+    """rf_scatter_add_rows: dst[rows[r]] += src[r] in place (rows int32, -1 = skip) for one or two
+    (src, dst) pairs; src (R, D) and dst (*, D) row-major in one dtype (bf16 or fp32)."""
+    lib = _lib.load()
+    _dev(rows, src0, dst0)
+    R, D = src0.shape
+    pairs = [(src0, dst0)] + ([(src1, dst1)] if src1 is not None else [])
+    for s_, d_ in pairs:
+        if s_.dtype != d_.dtype or s_.shape != (R, D) or d_.shape[1] != D or s_.stride(0) != src0.stride(0) \
+                or d_.stride(0) != dst0.stride(0):
+            raise ValueError("scatter_add_rows: src/dst shapes, dtypes or strides differ")
+    if rows.dtype != torch.int32 or rows.numel() != R:
+        raise ValueError("scatter_add_rows: rows must be int32 with one entry per src row")
+    check(lib.rf_scatter_add_rows(dtype_code(src0.dtype), R, D, _p(rows.contiguous()), _p(src0), _p(src1),
+                                  _rowmajor(src0, "src"), _p(dst0), _p(dst1), _rowmajor(dst0, "dst"),
+                                  _stream(dst0)), "rf_scatter_add_rows")
+    return dst0, dst1
+
+
 def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, tag: Optional[str] = None,
                        dqkv: Optional[torch.Tensor] = None):
     """Gradient of the local branch (rf_band_attn_bwd): q/k/v (pre-scaled q) and o, dout bf16

@@ -315,7 +315,7 @@ class _Attention(torch.autograd.Function):
                 ops.global_attention(qg.contiguous(), kg, vg, flags, gidx, B, Lp, H, out)
         ctx.save_for_backward(qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out)
         ctx.dims = (B, Lp, H, half_w)
-        ctx.grows = grows  # (rows, keep) of the pass, shared by its layers
+        ctx.grows = grows  # (rows, keep, rows as int32 with -1 for empty slots) of the pass
         return out
 
     @staticmethod
@@ -336,7 +336,11 @@ class _Attention(torch.autograd.Function):
         dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H, dqkv=dqkv)
         res = [None] * 7
         if gmax > 0:
-            rows, keep = ctx.grows if ctx.grows is not None else _global_rows(gidx, B, Lp)
+            if ctx.grows is not None:
+                rows, keep, rows32 = ctx.grows
+            else:
+                rows, keep = _global_rows(gidx, B, Lp)
+                rows32 = torch.where(keep, rows, -1).to(torch.int32)  # -1: empty slot, skipped
             # gradients of the global-key columns, reduced over every query of the sequence
             # bf16 operands, fp32 accumulation (no fp32 copies of the (B*Lp, D) q and dout)
             qh = q.reshape(B, Lp, H, 64)
@@ -344,9 +348,8 @@ class _Attention(torch.autograd.Function):
             dkg = torch.einsum("bhig,bihd->bghd", gds[..., :gmax].to(q.dtype), qh).reshape(B * gmax, D)
             dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :gmax].to(q.dtype), dh).reshape(B * gmax, D)
             # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
-            kf = keep[:, None].to(dkg.dtype)
-            dk.index_add_(0, rows, (dkg * kf).to(dk.dtype))  # bf16 throughout (dqkv is bf16)
-            dv.index_add_(0, rows, (dvg * kf).to(dv.dtype))
+            # added into dk / dv at the global positions (bf16, as dqkv) by one small kernel
+            ops.scatter_add_rows(rows32, dkg.to(dk.dtype).contiguous(), dk, dvg.to(dv.dtype).contiguous(), dv)
             # global branch: closed-form gradient of the fold algebra
             if any(ctx.needs_input_grad[1:7]):
                 gout = dout[rows].float() * keep[:, None].to(torch.float32)
@@ -486,7 +489,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     if gmax > 0:
         rows = (torch.arange(B, device=input_ids.device)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
         gvalid = (gidx >= 0).reshape(-1, 1)
-        grows = (rows, gvalid.view(-1))
+        grows = (rows, gvalid.view(-1), torch.where(gvalid.view(-1), rows, -1).to(torch.int32))
     # bf16 path: dropout + residual + LayerNorm as one HIP pass each way (_DropAddLN)
     fused = dt == torch.bfloat16 and D in (64, 128, 256, 384, 512, 768, 1024)
     h16 = None  # bf16 copy of h32 written by the previous layer's LayerNorm (fused path)

@@ -542,3 +542,25 @@ def test_drop_add_ln_dual(dev, D):
         ref = ops.drop_add_ln_bwd(ref_dy, x, mean, rstd, w, 0.1, 1234)
         for u, v in zip(got, ref):
             assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_scatter_add_rows(dev, dt):
+    """rf_scatter_add_rows: dst[rows[r]] += src[r] for two pairs, strided destinations (column
+    views of one wide tensor), skipped rows (-1) and a repeated row, against index_add_."""
+    g = torch.Generator(device=dev).manual_seed(5)
+    R, D, M = 9, 768, 50
+    rows = torch.tensor([3, -1, 7, 3, 0, 49, -1, 12, 7], dtype=torch.int32, device=dev)
+    src = [torch.randn(R, D, device=dev, generator=g).to(dt) for _ in range(2)]
+    wide = torch.randn(M, 3 * D, device=dev, generator=g).to(dt)
+    ref = wide.clone()
+    keep = rows >= 0
+    for i, s in enumerate(src):
+        col = ref[:, (i + 1) * D:(i + 2) * D].float()
+        col.index_add_(0, rows[keep].long(), s[keep].float())
+        ref[:, (i + 1) * D:(i + 2) * D] = col.to(dt)
+    ops.scatter_add_rows(rows, src[0], wide[:, D:2 * D], src[1], wide[:, 2 * D:])
+    torch.cuda.synchronize()
+    tol = 1e-5 if dt == torch.float32 else 1e-2  # repeated rows: addition order may differ
+    assert float((wide.float() - ref.float()).abs().max()) <= tol * 8
+    assert torch.equal(wide[:, :D], ref[:, :D])
