@@ -45,12 +45,20 @@ DW_SPLIT_K = True
 
 
 # ------------------------------------------------------------------------------------------
+def _mm_f32(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """x @ y (2-D or batched 3-D) with an fp32 result: hipBLASLt's fp32 output from bf16 operands
+    on the GPU (no bf16 rounding of the product), a cast elsewhere."""
+    f = torch.bmm if x.dim() == 3 else torch.mm
+    if x.is_cuda and x.dtype != torch.float32:
+        return f(x, y, out_dtype=torch.float32)
+    return f(x, y).float()
+
+
 def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
-    """dW = dC^T A (N, K), reduced over the M = B*Lp token rows. The layer weights are small
-    (N*K <= 3072*768: at most 36 tiles of 256^2) against a long reduction, so one GEMM leaves
-    most of the chip idle; with DW_SPLIT_K the rows are split into S chunks computed as one
-    batched GEMM (S times the tiles) and the S fp32 partials summed (bf16 result, as the single
-    GEMM's)."""
+    """dW = dC^T A (N, K) in fp32 (the master weight's dtype), reduced over the M = B*Lp token
+    rows. The layer weights are small (N*K <= 3072*768: at most 36 tiles of 256^2) against a long
+    reduction, so one GEMM leaves most of the chip idle; with DW_SPLIT_K the rows are split into
+    S chunks computed as one batched GEMM (S times the tiles) and the S fp32 partials summed."""
     M, N = dc.shape
     K = a.shape[1]
     S = 1
@@ -59,17 +67,21 @@ def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
         while S > 1 and (M % S or M // S < 2048):
             S //= 2
     if S == 1:
-        return dc.t() @ a
-    part = torch.bmm(dc.reshape(S, M // S, N).transpose(1, 2), a.reshape(S, M // S, K))  # (S, N, K)
-    return part.sum(0, dtype=torch.float32).to(dc.dtype)
+        return _mm_f32(dc.t(), a)
+    part = _mm_f32(dc.reshape(S, M // S, N).transpose(1, 2), a.reshape(S, M // S, K))  # (S, N, K)
+    return part.sum(0)
 
 
 class _Gemm(torch.autograd.Function):
+    """C = A.W^T + b on rf_gemm with W's compute-dtype copy w16 (not tracked); the gradient goes
+    to the master W (fp32 under autocast) directly, as fp32 dW — no cast node per weight."""
+
     @staticmethod
-    def forward(ctx, a, w, b, scale_cols: int, col_scale: float):
-        ctx.save_for_backward(a, w)
+    def forward(ctx, a, w, w16, b, scale_cols: int, col_scale: float):
+        ctx.save_for_backward(a, w16)
         ctx.sc = (scale_cols, col_scale)
-        return ops.gemm(a.contiguous(), w, b, ops.RF_EPI_BIAS, scale_cols=scale_cols, col_scale=col_scale)
+        ctx.wdt = w.dtype
+        return ops.gemm(a.contiguous(), w16, b, ops.RF_EPI_BIAS, scale_cols=scale_cols, col_scale=col_scale)
 
     @staticmethod
     def backward(ctx, dc):
@@ -84,14 +96,14 @@ class _Gemm(torch.autograd.Function):
             wa = w.clone()
             wa[:sc] *= s
         da = dc @ wa if ctx.needs_input_grad[0] else None
-        dw = _weight_grad(dc, a) if ctx.needs_input_grad[1] else None
-        db = ops.colsum(dc) if ctx.needs_input_grad[2] else None  # deterministic HIP column sums
+        dw = _weight_grad(dc, a).to(ctx.wdt) if ctx.needs_input_grad[1] else None
+        db = ops.colsum(dc) if ctx.needs_input_grad[3] else None  # deterministic HIP column sums
         if scaled:
             if dw is not None:
                 dw[:sc] *= s
             if db is not None:
                 db[:sc] *= s
-        return da, dw, db, None, None
+        return da, dw, None, db, None, None
 
 
 def _ln_backward(dy, x, mean, rstd, w):
@@ -431,18 +443,23 @@ def _cast(key, make):
 
 
 def _layer_weights(li: int, lyr, dt: torch.dtype) -> dict:
-    """The layer's weights as the forward consumes them (cached under shared_casts)."""
+    """The layer's weights as the forward consumes them (cached under shared_casts): each GEMM
+    weight as (master, untracked compute-dtype copy) for _Gemm; the global key/value weights as
+    tracked casts (the attention backward returns their gradients in the compute dtype)."""
     def make():
         sa, ao, fo = lyr.attention.self, lyr.attention.output, lyr.output
+
+        def pair(w):
+            return w, w.detach().to(dt)
         return {
-            "w_qkv": torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0).to(dt),
+            "w_qkv": pair(torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0)),
             "b_qkv": torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0).float(),
-            "w_qg": sa.query_global.weight.to(dt), "b_qg": sa.query_global.bias.float(),
+            "w_qg": pair(sa.query_global.weight), "b_qg": sa.query_global.bias.float(),
             "w_kg": sa.key_global.weight.to(dt), "b_kg": sa.key_global.bias.float(),
             "w_vg": sa.value_global.weight.to(dt), "b_vg": sa.value_global.bias.float(),
-            "w_o": ao.dense.weight.to(dt), "b_o": ao.dense.bias.float(),
-            "w_1": lyr.intermediate.dense.weight.to(dt), "b_1": lyr.intermediate.dense.bias.float(),
-            "w_2": fo.dense.weight.to(dt), "b_2": fo.dense.bias.float(),
+            "w_o": pair(ao.dense.weight), "b_o": ao.dense.bias.float(),
+            "w_1": pair(lyr.intermediate.dense.weight), "b_1": lyr.intermediate.dense.bias.float(),
+            "w_2": pair(fo.dense.weight), "b_2": fo.dense.bias.float(),
         }
     return _cast((id(lyr), li, dt), make)
 
@@ -497,25 +514,25 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     for li, lyr in enumerate(model.encoder.layer):
         lw = _layer_weights(li, lyr, dt)
         h = h16 if h16 is not None else h32.to(dt)
-        qkv = _Gemm.apply(h, lw["w_qkv"], lw["b_qkv"], D, scale)
+        qkv = _Gemm.apply(h, *lw["w_qkv"], lw["b_qkv"], D, scale)
         qg = None
         if gmax > 0:
             hg = h[rows] * gvalid.to(h.dtype)
-            qg = _Gemm.apply(hg, lw["w_qg"], lw["b_qg"], D, scale)
+            qg = _Gemm.apply(hg, *lw["w_qg"], lw["b_qg"], D, scale)
         ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
                                flags, gidx, B, Lp, H, windows[li] // 2, fold, grows)
         ao = lyr.attention.output
-        t = _Gemm.apply(ctx, lw["w_o"], lw["b_o"], 0, 1.0)
+        t = _Gemm.apply(ctx, *lw["w_o"], lw["b_o"], 0, 1.0)
         if fused:
             a32, a16 = _DropAddLN.apply(t, h32, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid, True)
         else:
             x1 = F.dropout(t.float(), p_hid, model.training) + h32
             a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
             a16 = a32.to(dt)
-        z = _Gemm.apply(a16, lw["w_1"], lw["b_1"], 0, 1.0)
+        z = _Gemm.apply(a16, *lw["w_1"], lw["b_1"], 0, 1.0)
         u = F.gelu(z)
         fo = lyr.output
-        t2 = _Gemm.apply(u, lw["w_2"], lw["b_2"], 0, 1.0)
+        t2 = _Gemm.apply(u, *lw["w_2"], lw["b_2"], 0, 1.0)
         if fused and li + 1 < nl:
             h32, h16 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, True)
         elif fused:

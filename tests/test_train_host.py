@@ -43,15 +43,15 @@ def test_global_bwd_closed_form_matches_autograd(B, Lp, H, G):
 
 
 def test_weight_grad_split_k_matches_single_gemm():
-    """train._weight_grad (split-K batched dW = dC^T A with fp32 partial sums) against the
-    single-GEMM product in fp64, within bf16 rounding."""
+    """train._weight_grad (split-K batched dW = dC^T A, fp32 partials and result) against the
+    product in fp64, within bf16 rounding (on the CPU the partials are bf16 products)."""
     g = torch.Generator().manual_seed(3)
     M, N, K = 16384, 48, 40
     dc = torch.randn(M, N, generator=g).to(torch.bfloat16)
     a = torch.randn(M, K, generator=g).to(torch.bfloat16)
     ref = dc.double().t() @ a.double()
     got = train._weight_grad(dc, a)
-    assert got.dtype == torch.bfloat16 and got.shape == (N, K)
+    assert got.dtype == torch.float32 and got.shape == (N, K)  # fp32: the master weight's dtype
     assert float((got.double() - ref).abs().max()) <= 2e-2 * float(ref.abs().max())
     # a short reduction stays one GEMM
-    assert torch.equal(train._weight_grad(dc[:1024], a[:1024]), dc[:1024].t() @ a[:1024])
+    assert torch.equal(train._weight_grad(dc[:1024], a[:1024]), (dc[:1024].t() @ a[:1024]).float())
