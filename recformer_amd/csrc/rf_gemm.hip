@@ -578,7 +578,13 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
       bf16x8 x;
 #pragma unroll
       for (int k = 0; k < 8; ++k) x[k] = (bf16)v[k];
+#if !defined(RF_GEMM_PLAIN_STORE)
+      // non-temporal: the tile's output is not re-read by this kernel; measured +0.8% per C2
+      // step (tools/gpu/gemm_var.sh: qkv -4%, FFN -1.5%)
+      __builtin_nontemporal_store(x, reinterpret_cast<bf16x8*>(out));
+#else
       *reinterpret_cast<bf16x8*>(out) = x;
+#endif
     } else {
       bf16x4 x;
 #pragma unroll

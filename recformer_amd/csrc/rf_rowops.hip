@@ -91,8 +91,19 @@ __device__ __forceinline__ void store_split(uint16_t* hi, uint16_t* lo, const fl
     h[j] = a;
     l[j] = b;
   }
+#if defined(RF_LN_NT_HI)
+  __builtin_nontemporal_store(h, reinterpret_cast<u16v*>(hi));
+#else
   *reinterpret_cast<u16v*>(hi) = h;
+#endif
+#if !defined(RF_LN_PLAIN_LO)
+  // non-temporal: the lo plane is next read by the following LayerNorm, after a GEMM and the
+  // attention have streamed through the caches (+0.5% per C2 step; the hi plane, the next GEMM's
+  // operand, stays a normal store)
+  __builtin_nontemporal_store(l, reinterpret_cast<u16v*>(lo));
+#else
   *reinterpret_cast<u16v*>(lo) = l;
+#endif
 }
 
 // ------------------------------------------------------------------------------------
