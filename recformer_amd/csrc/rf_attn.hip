@@ -588,6 +588,13 @@ __device__ __forceinline__ float mask_score(unsigned int bits, int bit, float sv
   return __int_as_float((m & __float_as_int(sv)) | (~m & (int)0xff800000u));  // v_bfi_b32
 }
 
+// Q / K / V chunks are read once per block walk: non-temporal DMA (with the LayerNorm's
+// non-temporal loads, +1.2% per C2 step in an alternating whole-step A/B of library builds)
+#if defined(RF_BAND_PLAIN_LOAD)
+#define BAND_GLDS glds16
+#else
+#define BAND_GLDS glds16_nt
+#endif
 __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb, const bf16* __restrict__ q,
                                                           const bf16* __restrict__ k,
                                                           const bf16* __restrict__ v, int ld,
@@ -640,14 +647,14 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
     for (int j = 0; j < 2; ++j) {
       const int kp = min(max(64 * c - 32 + prow + 8 * j, 0), Lp - 1);
       const uint32_t off = __umul24(kp, ld) + pch;
-      glds16(kb + off, base + j * 1024);
-      glds16(vb + off, base + 8192 + j * 1024);
+      BAND_GLDS(kb + off, base + j * 1024);
+      BAND_GLDS(vb + off, base + 8192 + j * 1024);
     }
   };
   auto dma_q = [&](int x) {
     char* base = smem + AP_Q + (x & 1) * 8192 + wave * 2048;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(qb + __umul24(64 * x + prow + 8 * j, ld) + pch, base + j * 1024);
+    for (int j = 0; j < 2; ++j) BAND_GLDS(qb + __umul24(64 * x + prow + 8 * j, ld) + pch, base + j * 1024);
   };
   dma_q(x0);
   dma_chunk(x0);

@@ -129,6 +129,13 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
       (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// the same with the non-temporal cache policy (read-once streams)
+__device__ __forceinline__ void glds16_nt(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)gsrc,
+      (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 2);
+}
+
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Byte offset of 16-B chunk `ch` (0..7) of row `row` in a [rows][64 x bf16] LDS tile

@@ -76,7 +76,11 @@ template <int VEC>
 __device__ __forceinline__ void load_split(const uint16_t* hi, const uint16_t* lo, float* o) {
   typedef __attribute__((ext_vector_type(VEC))) uint16_t u16v;
   const u16v h = *reinterpret_cast<const u16v*>(hi);
+#if !defined(RF_LN_PLAIN_LOAD)
+  const u16v l = __builtin_nontemporal_load(reinterpret_cast<const u16v*>(lo));
+#else
   const u16v l = *reinterpret_cast<const u16v*>(lo);
+#endif
 #pragma unroll
   for (int j = 0; j < VEC; ++j) o[j] = join_f32(h[j], l[j]);
 }
@@ -340,7 +344,11 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int e = c * LPR * VEC + gl * VEC;
+#if !defined(RF_LN_PLAIN_LOAD)  // the dense output and the lo plane are read once: non-temporal
+    const bf16x8 xb = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(x + (int64_t)row * ldx + e));
+#else
     const bf16x8 xb = *reinterpret_cast<const bf16x8*>(x + (int64_t)row * ldx + e);
+#endif
 #pragma unroll
     for (int j = 0; j < VEC; ++j) xv[c][j] = (float)xb[j];
     if (r_hi) {
