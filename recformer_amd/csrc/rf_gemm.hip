@@ -56,7 +56,10 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, fl
   }
   if (EPI != RF_EPI_NONE) v += e.bias[col];
   if (col < e.scale_cols) v *= e.col_scale;
-  if (EPI == RF_EPI_BIAS_GELU) v = (CF32 || sizeof(TIN) == 4) ? gelu_erf(v) : gelu_bf16out(v);
+  if (EPI == RF_EPI_BIAS_GELU_AUX)
+    reinterpret_cast<TIN*>(const_cast<void*>(e.R))[(int64_t)row * e.ldr + col] = from_f32<TIN>(v);
+  if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX)
+    v = (CF32 || sizeof(TIN) == 4) ? gelu_erf(v) : gelu_bf16out(v);
   if (EPI == RF_EPI_BIAS_RESID) {
     if (RF32)
       v += reinterpret_cast<const float*>(e.R)[(int64_t)row * e.ldr + col];
@@ -123,7 +126,17 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] *= e.col_scale;
   }
-  if (EPI == RF_EPI_BIAS_GELU) {
+  if (EPI == RF_EPI_BIAS_GELU_AUX) {
+    bf16* z = reinterpret_cast<bf16*>(const_cast<void*>(e.R)) + (int64_t)row * e.ldr + c0;
+#pragma unroll
+    for (int h8 = 0; h8 < 2; ++h8) {
+      bf16x8 x;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = (bf16)v[8 * h8 + k];
+      *reinterpret_cast<bf16x8*>(z + 8 * h8) = x;
+    }
+  }
+  if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = CF32 ? gelu_erf(v[k]) : gelu_bf16out(v[k]);
   }
@@ -524,7 +537,19 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] *= e.col_scale;
   }
-  if (EPI == RF_EPI_BIAS_GELU) {
+  if (EPI == RF_EPI_BIAS_GELU_AUX) {  // the pre-activation, bf16 (NV = 8 on this path)
+    bf16* z = reinterpret_cast<bf16*>(const_cast<void*>(e.R)) + (int64_t)row * e.ldr + c0;
+    if (NV == 8) {
+      bf16x8 x;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = (bf16)v[k];
+      *reinterpret_cast<bf16x8*>(z) = x;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) z[k] = (bf16)v[k];
+    }
+  }
+  if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
     if (CF32) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[k] = gelu_erf(v[k]);
@@ -1040,7 +1065,10 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
                        const float* rw, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && N > 0 && K > 0, "rf_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   RF_REQUIRE(lda >= K && ldw >= K && ldc >= N, "rf_gemm: bad leading dims");
-  RF_REQUIRE(epilogue >= RF_EPI_NONE && epilogue <= RF_EPI_COS, "rf_gemm: bad epilogue %d", epilogue);
+  RF_REQUIRE((epilogue >= RF_EPI_NONE && epilogue <= RF_EPI_COS) || epilogue == RF_EPI_BIAS_GELU_AUX,
+             "rf_gemm: bad epilogue %d", epilogue);
+  RF_REQUIRE(epilogue != RF_EPI_BIAS_GELU_AUX || (dtype == RF_BF16 && resid && ldr >= N && !(io_flags & 3)),
+             "rf_gemm: EPI_BIAS_GELU_AUX needs bf16 and a bf16 pre-activation output (resid)");
   RF_REQUIRE(epilogue == RF_EPI_NONE || epilogue == RF_EPI_COS || bias, "rf_gemm: bias required");
   RF_REQUIRE(epilogue != RF_EPI_BIAS_RESID || (resid && ldr >= N), "rf_gemm: residual required");
   RF_REQUIRE(epilogue != RF_EPI_COS || (ra && rw), "rf_gemm: norms required for EPI_COS");
@@ -1066,6 +1094,9 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
         break;
       case RF_EPI_BIAS_GELU:
         dispatch_tile<RF_EPI_BIAS_GELU, false, false>(M, N, K, A, lda, W, ldw, e, s);
+        break;
+      case RF_EPI_BIAS_GELU_AUX:
+        dispatch_tile<RF_EPI_BIAS_GELU_AUX, false, false>(M, N, K, A, lda, W, ldw, e, s);
         break;
       case RF_EPI_BIAS_RESID:
         if (cf && rf) dispatch_tile<RF_EPI_BIAS_RESID, true, true>(M, N, K, A, lda, W, ldw, e, s);

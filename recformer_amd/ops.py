@@ -12,7 +12,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF_EPI_COS,
+from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_GELU_AUX, RF_EPI_BIAS_RESID, RF_EPI_COS,
                    RF_EPI_NONE, RF_F32, check)
 
 __all__ = [
@@ -20,7 +20,7 @@ __all__ = [
     "gemm", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
-    "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
+    "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_GELU_AUX", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
 ]
 
 

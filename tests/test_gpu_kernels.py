@@ -564,3 +564,19 @@ def test_scatter_add_rows(dev, dt):
     tol = 1e-5 if dt == torch.float32 else 1e-2  # repeated rows: addition order may differ
     assert float((wide.float() - ref.float()).abs().max()) <= tol * 8
     assert torch.equal(wide[:, :D], ref[:, :D])
+
+
+@pytest.mark.parametrize("M,N", [(4096, 3072), (1000, 3072), (300, 200)])
+def test_gemm_gelu_aux(dev, M, N):
+    """EPI_BIAS_GELU_AUX (training FFN1): C equals the EPI_BIAS_GELU output and the written
+    pre-activation equals the EPI_BIAS output, bit for bit, on the ping-pong (large), tiled
+    (small) and ragged-edge paths."""
+    K = 768
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    a = (torch.randn(M, K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=dev, generator=g) * 0.1
+    z = torch.full((M, N), 7.0, device=dev, dtype=torch.bfloat16)
+    u = ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU_AUX, resid=z)
+    assert torch.equal(u, ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU))
+    assert torch.equal(z, ops.gemm(a, w, b, ops.RF_EPI_BIAS))

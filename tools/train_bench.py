@@ -26,7 +26,11 @@ def main():
     ap.add_argument("--negatives", type=int, default=0)
     ap.add_argument("--catalog", type=int, default=10000)
     ap.add_argument("--no-dw-split", action="store_true", help="A/B: weight gradients as one GEMM each")
+    ap.add_argument("--no-fused-gelu", action="store_true", help="A/B: FFN1 GEMM then F.gelu")
     a = ap.parse_args()
+    if a.no_fused_gelu:
+        from recformer_amd import train
+        train.FUSED_GELU = False
     if a.no_dw_split:
         from recformer_amd import train
         train.DW_SPLIT_K = False
