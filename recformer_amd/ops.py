@@ -584,13 +584,13 @@ def row_inv_norm(x: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
 
 def cos_scores(z: torch.Tensor, items: torch.Tensor, inv_temp: float,
                z_rnorm: Optional[torch.Tensor] = None,
-               items_rnorm: Optional[torch.Tensor] = None) -> torch.Tensor:
+               items_rnorm: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """(B,N) fp32 = cos(z_b, items_n) * inv_temp on the MFMA GEMM (Similarity, models.py:358-369)."""
     if z_rnorm is None:
         z_rnorm = row_inv_norm(z)
     if items_rnorm is None:
         items_rnorm = row_inv_norm(items)
-    return gemm(z, items, None, RF_EPI_COS, col_scale=inv_temp, ra=z_rnorm, rw=items_rnorm)
+    return gemm(z, items, None, RF_EPI_COS, col_scale=inv_temp, ra=z_rnorm, rw=items_rnorm, out=out)
 
 
 def cos_scores_cand(z: torch.Tensor, items: torch.Tensor, cand: torch.Tensor, inv_temp: float,

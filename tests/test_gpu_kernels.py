@@ -580,3 +580,20 @@ def test_gemm_gelu_aux(dev, M, N):
     u = ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU_AUX, resid=z)
     assert torch.equal(u, ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU))
     assert torch.equal(z, ops.gemm(a, w, b, ops.RF_EPI_BIAS))
+
+
+@pytest.mark.parametrize("B,N,block", [(256, 20000, 8192), (4096, 66536, 65536), (64, 1000, 1000)])
+def test_rank_catalog_matches_full_ranker(dev, B, N, block):
+    """ranker.rank_catalog (scores block by block, never the (B, N) matrix) gives the full-matrix
+    Ranker's metrics: identical strict ranks (the label scores are the same kernel's values), the
+    loss within fp32 rounding of the two log-sum-exp forms."""
+    from recformer_amd import Ranker
+    from recformer_amd.ranker import rank_catalog
+    g = torch.Generator(device=dev).manual_seed(B + N)
+    q = torch.randn(B, 768, device=dev, generator=g).to(torch.bfloat16)
+    items = torch.randn(N, 768, device=dev, generator=g).to(torch.bfloat16)
+    labels = torch.randint(0, N, (B,), device=dev, generator=g)
+    full = Ranker([10, 50])(ops.cos_scores(q, items, 20.0), labels)
+    got = rank_catalog(q, items, labels, [10, 50], 0.05, block=block)
+    assert got[:-1] == full[:-1]
+    assert got[-1] == pytest.approx(full[-1], rel=1e-5, abs=1e-5)

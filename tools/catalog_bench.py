@@ -17,6 +17,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from recformer_amd import Ranker, RecformerConfig, RecformerModel, dp, ops  # noqa: E402
+from recformer_amd.ranker import rank_catalog  # noqa: E402
 from recformer_amd.synth import BASE, synth_batch  # noqa: E402
 
 
@@ -52,20 +53,37 @@ def main():
         table = dp.gather_rows(local, a.items) if world > 1 else local
         q = torch.randn(a.queries, cfg.hidden_size, device=dev).to(torch.bfloat16)
         labels = torch.randint(0, a.items, (a.queries,), device=dev)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        rn = ops.row_inv_norm(table)
-        scores = ops.cos_scores(q, table, 1.0 / cfg.temp, items_rnorm=rn)
-        metrics = Ranker([10, 50])(scores, labels)
-        torch.cuda.synchronize()
-        t_score = time.perf_counter() - t0
+        t_parts = []
+        for _ in range(2):  # the first pass also pays the score buffer's allocation
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rn = ops.row_inv_norm(table)
+            scores = ops.cos_scores(q, table, 1.0 / cfg.temp, items_rnorm=rn)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            metrics = Ranker([10, 50])(scores, labels)
+            torch.cuda.synchronize()
+            t_parts.append((t1 - t0, time.perf_counter() - t1))
+            del scores
+        t_score = sum(t_parts[-1])
+        # the same metrics block by block (ranker.rank_catalog: no (B, N) score matrix)
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            metrics_blk = rank_catalog(q, table, labels, [10, 50], cfg.temp)
+            torch.cuda.synchronize()
+            t_blk = time.perf_counter() - t0
     if rank == 0:
         print(json.dumps({"workload": "C5-style retrieval: encode catalog (L=33->64) + score/rank queries",
                           "items": a.items, "queries": a.queries, "gpus": world,
                           "encode_s": round(t_enc, 3), "items_per_s": round((hi - lo) * world / t_enc, 1),
                           "score_rank_ms": round(1e3 * t_score, 2),
+                          "score_ms": round(1e3 * t_parts[-1][0], 2), "rank_ms": round(1e3 * t_parts[-1][1], 2),
+                          "first_pass_ms": round(1e3 * sum(t_parts[0]), 2),
+                          "blockwise_score_rank_ms": round(1e3 * t_blk, 2),
+                          "blockwise_metrics_equal": metrics_blk[:-1] == metrics[:-1],
                           "score_tflops": round(2 * a.queries * a.items * cfg.hidden_size / t_score / 1e12, 1),
-                          "scores_gb": round(scores.numel() * 4 / 2**30, 2), "metrics": [round(m, 4) for m in metrics]}))
+                          "scores_gb": round(a.queries * a.items * 4 / 2**30, 2), "metrics": [round(m, 4) for m in metrics]}))
     if world > 1:
         dist.destroy_process_group()
 
