@@ -818,10 +818,13 @@ __global__ void __launch_bounds__(512, 1)
   };
   // the MFMA half of a phase: barrier, retire this phase's LDS reads, MFMAs at raised priority
   auto compute = [&](int qm, int qn, bool live) {
+#ifndef RF_GEMM_PRIO
+#define RF_GEMM_PRIO 1
+#endif
 #if defined(RF_GEMM_DIAG) && (RF_GEMM_DIAG & 4)  // diagnostic: no barriers around the MFMAs
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (live) {
-      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(RF_GEMM_PRIO);
       mma(qm, qn);
       __builtin_amdgcn_s_setprio(0);
     }
@@ -831,7 +834,7 @@ __global__ void __launch_bounds__(512, 1)
     bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (live) {
-      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(RF_GEMM_PRIO);
       mma(qm, qn);
       __builtin_amdgcn_s_setprio(0);
     }
