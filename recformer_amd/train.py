@@ -166,8 +166,9 @@ class _DropAddLN(torch.autograd.Function):
     (no separate cast, cast-backward and gradient add per LayerNorm)."""
 
     @staticmethod
-    def forward(ctx, t, res, w, b, eps: float, p: float, dual: bool = False):
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+    def forward(ctx, t, res, w, b, eps: float, p: float, dual: bool = False, seed: Optional[int] = None):
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
         out = ops.drop_add_ln_fwd(t, res.contiguous(), w, b, eps, p, seed, want_bf16=dual)
         x, y, mean, rstd = out[:4]
         ctx.save_for_backward(x, mean, rstd, w)
@@ -178,10 +179,10 @@ class _DropAddLN(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, dy16=None):
         if dy is None and dy16 is None:
-            return None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         x, mean, rstd, w = ctx.saved_tensors
         dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16)
-        return dt, dres, dw, db, None, None, None
+        return dt, dres, dw, db, None, None, None, None
 
 
 class _EmbedLN(torch.autograd.Function):
@@ -538,6 +539,8 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     fused = dt == torch.bfloat16 and D in (64, 128, 256, 384, 512, 768, 1024)
     h16 = None  # bf16 copy of h32 written by the previous layer's LayerNorm (fused path)
     nl = len(model.encoder.layer)
+    # the pass's dropout seeds (two LayerNorms per layer) in one draw from torch's CPU generator
+    seeds = torch.randint(0, 2 ** 62, (2 * nl,)).tolist() if p_hid > 0 else [0] * (2 * nl)
     for li, lyr in enumerate(model.encoder.layer):
         lw = _layer_weights(li, lyr, dt)
         h = h16 if h16 is not None else h32.to(dt)
@@ -551,7 +554,8 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         ao = lyr.attention.output
         t = _Gemm.apply(ctx, *lw["w_o"], lw["b_o"], 0, 1.0)
         if fused:
-            a32, a16 = _DropAddLN.apply(t, h32, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid, True)
+            a32, a16 = _DropAddLN.apply(t, h32, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid, True,
+                                        seeds[2 * li])
         else:
             x1 = F.dropout(t.float(), p_hid, model.training) + h32
             a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
@@ -563,9 +567,11 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         fo = lyr.output
         t2 = _Gemm.apply(u, *lw["w_2"], lw["b_2"], 0, 1.0)
         if fused and li + 1 < nl:
-            h32, h16 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, True)
+            h32, h16 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, True,
+                                        seeds[2 * li + 1])
         elif fused:
-            h32 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid)
+            h32 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, False,
+                                   seeds[2 * li + 1])
         else:
             x2 = F.dropout(t2.float(), p_hid, model.training) + a32
             h32 = _LayerNorm.apply(x2, fo.LayerNorm.weight.float(), fo.LayerNorm.bias.float(), eps, torch.float32)
