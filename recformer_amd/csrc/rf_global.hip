@@ -997,7 +997,9 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
     RF_REQUIRE(D % 64 == 0 && D <= 1024, "rf_global_attn_fold_h: D=%d", D);
     // few row tiles: split u's columns over more blocks (each recomputes its tile's qg)
     int qsplit = 1;
-    while (qsplit < 4 && H * ((R + 63) / 64) * qsplit < 128 && (D / 16) % (2 * qsplit) == 0) qsplit *= 2;
+    int qmax = 8;  // C2 (R = 64): 8 column splits 51.3 vs 52.9 us for 4 (tools/gfold_bench.py)
+    if (const char* e = getenv("RF_GFOLD_QSPLIT")) qmax = std::max(1, atoi(e));  // A/B tools
+    while (qsplit < qmax && H * ((R + 63) / 64) * qsplit < 32 * qmax && (D / 16) % (2 * qsplit) == 0) qsplit *= 2;
     // Wkg slice: at most ceil(cols / 64) + 1 segments of 8 KiB; its own region when it fits
     const int nslice = std::min(D / 64, (D / qsplit + 63) / 64 + 1);
     const int sep = (size_t)D * 128 + (size_t)nslice * 8192 + 4 * 2048 <= 160 * 1024 ? 1 : 0;
