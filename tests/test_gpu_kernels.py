@@ -593,6 +593,9 @@ def test_rank_catalog_matches_full_ranker(dev, B, N, block):
     q = torch.randn(B, 768, device=dev, generator=g).to(torch.bfloat16)
     items = torch.randn(N, 768, device=dev, generator=g).to(torch.bfloat16)
     labels = torch.randint(0, N, (B,), device=dev, generator=g)
+    # exact ties: copies of some label items elsewhere in the catalog (strict ranks ignore them)
+    dup = labels[: min(B, 16)]
+    items[(dup + N // 2) % N] = items[dup]
     full = Ranker([10, 50])(ops.cos_scores(q, items, 20.0), labels)
     got = rank_catalog(q, items, labels, [10, 50], 0.05, block=block)
     assert got[:-1] == full[:-1]
