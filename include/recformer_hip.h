@@ -45,6 +45,11 @@ enum {
 
 const char* rf_last_error(void);
 int rf_abi_version(void);
+/* Diagnostics (A/B tools only, not used by the product path): set a launch-path tuning knob
+ * ("gemm_gn", "gemm_variant", "band_qpb", "band_path", "gfold_path", "gfold_qsplit") for the
+ * process; returns the previous value (INT32_MIN and rf_last_error() for an unknown name). The
+ * compiled defaults are the measured choices; no launch reads the environment. */
+int rf_debug_set_knob(const char* name, int value);
 
 /* A2 — RecformerModel.forward prologue, models.py:306-329 (_merge_to_attention_mask
  * 262-272, _pad_to_window_size 210-260) + create_position_ids_from_input_ids 68-79.

@@ -23,6 +23,7 @@ P = c_void_p
 SIGNATURES = {
     "rf_last_error": (ctypes.c_char_p, []),
     "rf_abi_version": (c_int, []),
+    "rf_debug_set_knob": (c_int, [ctypes.c_char_p, c_int]),
     "rf_prepare_inputs": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                   P, P, P, P, P, P, P]),
     "rf_embed_ln_fwd": (c_int, [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_float,
@@ -95,6 +96,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.argtypes = args
     _LIB = lib
     return lib
+
+
+def set_knob(name: str, value: int) -> int:
+    """Diagnostics (tools/ A/B scripts): set a launch-path tuning knob, return its old value."""
+    old = load().rf_debug_set_knob(name.encode(), int(value))
+    if old == -2 ** 31:
+        raise RecformerHipError(load().rf_last_error().decode(errors="replace"))
+    return old
 
 
 def check(rc: int, what: str) -> None:

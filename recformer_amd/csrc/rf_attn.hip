@@ -1009,11 +1009,11 @@ extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int hal
     RF_REQUIRE(half_w == 32, "rf_band_attn_fwd(bf16): window must be 64 (half 32), got half %d", half_w);
     RF_REQUIRE(Lp % 64 == 0, "rf_band_attn_fwd(bf16): Lp=%d must be a multiple of 64", Lp);
     RF_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0, "rf_band_attn_fwd(bf16): alignment");
-    if (gmax <= 32 && !getenv("RF_BAND_ONESHOT")) {
+    if (gmax <= 32 && g_knob[KNOB_BAND_PATH] != 2) {
       // pipelined: runs of qpb query blocks per workgroup, >= ~3 workgroups per CU slot
       const int nqb = Lp / 64;
       int qpb = nqb >= 16 ? (nqb + 1) / 2 : nqb;
-      if (const char* e = getenv("RF_BAND_QPB")) qpb = max(1, min(nqb, atoi(e)));  // A/B tools
+      if (g_knob[KNOB_BAND_QPB] > 0) qpb = min(nqb, g_knob[KNOB_BAND_QPB]);  // A/B tools
       const int nparts = (nqb + qpb - 1) / qpb;
       const size_t lds = AP_MK + (size_t)(qpb + 1) * 16;
       static bool attr = false;
@@ -1022,7 +1022,7 @@ extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int hal
         attr = true;
       }
       RF_REQUIRE(lds <= 80000, "rf_band_attn_fwd(bf16): Lp=%d too long for the pipelined kernel", Lp);
-      if (getenv("RF_BAND_V1")) {
+      if (g_knob[KNOB_BAND_PATH] == 1) {
         k_band_attn_pipe<<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
                                                            (const bf16*)v, ld_qkv, flags, gidx, gmax,
                                                            (bf16*)out, ld_out);

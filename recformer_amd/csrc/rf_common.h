@@ -39,6 +39,20 @@ void clear_error();
 
 inline hipStream_t as_stream(rf_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---- tuning knobs (A/B tools only) -------------------------------------------------------
+// Launch-path choices measured once and compiled in as defaults; tools/ switch them through
+// rf_debug_set_knob (one host call, no environment lookups on any launch).
+enum Knob {
+  KNOB_GEMM_GN = 0,     // ping-pong GEMM raster: column-group width (4)
+  KNOB_GEMM_VARIANT,    // bf16 GEMM kernel family (5 = ping-pong)
+  KNOB_BAND_QPB,        // band attention query blocks per workgroup (0 = auto)
+  KNOB_BAND_PATH,       // band attention kernel: 0 pipe2, 1 pipe (v1), 2 one-shot
+  KNOB_GFOLD_PATH,      // global fold GEMV/MFMA choice: 0 auto, 1 GEMV, 2 MFMA
+  KNOB_GFOLD_QSPLIT,    // global fold query/key kernel: max column splits (8)
+  KNOB_COUNT
+};
+extern int g_knob[KNOB_COUNT];
+
 // ---- scalar conversions ---------------------------------------------------------------
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }

@@ -51,7 +51,8 @@ template <typename TIN, int EPI, bool CF32, bool RF32>
 __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, float v) {
   if (row >= e.M || col >= e.N) return;
   if (EPI == RF_EPI_COS) {
-    reinterpret_cast<float*>(e.C)[(int64_t)row * e.ldc + col] = v * e.ra[row] * e.rw[col] * e.col_scale;
+    // same association as the vector epilogues (v * (ra * scale) * rw): one score, one rounding
+    reinterpret_cast<float*>(e.C)[(int64_t)row * e.ldc + col] = v * (e.ra[row] * e.col_scale) * e.rw[col];
     return;
   }
   if (EPI != RF_EPI_NONE) v += e.bias[col];
@@ -1010,19 +1011,13 @@ static void launch_bf16(int M, int N, int K, const void* A, int lda, const void*
       K, (const bf16*)A, lda, (const bf16*)W, ldw, e, nTn);
 }
 
-// Variant selector for A/B timing (RF_GEMM_VARIANT): 5 -> 256^2 ping-pong (default), 1 -> 256^2
+// Variant selector for A/B timing (knob gemm_variant): 5 -> 256^2 ping-pong (default), 1 -> 256^2
 // BK64 x2, 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 -> 256x128 / 128^2 tiles.
 static unsigned long long* g_stamps = nullptr;  // set by rf_debug_gemm_stamps (tools only)
 
-static int gemm_gn() {  // measured: 4 beats the full-width raster by ~4% on the FFN1 shape
-  const char* s = getenv("RF_GEMM_GN");
-  return s ? atoi(s) : 4;
-}
+static int gemm_gn() { return g_knob[KNOB_GEMM_GN]; }  // 4 beats the full-width raster by ~4% (FFN1)
 
-static int gemm_variant() {
-  const char* s = getenv("RF_GEMM_VARIANT");  // read per call so A/B tools can switch
-  return s ? atoi(s) : 5;
-}
+static int gemm_variant() { return g_knob[KNOB_GEMM_VARIANT]; }
 
 
 // The ping-pong kernel DMAs its epilogue column vectors (and EPI_COS row norms) as 16-B

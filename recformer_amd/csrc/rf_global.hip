@@ -873,11 +873,10 @@ extern "C" size_t rf_global_fold_workspace(int B, int Lp, int D, int H, int gmax
 // but launch only H * R/64 blocks; qg/u splits u's columns over up to 4 blocks and wins at any
 // R, while for out below a few hundred global rows (one CLS row per 1024-token sequence, C2)
 // the per-row GEMV kernel fills the chip better (tools/gfold_bench.py: C2 R=64 out 14.5 vs
-// 45 us; catalog R=4096 qu+out 970 vs 155 us). RF_GFOLD_PATH=gemv|mfma forces one.
+// 45 us; catalog R=4096 qu+out 970 vs 155 us). Knob gfold_path (1 GEMV, 2 MFMA) forces one.
 static bool gfold_use_mfma(int R, bool qu) {
-  const char* e = getenv("RF_GFOLD_PATH");
-  if (e && e[0] == 'g') return false;
-  if (e && e[0] == 'm') return true;
+  if (g_knob[KNOB_GFOLD_PATH] == 1) return false;
+  if (g_knob[KNOB_GFOLD_PATH] == 2) return true;
   return qu || R >= 256;  // qg/u: MFMA with a column split wins at any R (C2: 20 -> 12.5 us)
 }
 
@@ -997,8 +996,8 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
     RF_REQUIRE(D % 64 == 0 && D <= 1024, "rf_global_attn_fold_h: D=%d", D);
     // few row tiles: split u's columns over more blocks (each recomputes its tile's qg)
     int qsplit = 1;
-    int qmax = 8;  // C2 (R = 64): 8 column splits 51.3 vs 52.9 us for 4 (tools/gfold_bench.py)
-    if (const char* e = getenv("RF_GFOLD_QSPLIT")) qmax = std::max(1, atoi(e));  // A/B tools
+    // C2 (R = 64): 8 column splits 51.3 vs 52.9 us for 4 (tools/gfold_bench.py)
+    const int qmax = std::max(1, g_knob[KNOB_GFOLD_QSPLIT]);
     while (qsplit < qmax && H * ((R + 63) / 64) * qsplit < 32 * qmax && (D / 16) % (2 * qsplit) == 0) qsplit *= 2;
     // Wkg slice: at most ceil(cols / 64) + 1 segments of 8 KiB; its own region when it fits
     const int nslice = std::min(D / 64, (D / qsplit + 63) / 64 + 1);

@@ -5,11 +5,14 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <string.h>
+
 #include "rf_common.h"
 
 namespace rf {
 
 static thread_local char g_err[512];
+int g_knob[KNOB_COUNT] = {4, 5, 0, 0, 0, 8};
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -825,6 +828,19 @@ using namespace rf;
 extern "C" {
 
 const char* rf_last_error(void) { return rf::g_err; }
+
+int rf_debug_set_knob(const char* name, int value) {
+  static const char* names[rf::KNOB_COUNT] = {"gemm_gn", "gemm_variant", "band_qpb", "band_path", "gfold_path",
+                                              "gfold_qsplit"};
+  for (int i = 0; i < rf::KNOB_COUNT; ++i)
+    if (name && strcmp(name, names[i]) == 0) {
+      const int old = rf::g_knob[i];
+      rf::g_knob[i] = value;
+      return old;
+    }
+  rf::set_error("rf_debug_set_knob: unknown knob '%s'", name ? name : "(null)");
+  return INT32_MIN;
+}
 int rf_abi_version(void) { return 1; }
 
 int rf_prepare_inputs(const int64_t* input_ids, const int64_t* attention_mask,

@@ -11,7 +11,7 @@ import torch
 import torch.nn.functional as F
 
 from oracle import restatement as R
-from recformer_amd import ops
+from recformer_amd import _lib, ops
 
 pytestmark = pytest.mark.gpu
 
@@ -426,11 +426,12 @@ def test_global_fold_mfma_matches_gemv(dev, monkeypatch, B, Lp, H):
     bias = [_rand((D,), dev, torch.float32, 0.1, seed=64 + i) for i in range(3)]
     outs = {}
     for path in ("gemv", "mfma"):
-        monkeypatch.setenv("RF_GFOLD_PATH", path)
+        old = _lib.set_knob("gfold_path", 1 if path == "gemv" else 2)
         ctx = torch.zeros(B * Lp, D, dtype=dt, device=dev)
         ops.global_attention_fold_h(h, w[0], bias[0], 0.125, w[1], bias[1], w[2], bias[2], flags, gidx, B, Lp, H,
                                     ctx)
         torch.cuda.synchronize()
+        _lib.set_knob("gfold_path", old)
         outs[path] = ctx.float()
     err = (outs["gemv"] - outs["mfma"]).abs().max().item()
     assert err <= 2e-2, err
@@ -457,6 +458,48 @@ def test_ranker_matches_reference_formula(dev, N):
     for g, r in zip(got[:-1], ref[:-1]):
         assert abs(g - r) <= 1e-6, (got, ref)
     assert abs(got[-1] - ref[-1]) <= 1e-5 * max(1.0, abs(ref[-1]))
+
+
+@pytest.mark.parametrize("case", ["ties", "masked", "cosine"])
+def test_ranker_matches_reference_fixture(dev, case):
+    """Ranker on the device vs the real Ranker's outputs (tests/golden/ranker.npz made by
+    oracle/gen_golden_ranker.py from utils.py:76-108): exact ranks, ties, -MAX_VAL, B = 37."""
+    from recformer_amd import Ranker
+    from recformer_amd.ranker import rank_counts
+    from tests.common import load_golden
+    g = load_golden("ranker")
+    ks = [int(k) for k in g["ks"]]
+    s, lab = g[f"{case}_scores"], g[f"{case}_labels"]
+    gt, valid = rank_counts(s.to(dev), lab.to(dev))
+    assert torch.equal(gt.cpu().long(), g[f"{case}_rank"].long())
+    assert torch.equal(valid.cpu().long(), g[f"{case}_valid"].long())
+    got = Ranker(ks)(s.to(dev), lab.to(dev))
+    ref = g[f"{case}_metrics"].tolist()
+    for a, b in zip(got[:-1], ref[:-1]):
+        assert a == pytest.approx(b, abs=1e-6)
+    assert got[-1] == pytest.approx(ref[-1], rel=1e-5)
+
+
+@pytest.mark.parametrize("B,N,block", [(37, 1000, 1000), (37, 5003, 2048)])
+def test_rank_catalog_matches_restated_ranker(dev, B, N, block):
+    """rank_catalog against utils.py:76-108 restated (oracle, pinned by tests/golden/ranker.npz)
+    on the same fp32 cosine-score matrix: B not a multiple of 16, ragged column tails, every third
+    label in the last partial 16 columns of the catalog (or of a block), exact duplicate items."""
+    from recformer_amd.ranker import rank_catalog
+    g = torch.Generator(device=dev).manual_seed(B * N)
+    q = torch.randn(B, 768, device=dev, generator=g).to(torch.bfloat16)
+    items = torch.randn(N, 768, device=dev, generator=g).to(torch.bfloat16)
+    labels = torch.randint(0, N, (B,), device=dev, generator=g)
+    labels[::3] = N - 1 - torch.arange(len(labels[::3]), device=dev) % 8
+    labels[1::3] = (block - 1 - torch.arange(len(labels[1::3]), device=dev) % 8) % N
+    dup = labels[:8]
+    items[(dup + N // 2) % N] = items[dup]
+    s = ops.cos_scores(q, items, 20.0).cpu()
+    ref = R.ranker_metrics(s, labels.cpu(), [1, 10, 50])
+    got = rank_catalog(q, items, labels, [1, 10, 50], 0.05, block=block)
+    for a, b in zip(got[:-1], ref[:-1]):
+        assert a == pytest.approx(b, abs=1e-6), (got, ref)
+    assert got[-1] == pytest.approx(ref[-1], rel=1e-4)
 
 
 @pytest.mark.parametrize("M,D", [(333, 768), (64, 128), (1000, 1024)])

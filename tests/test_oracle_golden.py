@@ -65,3 +65,17 @@ def test_pretrain_two_views_mlm():
     assert int(correct) == int(g["cl_correct_num"])
     loss0, _, _ = R.pretrain_forward(sd_lf, sd_head, cfg, va, vb)
     assert abs(float(loss0) - float(g["loss_contrastive"])) <= 1e-5
+
+
+@pytest.mark.parametrize("case", ["ties", "masked", "cosine"])
+def test_ranker_restatement_matches_reference(case):
+    """utils.py:76-108 restated (oracle.restatement.ranker_metrics) vs the real Ranker's outputs
+    (tests/golden/ranker.npz, oracle/gen_golden_ranker.py): ties, -MAX_VAL entries, B = 37."""
+    g = load_golden("ranker")
+    ks = [int(k) for k in g["ks"]]
+    got = R.ranker_metrics(g[f"{case}_scores"].clone(), g[f"{case}_labels"].clone(), ks)
+    ref = g[f"{case}_metrics"].tolist()
+    assert len(got) == len(ref)
+    for a, b in zip(got[:-1], ref[:-1]):
+        assert a == pytest.approx(b, abs=1e-7)
+    assert got[-1] == pytest.approx(ref[-1], rel=1e-6)

@@ -1,4 +1,4 @@
-"""Band attention: query blocks per workgroup (RF_BAND_QPB) sweep at C2, one process.
+"""Band attention: query blocks per workgroup (knob band_qpb) sweep at C2, one process.
     python tools/band_qpb.py"""
 import os
 import sys
@@ -7,6 +7,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from recformer_amd import ops  # noqa: E402
+from recformer_amd._lib import set_knob  # noqa: E402
 from tools.kbench import timeit  # noqa: E402
 
 
@@ -22,7 +23,7 @@ def main():
     ref = None
     for rep in range(2):
         for qpb in (2, 4, 8, 16):
-            os.environ["RF_BAND_QPB"] = str(qpb)
+            set_knob("band_qpb", qpb)
             out = ops.band_attention(q, k, v, flags, gidx, B, L, H, 32)
             if ref is None:
                 ref = out.clone()

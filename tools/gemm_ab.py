@@ -1,4 +1,4 @@
-"""A/B the bf16 GEMM variants (RF_GEMM_VARIANT) on the layer's shapes: correctness vs an fp32
+"""A/B the bf16 GEMM variants (knob gemm_variant) on the layer's shapes: correctness vs an fp32
 torch reference, then time per variant and hipBLASLt (torch.matmul, no epilogue).
 
     python tools/gemm_ab.py [variants, default 1,5]
@@ -10,6 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from recformer_amd import ops  # noqa: E402
+from recformer_amd._lib import set_knob  # noqa: E402
 
 
 def timeit(fn, iters=20, warm=3):
@@ -36,7 +37,7 @@ def main():
         b = torch.randn(N, device=dev)
         ref = a.float() @ w.float().t() + b
         for v in variants:
-            os.environ["RF_GEMM_VARIANT"] = str(v)
+            set_knob("gemm_variant", v)
             out = ops.gemm(a, w, b, ops.RF_EPI_BIAS, out_f32=True)
             err = (out - ref).abs().max().item()
             print(f"check v{v} M={M} N={N} K={K}: max err {err:.3e}", flush=True)
@@ -52,7 +53,7 @@ def main():
         fl = 2 * M * N * K
         line = f"{name:5s} N={N} K={K}:"
         for v in variants:
-            os.environ["RF_GEMM_VARIANT"] = str(v)
+            set_knob("gemm_variant", v)
             t = timeit(lambda: ops.gemm(a, w, b, epi, resid=r, out_f32=f32))
             line += f"  v{v} {t*1e6:7.1f}us {fl/t/1e12:6.0f}TF"
         tt = timeit(lambda: torch.matmul(a, w.t()))

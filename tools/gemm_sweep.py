@@ -7,12 +7,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from recformer_amd import ops  # noqa: E402
+from recformer_amd._lib import set_knob  # noqa: E402
 from tools.gemm_ab import timeit  # noqa: E402
 
 
 def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 3072
-    os.environ["RF_GEMM_VARIANT"] = sys.argv[2] if len(sys.argv) > 2 else "5"
+    set_knob("gemm_variant", int(sys.argv[2]) if len(sys.argv) > 2 else 5)
     epi = int(sys.argv[3]) if len(sys.argv) > 3 else ops.RF_EPI_BIAS
     M = 65536
     dev = torch.device("cuda")

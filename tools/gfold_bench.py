@@ -13,6 +13,10 @@ import torch  # noqa: E402
 from recformer_amd import ops  # noqa: E402
 from tools.kbench import timeit  # noqa: E402
 
+if os.environ.get("RF_GFOLD_GEMV"):  # tools/gpu/gf.sh: force the GEMV fold kernels
+    from recformer_amd._lib import set_knob
+    set_knob("gfold_path", 1)
+
 
 def main():
     dev = torch.device("cuda")

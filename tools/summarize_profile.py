@@ -63,13 +63,16 @@ def load_dispatches(pattern):
 def main():
     out = sys.argv[1]
     jpath = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else os.path.join(out, "summary.json")
-    per = collections.defaultdict(lambda: {"calls": 0, "dur_ns": 0.0, "FETCH_SIZE": [], "WRITE_SIZE": []})
+    per = collections.defaultdict(lambda: {"calls": 0, "dur_ns": 0.0, "durs": [], "FETCH_SIZE": [], "WRITE_SIZE": [],
+                                           "SQ_VALU_MFMA_BUSY_CYCLES": [], "GRBM_GUI_ACTIVE": [],
+                                           "SQ_BUSY_CYCLES": []})
     tag = tagger()
     for r in load_dispatches(os.path.join(out, "trace", "**", "*kernel_trace.csv")):
         t = tag(r["Kernel_Name"], int(r.get("Grid_Size", 0) or 0))
         per[t]["calls"] += 1
         per[t]["dur_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    for kind in ("fetch", "write"):
+        per[t]["durs"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for kind in ("fetch", "write", "mfma"):
         tag = tagger()
         for r in load_dispatches(os.path.join(out, kind, "**", "*counter_collection.csv")):
             t = tag(r["Kernel_Name"], int(r["Grid_Size"]))
@@ -82,20 +85,33 @@ def main():
         f, w = v["FETCH_SIZE"], v["WRITE_SIZE"]
         rb = 2 * 1024 * sum(f) / len(f) if f else None
         wb = 1024 * sum(w) / len(w) if w else None
+        # MFMA busy: SQ_VALU_MFMA_BUSY_CYCLES (per-SIMD busy cycles, summed over the chip) over the
+        # SIMD-cycles of the dispatch: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 x 256 CUs x 4 SIMDs
+        mb, ga = v["SQ_VALU_MFMA_BUSY_CYCLES"], v["GRBM_GUI_ACTIVE"]
+        busy = None
+        if mb and ga and len(mb) == len(ga):
+            busy = round(sum(mb) / (sum(ga) / 8 * 256 * 4), 4)
+        d = sorted(v["durs"])
         res[t] = {"calls": v["calls"], "avg_us": round(v["dur_ns"] / v["calls"] / 1e3, 2),
+                  "median_us": round(d[len(d) // 2] / 1e3, 2), "mfma_busy": busy,
+                  "clock_ghz": round(sum(ga) / 8 / len(ga) / (sum(d) / len(d)), 3) if ga and d else None,
                   "share": round(v["dur_ns"] / total, 4),
                   "hbm_read_bytes": rb, "hbm_write_bytes": wb,
                   "hbm_bytes": (rb + wb) if rb is not None and wb is not None else None}
-    print(f"{'tag':24s} {'calls':>6s} {'avg_us':>9s} {'share':>6s} {'HBM MB/launch':>14s} {'GB/s':>7s}")
+    print(f"{'tag':24s} {'calls':>6s} {'avg_us':>9s} {'med_us':>9s} {'share':>6s} {'HBM MB/launch':>14s} "
+          f"{'GB/s':>7s} {'MFMA busy':>9s}")
     for t, r in sorted(res.items(), key=lambda kv: -kv[1]["share"]):
         hb = r["hbm_bytes"]
-        print(f"{t:24s} {r['calls']:6d} {r['avg_us']:9.1f} {100 * r['share']:6.2f} "
-              f"{hb / 1e6 if hb else float('nan'):14.1f} {hb / r['avg_us'] / 1e3 if hb else float('nan'):7.0f}")
+        mb = r["mfma_busy"]
+        print(f"{t:24s} {r['calls']:6d} {r['avg_us']:9.1f} {r['median_us']:9.1f} {100 * r['share']:6.2f} "
+              f"{hb / 1e6 if hb else float('nan'):14.1f} {hb / r['median_us'] / 1e3 if hb else float('nan'):7.0f} "
+              f"{mb if mb is not None else float('nan'):9.3f}")
     cfg = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "64,1024,12"
     B, L, layers = (int(x) for x in cfg.split(","))
     json.dump({"config": {"batch": B, "seq_len": L, "layers": layers},
-               "source": "rocprofv3 --kernel-trace --stats, then --pmc FETCH_SIZE and --pmc WRITE_SIZE "
-                         "in separate passes; hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB",
+               "source": "rocprofv3 --kernel-trace --stats, then --pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc "
+                         "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES in separate passes; "
+                         "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB; mfma_busy = MFMA_BUSY / (GRBM_GUI_ACTIVE/8 * 1024)",
                "tags": res}, open(jpath, "w"), indent=1, sort_keys=True)
 
 
