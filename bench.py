@@ -48,8 +48,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0,
                     help="target CPU work for the baseline samples, split over the thread counts (0 disables)")
     ap.add_argument("--cpu-threads", type=str, default="all,omp",
-                    help="thread counts for the CPU baseline: 'all' = every CPU this process may run on "
-                         "(os.sched_getaffinity), 'omp' = OMP_NUM_THREADS (the box's CPU share), or integers")
+                    help="thread counts for the CPU baseline: 'all' = every CPU this process may use "
+                         "(affinity capped by the cgroup CPU quota), 'omp' = OMP_NUM_THREADS, or integers")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--timing-steps", type=int, default=20,
                     help="steps of the separate HIP-event-instrumented pass (per-kernel times)")
@@ -92,11 +92,37 @@ def _cpu_model_name():
     return platform.processor() or "cpu"
 
 
-def _thread_counts(spec):
+def _cpu_quota():
+    """CPUs this process may use: the affinity set, capped by the cgroup's CPU quota (cgroup v2
+    cpu.max or v1 cfs_quota_us). On the GPU box os.cpu_count() shows the whole machine while the
+    quota is the per-GPU share; threads beyond the quota only contend."""
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        avail = max(1, min(avail, math.ceil(quota)))
+    return avail
+
+
+def _thread_counts(spec):
+    avail = _cpu_quota()
     out = []
     for tok in spec.split(","):
         tok = tok.strip()
@@ -121,6 +147,24 @@ def cpu_baseline(sd_cpu, cfg, items_cpu, L, target_s, spec):
     from recformer_amd.synth import synth_batch
 
     counts, avail = _thread_counts(spec)
+    if len(counts) > 1:
+        # thread counts past the CPUs really available (an unreported quota) only contend: probe
+        # each with a small fp32 GEMM and drop those slower than the best probe
+        x = torch.randn(512, 768)
+        w = torch.randn(768, 3072)
+        probe = {}
+        for T in counts:
+            torch.set_num_threads(T)
+            torch.mm(x, w)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                torch.mm(x, w)
+            probe[T] = time.perf_counter() - t0
+        best_p = min(probe.values())
+        skipped = {str(T): f"GEMM probe {probe[T] / best_p:.1f}x slower" for T in counts if probe[T] > 1.5 * best_p}
+        counts = [T for T in counts if probe[T] <= 1.5 * best_p]
+    else:
+        skipped = {}
     per = target_s / len(counts)
     b1 = synth_batch(1, L, cfg.vocab_size, seed=1234, item_len=21)
     bs = synth_batch(64, L, cfg.vocab_size, seed=4321, item_len=21)
@@ -141,10 +185,10 @@ def cpu_baseline(sd_cpu, cfg, items_cpu, L, target_s, spec):
         samples[T] = n
     best = max(by, key=by.get)
     return {"value": by[best], "unit": "user-seq/s", "cores": best, "kind": "port",
-            "by_threads": {str(t): round(v, 3) for t, v in by.items()},
+            "by_threads": {str(t): round(v, 3) for t, v in by.items()}, "skipped_threads": skipped,
             "sample": f"{samples[best]} sequences x L={L} (B=1 each) encode+score vs {items_cpu.shape[0]} items, "
                       f"fp32 oracle/restatement.py, {best} threads (fastest of {counts}) on {_cpu_model_name()} "
-                      f"(os.cpu_count()={os.cpu_count()}, affinity {avail} CPUs)"}
+                      f"(os.cpu_count()={os.cpu_count()}; {avail} usable: affinity capped by the cgroup CPU quota)"}
 
 
 def _free_port():
