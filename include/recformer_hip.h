@@ -177,6 +177,15 @@ int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int half_w, const 
 
 
 
+/* Training form with attention-probability dropout (TF:585-586, nn.functional.dropout on the
+ * softmax probabilities, p_drop in [0, 1)): the probabilities entering P.V are multiplied by a keep
+ * mask / (1 - p_drop); the mask is a counter hash of (seed, ((b*H + h)*Lp + i)*Lp + j) for query i
+ * and key j (never stored; rf_band_attn_bwd_drop regenerates it). p_drop = 0: rf_band_attn_fwd. */
+int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
+                          const void* k, const void* v, int ld_qkv, const uint8_t* flags,
+                          const int32_t* gidx, int gmax, void* out, int ld_out, float p_drop,
+                          uint64_t seed, rf_stream_t stream);
+
 /* Backward of the local branch (A5/A9: gradient of LongformerSelfAttention's sliding-window
  * attention TF:482-604 incl. its global-key columns TF:898-962), bf16 q/k/v/o/dout (q
  * pre-scaled, as the forward), fp32 gradients (B*Lp, ld_grad) dq, dk, dv. Workspace outputs:
@@ -196,6 +205,14 @@ int rf_band_attn_bwd_dt(int grad_dtype, int B, int Lp, int H, int hd, int half_w
                         const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx,
                         int gmax, void* dq, void* dk, void* dv, int ld_grad, float* lse2,
                         float* delta, float* gds, float* gpr, rf_stream_t stream);
+/* rf_band_attn_bwd_dt for a forward run with attention-probability dropout (same p_drop, seed):
+ * dP = mask/(1-p) o dO V^T, dS = P o (dP - dO.O); gpr holds the dropped probabilities. */
+int rf_band_attn_bwd_drop(int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
+                          const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
+                          const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx,
+                          int gmax, void* dq, void* dk, void* dv, int ld_grad, float* lse2,
+                          float* delta, float* gds, float* gpr, float p_drop, uint64_t seed,
+                          rf_stream_t stream);
 /* A6 — global query rows, _compute_global_attn_output_from_hidden TF:964-1057 + the
  * overwrite TF:612-629: for every (b, g < count_b): ctx[gidx[b,g], h] =
  * softmax(qg[b*gmax+g, h] . kg[b, :, h]^T over valid keys) . vg[b, :, h]. */

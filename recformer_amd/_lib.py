@@ -56,6 +56,10 @@ SIGNATURES = {
                                  P, P, c_int, P, P, P, c_int, P, P, P, P, P]),
     "rf_band_attn_bwd_dt": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, c_int, P, c_int,
                                     P, P, c_int, P, P, P, c_int, P, P, P, P, P]),
+    "rf_band_attn_fwd_drop": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
+                                      c_int, P, c_int, c_float, ctypes.c_uint64, P]),
+    "rf_band_attn_bwd_drop": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, c_int, P,
+                                      c_int, P, P, c_int, P, P, P, c_int, P, P, P, P, c_float, ctypes.c_uint64, P]),
     "rf_global_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P,
                                    P, c_int, P, c_int, P]),
     "rf_global_fold_workspace": (ctypes.c_size_t, [c_int, c_int, c_int, c_int, c_int]),

@@ -595,12 +595,15 @@ __device__ __forceinline__ float mask_score(unsigned int bits, int bit, float sv
 #else
 #define BAND_GLDS glds16_nt
 #endif
+// DROP (training): attention-probability dropout (TF:585-586) on the probabilities that enter
+// P.V; the normaliser is the undropped row sum, as softmax-then-dropout.
+template <bool DROP>
 __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb, const bf16* __restrict__ q,
                                                           const bf16* __restrict__ k,
                                                           const bf16* __restrict__ v, int ld,
                                                           const uint8_t* __restrict__ flags,
                                                           const int32_t* __restrict__ gidx, int gmax,
-                                                          bf16* __restrict__ out, int ldo) {
+                                                          bf16* __restrict__ out, int ldo, AttnDrop dr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
   const int nparts = (nqb + qpb - 1) / qpb;
@@ -785,13 +788,17 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
     f32x4 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // dropout mask row of this lane's query (b, h, i0 + 16 wave + li); keys are absolute positions
+    const uint64_t drow = DROP ? ((uint64_t)bh * Lp + i0 + 16 * wave + li) : 0;
 #pragma unroll
     for (int s2 = 0; s2 < 3; ++s2) {
       bf16x8 pf;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int t = 2 * s2 + (j >> 2);
-        pf[j] = (bf16)(t < 5 ? st[t < 5 ? t : 4][j & 3] : 0.f);
+        float pv = t < 5 ? st[t < 5 ? t : 4][j & 3] : 0.f;
+        if (DROP && t < 5) pv *= attn_keep_scale(dr, drow, Lp, i0 - 32 + 16 * wave + 16 * t + 4 * g + (j & 3));
+        pf[j] = (bf16)pv;
       }
       const int ga = 16 * wave + 32 * s2, gb = s2 < 2 ? ga + 16 : ga;  // finite rows for p = 0
       const uint32_t va = lds0 + (ga >= 64 ? sb1 : sb0) + 8192 + (ga & 63) * 128;
@@ -814,7 +821,14 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
     if (gt > 0) {
       bf16x8 pf;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pf[j] = (bf16)sg[j >> 2][j & 3];
+      for (int j = 0; j < 8; ++j) {
+        float pv = sg[j >> 2][j & 3];
+        if (DROP) {
+          const int gk = gp[16 * (j >> 2) + 4 * g + (j & 3)];
+          pv *= gk >= 0 ? attn_keep_scale(dr, drow, Lp, gk) : 0.f;
+        }
+        pf[j] = (bf16)pv;
+      }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vgf[dt], pf, o[dt], 0, 0, 0);
     }
@@ -866,10 +880,11 @@ __global__ void __launch_bounds__(256) k_band_attn_valu(int Lp, int half_w, cons
                                                          const T* __restrict__ v, int ld,
                                                          const uint8_t* __restrict__ flags,
                                                          const int32_t* __restrict__ gidx,
-                                                         int gmax, T* __restrict__ out, int ldo) {
+                                                         int gmax, T* __restrict__ out, int ldo, AttnDrop dr) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int h = blockIdx.y, b = blockIdx.z;
+  const uint64_t drow = ((uint64_t)b * gridDim.y + h) * Lp + i;  // dropout mask row (TF:585-586)
   if (i >= Lp) return;
   const int64_t rb = (int64_t)b * Lp;
   const int hoff = h * 64;
@@ -916,6 +931,7 @@ __global__ void __launch_bounds__(256) k_band_attn_valu(int Lp, int half_w, cons
       p = expf(s - mu);
     }
     lsum += wave_sum(p);
+    if (dr.thresh && kp >= 0) p *= attn_keep_scale(dr, drow, Lp, kp);  // after the normaliser's sum
     const int n = min(64, ntot - j0);
     for (int jj = 0; jj < n; ++jj) {
       const float pj = __shfl(p, jj, 64);
@@ -995,10 +1011,25 @@ __global__ void __launch_bounds__(256) k_global_attn(int Lp, const T* __restrict
 
 using namespace rf;
 
+extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, int half_w,
+                                     const void* q, const void* k, const void* v, int ld_qkv,
+                                     const uint8_t* flags, const int32_t* gidx, int gmax, void* out,
+                                     int ld_out, float p_drop, uint64_t seed, rf_stream_t stream);
+
 extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int half_w,
                                 const void* q, const void* k, const void* v, int ld_qkv,
                                 const uint8_t* flags, const int32_t* gidx, int gmax, void* out,
                                 int ld_out, rf_stream_t stream) {
+  return rf_band_attn_fwd_drop(dtype, B, Lp, H, hd, half_w, q, k, v, ld_qkv, flags, gidx, gmax, out, ld_out, 0.f,
+                               0, stream);
+}
+
+extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, int half_w,
+                                     const void* q, const void* k, const void* v, int ld_qkv,
+                                     const uint8_t* flags, const int32_t* gidx, int gmax, void* out,
+                                     int ld_out, float p_drop, uint64_t seed, rf_stream_t stream) {
+  RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_band_attn_fwd: dropout p=%g outside [0, 1)", p_drop);
+  const AttnDrop dr{seed, drop_thresh(p_drop), 1.0f / (1.0f - p_drop)};
   RF_REQUIRE(hd == 64, "rf_band_attn_fwd: head_dim must be 64 (got %d)", hd);
   RF_REQUIRE(B >= 0 && H > 0 && Lp >= 0 && gmax >= 0, "rf_band_attn_fwd: bad shape");
   RF_REQUIRE(ld_qkv >= H * hd && ld_out >= H * hd, "rf_band_attn_fwd: bad leading dims");
@@ -1009,7 +1040,8 @@ extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int hal
     RF_REQUIRE(half_w == 32, "rf_band_attn_fwd(bf16): window must be 64 (half 32), got half %d", half_w);
     RF_REQUIRE(Lp % 64 == 0, "rf_band_attn_fwd(bf16): Lp=%d must be a multiple of 64", Lp);
     RF_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0, "rf_band_attn_fwd(bf16): alignment");
-    if (gmax <= 32 && g_knob[KNOB_BAND_PATH] != 2) {
+    RF_REQUIRE(dr.thresh == 0 || gmax <= 32, "rf_band_attn_fwd(bf16): dropout needs gmax <= 32 (got %d)", gmax);
+    if (gmax <= 32 && (g_knob[KNOB_BAND_PATH] != 2 || dr.thresh)) {
       // pipelined: runs of qpb query blocks per workgroup, >= ~3 workgroups per CU slot
       const int nqb = Lp / 64;
       int qpb = nqb >= 16 ? (nqb + 1) / 2 : nqb;
@@ -1022,20 +1054,27 @@ extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int hal
         attr = true;
       }
       RF_REQUIRE(lds <= 80000, "rf_band_attn_fwd(bf16): Lp=%d too long for the pipelined kernel", Lp);
-      if (g_knob[KNOB_BAND_PATH] == 1) {
+      if (g_knob[KNOB_BAND_PATH] == 1 && dr.thresh == 0) {
         k_band_attn_pipe<<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
                                                            (const bf16*)v, ld_qkv, flags, gidx, gmax,
                                                            (bf16*)out, ld_out);
       } else {
         static bool attr2 = false;
         if (!attr2) {
-          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2, hipFuncAttributeMaxDynamicSharedMemorySize,
+          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    80000);
+          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     80000);
           attr2 = true;
         }
-        k_band_attn_pipe2<<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
-                                                            (const bf16*)v, ld_qkv, flags, gidx, gmax,
-                                                            (bf16*)out, ld_out);
+        if (dr.thresh)
+          k_band_attn_pipe2<true><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
+                                                                   (const bf16*)v, ld_qkv, flags, gidx, gmax,
+                                                                   (bf16*)out, ld_out, dr);
+        else
+          k_band_attn_pipe2<false><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
+                                                                    (const bf16*)v, ld_qkv, flags, gidx, gmax,
+                                                                    (bf16*)out, ld_out, dr);
       }
     } else {
       k_band_attn_bf16<<<(Lp / 64) * H * B, 256, 0, s>>>(Lp, (const bf16*)q, (const bf16*)k, (const bf16*)v,
@@ -1046,7 +1085,7 @@ extern "C" int rf_band_attn_fwd(int dtype, int B, int Lp, int H, int hd, int hal
     dim3 grid((Lp + 3) / 4, H, B);
     k_band_attn_valu<float><<<grid, 256, 0, s>>>(Lp, half_w, (const float*)q, (const float*)k,
                                                  (const float*)v, ld_qkv, flags, gidx, gmax,
-                                                 (float*)out, ld_out);
+                                                 (float*)out, ld_out, dr);
   } else {
     RF_REQUIRE(false, "rf_band_attn_fwd: bad dtype %d", dtype);
   }

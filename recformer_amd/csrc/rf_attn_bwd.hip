@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* _
                                                      const int32_t* __restrict__ gidx, int gmax,
                                                      GT* __restrict__ dq, int lddq, float* __restrict__ lse2,
                                                      float* __restrict__ delta, float* __restrict__ gds,
-                                                     float* __restrict__ gpr) {
+                                                     float* __restrict__ gpr, AttnDrop dr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -221,20 +221,29 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* _
   l += __shfl_xor(l, 32, 64);
   const bool live = qv && l > 0.f;
   const float il = live ? 1.0f / l : 0.f;
-  // P and dS = P (dP - delta)
+  // P and dS = P (dP - delta); with attention dropout (TF:585-586) the forward used P o Z (Z the
+  // regenerated keep mask times 1/(1-p)), so dP = Z o (dO V^T) and delta = dO . O is unchanged
+  const uint64_t drow = ((uint64_t)b * H + h) * Lp + myq;
 #pragma unroll
   for (int t = 0; t < 5; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       st[t][r] *= il;
-      dp[t][r] = st[t][r] * (dp[t][r] - dl);
+      const float z = dr.thresh ? attn_keep_scale(dr, drow, Lp, i0 - 32 + 16 * wave + 16 * t + 4 * g + r) : 1.f;
+      dp[t][r] = st[t][r] * (z * dp[t][r] - dl);
     }
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       sg[t][r] *= il;
-      dg[t][r] = sg[t][r] * (dg[t][r] - dl);
+      float z = 1.f;
+      if (dr.thresh) {
+        const int gk = gp[16 * t + 4 * g + r];
+        z = gk >= 0 ? attn_keep_scale(dr, drow, Lp, gk) : 0.f;
+      }
+      dg[t][r] = sg[t][r] * (z * dg[t][r] - dl);
+      sg[t][r] *= z;  // gpr: the dropped probabilities (dv of the global-key columns)
     }
   // dq^T[dim][query] = K^T dS^T over 3 key steps of 32 (the last pairs tile 4 with zeros) + globals
   f32x4 acc[4];
@@ -304,7 +313,7 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
                                                       const uint8_t* __restrict__ flags,
                                                       const float* __restrict__ lse2,
                                                       const float* __restrict__ delta, GT* __restrict__ dk,
-                                                      GT* __restrict__ dv, int lddkv) {
+                                                      GT* __restrict__ dv, int lddkv, AttnDrop dr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -375,8 +384,13 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
     for (int r = 0; r < 4; ++r) {
       const bool ok = (bw[t >> 1] >> (16 * (t & 1) + r)) & 1u;
       const float p = ok ? __builtin_amdgcn_exp2f(fmaf(st[t][r], BW_LOG2E, -lq[r])) : 0.f;
-      st[t][r] = p;
-      dp[t][r] = p * (dp[t][r] - dq4[r]);
+      // dropout (TF:585-586): dv from P o Z, dS = P (Z dP' - delta); query row j0 - 32 + 16 w + 16 t + 4 g + r
+      const float z = (dr.thresh && ok)
+                          ? attn_keep_scale(dr, ((uint64_t)b * H + h) * Lp + (j0 - 32 + 16 * wave + 16 * t + 4 * g + r),
+                                            Lp, myk)
+                          : 1.f;
+      st[t][r] = p * z;
+      dp[t][r] = p * (z * dp[t][r] - dq4[r]);
     }
   }
   // dv^T[dim][key] = dO^T P, dk^T[dim][key] = Q^T dS over 3 query steps of 32
@@ -423,7 +437,7 @@ template <typename GT>
 static void launch_band_bwd(int B, int Lp, int H, const void* q, const void* k, const void* v, int ld_qkv,
                             const void* o, int ld_o, const void* dout, int ld_do, const uint8_t* flags,
                             const int32_t* gidx, int gmax, GT* dq, GT* dk, GT* dv, int ld_grad, float* lse2,
-                            float* delta, float* gds, float* gpr, hipStream_t s) {
+                            float* delta, float* gds, float* gpr, const AttnDrop& dr, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_band_bwd_q<GT>, hipFuncAttributeMaxDynamicSharedMemorySize, BQ_LDS);
@@ -433,16 +447,18 @@ static void launch_band_bwd(int B, int Lp, int H, const void* q, const void* k, 
   const int nblk = (Lp / 64) * H * B;
   k_band_bwd_q<GT><<<nblk, 256, BQ_LDS, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
                                              (const bf16*)o, ld_o, (const bf16*)dout, ld_do, flags, gidx, gmax, dq,
-                                             ld_grad, lse2, delta, gds, gpr);
+                                             ld_grad, lse2, delta, gds, gpr, dr);
   k_band_bwd_kv<GT><<<nblk, 256, BK_LDS, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
-                                              (const bf16*)dout, ld_do, flags, lse2, delta, dk, dv, ld_grad);
+                                              (const bf16*)dout, ld_do, flags, lse2, delta, dk, dv, ld_grad, dr);
 }
 
-extern "C" int rf_band_attn_bwd_dt(int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
-                                   const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
-                                   const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx, int gmax,
-                                   void* dq, void* dk, void* dv, int ld_grad, float* lse2, float* delta, float* gds,
-                                   float* gpr, rf_stream_t stream) {
+extern "C" int rf_band_attn_bwd_drop(int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
+                                     const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
+                                     const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx,
+                                     int gmax, void* dq, void* dk, void* dv, int ld_grad, float* lse2, float* delta,
+                                     float* gds, float* gpr, float p_drop, uint64_t seed, rf_stream_t stream) {
+  RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_band_attn_bwd: dropout p=%g outside [0, 1)", p_drop);
+  const AttnDrop dr{seed, drop_thresh(p_drop), 1.0f / (1.0f - p_drop)};
   RF_REQUIRE(grad_dtype == RF_F32 || grad_dtype == RF_BF16, "rf_band_attn_bwd: bad gradient dtype %d", grad_dtype);
   RF_REQUIRE(hd == 64 && half_w == 32, "rf_band_attn_bwd: head_dim 64 and window 64 only (got %d, %d)", hd,
              2 * half_w);
@@ -457,11 +473,20 @@ extern "C" int rf_band_attn_bwd_dt(int grad_dtype, int B, int Lp, int H, int hd,
   hipStream_t s = as_stream(stream);
   if (grad_dtype == RF_BF16)
     launch_band_bwd<bf16>(B, Lp, H, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx, gmax, (bf16*)dq, (bf16*)dk,
-                          (bf16*)dv, ld_grad, lse2, delta, gds, gpr, s);
+                          (bf16*)dv, ld_grad, lse2, delta, gds, gpr, dr, s);
   else
     launch_band_bwd<float>(B, Lp, H, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx, gmax, (float*)dq,
-                           (float*)dk, (float*)dv, ld_grad, lse2, delta, gds, gpr, s);
+                           (float*)dk, (float*)dv, ld_grad, lse2, delta, gds, gpr, dr, s);
   RF_LAUNCH_CHECK("rf_band_attn_bwd");
+}
+
+extern "C" int rf_band_attn_bwd_dt(int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
+                                   const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
+                                   const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx, int gmax,
+                                   void* dq, void* dk, void* dv, int ld_grad, float* lse2, float* delta, float* gds,
+                                   float* gpr, rf_stream_t stream) {
+  return rf_band_attn_bwd_drop(grad_dtype, B, Lp, H, hd, half_w, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx,
+                               gmax, dq, dk, dv, ld_grad, lse2, delta, gds, gpr, 0.f, 0, stream);
 }
 
 extern "C" int rf_band_attn_bwd(int B, int Lp, int H, int hd, int half_w, const void* q, const void* k,

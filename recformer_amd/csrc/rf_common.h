@@ -115,6 +115,34 @@ __device__ __forceinline__ float join_f32(uint32_t hi, uint32_t lo) {
   return __uint_as_float(((hi - (lo >> 15)) << 16) | lo);
 }
 
+// ---- dropout keep masks (training path) ------------------------------------------------------
+// Counter hash of (seed, element index): regenerated by each backward, never stored. P(keep) =
+// 1 - thresh / 2^32 with thresh = drop_thresh(p); kept values are scaled by 1 / (1 - p)
+// (nn.functional.dropout). recformer_amd/dropout.py restates it bit-exactly in torch.
+__host__ __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  uint32_t h = (uint32_t)idx * 0x9E3779B1u ^ (uint32_t)(idx >> 32) * 0x85EBCA77u ^ (uint32_t)seed;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= (uint32_t)(seed >> 32);
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h >= thresh;
+}
+inline uint32_t drop_thresh(float p) {
+  return p <= 0.f ? 0u : (p >= 1.f ? 0xFFFFFFFFu : (uint32_t)((double)p * 4294967296.0));
+}
+// Attention-probability dropout (TF:585-586 local rows, TF:1036-1037 global rows): one mask entry
+// per (sequence b, head h, query position i, key position j), index ((b H + h) Lp + i) Lp + j.
+struct AttnDrop {
+  uint64_t seed;
+  uint32_t thresh;  // 0: off
+  float scale;      // 1 / (1 - p)
+};
+__device__ __forceinline__ float attn_keep_scale(const AttnDrop& d, uint64_t row, int Lp, int key) {
+  return drop_keep(d.seed, row * (uint64_t)Lp + (uint64_t)key, d.thresh) ? d.scale : 0.f;
+}
+
 // Bijective XCD-aware remap of a 1-D block id (guide §5 T1): the hardware deals block ids
 // round-robin over the 8 XCDs; the returned index is contiguous per XCD, so blocks that share
 // data (neighbouring tiles, windows) run on one XCD's L2.

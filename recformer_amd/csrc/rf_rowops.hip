@@ -395,16 +395,6 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
 // Forward: x = dropout(t) + res, y = LN(x) in one pass (t the bf16 dense output, res the fp32
 // stream); x (the backward's input) and the row stats are written. The keep mask is a counter
 // hash of (seed, element index) — regenerated by the backward, never stored.
-__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
-  uint32_t h = (uint32_t)idx * 0x9E3779B1u ^ (uint32_t)(idx >> 32) * 0x85EBCA77u ^ (uint32_t)seed;
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= (uint32_t)(seed >> 32);
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
-  return h >= thresh;  // P(keep) = 1 - thresh / 2^32
-}
 
 template <int VEC, int NCH>
 __global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const bf16* __restrict__ t, int ldt,
@@ -988,9 +978,6 @@ static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, c
                        bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
                        const bf16* dy2 = nullptr);
 
-static uint32_t drop_thresh(float p) {
-  return p <= 0.f ? 0u : (p >= 1.f ? 0xFFFFFFFFu : (uint32_t)((double)p * 4294967296.0));
-}
 
 int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
                        const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,

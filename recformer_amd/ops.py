@@ -382,11 +382,12 @@ def scatter_add_rows(rows: torch.Tensor, src0, dst0, src1=None, dst1=None):
 
 
 def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, tag: Optional[str] = None,
-                       dqkv: Optional[torch.Tensor] = None):
+                       dqkv: Optional[torch.Tensor] = None, p_drop: float = 0.0, seed: int = 0):
     """Gradient of the local branch (rf_band_attn_bwd): q/k/v (pre-scaled q) and o, dout bf16
     (B*Lp, >=H*64) views; returns (dq, dk, dv) of shape (B*Lp, H*64) — fp32, or column views of
     `dqkv` (B*Lp, 3*H*64) in its dtype (fp32 or bf16) when given — plus, when there are global keys, gds / gpr
-    (B, H, Lp, gmax): dS and P of the global-key columns."""
+    (B, H, Lp, gmax): dS and P of the global-key columns (P times the dropout mask / (1 - p_drop) when
+    the forward ran with attention-probability dropout p_drop, seed; rf_band_attn_bwd_drop)."""
     lib = _lib.load()
     _dev(q, k, v, o, dout, flags)
     ld = _rowmajor(q, "q")
@@ -410,10 +411,10 @@ def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, t
     gds = torch.empty(B, H, Lp, max(gmax, 1), dtype=torch.float32, device=dev) if gmax else None
     gpr = torch.empty_like(gds) if gmax else None
     with _region(tag):
-        rc = lib.rf_band_attn_bwd_dt(dtype_code(dq.dtype), B, Lp, H, 64, 32, _p(q), _p(k), _p(v), ld, _p(o),
-                                     _rowmajor(o, "o"), _p(dout), _rowmajor(dout, "dout"), _p(flags),
-                                     _p(gidx.contiguous()) if gmax else None, gmax, _p(dq), _p(dk), _p(dv), ldg,
-                                     _p(lse2), _p(delta), _p(gds), _p(gpr), _stream(q))
+        rc = lib.rf_band_attn_bwd_drop(dtype_code(dq.dtype), B, Lp, H, 64, 32, _p(q), _p(k), _p(v), ld, _p(o),
+                                       _rowmajor(o, "o"), _p(dout), _rowmajor(dout, "dout"), _p(flags),
+                                       _p(gidx.contiguous()) if gmax else None, gmax, _p(dq), _p(dk), _p(dv), ldg,
+                                       _p(lse2), _p(delta), _p(gds), _p(gpr), float(p_drop), int(seed), _stream(q))
     check(rc, "rf_band_attn_bwd")
     return dq, dk, dv, gds, gpr
 
@@ -443,9 +444,11 @@ def add_layernorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.
 
 
 def band_attention(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int,
-                   out: Optional[torch.Tensor] = None, tag: Optional[str] = None):
+                   out: Optional[torch.Tensor] = None, tag: Optional[str] = None, p_drop: float = 0.0,
+                   seed: int = 0):
     """q/k/v: (B*Lp, >=H*64) row-major views sharing one leading dim (e.g. column slices of
-    the fused projection output)."""
+    the fused projection output). p_drop > 0: attention-probability dropout (training, TF:585-586)
+    with the counter-hash mask of `seed` (rf_band_attn_fwd_drop)."""
     lib = _lib.load()
     _dev(q, k, v, flags)
     ld = _rowmajor(q, "q")
@@ -456,9 +459,9 @@ def band_attention(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int,
         out = torch.empty(B * Lp, D, dtype=q.dtype, device=q.device)
     gmax = gidx.shape[1]
     with _region(tag):
-        rc = lib.rf_band_attn_fwd(dtype_code(q.dtype), B, Lp, H, 64, half_w, _p(q), _p(k), _p(v), ld,
-                                  _p(flags), _p(gidx) if gmax else None, gmax, _p(out),
-                                  _rowmajor(out, "out"), _stream(out))
+        rc = lib.rf_band_attn_fwd_drop(dtype_code(q.dtype), B, Lp, H, 64, half_w, _p(q), _p(k), _p(v), ld,
+                                       _p(flags), _p(gidx) if gmax else None, gmax, _p(out),
+                                       _rowmajor(out, "out"), float(p_drop), int(seed), _stream(out))
     check(rc, "rf_band_attn_fwd")
     return out
 

@@ -23,8 +23,11 @@ copies are autograd-tracked casts, so gradients reach the fp32 masters).
 
 Dropout: hidden dropout (embeddings, attention output, FFN output; TF:1069, 1128, models.py:137)
 is applied with torch's RNG, except in the bf16 path's fused dropout + residual + LayerNorm
-(_DropAddLN), whose keep mask is a counter hash of a seed drawn from torch's RNG. Attention-probability dropout (TF:581) is not implemented: training
-with attention_probs_dropout_prob > 0 raises.
+(_DropAddLN), whose keep mask is a counter hash of a seed drawn from torch's RNG.
+Attention-probability dropout (TF:585-586, 1036-1037): the band kernels apply and regenerate a
+counter-hash mask per (sequence, head, query, key) (rf_band_attn_fwd_drop / _bwd_drop); the
+global query rows use the same hash as torch ops (recformer_amd/dropout.py). The masks cannot
+equal torch's RNG draws, so dropout-on runs match the reference in distribution, not bitwise.
 """
 from __future__ import annotations
 
@@ -34,7 +37,7 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from . import ops
+from . import dropout, ops
 
 __all__ = ["encode_train"]
 
@@ -213,11 +216,12 @@ class _EmbedLN(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------------
-def _local_torch(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int):
+def _local_torch(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int, drop=None):
     """fp32 recompute of the local branch (band keys + the local K/V rows at the global
     positions); padded query rows 0. q, k, v (B*Lp, D), q pre-scaled; flags (B, Lp)
     {0 pad, 1 local, 2 global}; gidx (B, gmax). The global query rows' values are replaced by
-    the global branch in _attention_torch."""
+    the global branch in _attention_torch. drop = (p, seed): attention-probability dropout
+    (TF:585-586) with the kernels' counter-hash mask (recformer_amd/dropout.py)."""
     D = q.shape[1]
     hd = D // H
     f = flags.long()
@@ -255,6 +259,18 @@ def _local_torch(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int):
     m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
     p = torch.exp(s - m)
     p = p / p.sum(-1, keepdim=True).clamp_min(1e-30)
+    if drop is not None and drop[0] > 0:
+        dev = q.device
+        bi = torch.arange(B, device=dev).view(B, 1, 1, 1, 1)
+        ci = torch.arange(nb, device=dev).view(1, nb, 1, 1, 1)
+        hi = torch.arange(H, device=dev).view(1, 1, H, 1, 1)
+        qi = torch.arange(W, device=dev).view(1, 1, 1, W, 1)
+        row = (bi * H + hi) * Lp + ci * W + qi                                  # (B, nb, H, W, 1)
+        keys = ci * W - half_w + torch.arange(2 * W, device=dev).view(1, 1, 1, 1, 2 * W)
+        z = dropout.attn_scale(drop[1], drop[0], row, keys, Lp)
+        if gmax > 0:
+            z = torch.cat([z, dropout.attn_scale(drop[1], drop[0], row, gidx.view(B, 1, 1, 1, gmax), Lp)], -1)
+        p = p * z
     o = torch.einsum("bchij,bchdj->bcihd", p[..., :2 * W], vw)
     if gmax > 0:
         o = o + torch.einsum("bchig,bghd->bcihd", p[..., 2 * W:], vg_loc)
@@ -262,11 +278,23 @@ def _local_torch(q, k, v, flags, gidx, B: int, Lp: int, H: int, half_w: int):
     return o.reshape(B * Lp, D)
 
 
-def _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B: int, Lp: int, H: int):
+def _global_keep(gidx, B: int, Lp: int, H: int, p: float, seed: int):
+    """Dropout scale (B, H, gmax, Lp) of the global query rows' probabilities (TF:1036-1037):
+    mask row (b*H + h)*Lp + gidx[b, g], key l (the kernels' hash, recformer_amd/dropout.py)."""
+    G = gidx.shape[1]
+    dev = gidx.device
+    row = (torch.arange(B, device=dev).view(B, 1, 1, 1) * H + torch.arange(H, device=dev).view(1, H, 1, 1)) * Lp \
+        + gidx.clamp(min=0).to(torch.int64).view(B, 1, G, 1)
+    return dropout.attn_scale(seed, p, row, torch.arange(Lp, device=dev).view(1, 1, 1, Lp), Lp)
+
+
+def _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B: int, Lp: int, H: int, z=None):
     """Global query rows (TF:964-1057), (B*gmax, D): key_global / value_global over all tokens
     through the fold (rf_global.hip): s = (Wkg_h^T qg_h) . h_l + qg_h . bkg_h and
     out = Wvg_h (sum_l p_l h_l) + bvg_h, so no (B*Lp, D) projection is materialised and autograd
-    differentiates the same algebra."""
+    differentiates the same algebra. z (B, H, gmax, Lp): attention-probability dropout scale
+    (_global_keep); the dropped probabilities no longer sum to 1, so the value bias enters as
+    bvg_h * sum_l p'_l."""
     D = h.shape[1]
     hd = D // H
     gmax = qg.shape[0] // B
@@ -277,16 +305,23 @@ def _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B: int, Lp: int, H: int):
     sgg = torch.einsum("bghk,blk->bhgl", u, hf) + torch.einsum("bghd,hd->bhg", qgh, bkg.float().view(H, hd))[..., None]
     sgg = sgg.masked_fill(~valid[:, None, None, :], float("-inf"))
     pg = torch.softmax(sgg, -1)
+    if z is not None:
+        pg = pg * z
     w = torch.einsum("bhgl,blk->bghk", pg, hf)
-    og = torch.einsum("bghk,hdk->bghd", w, wvg.float().view(H, hd, D)) + bvg.float().view(H, hd)
+    og = torch.einsum("bghk,hdk->bghd", w, wvg.float().view(H, hd, D))
+    if z is None:
+        og = og + bvg.float().view(H, hd)
+    else:
+        og = og + pg.sum(-1).transpose(1, 2)[..., None] * bvg.float().view(H, hd)
     return og.reshape(B * gmax, D)
 
 
-def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout):
+def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout, z=None, bvg=None):
     """Closed-form gradient of _global_torch (the fold algebra, TF:964-1057) for the output
     gradient gout (B*gmax, D) — batched matmuls instead of autograd over einsums (a third of the
     ops, no nested graph). Returns fp32 (dqg, dh, dwkg, dbkg, dwvg, dbvg); dbkg is exactly zero:
-    the key bias adds q.bkg to every score of a row, which the softmax cancels."""
+    the key bias adds q.bkg to every score of a row, which the softmax cancels. z (B, H, gmax, Lp):
+    the forward's attention-dropout scale (then bvg, the value bias, is needed too)."""
     D = h.shape[1]
     hd = D // H
     G = qg.shape[0] // B
@@ -300,16 +335,24 @@ def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout):
     s = torch.bmm(u, hf.transpose(1, 2))                                     # (B, HG, Lp)
     s.masked_fill_((flags == 0).view(B, 1, Lp), float("-inf"))
     p = torch.softmax(s, -1)
-    w = torch.bmm(p, hf)                                                     # (B, HG, D)
+    pd = p if z is None else p * z.reshape(B, HG, Lp)                        # dropped probabilities
+    w = torch.bmm(pd, hf)                                                    # (B, HG, D)
     wH = w.view(B, H, G, D).transpose(0, 1).reshape(H, B * G, D)             # (H, BG, D)
     doH = gout.float().view(B * G, H, hd).transpose(0, 1)                    # (H, BG, hd)
-    dbvg = doH.sum(1).reshape(D)
+    if z is None:
+        dbvg = doH.sum(1).reshape(D)
+    else:  # out += bvg * S' with S' = sum_l p'_l per (b, h, g)
+        sH = pd.sum(-1).view(B, H, G).permute(1, 0, 2).reshape(H, B * G, 1)
+        dbvg = (doH * sH).sum(1).reshape(D)
     dwvg = torch.bmm(doH.transpose(1, 2), wH).reshape(D, D)                  # (H, hd, D)
     dwH = torch.bmm(doH, wv)                                                 # (H, BG, D)
     dw = dwH.view(H, B, G, D).transpose(0, 1).reshape(B, HG, D)
-    dp = torch.bmm(dw, hf.transpose(1, 2))                                   # (B, HG, Lp)
+    dp = torch.bmm(dw, hf.transpose(1, 2))                                   # (B, HG, Lp): d/dp'
+    if z is not None:
+        dS = (doH * bvg.float().view(H, 1, hd)).sum(-1)                       # (H, BG): d/dS'
+        dp = (dp + dS.view(H, B, G).permute(1, 0, 2).reshape(B, HG, 1)) * z.reshape(B, HG, Lp)
     ds = p * (dp - (p * dp).sum(-1, keepdim=True))
-    dh = torch.bmm(p.transpose(1, 2), dw).add_(torch.bmm(ds.transpose(1, 2), u))  # (B, Lp, D)
+    dh = torch.bmm(pd.transpose(1, 2), dw).add_(torch.bmm(ds.transpose(1, 2), u))  # (B, Lp, D)
     du = torch.bmm(ds, hf)                                                   # (B, HG, D)
     duH = du.view(B, H, G, D).transpose(0, 1).reshape(H, B * G, D)
     dq = torch.bmm(duH, wk.transpose(1, 2)).transpose(0, 1).reshape(B * G, D)
@@ -323,11 +366,14 @@ def _global_rows(gidx, B: int, Lp: int):
     return rows, (gidx >= 0).reshape(-1)
 
 
-def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, half_w: int):
-    """fp32 recompute of the whole attention block (same contract as the HIP kernels)."""
-    o = _local_torch(q, k, v, flags, gidx, B, Lp, H, half_w)
+def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, half_w: int,
+                     drop=None):
+    """fp32 recompute of the whole attention block (same contract as the HIP kernels); drop =
+    (p, seed) applies attention-probability dropout with the kernels' mask."""
+    o = _local_torch(q, k, v, flags, gidx, B, Lp, H, half_w, drop)
     if gidx.shape[1] > 0:
-        og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H)
+        z = _global_keep(gidx, B, Lp, H, *drop) if drop is not None and drop[0] > 0 else None
+        og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H, z)
         rows, keep = _global_rows(gidx, B, Lp)
         # overwrite the valid global rows (TF:621-629) without boolean-mask indexing (a host
         # sync): padded slots point at row 0 of their sequence and add exactly zero
@@ -336,16 +382,48 @@ def _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp
     return o
 
 
+def _put_global_rows(out, og, rows, keep, B: int, G: int):
+    """out[rows[s]] = og[s] for the valid global slots s (TF:621-629), no boolean indexing (a host
+    sync): an empty slot rewrites its sequence's first slot row with that slot's own value, so
+    repeated rows always receive identical values."""
+    r = rows.view(B, G)
+    k = keep.view(B, G)
+    r0 = r[:, :1].expand(B, G)
+    src0 = torch.where(k[:, :1, None], og.view(B, G, -1)[:, :1], out[r[:, 0]].to(og.dtype)[:, None])
+    src = torch.where(k[..., None], og.view(B, G, -1), src0.expand(B, G, og.shape[1]))
+    out.index_copy_(0, torch.where(k, r, r0).reshape(-1), src.reshape(B * G, -1).to(out.dtype))
+    return out
+
+
 class _Attention(torch.autograd.Function):
     """Takes the fused (B*Lp, 3D) q|k|v projection and returns its gradient as one tensor (no
-    per-slice zero-fill + accumulate in autograd)."""
+    per-slice zero-fill + accumulate in autograd). attn_p > 0: attention-probability dropout
+    (TF:585-586 local rows on the band kernels, TF:1036-1037 global rows as torch ops) with the
+    counter-hash mask of `seed`, regenerated in the backward."""
 
     @staticmethod
-    def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold, grows=None):
+    def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold, grows=None,
+                attn_p: float = 0.0, seed: int = 0):
         D = qkv.shape[1] // 3
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
-        out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w)
-        if gidx.shape[1] > 0:
+        G = gidx.shape[1]
+        ctx.drop = (attn_p, seed) if attn_p > 0 else None
+        ctx.gz = None
+        if ctx.drop is not None and q.dtype != torch.float32 and G > 32:
+            # the band kernel's dropout form takes <= 32 global keys: recompute in fp32 (the
+            # backward of this case is the fp32 recompute as well)
+            out = _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w,
+                                   ctx.drop).to(q.dtype)
+        elif ctx.drop is not None:
+            out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w, p_drop=attn_p, seed=seed)
+            if G > 0:
+                ctx.gz = _global_keep(gidx, B, Lp, H, attn_p, seed)
+                og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H, ctx.gz)
+                rows, keep = grows[:2] if grows is not None else _global_rows(gidx, B, Lp)
+                _put_global_rows(out, og, rows, keep, B, G)
+        else:
+            out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w)
+        if ctx.drop is None and G > 0:
             if fold:
                 ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg,
                                           wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out)
@@ -368,12 +446,14 @@ class _Attention(torch.autograd.Function):
         hip_local = q.dtype == torch.bfloat16 and half_w == 32 and D == 64 * H and gmax <= 32
         if not hip_local:
             return _Attention._backward_torch(ctx, dout)
+        p_drop, seed = ctx.drop if ctx.drop is not None else (0.0, 0)
         # local branch on the HIP backward kernels (rf_attn_bwd.hip); global rows of dout belong
         # to the global branch only (their local output was overwritten)
         d16 = dout.to(torch.bfloat16).contiguous()
         # gradients written in the projection's dtype (bf16): no fp32 copy and cast per layer
         dqkv = torch.empty(B * Lp, 3 * D, dtype=qkv.dtype, device=q.device)
-        dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H, dqkv=dqkv)
+        dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H, dqkv=dqkv,
+                                                      p_drop=p_drop, seed=seed)
         res = [None] * 7
         if gmax > 0:
             if ctx.grows is not None:
@@ -395,11 +475,11 @@ class _Attention(torch.autograd.Function):
                 gout = dout[rows].float() * keep[:, None].to(torch.float32)
                 if GLOBAL_BWD_CLOSED_FORM:
                     with torch.autocast("cuda", enabled=False):
-                        grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout)
+                        grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, ctx.gz, bvg)
                 else:
                     gin = [t.detach().requires_grad_(True) for t in (qg, h, wkg, bkg, wvg, bvg)]
                     with torch.enable_grad(), torch.autocast("cuda", enabled=False):
-                        og = _global_torch(*gin, flags, B, Lp, H)
+                        og = _global_torch(*gin, flags, B, Lp, H, ctx.gz)
                         grads = torch.autograd.grad(og, gin, gout, allow_unused=True)
                 for n, t in enumerate((qg, h, wkg, bkg, wvg, bvg)):
                     if ctx.needs_input_grad[1 + n]:
@@ -407,7 +487,7 @@ class _Attention(torch.autograd.Function):
                         res[1 + n] = None if g is None else g.to(t.dtype)
         if ctx.needs_input_grad[0]:
             res[0] = dqkv.to(qkv.dtype)
-        return (*res, None, None, None, None, None, None, None, None)
+        return (*res, None, None, None, None, None, None, None, None, None, None)
 
     @staticmethod
     def _backward_torch(ctx, dout):
@@ -419,7 +499,7 @@ class _Attention(torch.autograd.Function):
                   zip((qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], qg, h, wkg, bkg, wvg, bvg),
                       (need[0],) * 3 + tuple(need[1:7]))]
         with torch.enable_grad(), torch.autocast("cuda", enabled=False):
-            o = _attention_torch(*inputs, flags, gidx, B, Lp, H, half_w)
+            o = _attention_torch(*inputs, flags, gidx, B, Lp, H, half_w, ctx.drop)
             want = [t for t in inputs if t.requires_grad]
             grads = torch.autograd.grad(o, want, dout.float(), allow_unused=True) if want else []
         it = iter(grads)
@@ -435,7 +515,7 @@ class _Attention(torch.autograd.Function):
             res = [torch.cat(z, 1)] + res[3:]
         else:
             res = [None] + res[3:]
-        return (*res, None, None, None, None, None, None, None, None)
+        return (*res, None, None, None, None, None, None, None, None, None, None)
 
 
 # ------------------------------------------------------------------------------------------
@@ -498,10 +578,6 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     """Autograd forward of RecformerModel (same outputs as RecformerModel._encode)."""
     from .models import _compute_dtype
     cfg = model.config
-    if model.training and cfg.attention_probs_dropout_prob > 0:
-        raise NotImplementedError(
-            "recformer_amd: attention-probability dropout is not implemented on the training path; "
-            "set config.attention_probs_dropout_prob = 0")
     B, L = input_ids.shape
     Wn = model._window()
     Lp = L + (Wn - L % Wn) % Wn
@@ -510,6 +586,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     dt = _compute_dtype(model.dtype)
     eps = cfg.layer_norm_eps
     p_hid = cfg.hidden_dropout_prob if model.training else 0.0
+    p_att = cfg.attention_probs_dropout_prob if model.training else 0.0
     if global_attention_mask is not None:
         gm = global_attention_mask != 0
         if attention_mask is not None:
@@ -541,6 +618,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     nl = len(model.encoder.layer)
     # the pass's dropout seeds (two LayerNorms per layer) in one draw from torch's CPU generator
     seeds = torch.randint(0, 2 ** 62, (2 * nl,)).tolist() if p_hid > 0 else [0] * (2 * nl)
+    att_seeds = torch.randint(0, 2 ** 62, (nl,)).tolist() if p_att > 0 else [0] * nl
     for li, lyr in enumerate(model.encoder.layer):
         lw = _layer_weights(li, lyr, dt)
         h = h16 if h16 is not None else h32.to(dt)
@@ -550,7 +628,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
             hg = h[rows] * gvalid.to(h.dtype)
             qg = _Gemm.apply(hg, *lw["w_qg"], lw["b_qg"], D, scale)
         ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
-                               flags, gidx, B, Lp, H, windows[li] // 2, fold, grows)
+                               flags, gidx, B, Lp, H, windows[li] // 2, fold, grows, p_att, att_seeds[li])
         ao = lyr.attention.output
         t = _Gemm.apply(ctx, *lw["w_o"], lw["b_o"], 0, 1.0)
         if fused:

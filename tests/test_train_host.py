@@ -1,15 +1,19 @@
 """Host-side (CPU) checks of the training path's torch algebra (no GPU needed)."""
+import numpy as np
 import pytest
 import torch
 
 from recformer_amd import train
 
 
+@pytest.mark.parametrize("drop", [False, True])
 @pytest.mark.parametrize("B,Lp,H,G", [(2, 64, 2, 1), (3, 128, 3, 2), (1, 192, 12, 3)])
-def test_global_bwd_closed_form_matches_autograd(B, Lp, H, G):
+def test_global_bwd_closed_form_matches_autograd(B, Lp, H, G, drop):
     """train._global_bwd (closed-form gradient of the global rows' fold algebra, TF:964-1057)
     against autograd through train._global_torch on the same inputs: ragged valid lengths,
-    several global slots, one empty slot (zero query row and zero output gradient)."""
+    several global slots, one empty slot (zero query row and zero output gradient); with
+    attention-probability dropout (TF:1036-1037: the dropped probabilities also scale the value
+    bias) through the kernels' hash mask."""
     g = torch.Generator().manual_seed(B * 100 + Lp + H + G)
     D = 64 * H
     qg = torch.randn(B * G, D, generator=g, dtype=torch.float64)
@@ -26,10 +30,15 @@ def test_global_bwd_closed_form_matches_autograd(B, Lp, H, G):
     if G > 1:
         qg[G - 1] = 0  # an empty slot of sequence 0
         gout[G - 1] = 0
+    z = None
+    if drop:
+        gidx = torch.stack([torch.arange(G) * 5 for _ in range(B)]).to(torch.int32)
+        z = train._global_keep(gidx, B, Lp, H, 0.3, 12345)
+        assert 0.55 < float((z > 0).double().mean()) < 0.85
     ins = [t.clone().requires_grad_(True) for t in (qg, h, wkg, bkg, wvg, bvg)]
-    og = train._global_torch(*ins, flags, B, Lp, H)
+    og = train._global_torch(*ins, flags, B, Lp, H, z)
     ref = torch.autograd.grad(og, ins, gout.float(), allow_unused=True)
-    got = train._global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout)
+    got = train._global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, z, bvg)
     names = ("dqg", "dh", "dwkg", "dbkg", "dwvg", "dbvg")
     # the key bias only shifts each softmax row: its gradient is zero (autograd: rounding noise)
     assert torch.count_nonzero(got[3]) == 0
@@ -55,3 +64,37 @@ def test_weight_grad_split_k_matches_single_gemm():
     assert float((got.double() - ref).abs().max()) <= 2e-2 * float(ref.abs().max())
     # a short reduction stays one GEMM
     assert torch.equal(train._weight_grad(dc[:1024], a[:1024]), (dc[:1024].t() @ a[:1024]).float())
+
+
+def _drop_keep_np(seed, idx, thresh):
+    """rf_common.h drop_keep written with numpy uint32 wrap-around arithmetic."""
+    u32 = np.uint32
+    with np.errstate(over="ignore"):
+        idx = np.asarray(idx, dtype=np.uint64)
+        h = (idx & 0xFFFFFFFF).astype(u32) * u32(0x9E3779B1) ^ (idx >> 32).astype(u32) * u32(0x85EBCA77) \
+            ^ u32(seed & 0xFFFFFFFF)
+        h ^= h >> u32(16)
+        h *= u32(0x85EBCA6B)
+        h ^= u32((seed >> 32) & 0xFFFFFFFF)
+        h ^= h >> u32(13)
+        h *= u32(0xC2B2AE35)
+        h ^= h >> u32(16)
+    return h >= u32(thresh)
+
+
+@pytest.mark.parametrize("p", [0.1, 0.5, 0.9])
+def test_dropout_hash_torch_matches_c(p):
+    """recformer_amd.dropout.keep (int64 torch ops) is the kernels' counter hash bit for bit, and
+    keeps a 1 - p fraction; thresh / scale are the kernels' fp32-derived values."""
+    from recformer_amd import dropout
+    thresh, scale = dropout.drop_params(p)
+    assert thresh == int(float(np.float32(p)) * 2 ** 32)
+    assert scale == float(np.float32(1) / (np.float32(1) - np.float32(p)))
+    g = torch.Generator().manual_seed(5)
+    idx = torch.cat([torch.randint(0, 2 ** 62, (20000,), generator=g), torch.arange(20000),
+                     torch.tensor([2 ** 32 - 1, 2 ** 32, 2 ** 40 + 7])])
+    for seed in (0, 1, 2 ** 61 + 12345, 0xDEADBEEFCAFE):
+        got = dropout.keep(seed, idx, thresh).numpy()
+        ref = _drop_keep_np(seed, idx.numpy(), thresh)
+        assert (got == ref).all()
+        assert abs(got[:20000].mean() - (1 - p)) < 0.02
