@@ -74,9 +74,14 @@ def main():
         per[t]["durs"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     for kind in ("fetch", "write", "mfma"):
         tag = tagger()
+        last_id, t = None, None
         for r in load_dispatches(os.path.join(out, kind, "**", "*counter_collection.csv")):
-            t = tag(r["Kernel_Name"], int(r["Grid_Size"]))
+            if r["Dispatch_Id"] != last_id:  # a pass with several counters has one row per counter
+                last_id = r["Dispatch_Id"]
+                t = tag(r["Kernel_Name"], int(r["Grid_Size"]))
             per[t][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                per[t].setdefault("pmc_durs", []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     total = sum(v["dur_ns"] for v in per.values())
     res = {}
     for t, v in per.items():
@@ -88,13 +93,15 @@ def main():
         # MFMA busy: SQ_VALU_MFMA_BUSY_CYCLES (per-SIMD busy cycles, summed over the chip) over the
         # SIMD-cycles of the dispatch: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 x 256 CUs x 4 SIMDs
         mb, ga = v["SQ_VALU_MFMA_BUSY_CYCLES"], v["GRBM_GUI_ACTIVE"]
+        # the PMC pass's own per-dispatch durations give the clock (GRBM_GUI_ACTIVE / 8 per second)
+        pd = v.setdefault("pmc_durs", [])
         busy = None
         if mb and ga and len(mb) == len(ga):
             busy = round(sum(mb) / (sum(ga) / 8 * 256 * 4), 4)
         d = sorted(v["durs"])
         res[t] = {"calls": v["calls"], "avg_us": round(v["dur_ns"] / v["calls"] / 1e3, 2),
                   "median_us": round(d[len(d) // 2] / 1e3, 2), "mfma_busy": busy,
-                  "clock_ghz": round(sum(ga) / 8 / len(ga) / (sum(d) / len(d)), 3) if ga and d else None,
+                  "clock_ghz": round(sum(ga) / 8 / sum(pd), 3) if ga and pd and len(pd) == len(ga) else None,
                   "share": round(v["dur_ns"] / total, 4),
                   "hbm_read_bytes": rb, "hbm_write_bytes": wb,
                   "hbm_bytes": (rb + wb) if rb is not None and wb is not None else None}
