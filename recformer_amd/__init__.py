@@ -4,7 +4,7 @@ Drop-in for the reference package `recformer` (recformer/__init__.py:1-3): the s
 names and forward() signatures, backed by hand-written HIP kernels in librecformer_hip.so.
 """
 from .config import RecformerConfig
-from .ranker import Ranker, rank_catalog
+from .ranker import CatalogShard, Ranker, rank_catalog, retrieve
 from .models import (RecformerEmbeddings, RecformerForPretraining, RecformerForSeqRec,
                      RecformerModel, RecformerModelOutput, RecformerPooler,
                      RecformerPretrainingOutput, Similarity, create_position_ids_from_input_ids)
@@ -23,6 +23,6 @@ def __getattr__(name):  # host-side pieces load transformers / the host library 
 __all__ = [
     "RecformerConfig", "RecformerModel", "RecformerForSeqRec", "RecformerForPretraining",
     "RecformerPretrainingOutput", "RecformerModelOutput", "RecformerEmbeddings", "RecformerPooler",
-    "Similarity", "create_position_ids_from_input_ids", "Ranker", "rank_catalog", "RecformerTokenizer",
+    "Similarity", "create_position_ids_from_input_ids", "Ranker", "rank_catalog", "CatalogShard", "retrieve", "RecformerTokenizer",
     "FinetuneDataCollatorWithPadding", "EvalDataCollatorWithPadding", "LitWrapper",
 ]

@@ -13,7 +13,7 @@ from typing import Optional
 LIB_PATH = os.environ.get("RF_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                         "librecformer_hip.so")  # env: diagnostic builds
 
-RF_F32, RF_BF16 = 0, 1
+RF_F32, RF_BF16, RF_F16 = 0, 1, 2
 RF_IO_C_F32, RF_IO_R_F32 = 1, 2
 RF_EPI_NONE, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF_EPI_COS = 0, 1, 2, 3, 4
 RF_EPI_BIAS_GELU_AUX = 6
@@ -74,6 +74,14 @@ SIGNATURES = {
     "rf_cos_score_cand": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P,
                                   c_float, P, P]),
     "rf_rank_accum": (c_int, [c_int, c_int, P, ctypes.c_int64, P, c_float, c_float, P, P, P, P]),
+    "rf_label_scores": (c_int, [c_int, c_int, c_int, P, c_int, P, P, c_int, P, c_int, P, ctypes.c_int64, c_float, P,
+                                P]),
+    "rf_score_rank": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, c_int, c_int, c_float, P,
+                              c_float, c_float, P, P, ctypes.c_int64, P, P, P, c_int, ctypes.c_int32, P, P, c_int, P]),
+    "rf_score_rank_tiles": (c_int, [c_int]),
+    "rf_rank_reduce": (c_int, [c_int, c_int, P, P, P, P, P, P]),
+    "rf_topk_dense": (c_int, [c_int, c_int, P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int32, c_int, P, P, P]),
+    "rf_topk_merge": (c_int, [c_int, c_int, P, P, c_int, P, P, P, c_int, c_int, P, P, P, P]),
     "rf_cross_entropy_fwd": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, ctypes.c_int64, P, P, P]),
 }
 

@@ -73,6 +73,32 @@ template <> struct Vec<bf16, 1> {
   static __device__ __forceinline__ void load(const bf16* p, float* o) { o[0] = (float)*p; }
   static __device__ __forceinline__ void store(bf16* p, const float* o) { *p = (bf16)o[0]; }
 };
+template <> struct Vec<f16, 4> {
+  static __device__ __forceinline__ void load(const f16* p, float* o) {
+    f16x4 v = *reinterpret_cast<const f16x4*>(p);
+    o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+  }
+  static __device__ __forceinline__ void store(f16* p, const float* o) {
+    f16x4 v;
+    v[0] = (f16)o[0]; v[1] = (f16)o[1]; v[2] = (f16)o[2]; v[3] = (f16)o[3];
+    *reinterpret_cast<f16x4*>(p) = v;
+  }
+};
+template <> struct Vec<f16, 2> {
+  static __device__ __forceinline__ void load(const f16* p, float* o) {
+    f16x2 v = *reinterpret_cast<const f16x2*>(p);
+    o[0] = (float)v[0]; o[1] = (float)v[1];
+  }
+  static __device__ __forceinline__ void store(f16* p, const float* o) {
+    f16x2 v;
+    v[0] = (f16)o[0]; v[1] = (f16)o[1];
+    *reinterpret_cast<f16x2*>(p) = v;
+  }
+};
+template <> struct Vec<f16, 1> {
+  static __device__ __forceinline__ void load(const f16* p, float* o) { o[0] = (float)*p; }
+  static __device__ __forceinline__ void store(f16* p, const float* o) { *p = (f16)o[0]; }
+};
 
 // VEC consecutive elements of the split fp32 stream (rf_common.h split_f32 / join_f32)
 template <int VEC>
@@ -1056,6 +1082,10 @@ int rf_row_inv_norm(int dtype, int M, int D, const void* x, int ldx, float eps, 
 #undef L_
   } else if (dtype == RF_F32) {
 #define L_(V, N) k_row_inv_norm<float, V, N><<<grid, 256, 0, s>>>(M, (const float*)x, ldx, eps, out)
+    RF_ROW_DISPATCH(D, L_);
+#undef L_
+  } else if (dtype == RF_F16) {
+#define L_(V, N) k_row_inv_norm<f16, V, N><<<grid, 256, 0, s>>>(M, (const f16*)x, ldx, eps, out)
     RF_ROW_DISPATCH(D, L_);
 #undef L_
   } else {

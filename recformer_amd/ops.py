@@ -59,7 +59,9 @@ def dtype_code(dt: torch.dtype) -> int:
         return RF_BF16
     if dt == torch.float32:
         return RF_F32
-    raise TypeError(f"recformer_amd: unsupported compute dtype {dt} (bf16 or fp32)")
+    if dt == torch.float16:
+        return _lib.RF_F16
+    raise TypeError(f"recformer_amd: unsupported compute dtype {dt} (bf16, fp16 or fp32)")
 
 
 def _dev(*ts: Optional[torch.Tensor]) -> None:

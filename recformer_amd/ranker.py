@@ -54,51 +54,11 @@ class Ranker(nn.Module):
             print(labels.size())
             loss = 0.0
         gt, valid = rank_counts(scores, labels.reshape(-1))
-        rank = gt.float()
-        res = []
-        for k in self.ks:
-            indicator = (rank < k).float()
-            res.append(((1 / torch.log2(rank + 2)) * indicator).mean().item())  # ndcg@k
-            res.append(indicator.mean().item())  # hr@k
-        res.append((1 / (rank + 1)).mean().item())  # MRR
-        res.append((1 - (rank / valid.float())).mean().item())  # AUC
-        return res + [loss]
+        return _metrics(gt, valid, loss, self.ks)
 
 
-def rank_catalog(queries: torch.Tensor, items: torch.Tensor, labels: torch.Tensor, metrics_ks: Sequence[int],
-                 temp: float, block: int = 65536, items_rnorm: Optional[torch.Tensor] = None) -> List[float]:
-    """Ranker(metrics_ks)(Similarity(queries, items) / temp, labels) without the (B, N) score matrix
-    (finetune.py:70-92 over a whole catalog): the cosine scores are produced
-    `block` columns at a time into one reused buffer by the EPI_COS GEMM and folded into the
-    per-row counts (rf_rank_accum: strict rank, valid length) and the cross entropy's sum of
-    exp(s - 1/temp) (|s| <= 1/temp, so no row max is needed). The label scores are the same
-    kernel's values (the diagonal of the queries x label-items product), so the strict counts
-    match the full-matrix Ranker. Returns the Ranker's list [NDCG@k, HR@k ..., MRR, AUC, loss]."""
-    lib = _lib.load()
-    if not (queries.is_cuda and items.is_cuda):
-        raise _lib.RecformerHipError("rank_catalog needs ROCm device tensors (no CPU fallback)")
-    B, N = queries.shape[0], items.shape[0]
-    inv_t = 1.0 / temp
-    shift = inv_t  # |cos| <= 1
-    qn = ops.row_inv_norm(queries)
-    rn = ops.row_inv_norm(items) if items_rnorm is None else items_rnorm
-    lab = labels.reshape(-1).long()
-    s_label = ops.cos_scores(queries, items.index_select(0, lab).contiguous(), inv_t, z_rnorm=qn,
-                             items_rnorm=rn.index_select(0, lab).contiguous()).diagonal().contiguous()
-    gt = torch.zeros(B, dtype=torch.int32, device=queries.device)
-    valid = torch.zeros_like(gt)
-    sexp = torch.zeros(B, dtype=torch.float32, device=queries.device)
-    blk = min(block, N)
-    buf = torch.empty(B, (blk + 7) // 8 * 8, dtype=torch.float32, device=queries.device)
-    stream = torch.cuda.current_stream(queries.device).cuda_stream
-    for off in range(0, N, blk):
-        n = min(blk, N - off)
-        sc = ops.cos_scores(queries, items[off:off + n], inv_t, z_rnorm=qn, items_rnorm=rn[off:off + n],
-                            out=buf[:, :n])
-        _lib.check(lib.rf_rank_accum(B, n, sc.data_ptr(), sc.stride(0), s_label.data_ptr(), float(MAX_VAL),
-                                     float(shift), gt.data_ptr(), valid.data_ptr(), sexp.data_ptr(), stream),
-                   "rf_rank_accum")
-    loss = float((torch.log(sexp) + shift - s_label).mean())
+def _metrics(gt: torch.Tensor, valid: torch.Tensor, loss: float, metrics_ks: Sequence[int]) -> List[float]:
+    """The Ranker's list (utils.py:95-108) from per-row strict ranks and valid lengths."""
     rank = gt.float()
     res = []
     for k in metrics_ks:
@@ -108,3 +68,210 @@ def rank_catalog(queries: torch.Tensor, items: torch.Tensor, labels: torch.Tenso
     res.append((1 / (rank + 1)).mean().item())  # MRR
     res.append((1 - (rank / valid.float())).mean().item())  # AUC
     return res + [loss]
+
+
+# ---- C5 retrieval: catalog shards, fused score + rank + top-k (rf_retrieval.hip) -----------------
+TOPK_SAMPLE = 8192  # dense seed block that sets each row's candidate threshold
+TOPK_CAP = 32       # candidate slots per (row, 256-item tile)
+
+
+class CatalogShard:
+    """One GPU's shard of the item table for retrieval (the 1M-item catalog sharded
+    over the GPUs of a node): items (N_s, d) in bf16 or fp16 with global ids base .. base + N_s - 1,
+    and their inverse norms (Similarity's clamp, models.py:366) computed once."""
+
+    def __init__(self, items: torch.Tensor, base: int = 0, rnorm: Optional[torch.Tensor] = None):
+        if not items.is_cuda:
+            raise _lib.RecformerHipError("CatalogShard needs a ROCm device tensor (no CPU fallback)")
+        if items.dtype not in (torch.bfloat16, torch.float16):
+            raise TypeError("CatalogShard: items must be bf16 or fp16")
+        self.items = items.contiguous()
+        self.base = int(base)
+        self.rnorm = ops.row_inv_norm(self.items) if rnorm is None else rnorm.float().contiguous()
+
+    @property
+    def n(self) -> int:
+        return self.items.shape[0]
+
+
+def _check_q(queries: torch.Tensor, shard: CatalogShard) -> torch.Tensor:
+    q = queries.contiguous()
+    if q.dtype != shard.items.dtype or q.shape[1] != shard.items.shape[1]:
+        raise ValueError("queries and catalog must share dtype and width")
+    if q.shape[1] % 32 or q.data_ptr() % 16 or shard.items.data_ptr() % 16:
+        raise ValueError("retrieval kernels need d % 32 == 0 and 16-B aligned rows")
+    return q
+
+
+def label_scores(queries: torch.Tensor, shard: CatalogShard, labels: torch.Tensor, temp: float,
+                 q_rnorm: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cos(q_b, E[label_b]) / temp for the labels inside this shard, 0 for the others (summed over
+    the shards this is every row's label score, bit-identical to the ranking kernel's value)."""
+    q = _check_q(queries, shard)
+    qn = ops.row_inv_norm(q) if q_rnorm is None else q_rnorm
+    lab = labels.reshape(-1).to(torch.int64).contiguous()
+    out = torch.empty(q.shape[0], dtype=torch.float32, device=q.device)
+    _lib.check(_lib.load().rf_label_scores(ops.dtype_code(q.dtype), q.shape[0], q.shape[1], q.data_ptr(), q.stride(0),
+                                           qn.data_ptr(), shard.items.data_ptr(), shard.items.stride(0),
+                                           shard.rnorm.data_ptr(), shard.n, lab.data_ptr(), shard.base,
+                                           float(1.0 / temp), out.data_ptr(), ops._stream(q)), "rf_label_scores")
+    return out
+
+
+def _score_rank(q, qn, shard, s_label, inv_t, mode, col0, ncols, part_cnt, part_sexp, tn0, dense=None, tau=None,
+                cand=None, max_val=MAX_VAL):
+    lib = _lib.load()
+    cval, cidx, ccnt, cap = cand if cand is not None else (None, None, None, 1)
+    p = ops._p
+    _lib.check(lib.rf_score_rank(ops.dtype_code(q.dtype), mode, q.shape[0], q.shape[1], q.data_ptr(), q.stride(0),
+                                 qn.data_ptr(), shard.items.data_ptr(), shard.items.stride(0), shard.rnorm.data_ptr(),
+                                 col0, ncols, float(inv_t), s_label.data_ptr(), float(max_val), float(inv_t), p(tau),
+                                 p(dense), dense.stride(0) if dense is not None else 0, p(cval), p(cidx), p(ccnt), cap,
+                                 shard.base, part_cnt.data_ptr(), part_sexp.data_ptr(), tn0, ops._stream(q)),
+               "rf_score_rank")
+
+
+def _topk_dense(vals: torch.Tensor, k: int, idx: Optional[torch.Tensor] = None, idx_base: int = 0):
+    B, n = vals.shape
+    ov = torch.empty(B, k, dtype=torch.float32, device=vals.device)
+    oi = torch.empty(B, k, dtype=torch.int32, device=vals.device)
+    _lib.check(_lib.load().rf_topk_dense(B, n, vals.data_ptr(), vals.stride(0), ops._p(idx),
+                                         idx.stride(0) if idx is not None else 0, idx_base, k, ov.data_ptr(),
+                                         oi.data_ptr(), ops._stream(vals)), "rf_topk_dense")
+    return ov, oi
+
+
+def _dense_topk_rows(q, qn, shard, s_label, inv_t, k, chunk=TOPK_SAMPLE):
+    """Exact top-k of the rows of q over the whole shard, chunk by chunk (the overflow path)."""
+    B = q.shape[0]
+    nt = _lib.load().rf_score_rank_tiles(chunk)
+    pc = torch.empty(nt, B, dtype=torch.int32, device=q.device)
+    ps = torch.empty(nt, B, dtype=torch.float32, device=q.device)
+    dense = torch.empty(B, chunk, dtype=torch.float32, device=q.device)
+    bv = bi = None
+    for off in range(0, shard.n, chunk):
+        n = min(chunk, shard.n - off)
+        _score_rank(q, qn, shard, s_label, inv_t, 0, off, n, pc, ps, 0, dense=dense)
+        v, i = _topk_dense(dense[:, :n], k, idx_base=shard.base + off)
+        if bv is not None:
+            v, i = _topk_dense(torch.cat([bv, v], 1), k, idx=torch.cat([bi, i], 1).contiguous())
+        bv, bi = v, i
+    return bv, bi
+
+
+def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor, temp: float, k: int = 50,
+               q_rnorm: Optional[torch.Tensor] = None, sample: int = TOPK_SAMPLE, cap: int = TOPK_CAP,
+               max_val: float = MAX_VAL):
+    """One shard's part of the ranking (rf_retrieval.hip): per query the strict rank count
+    #{s > s_label}, #{s > -max_val} and sum exp(s - 1/temp) over the shard, and (k > 0) the shard's
+    top-k (scores descending, ties by lower item id; global ids). The scores are produced tile by
+    tile and consumed in the kernel's epilogue; only a (B, sample) seed block is ever written."""
+    q = _check_q(queries, shard)
+    qn = ops.row_inv_norm(q) if q_rnorm is None else q_rnorm
+    lib = _lib.load()
+    B, N = q.shape[0], shard.n
+    inv_t = 1.0 / temp
+    dev = q.device
+    s0 = min(N, sample) if k > 0 else 0
+    nt0 = lib.rf_score_rank_tiles(s0)
+    nt1 = lib.rf_score_rank_tiles(N - s0)
+    part_cnt = torch.empty(nt0 + nt1, B, dtype=torch.int32, device=dev)
+    part_sexp = torch.empty(nt0 + nt1, B, dtype=torch.float32, device=dev)
+    topv = topi = None
+    if k > 0:
+        dense = torch.empty(B, (s0 + 3) // 4 * 4, dtype=torch.float32, device=dev)
+        _score_rank(q, qn, shard, s_label, inv_t, 0, 0, s0, part_cnt, part_sexp, 0, dense=dense, max_val=max_val)
+        topv, topi = _topk_dense(dense[:, :s0], k, idx_base=shard.base)
+        if N > s0:
+            tau = topv[:, k - 1].contiguous()  # the seed block's k-th score: a lower bound of the row's
+            cval = torch.empty(nt1, B, cap, dtype=torch.float32, device=dev)
+            cidx = torch.empty(nt1, B, cap, dtype=torch.int32, device=dev)
+            ccnt = torch.empty(nt1, B, dtype=torch.int32, device=dev)
+            _score_rank(q, qn, shard, s_label, inv_t, 1, s0, N - s0, part_cnt, part_sexp, nt0, tau=tau,
+                        cand=(cval, cidx, ccnt, cap), max_val=max_val)
+            mv = torch.empty(B, k, dtype=torch.float32, device=dev)
+            mi = torch.empty(B, k, dtype=torch.int32, device=dev)
+            over = torch.empty(B, dtype=torch.int32, device=dev)
+            _lib.check(lib.rf_topk_merge(B, k, topv.data_ptr(), topi.data_ptr(), nt1, cval.data_ptr(), cidx.data_ptr(),
+                                         ccnt.data_ptr(), cap, k, mv.data_ptr(), mi.data_ptr(), over.data_ptr(),
+                                         ops._stream(q)), "rf_topk_merge")
+            rows = torch.nonzero(over).flatten()
+            if rows.numel():  # slots overflowed (many near-equal scores): exact re-rank of those rows
+                fv, fi = _dense_topk_rows(q.index_select(0, rows).contiguous(), qn.index_select(0, rows).contiguous(),
+                                          shard, s_label.index_select(0, rows).contiguous(), inv_t, k)
+                mv.index_copy_(0, rows, fv)
+                mi.index_copy_(0, rows, fi)
+            topv, topi = mv, mi
+    else:
+        _score_rank(q, qn, shard, s_label, inv_t, 2, 0, N, part_cnt, part_sexp, 0, max_val=max_val)
+    gt = torch.empty(B, dtype=torch.int32, device=dev)
+    valid = torch.empty(B, dtype=torch.int32, device=dev)
+    sexp = torch.empty(B, dtype=torch.float32, device=dev)
+    _lib.check(lib.rf_rank_reduce(B, nt0 + nt1, part_cnt.data_ptr(), part_sexp.data_ptr(), gt.data_ptr(),
+                                  valid.data_ptr(), sexp.data_ptr(), ops._stream(q)), "rf_rank_reduce")
+    return {"gt": gt, "valid": valid, "sexp": sexp, "topv": topv, "topi": topi, "shift": inv_t}
+
+
+def merge_topk(vals: torch.Tensor, ids: torch.Tensor, k: int):
+    """Top-k of each row of (B, M) candidate lists (e.g. the shards' top-k side by side): scores
+    descending, ties by lower id — the order rf_topk_* produce. Plain torch sorts (tiny inputs)."""
+    o = torch.argsort(ids, dim=1, stable=True)
+    v = torch.gather(vals, 1, o)
+    i = torch.gather(ids, 1, o)
+    v, o2 = torch.sort(v, dim=1, descending=True, stable=True)
+    return v[:, :k], torch.gather(i, 1, o2)[:, :k]
+
+
+def combine_shards(parts, k: int, group=None):
+    """Combine shard results across the ranks of `group` (all-reduce of the rank
+    counts and exp-sum partials, all-gather of the per-shard top-k); identity for one rank."""
+    import torch.distributed as dist
+    gt, valid, sexp = parts["gt"], parts["valid"], parts["sexp"]
+    topv, topi = parts["topv"], parts["topi"]
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        w = dist.get_world_size(group)
+        for t in (gt, valid, sexp):
+            dist.all_reduce(t, group=group)
+        if k > 0:
+            gv = [torch.empty_like(topv) for _ in range(w)]
+            gi = [torch.empty_like(topi) for _ in range(w)]
+            dist.all_gather(gv, topv.contiguous(), group=group)
+            dist.all_gather(gi, topi.contiguous(), group=group)
+            topv, topi = merge_topk(torch.cat(gv, 1), torch.cat(gi, 1), k)
+    return {"gt": gt, "valid": valid, "sexp": sexp, "topv": topv, "topi": topi, "shift": parts["shift"]}
+
+
+def retrieve(queries: torch.Tensor, shard: CatalogShard, labels: torch.Tensor, metrics_ks: Sequence[int], temp: float,
+             k: int = 50, group=None):
+    """C5 retrieval over a sharded catalog (every rank holds all queries — all-gathered CLS vectors —
+    and its own CatalogShard): Ranker(metrics_ks)(Similarity(queries, catalog) / temp, labels)
+    (utils.py:76-108) without the (B, N) score matrix, plus the top-k items per query over the whole
+    catalog. Returns (metrics list, top-k scores (B, k), top-k item ids (B, k))."""
+    import torch.distributed as dist
+    q = _check_q(queries, shard)
+    qn = ops.row_inv_norm(q)
+    sl = label_scores(q, shard, labels, temp, qn)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(sl, group=group)  # the owner's value plus zeros: exact
+    parts = combine_shards(shard_rank(q, shard, sl, temp, k, qn), k, group)
+    loss = float((torch.log(parts["sexp"]) + parts["shift"] - sl).mean())
+    return _metrics(parts["gt"], parts["valid"], loss, metrics_ks), parts["topv"], parts["topi"]
+
+
+def rank_catalog(queries: torch.Tensor, items: torch.Tensor, labels: torch.Tensor, metrics_ks: Sequence[int],
+                 temp: float, block: int = 65536, items_rnorm: Optional[torch.Tensor] = None) -> List[float]:
+    """Ranker(metrics_ks)(Similarity(queries, items) / temp, labels) without the (B, N) score matrix
+    (finetune.py:70-92 over a whole catalog): one fused score + rank kernel pass
+    (rf_score_rank, counts only) after the label scores (rf_label_scores, bit-identical to the
+    kernel's own value for that column, so the strict ranks match the full-matrix Ranker). `block`
+    is accepted for compatibility (the kernel tiles the catalog itself). Returns the Ranker's list
+    [NDCG@k, HR@k ..., MRR, AUC, loss]."""
+    if not (queries.is_cuda and items.is_cuda):
+        raise _lib.RecformerHipError("rank_catalog needs ROCm device tensors (no CPU fallback)")
+    shard = CatalogShard(items, 0, items_rnorm)
+    q = _check_q(queries, shard)
+    qn = ops.row_inv_norm(q)
+    sl = label_scores(q, shard, labels, temp, qn)
+    parts = shard_rank(q, shard, sl, temp, 0, qn)
+    loss = float((torch.log(parts["sexp"]) + parts["shift"] - sl).mean())
+    return _metrics(parts["gt"], parts["valid"], loss, metrics_ks)

@@ -1,0 +1,117 @@
+"""C5 retrieval (rf_retrieval.hip, recformer_amd.ranker): the fused score + rank + top-k kernels
+against the Ranker restated from utils.py:76-108 (oracle.restatement.ranker_metrics, pinned to the
+real Ranker's outputs by tests/golden/ranker.npz) on the scores of the same kernel written densely
+(bit-identical by construction: same MFMA chain, same epilogue expression), and the top-k against
+a full sort of those scores (ties by lower item id)."""
+import pytest
+import torch
+
+from oracle import restatement as R
+from recformer_amd import _lib, ops
+from recformer_amd.ranker import (CatalogShard, _score_rank, combine_shards, label_scores, merge_topk, rank_catalog,
+                                  shard_rank)
+
+pytestmark = pytest.mark.gpu
+KS = [1, 5, 10, 20, 50]
+
+
+def _dense_scores(q, shard, s_label, temp, chunk=8192):
+    """(B, N) fp32 scores from rf_score_rank's dense mode, chunk by chunk."""
+    B, N = q.shape[0], shard.n
+    qn = ops.row_inv_norm(q)
+    nt = _lib.load().rf_score_rank_tiles(chunk)
+    pc = torch.empty(nt, B, dtype=torch.int32, device=q.device)
+    ps = torch.empty(nt, B, dtype=torch.float32, device=q.device)
+    out = torch.empty(B, N, dtype=torch.float32, device=q.device)
+    buf = torch.empty(B, chunk, dtype=torch.float32, device=q.device)
+    for off in range(0, N, chunk):
+        n = min(chunk, N - off)
+        _score_rank(q, qn, shard, s_label, 1.0 / temp, 0, off, n, pc, ps, 0, dense=buf)
+        out[:, off:off + n] = buf[:, :n]
+    return out
+
+
+def _case(dev, dt, B, N, seed, dup=True, cluster=0):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    q = torch.randn(B, 768, device=dev, generator=g)
+    items = torch.randn(N, 768, device=dev, generator=g)
+    labels = torch.randint(0, N, (B,), device=dev, generator=g)
+    labels[::3] = N - 1 - torch.arange(len(labels[::3]), device=dev) % 7  # last (partial) tile
+    if dup:  # exact duplicates of some label items elsewhere (ties with the label score)
+        d = labels[: min(B, 16)]
+        items[(d + N // 2) % N] = items[d]
+    if cluster:  # `cluster` near-copies of query 0 inside one 256-item tile: its candidate slots overflow
+        items[256:256 + cluster] = q[0] + 1e-3 * torch.randn(cluster, 768, device=dev, generator=g)
+    return q.to(dt), items.to(dt), labels
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_label_scores_bit_identical_to_ranking_kernel(dev, dt):
+    q, items, labels = _case(dev, dt, 77, 5003, 1)
+    shard = CatalogShard(items)
+    sl = label_scores(q, shard, labels, 0.05)
+    dense = _dense_scores(q, shard, sl, 0.05)
+    assert torch.equal(sl, dense.gather(1, labels[:, None]).squeeze(1))
+    # labels outside a shard contribute exactly 0
+    half = CatalogShard(items[:2500], base=0)
+    s_half = label_scores(q, half, labels, 0.05)
+    assert torch.equal(s_half[labels >= 2500], torch.zeros_like(s_half[labels >= 2500]))
+
+
+@pytest.mark.parametrize("dt,B,N,cluster", [(torch.bfloat16, 37, 20011, 0), (torch.float16, 300, 33000, 0),
+                                            (torch.bfloat16, 64, 12000, 200)])
+def test_shard_rank_matches_restated_ranker_and_sort(dev, dt, B, N, cluster):
+    """Strict ranks, valid lengths and the Ranker metrics equal the restated Ranker on the same
+    scores; the top-50 equals a full stable sort; a row whose candidate slots overflow (cluster of
+    near-copies in one tile) is re-ranked exactly."""
+    q, items, labels = _case(dev, dt, B, N, B + N, cluster=cluster)
+    shard = CatalogShard(items)
+    sl = label_scores(q, shard, labels, 0.05)
+    parts = shard_rank(q, shard, sl, 0.05, k=50)
+    dense = _dense_scores(q, shard, sl, 0.05)
+    ref_rank = (dense > sl[:, None]).sum(1)
+    assert torch.equal(parts["gt"].long(), ref_rank)
+    assert torch.equal(parts["valid"].long(), torch.full_like(ref_rank, N))
+    ref = R.ranker_metrics(dense.cpu(), labels.cpu(), KS)
+    loss = float((torch.log(parts["sexp"]) + parts["shift"] - sl).mean())
+    from recformer_amd.ranker import _metrics
+    got = _metrics(parts["gt"], parts["valid"], loss, KS)
+    for a, b in zip(got[:-1], ref[:-1]):
+        assert a == pytest.approx(b, abs=1e-6)
+    assert got[-1] == pytest.approx(ref[-1], rel=1e-4)
+    ids = torch.arange(N, device=dev, dtype=torch.int32).expand(B, N)
+    rv, ri = merge_topk(dense, ids, 50)
+    assert torch.equal(parts["topv"], rv)
+    assert torch.equal(parts["topi"], ri)
+
+
+def test_two_shards_combine_to_one(dev):
+    """The catalog split in two shards (global ids), label scores summed, counts summed and the
+    shards' top-k merged (what combine_shards does across ranks) equals the single-shard result."""
+    q, items, labels = _case(dev, torch.float16, 129, 30000, 5)
+    whole = CatalogShard(items)
+    sl = label_scores(q, whole, labels, 0.05)
+    one = shard_rank(q, whole, sl, 0.05, k=50)
+    a, b = CatalogShard(items[:17000], 0), CatalogShard(items[17000:], 17000)
+    sl2 = label_scores(q, a, labels, 0.05) + label_scores(q, b, labels, 0.05)
+    assert torch.equal(sl2, sl)
+    pa, pb = shard_rank(q, a, sl2, 0.05, k=50), shard_rank(q, b, sl2, 0.05, k=50)
+    assert torch.equal(pa["gt"] + pb["gt"], one["gt"])
+    v, i = merge_topk(torch.cat([pa["topv"], pb["topv"]], 1), torch.cat([pa["topi"], pb["topi"]], 1), 50)
+    assert torch.equal(v, one["topv"]) and torch.equal(i, one["topi"])
+    single = combine_shards(one, 50)  # one rank: identity
+    assert single["topi"] is one["topi"]
+
+
+def test_rank_catalog_large_fp16(dev):
+    """N >= 262k: rank_catalog (counts-only kernel mode) vs the restated Ranker
+    on the dense scores of the same kernel; fp16 operands."""
+    q, items, labels = _case(dev, torch.float16, 512, 262144 + 37, 9)
+    shard = CatalogShard(items)
+    sl = label_scores(q, shard, labels, 0.05)
+    dense = _dense_scores(q, shard, sl, 0.05)
+    ref = R.ranker_metrics(dense.cpu(), labels.cpu(), KS)
+    got = rank_catalog(q, items, labels, KS, 0.05)
+    for x, y in zip(got[:-1], ref[:-1]):
+        assert x == pytest.approx(y, abs=1e-6)
+    assert got[-1] == pytest.approx(ref[-1], rel=1e-4)
