@@ -298,30 +298,30 @@ int rf_rank_accum(int M, int N, const float* scores, int64_t ld, const float* s_
  * columns); per tile column t and row b writes part_cnt[(tn0 + t) * B + b] = #{s > s_label[b]} |
  * #{s > -max_val} << 16 and part_sexp[...] = sum exp(s - shift) (shift >= max |s|). mode 0 also
  * writes the scores to dense (B x ncols, ldd); mode 1 appends the scores s >= tau[b] with their item
- * ids to cval / cidx[(t * B + b) * cap + j] and their number (may exceed cap) to ccnt[t * B + b];
- * mode 2 writes only the partials. 
+ * ids to the row's list cval / cidx[b * capr + j], j < rcnt[b] (rcnt zeroed by the caller; it exceeds
+ * capr when the list or a tile's 32-entry stage overflowed); mode 2 writes only the partials.
  * rf_rank_reduce: gt / valid / sexp per row = the partials summed over ntiles tile columns in order.
- * rf_topk_dense: top-k (k <= 256) of each row of a dense (B, n <= 8192) block, value descending, ties
+ * rf_topk_dense: top-k (k <= 256) of each row of a dense (B, n <= 2048) block, value descending, ties
  * by lower id (ids from idx (B, n) or idx_base + column).
- * rf_topk_merge: top-k of each row over a seed list (v0 / i0, B x k0; id < 0 skipped) and the
- * candidate slots of ntiles tile columns; overflow[b] = 1 when a slot overflowed or the row has more
- * than 6144 candidates (its outputs are then not written: re-rank the row densely). */
+ * rf_topk_merge: top-k of each row over a seed list (v0 / i0, B x k0; id < 0 skipped) and the row's
+ * candidate list (mode 1); a row whose list overflowed keeps its seed list and gets overflow[b] = 1
+ * (never cleared: re-rank such rows densely). */
 int rf_label_scores(int dtype, int B, int D, const void* q, int ldq, const float* rq, const void* items, int ldi,
                     const float* ri, int nshard, const int64_t* labels, int64_t label_base, float inv_temp,
                     float* s_label, rf_stream_t stream);
 int rf_score_rank(int dtype, int mode, int B, int D, const void* q, int ldq, const float* rq, const void* items,
                   int ldi, const float* ri, int col0, int ncols, float inv_temp, const float* s_label,
                   float max_val, float shift, const float* tau, float* dense, int64_t ldd, float* cval,
-                  int32_t* cidx, int32_t* ccnt, int cap, int32_t idx_base, int32_t* part_cnt, float* part_sexp,
+                  int32_t* cidx, int32_t* rcnt, int capr, int32_t idx_base, int32_t* part_cnt, float* part_sexp,
                   int tn0, rf_stream_t stream);
 int rf_score_rank_tiles(int ncols);
 int rf_rank_reduce(int B, int ntiles, const int32_t* part_cnt, const float* part_sexp, int32_t* gt,
                    int32_t* valid, float* sexp, rf_stream_t stream);
 int rf_topk_dense(int B, int n, const float* vals, int64_t ldv, const int32_t* idx, int64_t ldi, int32_t idx_base,
                   int k, float* out_v, int32_t* out_i, rf_stream_t stream);
-int rf_topk_merge(int B, int k0, const float* v0, const int32_t* i0, int ntiles, const float* cval,
-                  const int32_t* cidx, const int32_t* ccnt, int cap, int k, float* out_v, int32_t* out_i,
-                  int32_t* overflow, rf_stream_t stream);
+int rf_topk_merge(int B, int k0, const float* v0, const int32_t* i0, const float* cval, const int32_t* cidx,
+                  const int32_t* rcnt, int capr, int k, float* out_v, int32_t* out_i, int32_t* overflow,
+                  rf_stream_t stream);
 
 #ifdef __cplusplus
 }

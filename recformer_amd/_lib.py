@@ -81,7 +81,7 @@ SIGNATURES = {
     "rf_score_rank_tiles": (c_int, [c_int]),
     "rf_rank_reduce": (c_int, [c_int, c_int, P, P, P, P, P, P]),
     "rf_topk_dense": (c_int, [c_int, c_int, P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int32, c_int, P, P, P]),
-    "rf_topk_merge": (c_int, [c_int, c_int, P, P, c_int, P, P, P, c_int, c_int, P, P, P, P]),
+    "rf_topk_merge": (c_int, [c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, P, P]),
     "rf_cross_entropy_fwd": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, ctypes.c_int64, P, P, P]),
 }
 

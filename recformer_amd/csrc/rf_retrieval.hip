@@ -89,10 +89,10 @@ struct RankArgs {
   const float* tau;         // MODE 1: candidate threshold per row
   float* dense;             // MODE 0: (B, ncols) scores
   int64_t ldd;
-  float* cval;              // MODE 1: candidate slots [tn * B + row][cap] (tn: tile column of this launch)
+  float* cval;              // MODE 1: per-row candidate lists [row][capr]
   int32_t* cidx;
-  int32_t* ccnt;            // MODE 1: [tn * B + row] candidates (> cap: overflow)
-  int cap;
+  int32_t* rcnt;            // MODE 1: per-row candidate count (> capr: overflow)
+  int capr;
   int32_t idx_base;         // item id of shard row 0
   int32_t* part_cnt;        // [(tn0 + tn) * B + row] gt | valid << 16
   float* part_sexp;
@@ -106,6 +106,9 @@ constexpr int RK_LDS = RK_NS * RK_STAGE;           // 128 KiB
 constexpr int RK_EPI_LD = 68;                      // fp32 slab row stride
 constexpr int RK_PART = 8 * 16 * RK_EPI_LD * 4;    // after the 8 waves' slabs
 constexpr int RK_CNT = RK_PART + 256 * 4 * 12;     // per-row candidate counters
+constexpr int RK_TCAP = 32;                        // candidates per (row, tile) staged in LDS
+constexpr int RK_CAND = RK_CNT + 1024;             // [256][RK_TCAP] values, then ids
+static_assert(RK_CAND + 256 * RK_TCAP * 8 <= RK_LDS, "retrieval epilogue scratch");
 
 __device__ __forceinline__ int rk_slot(int r, int c) { return c ^ ((-(r >> 2)) & 3); }
 
@@ -206,6 +209,8 @@ __global__ void __launch_bounds__(512, 1) k_score_rank(int K, const T* __restric
   __syncthreads();  // the ring becomes epilogue scratch
 
   int* cnt = reinterpret_cast<int*>(smem + RK_CNT);
+  float* cv = reinterpret_cast<float*>(smem + RK_CAND);                      // [256 rows][RK_TCAP]
+  int32_t* ci = reinterpret_cast<int32_t*>(smem + RK_CAND + 256 * RK_TCAP * 4);
   int* pc = reinterpret_cast<int*>(smem + RK_PART);             // [256 rows][4 wn] packed counts
   float* ps = reinterpret_cast<float*>(smem + RK_PART + 4096);  // [256 rows][4 wn] sexp
   if (threadIdx.x < 256) cnt[threadIdx.x] = 0;
@@ -265,16 +270,16 @@ __global__ void __launch_bounds__(512, 1) k_score_rank(int K, const T* __restric
       }
     }
     if (MODE == 1 && rok && cmask) {
+      // stage in LDS per tile row (slot order within a (row, tile) is free: the merge sorts)
       const int n = __builtin_popcount(cmask);
-      const int base = atomicAdd(&cnt[rl], n);  // LDS atomic: slot order within (row, tile) is free
-      const int64_t slot0 = ((int64_t)tn * a.B + row) * a.cap;
+      const int base = atomicAdd(&cnt[rl], n);
       int t = 0;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         if (cmask & (1u << k)) {
-          if (base + t < a.cap) {
-            a.cval[slot0 + base + t] = v[k];
-            a.cidx[slot0 + base + t] = a.idx_base + a.col0 + c0 + k;
+          if (base + t < RK_TCAP) {
+            cv[rl * RK_TCAP + base + t] = v[k];
+            ci[rl * RK_TCAP + base + t] = a.idx_base + a.col0 + c0 + k;
           }
           ++t;
         }
@@ -298,30 +303,61 @@ __global__ void __launch_bounds__(512, 1) k_score_rank(int K, const T* __restric
       const int64_t o = (int64_t)(a.tn0 + tn) * a.B + row;
       a.part_cnt[o] = pc[rl * 4] + pc[rl * 4 + 1] + pc[rl * 4 + 2] + pc[rl * 4 + 3];
       a.part_sexp[o] = ((ps[rl * 4] + ps[rl * 4 + 1]) + ps[rl * 4 + 2]) + ps[rl * 4 + 3];
-      if (MODE == 1) a.ccnt[(int64_t)tn * a.B + row] = cnt[rl];
+      if (MODE == 1) {
+        // the tile's candidates of this row appended to the row's list: one global atomic per
+        // (row, tile) with candidates; a tile overflow poisons the row's count (> capr)
+        const int c = cnt[rl];
+        if (c > 0) {
+          const int m = min(c, RK_TCAP);
+          const int gbase = atomicAdd(a.rcnt + row, c > RK_TCAP ? a.capr + 1 : m);
+          if (c <= RK_TCAP && gbase + m <= a.capr) {
+            float* dv = a.cval + (int64_t)row * a.capr + gbase;
+            int32_t* di = a.cidx + (int64_t)row * a.capr + gbase;
+            for (int j = 0; j < m; ++j) {
+              dv[j] = cv[rl * RK_TCAP + j];
+              di[j] = ci[rl * RK_TCAP + j];
+            }
+          }
+        }
+      }
     }
   }
 }
 
+// 16 threads per row, each summing every 16th tile in order, then a fixed-order combine:
+// deterministic, and enough threads to hide the partials' load latency
 __global__ void __launch_bounds__(256) k_rank_reduce(int B, int ntiles, const int32_t* __restrict__ part_cnt,
                                                      const float* __restrict__ part_sexp, int32_t* __restrict__ gt,
                                                      int32_t* __restrict__ valid, float* __restrict__ sexp) {
-  const int row = blockIdx.x * 256 + threadIdx.x;
-  if (row >= B) return;
-  int g = 0, v = 0;
-  float s = 0.f;
-  for (int t = 0; t < ntiles; ++t) {
-    const int p = part_cnt[(int64_t)t * B + row];
-    g += p & 0xFFFF;
-    v += p >> 16;
-    s += part_sexp[(int64_t)t * B + row];
+  __shared__ int sc[16][17];
+  __shared__ float ss[16][17];
+  const int rl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int row = blockIdx.x * 16 + rl;
+  int c = 0;
+  float e = 0.f;
+  if (row < B)
+    for (int t = grp; t < ntiles; t += 16) {
+      c += part_cnt[(int64_t)t * B + row];
+      e += part_sexp[(int64_t)t * B + row];
+    }
+  sc[rl][grp] = c;
+  ss[rl][grp] = e;
+  __syncthreads();
+  if (grp == 0 && row < B) {
+    int g = 0, v = 0;
+    float x = 0.f;
+    for (int j = 0; j < 16; ++j) {
+      g += sc[rl][j] & 0xFFFF;
+      v += sc[rl][j] >> 16;
+      x += ss[rl][j];
+    }
+    gt[row] = g;
+    valid[row] = v;
+    sexp[row] = x;
   }
-  gt[row] = g;
-  valid[row] = v;
-  sexp[row] = s;
 }
 
-// ---- exact top-k per row --------------------------------------------------------------------
+// ---- exact top-k per row, one wave per row ----------------------------------------------------
 // order-preserving key: larger float -> larger unsigned key
 __device__ __forceinline__ uint32_t fkey(float f) {
   const uint32_t u = __float_as_uint(f);
@@ -330,157 +366,209 @@ __device__ __forceinline__ uint32_t fkey(float f) {
 __device__ __forceinline__ float kfloat(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
+__device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 
-// Top-k of the n (key, idx) pairs in LDS (n <= cap of the arrays), value descending, ties by
-// lower idx; 256 threads. Writes k outputs (missing entries: -inf, -1). `tie` is scratch of n ints,
-// `sel` of k ints.
-__device__ void lds_topk(const uint32_t* keys, const int32_t* idx, int n, int k, int* tie, int* sel, float* out_v,
-                         int32_t* out_i) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t s_prefix, s_need;
-  __shared__ int s_nsel, s_ntie;
-  const int t = threadIdx.x;
+// Top-k of the n (key, id) pairs in this wave's LDS arrays: value descending, ties by lower id;
+// missing entries (-inf, -1). The k-th largest key is found by a radix select on the observed
+// key RANGE (each pass splits [lo, hi] into 256 bins: close scores spread over the bins instead of
+// piling into one bin of the top byte), then the entries above it and the lowest-id ties are
+// ranked. hist: 256 ints, sel: >= k ints, tie: >= n ints of this wave's scratch.
+__device__ void wave_topk(const uint32_t* keys, const int32_t* ids, int n, int k, int* hist, int* sel, int* tie,
+                          float* out_v, int32_t* out_i) {
+  const int lane = threadIdx.x & 63;
   const int kk = min(k, n);
-  if (t == 0) {
-    s_prefix = 0;
-    s_need = kk;
-    s_nsel = 0;
-    s_ntie = 0;
-  }
-  uint32_t mask = 0;
-  __syncthreads();
+  uint32_t tau = 0;
+  int need = 0;
   if (kk > 0) {
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      hist[t] = 0;
-      __syncthreads();
-      const uint32_t prefix = s_prefix;
-      for (int e = t; e < n; e += 256) {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (int e = lane; e < n; e += 64) {
+      lo = min(lo, keys[e]);
+      hi = max(hi, keys[e]);
+    }
+    lo = wave_min_u(lo);
+    hi = wave_max_u(hi);
+    need = kk;
+    while (hi > lo) {
+      const uint64_t w = ((uint64_t)(hi - lo)) / 256 + 1;
+      for (int b = lane; b < 256; b += 64) hist[b] = 0;
+      __builtin_amdgcn_wave_barrier();
+      for (int e = lane; e < n; e += 64) {
         const uint32_t key = keys[e];
-        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        if (key >= lo && key <= hi) atomicAdd(&hist[(int)((key - lo) / w)], 1);
       }
-      __syncthreads();
-      if (t == 0) {
-        uint32_t cum = 0, need = s_need;
-        for (int b = 255; b >= 0; --b) {
-          if (cum + hist[b] >= need) {
-            s_prefix = prefix | ((uint32_t)b << shift);
-            s_need = need - cum;
-            break;
+      __builtin_amdgcn_wave_barrier();
+      // bins from the top: lane l owns bins 255 - 4l .. 252 - 4l; suffix sums across lanes
+      int c4[4], own = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c4[j] = hist[255 - 4 * lane - j];
+        own += c4[j];
+      }
+      int incl = own;  // inclusive prefix over lanes 0..lane (= bins from the top)
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += x;
+      }
+      const int excl = incl - own;
+      int bsel = -1, above = 0;
+      if (excl < need && incl >= need) {
+        int cum = excl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (bsel < 0 && cum + c4[j] >= need) {
+            bsel = 255 - 4 * lane - j;
+            above = cum;
           }
-          cum += hist[b];
+          cum += c4[j];
         }
       }
-      mask |= 255u << shift;
-      __syncthreads();
+      const unsigned long long found = __ballot(bsel >= 0);
+      const int src = __ffsll((long long)found) - 1;
+      bsel = __shfl(bsel, src, 64);
+      above = __shfl(above, src, 64);
+      need -= above;
+      const uint64_t nlo = (uint64_t)lo + (uint64_t)bsel * w;
+      const uint64_t nhi = min((uint64_t)hi, nlo + w - 1);
+      lo = (uint32_t)nlo;
+      hi = (uint32_t)nhi;
+      __builtin_amdgcn_wave_barrier();
     }
+    tau = lo;
   }
-  const uint32_t tau = s_prefix;
-  const int need = (int)s_need;  // entries equal to tau to take
-  // keys above tau, and the tie list
-  for (int e = t; e < n && kk > 0; e += 256) {
-    const uint32_t key = keys[e];
-    if (key > tau) sel[atomicAdd(&s_nsel, 1)] = e;
-    else if (key == tau) tie[atomicAdd(&s_ntie, 1)] = e;
+  // entries above tau (kk - need of them) and the ties
+  int ngt = 0, nt = 0;
+  for (int e0 = 0; e0 < n && kk > 0; e0 += 64) {
+    const int e = e0 + lane;
+    const uint32_t key = e < n ? keys[e] : 0u;
+    const bool g = e < n && key > tau, q = e < n && key == tau;
+    const unsigned long long mg = __ballot(g), mq = __ballot(q);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    if (g) sel[ngt + __popcll(mg & below)] = e;
+    if (q) tie[nt + __popcll(mq & below)] = e;
+    ngt += __popcll(mg);
+    nt += __popcll(mq);
   }
-  __syncthreads();
-  const int ngt = s_nsel, nt = s_ntie;
-  // the `need` ties with the lowest idx (ranked among the ties)
-  for (int a = t; a < nt; a += 256) {
+  __builtin_amdgcn_wave_barrier();
+  for (int a = lane; a < nt; a += 64) {  // the `need` ties with the lowest ids
     const int ea = tie[a];
-    int r = 0;
-    for (int b = 0; b < nt && r < need; ++b) r += idx[tie[b]] < idx[ea] ? 1 : 0;
+    int r = a;
+    if (nt > need) {
+      r = 0;
+      for (int b = 0; b < nt && r < need; ++b) r += ids[tie[b]] < ids[ea] ? 1 : 0;
+    }
     if (r < need) sel[ngt + r] = ea;
   }
-  __syncthreads();
-  // final order: key descending, idx ascending
-  for (int a = t; a < kk; a += 256) {
+  __builtin_amdgcn_wave_barrier();
+  for (int a = lane; a < kk; a += 64) {  // final order: key descending, id ascending
     const int ea = sel[a];
     const uint32_t ka = keys[ea];
-    const int ia = idx[ea];
+    const int ia = ids[ea];
     int r = 0;
     for (int b = 0; b < kk; ++b) {
       const int eb = sel[b];
       const uint32_t kb = keys[eb];
-      r += (kb > ka || (kb == ka && idx[eb] < ia)) ? 1 : 0;
+      r += (kb > ka || (kb == ka && ids[eb] < ia)) ? 1 : 0;
     }
     out_v[r] = kfloat(ka);
     out_i[r] = ia;
   }
-  for (int a = kk + t; a < k; a += 256) {
+  for (int a = kk + lane; a < k; a += 64) {
     out_v[a] = -__builtin_inff();
     out_i[a] = -1;
   }
 }
 
-constexpr int TK_DENSE_MAX = 8192;
-constexpr int TK_MERGE_MAX = 6144;
+constexpr int TK_DENSE_MAX = 2048;  // entries per row of a dense block (per wave)
+constexpr int TK_MERGE_MAX = 2048;  // seed list + candidates per row (per wave)
 constexpr int TK_KMAX = 256;
+constexpr int TK_WAVES = 4;         // rows per workgroup
+// per-wave LDS: keys, ids, ties (n each), hist 256, sel k
+constexpr int TK_WAVE_LDS = TK_DENSE_MAX * 12 + 256 * 4 + TK_KMAX * 4;
 
-__global__ void __launch_bounds__(256) k_topk_dense(int n, const float* __restrict__ vals, int64_t ldv,
+__global__ void __launch_bounds__(256) k_topk_dense(int B, int n, const float* __restrict__ vals, int64_t ldv,
                                                     const int32_t* __restrict__ idx, int64_t ldi, int32_t idx_base,
                                                     int k, float* __restrict__ out_v, int32_t* __restrict__ out_i) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint32_t* keys = reinterpret_cast<uint32_t*>(smem);
-  int32_t* ids = reinterpret_cast<int32_t*>(smem + TK_DENSE_MAX * 4);
-  int* tie = reinterpret_cast<int*>(smem + TK_DENSE_MAX * 8);
-  int* sel = reinterpret_cast<int*>(smem + TK_DENSE_MAX * 12);
-  const int row = blockIdx.x;
-  for (int e = threadIdx.x; e < n; e += 256) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * TK_WAVES + wave;
+  if (row >= B) return;
+  char* base = smem + wave * TK_WAVE_LDS;
+  uint32_t* keys = reinterpret_cast<uint32_t*>(base);
+  int32_t* ids = reinterpret_cast<int32_t*>(base + TK_DENSE_MAX * 4);
+  int* tie = reinterpret_cast<int*>(base + TK_DENSE_MAX * 8);
+  int* hist = reinterpret_cast<int*>(base + TK_DENSE_MAX * 12);
+  int* sel = hist + 256;
+  for (int e = lane; e < n; e += 64) {
     keys[e] = fkey(vals[(int64_t)row * ldv + e]);
     ids[e] = idx ? idx[(int64_t)row * ldi + e] : idx_base + e;
   }
-  __syncthreads();
-  lds_topk(keys, ids, n, k, tie, sel, out_v + (int64_t)row * k, out_i + (int64_t)row * k);
+  __builtin_amdgcn_wave_barrier();
+  wave_topk(keys, ids, n, k, hist, sel, tie, out_v + (int64_t)row * k, out_i + (int64_t)row * k);
 }
 
 __global__ void __launch_bounds__(256) k_topk_merge(int B, int k0, const float* __restrict__ v0,
-                                                    const int32_t* __restrict__ i0, int ntiles,
-                                                    const float* __restrict__ cval, const int32_t* __restrict__ cidx,
-                                                    const int32_t* __restrict__ ccnt, int cap, int k,
-                                                    float* __restrict__ out_v, int32_t* __restrict__ out_i,
-                                                    int32_t* __restrict__ overflow) {
+                                                    const int32_t* __restrict__ i0, const float* __restrict__ cval,
+                                                    const int32_t* __restrict__ cidx, const int32_t* __restrict__ rcnt,
+                                                    int capr, int k, float* __restrict__ out_v,
+                                                    int32_t* __restrict__ out_i, int32_t* __restrict__ overflow) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint32_t* keys = reinterpret_cast<uint32_t*>(smem);
-  int32_t* ids = reinterpret_cast<int32_t*>(smem + TK_MERGE_MAX * 4);
-  int* tie = reinterpret_cast<int*>(smem + TK_MERGE_MAX * 8);
-  int* sel = reinterpret_cast<int*>(smem + TK_MERGE_MAX * 12);
-  __shared__ int s_n, s_over;
-  const int row = blockIdx.x, t = threadIdx.x;
-  if (t == 0) {
-    s_n = 0;
-    s_over = 0;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * TK_WAVES + wave;
+  if (row >= B) return;
+  char* base = smem + wave * TK_WAVE_LDS;
+  uint32_t* keys = reinterpret_cast<uint32_t*>(base);
+  int32_t* ids = reinterpret_cast<int32_t*>(base + TK_MERGE_MAX * 4);
+  int* tie = reinterpret_cast<int*>(base + TK_MERGE_MAX * 8);
+  int* hist = reinterpret_cast<int*>(base + TK_MERGE_MAX * 12);
+  int* sel = hist + 256;
+  const int c = rcnt[row];
+  float* ov = out_v + (int64_t)row * k;
+  int32_t* oi = out_i + (int64_t)row * k;
+  if (c > capr || k0 + c > TK_MERGE_MAX) {
+    // overflowed: keep the previous list (a valid lower bound for the next threshold) and flag the
+    // row for an exact dense re-rank
+    for (int e = lane; e < k; e += 64) {
+      ov[e] = e < k0 ? v0[(int64_t)row * k0 + e] : -__builtin_inff();
+      oi[e] = e < k0 ? i0[(int64_t)row * k0 + e] : -1;
+    }
+    if (lane == 0) overflow[row] = 1;
+    return;
   }
-  __syncthreads();
-  for (int e = t; e < k0; e += 256) {
-    const int id = i0[(int64_t)row * k0 + e];
-    if (id >= 0) {
-      const int p = atomicAdd(&s_n, 1);
+  int n = 0;
+  for (int e0 = 0; e0 < k0; e0 += 64) {  // seed list (entries with id < 0 are empty)
+    const int e = e0 + lane;
+    const int id = e < k0 ? i0[(int64_t)row * k0 + e] : -1;
+    const bool ok = id >= 0;
+    const unsigned long long m = __ballot(ok);
+    if (ok) {
+      const int p = n + __popcll(m & ((1ull << lane) - 1ull));
       keys[p] = fkey(v0[(int64_t)row * k0 + e]);
       ids[p] = id;
     }
+    n += __popcll(m);
   }
-  for (int tt = t; tt < ntiles; tt += 256) {
-    const int64_t o = (int64_t)tt * B + row;
-    const int c = ccnt[o];
-    if (c > cap) s_over = 1;
-    const int m = min(c, cap);
-    if (m > 0) {
-      const int p = atomicAdd(&s_n, m);
-      if (p + m <= TK_MERGE_MAX) {
-        for (int j = 0; j < m; ++j) {
-          keys[p + j] = fkey(cval[o * cap + j]);
-          ids[p + j] = cidx[o * cap + j];
-        }
-      } else {
-        s_over = 1;
-      }
-    }
+  for (int e = lane; e < c; e += 64) {
+    keys[n + e] = fkey(cval[(int64_t)row * capr + e]);
+    ids[n + e] = cidx[(int64_t)row * capr + e];
   }
-  __syncthreads();
-  const int n = min(s_n, TK_MERGE_MAX);
-  if (t == 0) overflow[row] = s_over;
-  if (s_over) return;  // the caller re-ranks this row densely
-  lds_topk(keys, ids, n, k, tie, sel, out_v + (int64_t)row * k, out_i + (int64_t)row * k);
+  n += c;
+  __builtin_amdgcn_wave_barrier();
+  wave_topk(keys, ids, n, k, hist, sel, tie, ov, oi);
 }
 
 }  // namespace rf
@@ -509,18 +597,18 @@ extern "C" int rf_label_scores(int dtype, int B, int D, const void* q, int ldq, 
 extern "C" int rf_score_rank(int dtype, int mode, int B, int D, const void* q, int ldq, const float* rq,
                              const void* items, int ldi, const float* ri, int col0, int ncols, float inv_temp,
                              const float* s_label, float max_val, float shift, const float* tau, float* dense,
-                             int64_t ldd, float* cval, int32_t* cidx, int32_t* ccnt, int cap, int32_t idx_base,
+                             int64_t ldd, float* cval, int32_t* cidx, int32_t* rcnt, int capr, int32_t idx_base,
                              int32_t* part_cnt, float* part_sexp, int tn0, rf_stream_t stream) {
   RF_REQUIRE(mode >= 0 && mode <= 2, "rf_score_rank: mode must be 0 (dense), 1 (candidates) or 2 (counts)");
   RF_REQUIRE(B >= 0 && ncols >= 0 && col0 >= 0 && D > 0 && D % 32 == 0, "rf_score_rank: bad shape (D %% 32 == 0)");
   RF_REQUIRE(ldq % 8 == 0 && ldi % 8 == 0, "rf_score_rank: leading dims must be multiples of 8");
   RF_REQUIRE(s_label && part_cnt && part_sexp && rq && ri, "rf_score_rank: null pointer");
-  RF_REQUIRE(mode == 2 || (mode == 0 ? (dense && ldd >= ncols && ldd % 4 == 0) : (tau && cval && cidx && ccnt && cap > 0)),
+  RF_REQUIRE(mode == 2 || (mode == 0 ? (dense && ldd >= ncols && ldd % 4 == 0) : (tau && cval && cidx && rcnt && capr > 0)),
              "rf_score_rank: mode %d outputs missing or misaligned", mode);
   if (B == 0 || ncols == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
   RankArgs a{B, ncols, col0, rq, ri, inv_temp, s_label, max_val, shift, tau, dense, ldd,
-             cval, cidx, ccnt, cap, idx_base, part_cnt, part_sexp, tn0};
+             cval, cidx, rcnt, capr, idx_base, part_cnt, part_sexp, tn0};
   const int nTm = (B + RK_BM - 1) / RK_BM, nTn = (ncols + RK_BN - 1) / RK_BN;
   static bool attr = false;
   if (!attr) {
@@ -555,8 +643,12 @@ extern "C" int rf_rank_reduce(int B, int ntiles, const int32_t* part_cnt, const 
                               int32_t* valid, float* sexp, rf_stream_t stream) {
   RF_REQUIRE(B >= 0 && ntiles >= 0, "rf_rank_reduce: bad shape");
   if (B == 0) return RF_OK;
-  k_rank_reduce<<<(B + 255) / 256, 256, 0, as_stream(stream)>>>(B, ntiles, part_cnt, part_sexp, gt, valid, sexp);
+  k_rank_reduce<<<(B + 15) / 16, 256, 0, as_stream(stream)>>>(B, ntiles, part_cnt, part_sexp, gt, valid, sexp);
   RF_LAUNCH_CHECK("rf_rank_reduce");
+}
+
+static void topk_lds_attr(const void* fn) {
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, TK_WAVES * TK_WAVE_LDS);
 }
 
 extern "C" int rf_topk_dense(int B, int n, const float* vals, int64_t ldv, const int32_t* idx, int64_t ldi,
@@ -564,29 +656,28 @@ extern "C" int rf_topk_dense(int B, int n, const float* vals, int64_t ldv, const
   RF_REQUIRE(B >= 0 && n >= 0 && n <= TK_DENSE_MAX && k > 0 && k <= TK_KMAX,
              "rf_topk_dense: n=%d must be <= %d and k=%d in [1, %d]", n, TK_DENSE_MAX, k, TK_KMAX);
   if (B == 0) return RF_OK;
-  const size_t lds = (size_t)TK_DENSE_MAX * 12 + TK_KMAX * 4;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_topk_dense, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    topk_lds_attr((const void*)k_topk_dense);
     attr = true;
   }
-  k_topk_dense<<<B, 256, lds, as_stream(stream)>>>(n, vals, ldv, idx, ldi, idx_base, k, out_v, out_i);
+  k_topk_dense<<<(B + TK_WAVES - 1) / TK_WAVES, 64 * TK_WAVES, TK_WAVES * TK_WAVE_LDS, as_stream(stream)>>>(
+      B, n, vals, ldv, idx, ldi, idx_base, k, out_v, out_i);
   RF_LAUNCH_CHECK("rf_topk_dense");
 }
 
-extern "C" int rf_topk_merge(int B, int k0, const float* v0, const int32_t* i0, int ntiles, const float* cval,
-                             const int32_t* cidx, const int32_t* ccnt, int cap, int k, float* out_v, int32_t* out_i,
+extern "C" int rf_topk_merge(int B, int k0, const float* v0, const int32_t* i0, const float* cval,
+                             const int32_t* cidx, const int32_t* rcnt, int capr, int k, float* out_v, int32_t* out_i,
                              int32_t* overflow, rf_stream_t stream) {
-  RF_REQUIRE(B >= 0 && k0 >= 0 && k0 <= TK_MERGE_MAX && ntiles >= 0 && cap > 0 && k > 0 && k <= TK_KMAX,
+  RF_REQUIRE(B >= 0 && k0 >= 0 && k0 <= TK_KMAX && capr > 0 && k > 0 && k <= TK_KMAX,
              "rf_topk_merge: bad arguments");
   if (B == 0) return RF_OK;
-  const size_t lds = (size_t)TK_MERGE_MAX * 12 + TK_KMAX * 4;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    topk_lds_attr((const void*)k_topk_merge);
     attr = true;
   }
-  k_topk_merge<<<B, 256, lds, as_stream(stream)>>>(B, k0, v0, i0, ntiles, cval, cidx, ccnt, cap, k, out_v, out_i,
-                                                   overflow);
+  k_topk_merge<<<(B + TK_WAVES - 1) / TK_WAVES, 64 * TK_WAVES, TK_WAVES * TK_WAVE_LDS, as_stream(stream)>>>(
+      B, k0, v0, i0, cval, cidx, rcnt, capr, k, out_v, out_i, overflow);
   RF_LAUNCH_CHECK("rf_topk_merge");
 }

@@ -71,8 +71,8 @@ def _metrics(gt: torch.Tensor, valid: torch.Tensor, loss: float, metrics_ks: Seq
 
 
 # ---- C5 retrieval: catalog shards, fused score + rank + top-k (rf_retrieval.hip) -----------------
-TOPK_SAMPLE = 8192  # dense seed block that sets each row's candidate threshold
-TOPK_CAP = 32       # candidate slots per (row, 256-item tile)
+TOPK_SAMPLE = 2048  # dense seed block that sets each row's first candidate threshold
+TOPK_CAP = 1024     # candidate list per row and chunk
 
 
 class CatalogShard:
@@ -121,12 +121,13 @@ def label_scores(queries: torch.Tensor, shard: CatalogShard, labels: torch.Tenso
 def _score_rank(q, qn, shard, s_label, inv_t, mode, col0, ncols, part_cnt, part_sexp, tn0, dense=None, tau=None,
                 cand=None, max_val=MAX_VAL):
     lib = _lib.load()
-    cval, cidx, ccnt, cap = cand if cand is not None else (None, None, None, 1)
+    cval, cidx, rcnt = cand if cand is not None else (None, None, None)
+    capr = cval.shape[1] if cval is not None else 1
     p = ops._p
     _lib.check(lib.rf_score_rank(ops.dtype_code(q.dtype), mode, q.shape[0], q.shape[1], q.data_ptr(), q.stride(0),
                                  qn.data_ptr(), shard.items.data_ptr(), shard.items.stride(0), shard.rnorm.data_ptr(),
                                  col0, ncols, float(inv_t), s_label.data_ptr(), float(max_val), float(inv_t), p(tau),
-                                 p(dense), dense.stride(0) if dense is not None else 0, p(cval), p(cidx), p(ccnt), cap,
+                                 p(dense), dense.stride(0) if dense is not None else 0, p(cval), p(cidx), p(rcnt), capr,
                                  shard.base, part_cnt.data_ptr(), part_sexp.data_ptr(), tn0, ops._stream(q)),
                "rf_score_rank")
 
@@ -141,21 +142,20 @@ def _topk_dense(vals: torch.Tensor, k: int, idx: Optional[torch.Tensor] = None, 
     return ov, oi
 
 
-def _dense_topk_rows(q, qn, shard, s_label, inv_t, k, chunk=TOPK_SAMPLE):
-    """Exact top-k of the rows of q over the whole shard, chunk by chunk (the overflow path)."""
+def _dense_topk_rows(q, qn, shard, s_label, inv_t, k, col0, ncols, prev_v, prev_i, chunk=TOPK_SAMPLE):
+    """Exact top-k of the rows of q over shard rows [col0, col0 + ncols) merged with their running
+    top-k (prev_v, prev_i), densely chunk by chunk (the candidate-overflow path)."""
     B = q.shape[0]
     nt = _lib.load().rf_score_rank_tiles(chunk)
     pc = torch.empty(nt, B, dtype=torch.int32, device=q.device)
     ps = torch.empty(nt, B, dtype=torch.float32, device=q.device)
     dense = torch.empty(B, chunk, dtype=torch.float32, device=q.device)
-    bv = bi = None
-    for off in range(0, shard.n, chunk):
-        n = min(chunk, shard.n - off)
+    bv, bi = prev_v, prev_i
+    for off in range(col0, col0 + ncols, chunk):
+        n = min(chunk, col0 + ncols - off)
         _score_rank(q, qn, shard, s_label, inv_t, 0, off, n, pc, ps, 0, dense=dense)
         v, i = _topk_dense(dense[:, :n], k, idx_base=shard.base + off)
-        if bv is not None:
-            v, i = _topk_dense(torch.cat([bv, v], 1), k, idx=torch.cat([bi, i], 1).contiguous())
-        bv, bi = v, i
+        bv, bi = _topk_dense(torch.cat([bv, v], 1), k, idx=torch.cat([bi, i], 1).contiguous())
     return bv, bi
 
 
@@ -173,41 +173,59 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     inv_t = 1.0 / temp
     dev = q.device
     s0 = min(N, sample) if k > 0 else 0
-    nt0 = lib.rf_score_rank_tiles(s0)
-    nt1 = lib.rf_score_rank_tiles(N - s0)
-    part_cnt = torch.empty(nt0 + nt1, B, dtype=torch.int32, device=dev)
-    part_sexp = torch.empty(nt0 + nt1, B, dtype=torch.float32, device=dev)
+    # column chunks after the seed block: each as large as everything before it
+    plan, off = [], s0
+    while k > 0 and off < N:
+        plan.append((off, min(N - off, max(off, sample))))
+        off += plan[-1][1]
+    nt0 = lib.rf_score_rank_tiles(s0 if k > 0 else N)
+    ntiles = nt0 + sum(lib.rf_score_rank_tiles(n) for _, n in plan)
+    part_cnt = torch.empty(ntiles, B, dtype=torch.int32, device=dev)
+    part_sexp = torch.empty(ntiles, B, dtype=torch.float32, device=dev)
     topv = topi = None
     if k > 0:
         dense = torch.empty(B, (s0 + 3) // 4 * 4, dtype=torch.float32, device=dev)
         _score_rank(q, qn, shard, s_label, inv_t, 0, 0, s0, part_cnt, part_sexp, 0, dense=dense, max_val=max_val)
         topv, topi = _topk_dense(dense[:, :s0], k, idx_base=shard.base)
-        if N > s0:
-            tau = topv[:, k - 1].contiguous()  # the seed block's k-th score: a lower bound of the row's
-            cval = torch.empty(nt1, B, cap, dtype=torch.float32, device=dev)
-            cidx = torch.empty(nt1, B, cap, dtype=torch.int32, device=dev)
-            ccnt = torch.empty(nt1, B, dtype=torch.int32, device=dev)
-            _score_rank(q, qn, shard, s_label, inv_t, 1, s0, N - s0, part_cnt, part_sexp, nt0, tau=tau,
-                        cand=(cval, cidx, ccnt, cap), max_val=max_val)
+        del dense
+        # the rest in chunks that double with the items already seen: the running k-th score is a
+        # lower bound of the final one, so only s >= it can enter the top-k (about k per row per
+        # chunk); each chunk's candidates are merged before the next chunk's threshold is read.
+        # Rows whose candidate lists overflow keep their list (still a lower bound) and are re-ranked
+        # exactly at the end.
+        tn = nt0
+        cval = torch.empty(B, cap, dtype=torch.float32, device=dev)
+        cidx = torch.empty(B, cap, dtype=torch.int32, device=dev)
+        rcnt = torch.empty(B, dtype=torch.int32, device=dev)
+        over = torch.zeros(B, dtype=torch.int32, device=dev)
+        for off, n in plan:
+            rcnt.zero_()
+            tau = topv[:, k - 1].contiguous()
+            _score_rank(q, qn, shard, s_label, inv_t, 1, off, n, part_cnt, part_sexp, tn, tau=tau,
+                        cand=(cval, cidx, rcnt), max_val=max_val)
             mv = torch.empty(B, k, dtype=torch.float32, device=dev)
             mi = torch.empty(B, k, dtype=torch.int32, device=dev)
-            over = torch.empty(B, dtype=torch.int32, device=dev)
-            _lib.check(lib.rf_topk_merge(B, k, topv.data_ptr(), topi.data_ptr(), nt1, cval.data_ptr(), cidx.data_ptr(),
-                                         ccnt.data_ptr(), cap, k, mv.data_ptr(), mi.data_ptr(), over.data_ptr(),
+            _lib.check(lib.rf_topk_merge(B, k, topv.data_ptr(), topi.data_ptr(), cval.data_ptr(), cidx.data_ptr(),
+                                         rcnt.data_ptr(), cap, k, mv.data_ptr(), mi.data_ptr(), over.data_ptr(),
                                          ops._stream(q)), "rf_topk_merge")
-            rows = torch.nonzero(over).flatten()
-            if rows.numel():  # slots overflowed (many near-equal scores): exact re-rank of those rows
-                fv, fi = _dense_topk_rows(q.index_select(0, rows).contiguous(), qn.index_select(0, rows).contiguous(),
-                                          shard, s_label.index_select(0, rows).contiguous(), inv_t, k)
-                mv.index_copy_(0, rows, fv)
-                mi.index_copy_(0, rows, fi)
             topv, topi = mv, mi
+            tn += lib.rf_score_rank_tiles(n)
+        if plan:
+            rows = torch.nonzero(over).flatten()
+            if rows.numel():  # many near-equal scores overflowed the lists: exact dense re-rank
+                empty_v = torch.full((rows.numel(), k), float("-inf"), device=dev)
+                empty_i = torch.full((rows.numel(), k), -1, dtype=torch.int32, device=dev)
+                fv, fi = _dense_topk_rows(q.index_select(0, rows).contiguous(), qn.index_select(0, rows).contiguous(),
+                                          shard, s_label.index_select(0, rows).contiguous(), inv_t, k, 0, N,
+                                          empty_v, empty_i)
+                topv = topv.index_copy(0, rows, fv)
+                topi = topi.index_copy(0, rows, fi)
     else:
         _score_rank(q, qn, shard, s_label, inv_t, 2, 0, N, part_cnt, part_sexp, 0, max_val=max_val)
     gt = torch.empty(B, dtype=torch.int32, device=dev)
     valid = torch.empty(B, dtype=torch.int32, device=dev)
     sexp = torch.empty(B, dtype=torch.float32, device=dev)
-    _lib.check(lib.rf_rank_reduce(B, nt0 + nt1, part_cnt.data_ptr(), part_sexp.data_ptr(), gt.data_ptr(),
+    _lib.check(lib.rf_rank_reduce(B, ntiles, part_cnt.data_ptr(), part_sexp.data_ptr(), gt.data_ptr(),
                                   valid.data_ptr(), sexp.data_ptr(), ops._stream(q)), "rf_rank_reduce")
     return {"gt": gt, "valid": valid, "sexp": sexp, "topv": topv, "topi": topi, "shift": inv_t}
 

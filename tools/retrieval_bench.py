@@ -1,0 +1,59 @@
+"""C5 scoring throughput (BASELINE configs[4]): Q queries against a catalog shard with the fused
+score + rank + top-50 kernels (recformer_amd.ranker.shard_rank), one GPU.
+
+    python tools/retrieval_bench.py [--queries 4096] [--items 125000,1000000] [--dtype fp16]
+
+Prints per shard size: ms per call, query-item pairs/s, TFLOP/s of the score GEMM (2*Q*N*d) and
+its fraction of the 2.5 PF dense fp16/bf16 MFMA peak; the counts-only mode (rank_catalog) too."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from recformer_amd.ranker import CatalogShard, label_scores, shard_rank  # noqa: E402
+
+
+def timeit(fn, iters=10, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--queries", type=int, default=4096)
+    ap.add_argument("--items", type=str, default="125000,1000000")
+    ap.add_argument("--dtype", type=str, default="fp16")
+    ap.add_argument("--k", type=int, default=50)
+    args = ap.parse_args()
+    dt = {"fp16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    Q, d = args.queries, 768
+    q = torch.randn(Q, d, device=dev, generator=g).to(dt)
+    for N in (int(x) for x in args.items.split(",")):
+        items = torch.randn(N, d, device=dev, generator=g).to(dt)
+        labels = torch.randint(0, N, (Q,), device=dev, generator=g)
+        shard = CatalogShard(items)
+        sl = label_scores(q, shard, labels, 0.05)
+        t_top = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=args.k))
+        t_cnt = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=0))
+        fl = 2.0 * Q * N * d
+        for name, t in (("rank+top%d" % args.k, t_top), ("rank only", t_cnt)):
+            print(json.dumps({"items": N, "queries": Q, "dtype": args.dtype, "mode": name, "ms": round(t * 1e3, 3),
+                              "pairs_per_s": round(Q * N / t / 1e9, 2), "tflops": round(fl / t / 1e12, 1),
+                              "frac_of_2.5PF": round(fl / t / 2.5e15, 3)}), flush=True)
+        del items, shard
+
+
+if __name__ == "__main__":
+    main()
