@@ -109,3 +109,90 @@ def allreduce_grads(params, bucket_bytes: int = 64 << 20, average: bool = True) 
                 n += 1
             bucket, size = ([g], g.numel() * g.element_size()) if g is not None else ([], 0)
     return n
+
+
+class GradBucketer:
+    """Bucketed gradient all-reduce overlapped with backward (RCCL all-reduce of the
+    gradients in ~25-50 MB buckets launched in reverse layer order during backward).
+
+    Parameters are grouped, in reverse registration order (the order backward produces their
+    gradients), into buckets of <= bucket_bytes per (dtype, device). A post-accumulate-grad hook
+    counts each bucket's ready gradients; when the last one lands, the bucket is flattened and its
+    all-reduce is launched asynchronously, so communication of late layers overlaps the backward of
+    early ones. `finish()` waits for every bucket, divides by the world size (average: the mean of
+    the ranks' gradients, as DistributedDataParallel) and copies back into each .grad. Parameters
+    that received no gradient in a step are reduced as zeros, so every rank issues the same
+    collectives in the same order. With one rank it does nothing.
+
+        b = GradBucketer(model.parameters()); loss.backward(); b.finish(); opt.step()
+    """
+
+    def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, group=None):
+        self.rank, self.ws = world()
+        self.average = average
+        self.group = group
+        self.params = [p for p in params if p.requires_grad]
+        self.buckets = []
+        self._handles = []
+        if self.ws == 1:
+            return
+        by = {}
+        for p in reversed(self.params):
+            by.setdefault((p.dtype, p.device), []).append(p)
+        for ps in by.values():
+            cur, size = [], 0
+            for p in ps:
+                nb = p.numel() * p.element_size()
+                if cur and size + nb > bucket_bytes:
+                    self.buckets.append(cur)
+                    cur, size = [], 0
+                cur.append(p)
+                size += nb
+            if cur:
+                self.buckets.append(cur)
+        self._of = {}
+        for bi, ps in enumerate(self.buckets):
+            for p in ps:
+                self._of[id(p)] = bi
+                p.register_post_accumulate_grad_hook(self._hook)
+        self._ready = [0] * len(self.buckets)
+        self._flat = [None] * len(self.buckets)
+
+    def _hook(self, p):
+        bi = self._of[id(p)]
+        self._ready[bi] += 1
+        if self._ready[bi] == len(self.buckets[bi]):
+            self._launch(bi)
+
+    def _launch(self, bi):
+        ps = self.buckets[bi]
+        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps])
+        self._flat[bi] = flat
+        self._handles.append((bi, dist.all_reduce(flat, group=self.group, async_op=True)))
+
+    def finish(self) -> int:
+        """Wait for the step's buckets (launching any whose gradients never all arrived), average,
+        write back; returns the number of collectives issued this step."""
+        if self.ws == 1:
+            return 0
+        for bi in range(len(self.buckets)):
+            if self._flat[bi] is None:
+                self._launch(bi)
+        n = len(self._handles)
+        for bi, h in sorted(self._handles, key=lambda t: t[0]):
+            h.wait()
+            flat = self._flat[bi]
+            if self.average:
+                flat /= self.ws
+            off = 0
+            for p in self.buckets[bi]:
+                g = flat[off:off + p.numel()].view_as(p)
+                if p.grad is None:
+                    p.grad = g.clone()
+                else:
+                    p.grad.copy_(g)
+                off += p.numel()
+        self._handles = []
+        self._ready = [0] * len(self.buckets)
+        self._flat = [None] * len(self.buckets)
+        return n

@@ -126,3 +126,68 @@ def test_allreduce_grads_matches_full_batch():
     for g, p in zip(grads, net.parameters()):
         assert torch.allclose(g, p.grad, atol=1e-6)
     assert n >= 2  # 1 KiB buckets force more than one collective
+
+
+def _pretrain_worker(rank, ws, port, out_q, bucketed):
+    """One rank of data-parallel pretraining's contrastive head (models.py:472-497): z from a
+    shared projection of this rank's half batch, the all-gather keeping the local slot's graph,
+    gradients averaged by dp.GradBucketer (during backward) or dp.allreduce_grads (after)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        out = _pretrain_step(rank, ws, bucketed)
+        if rank == 0:
+            out_q.put(out)
+        else:
+            out_q.put(None)
+    finally:
+        dist.destroy_process_group()
+
+
+def _pretrain_step(rank, ws, bucketed):
+    import types
+
+    from recformer_amd import models
+    from recformer_amd.config import RecformerConfig
+    torch.manual_seed(0)
+    proj = torch.nn.Sequential(torch.nn.Linear(24, 32), torch.nn.Tanh(), torch.nn.Linear(32, 16))
+    xa, xb = torch.randn(6, 24), torch.randn(6, 24)
+    B = 6 // ws
+    xa, xb = xa[rank * B:(rank + 1) * B], xb[rank * B:(rank + 1) * B]
+    bucketer = dp.GradBucketer(proj.parameters(), bucket_bytes=1024) if bucketed else None
+    z1, z2 = proj(xa), proj(xb)
+    z1.retain_grad()
+    z2.retain_grad()
+    stub = types.SimpleNamespace(config=RecformerConfig(hidden_size=16, temp=0.05), training=True, lm_head=None)
+    outs = types.SimpleNamespace(hidden_states=None, attentions=None, global_attentions=None)
+    res = models._pretrain_train_losses(stub, z1, z2, outs, None, None, None, None, B)
+    res.loss.backward()
+    n = bucketer.finish() if bucketed else dp.allreduce_grads(list(proj.parameters()), bucket_bytes=1024)
+    return (float(res.loss), int(res.cl_correct_num), z1.grad.clone(), z2.grad.clone(),
+            [p.grad.clone() for p in proj.parameters()], n)
+
+
+@pytest.mark.parametrize("bucketed", [False, True])
+def test_pretrain_contrastive_dp_world2_matches_single_process(bucketed):
+    """world-2 gloo pretraining step (models.py:474-490 all_gather of z; local slot keeps its graph):
+    every rank's loss and correct count equal one process on the whole batch; each rank's dL/dz is
+    that process's gradient for its rows; the averaged parameter gradients are the single-process
+    ones / world size (the reference's DDP averaging of identical global losses)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pretrain_worker, args=(r, 2, port, q, bucketed)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    loss, correct, gz1, gz2, grads, n = [g for g in got if g is not None][0]
+    ref_loss, ref_correct, rz1, rz2, ref_grads, _ = _pretrain_step(0, 1, False)
+    assert loss == pytest.approx(ref_loss, rel=1e-6)
+    assert correct == ref_correct
+    assert torch.allclose(gz1, rz1[:3], atol=1e-6) and torch.allclose(gz2, rz2[:3], atol=1e-6)
+    for g, r in zip(grads, ref_grads):
+        assert torch.allclose(g * 2, r, atol=1e-5, rtol=1e-5)
+    assert n >= 2

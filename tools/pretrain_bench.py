@@ -1,6 +1,6 @@
 """C4 pretraining-step throughput (BASELINE configs[3]): RecformerForPretraining (two views,
 MLM on both, item-item contrastive with the z all-gather across ranks, models.py:382-520) forward +
-backward + bucketed RCCL gradient all-reduce (recformer_amd.dp.allreduce_grads) + AdamW, bf16
+backward + bucketed RCCL gradient all-reduce overlapped with it (recformer_amd.dp.GradBucketer) + AdamW, bf16
 autocast, 12L/768d. Per rank B sequences: view a = a 1024-token item prefix, view b = one item
 (<s> + 96 tokens -> 128), 15% of the tokens masked (mask id 50264, labels elsewhere -100).
 
@@ -70,12 +70,14 @@ def main():
     batch.update(mlm_input_ids_a=mlm_a, mlm_labels_a=lab_a, mlm_input_ids_b=mlm_b, mlm_labels_b=lab_b)
     batch = {k: v.to(dev) for k, v in batch.items()}
 
+    bucketer = dp.GradBucketer(model.parameters()) if world > 1 else None
+
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = model(**batch)
         out.loss.backward()
-        if world > 1:
-            dp.allreduce_grads(model.parameters())
+        if bucketer is not None:  # buckets were launched during backward; wait + average
+            bucketer.finish()
         opt.step()
         opt.zero_grad(set_to_none=True)
         return out
