@@ -14,7 +14,8 @@
  *    every call is asynchronous on it and safe to capture in a hipGraph;
  *  - matrices are row-major with explicit leading dimensions in ELEMENTS;
  *  - `dtype` selects the storage/compute type of activations and weights:
- *    RF_F32 (fp32 storage, exact-fp32 MFMA) or RF_BF16 (bf16 storage, fp32 accumulate);
+ *    RF_F32 (fp32 storage, exact-fp32 MFMA), RF_BF16 or RF_F16 (16-bit storage, fp32
+ *    accumulate; RF_F16 = the fp16 autocast of the reference's drivers);
  *    biases, LayerNorm affine parameters, norms and scores are always fp32;
  *  - return 0 on success; otherwise rf_last_error() holds a thread-local message.
  */
@@ -151,6 +152,14 @@ int rf_drop_add_ln_fwd_dual(int M, int D, const void* t, int ldt, const float* r
 int rf_drop_add_ln_bwd_dual(int M, int D, const float* dy, const void* dy16, const float* x, const float* mean,
                             const float* rstd, const float* w, float p, uint64_t seed, float* dres, void* dt,
                             float* dw, float* db, void* workspace, rf_stream_t stream);
+/* The same pair with the dense output t / y16 / dt / dy16 in dtype (RF_BF16 or RF_F16: the fp16
+ * autocast path, finetune.py:106-110). */
+int rf_drop_add_ln_fwd_t(int dtype, int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
+                         const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,
+                         void* y16, rf_stream_t stream);
+int rf_drop_add_ln_bwd_t(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
+                         const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
+                         void* dt, float* dw, float* db, void* workspace, rf_stream_t stream);
 /* Column sums out[n] = sum_m x[m][n] (fp32 out; x in dtype, row-major, leading dim ldx), two
  * deterministic stages through rf_colsum_workspace(M, N) bytes — the bias gradient of the
  * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias). */
@@ -206,8 +215,9 @@ int rf_band_attn_bwd_dt(int grad_dtype, int B, int Lp, int H, int hd, int half_w
                         int gmax, void* dq, void* dk, void* dv, int ld_grad, float* lse2,
                         float* delta, float* gds, float* gpr, rf_stream_t stream);
 /* rf_band_attn_bwd_dt for a forward run with attention-probability dropout (same p_drop, seed):
- * dP = mask/(1-p) o dO V^T, dS = P o (dP - dO.O); gpr holds the dropped probabilities. */
-int rf_band_attn_bwd_drop(int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
+ * dP = mask/(1-p) o dO V^T, dS = P o (dP - dO.O); gpr holds the dropped probabilities. Operands
+ * q/k/v/o/dout in dtype (RF_BF16 or RF_F16), gradients in grad_dtype (RF_F32 or dtype). */
+int rf_band_attn_bwd_drop(int dtype, int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
                           const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
                           const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx,
                           int gmax, void* dq, void* dk, void* dv, int ld_grad, float* lse2,

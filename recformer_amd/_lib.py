@@ -46,6 +46,10 @@ SIGNATURES = {
                                         P, P, P]),
     "rf_drop_add_ln_bwd_dual": (c_int, [c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
                                         P]),
+    "rf_drop_add_ln_fwd_t": (c_int, [c_int, c_int, c_int, P, c_int, P, c_float, ctypes.c_uint64, P, P, c_float, P, P,
+                                     P, P, P, P]),
+    "rf_drop_add_ln_bwd_t": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
+                                     P]),
     "rf_colsum_workspace": (ctypes.c_size_t, [c_int, c_int]),
     "rf_scatter_add_rows": (c_int, [c_int, c_int, c_int, P, P, P, c_int, P, P, c_int, P]),
     "rf_colsum": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, P, P]),
@@ -58,7 +62,7 @@ SIGNATURES = {
                                     P, P, c_int, P, P, P, c_int, P, P, P, P, P]),
     "rf_band_attn_fwd_drop": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
                                       c_int, P, c_int, c_float, ctypes.c_uint64, P]),
-    "rf_band_attn_bwd_drop": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, c_int, P,
+    "rf_band_attn_bwd_drop": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, c_int, P,
                                       c_int, P, P, c_int, P, P, P, c_int, P, P, P, P, c_float, ctypes.c_uint64, P]),
     "rf_global_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P,
                                    P, c_int, P, c_int, P]),

@@ -57,17 +57,22 @@ __device__ __forceinline__ void tr_read2(uint32_t a0, uint32_t a1, bf16x4& v0, b
       : "memory");
 }
 
-__device__ __forceinline__ bf16x4 tr_read(const char* lds_base, int off) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds_base + off));
+template <typename E>
+__device__ __forceinline__ typename H16<E>::x4 tr_read(const char* lds_base, int off) {
+  // the transposed 16-bit read moves bit patterns: one instruction for bf16 and fp16
+  return __builtin_bit_cast(typename H16<E>::x4, __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds_base + off)));
 }
 
-__global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __restrict__ q,
-                                                         const bf16* __restrict__ k,
-                                                         const bf16* __restrict__ v, int ld,
+template <typename E>
+__global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const E* __restrict__ q,
+                                                         const E* __restrict__ k,
+                                                         const E* __restrict__ v, int ld,
                                                          const uint8_t* __restrict__ flags,
                                                          const int32_t* __restrict__ gidx,
-                                                         int gmax, bf16* __restrict__ out,
+                                                         int gmax, E* __restrict__ out,
                                                          int ldo, int H) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
   __shared__ __attribute__((aligned(16))) char smem[AT_LDS];
   // 1-D grid, XCD-remapped: the Lp/64 query blocks of one (sequence, head) are consecutive
   // on one XCD, so the half-overlapping K/V windows of neighbouring blocks hit its L2
@@ -117,10 +122,10 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __re
   const int qw = i0 + 16 * wave;
   const int myq = qw + li;
   const int ks = min(16 * wave, 32);  // first LDS window row of the wave's 96-key span
-  bf16x8 qf[2];
+  V8 qf[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s)
-    qf[s] = *reinterpret_cast<const bf16x8*>(q + (rb + myq) * ld + hoff + 32 * s + 8 * g);
+    qf[s] = *reinterpret_cast<const V8*>(q + (rb + myq) * ld + hoff + 32 * s + 8 * g);
 
   wait_vmcnt0();
   __syncthreads();
@@ -132,8 +137,8 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __re
     st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(smem + AT_KW + swz128(ks + 16 * t + li, 4 * s + g));
-      st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], st[t], 0, 0, 0);
+      const V8 kf = *reinterpret_cast<const V8*>(smem + AT_KW + swz128(ks + 16 * t + li, 4 * s + g));
+      st[t] = mfma16(kf, qf[s], st[t]);
     }
   }
   float mx = RF_NEG_INF;
@@ -169,19 +174,19 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __re
   // PV: 3 k-steps of 32 keys; key(g, j) = 32*s + 16*(j>>2) + 4*g + (j&3)
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
-    bf16x8 pf;
+    V8 pf;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pf[j] = (bf16)st[2 * s + (j >> 2)][j & 3];
+    for (int j = 0; j < 8; ++j) pf[j] = (E)st[2 * s + (j >> 2)][j & 3];
     const int r0 = ks + 32 * s + 4 * g + (li >> 2);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const int col = 16 * dt + 4 * (li & 3);
-      const bf16x4 v0 = tr_read(smem + AT_VW, swz_el(r0, col));
-      const bf16x4 v1 = tr_read(smem + AT_VW, swz_el(r0 + 16, col));
-      bf16x8 vf;
+      const V4 v0 = tr_read<E>(smem + AT_VW, swz_el(r0, col));
+      const V4 v1 = tr_read<E>(smem + AT_VW, swz_el(r0 + 16, col));
+      V8 vf;
       vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v0[2]; vf[3] = v0[3];
       vf[4] = v1[0]; vf[5] = v1[1]; vf[6] = v1[2]; vf[7] = v1[3];
-      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+      o[dt] = mfma16(vf, pf, o[dt]);
     }
   }
 
@@ -199,8 +204,8 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __re
       sg[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(smem + AT_KG + swz128(16 * t + li, 4 * s + g));
-        sg[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], sg[t], 0, 0, 0);
+        const V8 kf = *reinterpret_cast<const V8*>(smem + AT_KG + swz128(16 * t + li, 4 * s + g));
+        sg[t] = mfma16(kf, qf[s], sg[t]);
       }
     }
     float cmx = RF_NEG_INF;
@@ -230,19 +235,19 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __re
         lsum += p;
       }
     m = mn;
-    bf16x8 pf;
+    V8 pf;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pf[j] = (bf16)sg[j >> 2][j & 3];
+    for (int j = 0; j < 8; ++j) pf[j] = (E)sg[j >> 2][j & 3];
     const int r0 = 4 * g + (li >> 2);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const int col = 16 * dt + 4 * (li & 3);
-      const bf16x4 v0 = tr_read(smem + AT_VG, swz_el(r0, col));
-      const bf16x4 v1 = tr_read(smem + AT_VG, swz_el(r0 + 16, col));
-      bf16x8 vf;
+      const V4 v0 = tr_read<E>(smem + AT_VG, swz_el(r0, col));
+      const V4 v1 = tr_read<E>(smem + AT_VG, swz_el(r0 + 16, col));
+      V8 vf;
       vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v0[2]; vf[3] = v0[3];
       vf[4] = v1[0]; vf[5] = v1[1]; vf[6] = v1[2]; vf[7] = v1[3];
-      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+      o[dt] = mfma16(vf, pf, o[dt]);
     }
   }
 
@@ -251,13 +256,13 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const bf16* __re
   lsum += __shfl_xor(lsum, 32, 64);
   const bool qvalid = fl[32 + 16 * wave + li] != 0;
   const float inv = (qvalid && lsum > 0.f) ? 1.0f / lsum : 0.f;
-  bf16* orow = out + (rb + myq) * ldo + hoff + 4 * g;
+  E* orow = out + (rb + myq) * ldo + hoff + 4 * g;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    bf16x4 w;
+    V4 w;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) w[r] = (bf16)(qvalid ? o[dt][r] * inv : 0.f);
-    *reinterpret_cast<bf16x4*>(orow + 16 * dt) = w;
+    for (int r = 0; r < 4; ++r) w[r] = (E)(qvalid ? o[dt][r] * inv : 0.f);
+    *reinterpret_cast<V4*>(orow + 16 * dt) = w;
   }
 }
 
@@ -567,7 +572,8 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe(int Lp, int H, int qpb, 
 //    online rescale of O); their K fragments and V^T fragments are loop-invariant registers;
 //  - masks: one bit-extract + bit-select per score; ring-slot and DMA offsets are wave-uniform
 //    or 24-bit products precomputed per lane; V^T reads are batched 8 per wait.
-__device__ __forceinline__ void tr_read8(const uint32_t* a, bf16x4* v) {
+template <typename V4>
+__device__ __forceinline__ void tr_read8(const uint32_t* a, V4* v) {
   asm volatile(
       "ds_read_b64_tr_b16 %0, %8\n\t"
       "ds_read_b64_tr_b16 %1, %9\n\t"
@@ -597,13 +603,15 @@ __device__ __forceinline__ float mask_score(unsigned int bits, int bit, float sv
 #endif
 // DROP (training): attention-probability dropout (TF:585-586) on the probabilities that enter
 // P.V; the normaliser is the undropped row sum, as softmax-then-dropout.
-template <bool DROP>
-__global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb, const bf16* __restrict__ q,
-                                                          const bf16* __restrict__ k,
-                                                          const bf16* __restrict__ v, int ld,
+template <typename E, bool DROP>
+__global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb, const E* __restrict__ q,
+                                                          const E* __restrict__ k,
+                                                          const E* __restrict__ v, int ld,
                                                           const uint8_t* __restrict__ flags,
                                                           const int32_t* __restrict__ gidx, int gmax,
-                                                          bf16* __restrict__ out, int ldo, AttnDrop dr) {
+                                                          E* __restrict__ out, int ldo, AttnDrop dr) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
   const int nparts = (nqb + qpb - 1) / qpb;
@@ -615,10 +623,10 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int64_t rb = (int64_t)b * Lp;
-  const bf16* kb = k + rb * ld + h * 64;
-  const bf16* vb = v + rb * ld + h * 64;
-  const bf16* qb = q + rb * ld + h * 64;
-  bf16* ob = out + rb * ldo + h * 64;
+  const E* kb = k + rb * ld + h * 64;
+  const E* vb = v + rb * ld + h * 64;
+  const E* qb = q + rb * ld + h * 64;
+  E* ob = out + rb * ldo + h * 64;
   int* gp = reinterpret_cast<int*>(smem + AP_GP);
   unsigned long long* mk = reinterpret_cast<unsigned long long*>(smem + AP_MK);
   const int gt = gmax > 16 ? 2 : (gmax > 0 ? 1 : 0);  // 16-key tiles of global keys
@@ -678,7 +686,7 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
   // band bits of the wave's 80-key span [16w, 16w + 80): relative rows [li, li + 64]
   const unsigned int band0 = ~0u << li, band2 = (2u << li) - 1u;
 
-  bf16x8 kgf[2][2], vgf[4];
+  V8 kgf[2][2], vgf[4];
   unsigned int gbits = 0;
   for (int x = x0; x < x1; ++x) {
     // retire chunks x, x+1 and Q(x); still in flight (issue order, newest last): the O stores of
@@ -691,9 +699,9 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
-          kgf[t][s2] = *reinterpret_cast<const bf16x8*>(smem + AP_KG + t * 2048 + koff[s2]);
+          kgf[t][s2] = *reinterpret_cast<const V8*>(smem + AP_KG + t * 2048 + koff[s2]);
       uint32_t a[8];
-      bf16x4 vv[8];
+      V4 vv[8];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         a[2 * dt] = lds0 + AP_VG + voff[dt];
@@ -702,7 +710,7 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
       tr_read8(a, vv);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        vgf[dt] = bf16x8{vv[2 * dt][0], vv[2 * dt][1], vv[2 * dt][2], vv[2 * dt][3],
+        vgf[dt] = V8{vv[2 * dt][0], vv[2 * dt][1], vv[2 * dt][2], vv[2 * dt][3],
                          vv[2 * dt + 1][0], vv[2 * dt + 1][1], vv[2 * dt + 1][2], vv[2 * dt + 1][3]};
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -713,10 +721,10 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
     const int sb0 = AP_KV + (x % 3) * 16384, sb1 = AP_KV + ((x + 1) % 3) * 16384;
     const unsigned long long ml0 = mk[2 * (x - x0)], ml1 = mk[2 * (x - x0) + 2];
     const unsigned long long mv0 = mk[2 * (x - x0) + 1], mv1 = mk[2 * (x - x0) + 3];
-    bf16x8 qf[2];
+    V8 qf[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
-      qf[s2] = *reinterpret_cast<const bf16x8*>(smem + AP_Q + (x & 1) * 8192 + 16 * wave * 128 + koff[s2]);
+      qf[s2] = *reinterpret_cast<const V8*>(smem + AP_Q + (x & 1) * 8192 + 16 * wave * 128 + koff[s2]);
 
     // ---- scores: 5 local key tiles (window rows 16w + 16t) + gt global tiles ----
     f32x4 st[5], sg[2];
@@ -727,8 +735,8 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
       st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
-        st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(kt + koff[s2]), qf[s2],
-                                                        st[t], 0, 0, 0);
+        st[t] = mfma16(*reinterpret_cast<const V8*>(kt + koff[s2]), qf[s2],
+                                                        st[t]);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -736,7 +744,7 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
       if (t < gt) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
-          sg[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kgf[t][s2], qf[s2], sg[t], 0, 0, 0);
+          sg[t] = mfma16(kgf[t][s2], qf[s2], sg[t]);
       }
     }
     // allowed local keys: valid & local (chunk ballots) & band, as 3 words over the span,
@@ -792,19 +800,19 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
     const uint64_t drow = DROP ? ((uint64_t)bh * Lp + i0 + 16 * wave + li) : 0;
 #pragma unroll
     for (int s2 = 0; s2 < 3; ++s2) {
-      bf16x8 pf;
+      V8 pf;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int t = 2 * s2 + (j >> 2);
         float pv = t < 5 ? st[t < 5 ? t : 4][j & 3] : 0.f;
         if (DROP && t < 5) pv *= attn_keep_scale(dr, drow, Lp, i0 - 32 + 16 * wave + 16 * t + 4 * g + (j & 3));
-        pf[j] = (bf16)pv;
+        pf[j] = (E)pv;
       }
       const int ga = 16 * wave + 32 * s2, gb = s2 < 2 ? ga + 16 : ga;  // finite rows for p = 0
       const uint32_t va = lds0 + (ga >= 64 ? sb1 : sb0) + 8192 + (ga & 63) * 128;
       const uint32_t vb2 = lds0 + (gb >= 64 ? sb1 : sb0) + 8192 + (gb & 63) * 128;
       uint32_t a[8];
-      bf16x4 vv[8];
+      V4 vv[8];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         a[2 * dt] = va + voff[dt];
@@ -813,13 +821,13 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
       tr_read8(a, vv);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8 vf = bf16x8{vv[2 * dt][0], vv[2 * dt][1], vv[2 * dt][2], vv[2 * dt][3],
+        const V8 vf = V8{vv[2 * dt][0], vv[2 * dt][1], vv[2 * dt][2], vv[2 * dt][3],
                                  vv[2 * dt + 1][0], vv[2 * dt + 1][1], vv[2 * dt + 1][2], vv[2 * dt + 1][3]};
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+        o[dt] = mfma16(vf, pf, o[dt]);
       }
     }
     if (gt > 0) {
-      bf16x8 pf;
+      V8 pf;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float pv = sg[j >> 2][j & 3];
@@ -827,10 +835,10 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
           const int gk = gp[16 * (j >> 2) + 4 * g + (j & 3)];
           pv *= gk >= 0 ? attn_keep_scale(dr, drow, Lp, gk) : 0.f;
         }
-        pf[j] = (bf16)pv;
+        pf[j] = (E)pv;
       }
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vgf[dt], pf, o[dt], 0, 0, 0);
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(vgf[dt], pf, o[dt]);
     }
 
     lsum += __shfl_xor(lsum, 16, 64);
@@ -848,16 +856,16 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
     char* ostg = smem + sb0 + wave * 2048;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      bf16x4 w;
+      V4 w;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv);
-      *reinterpret_cast<bf16x4*>(ostg + li * 128 + (((2 * dt + (g >> 1)) ^ (li & 7)) << 4) + (g & 1) * 8) = w;
+      for (int r = 0; r < 4; ++r) w[r] = (E)(o[dt][r] * inv);
+      *reinterpret_cast<V4*>(ostg + li * 128 + (((2 * dt + (g >> 1)) ^ (li & 7)) << 4) + (g & 1) * 8) = w;
     }
-    bf16x8 ov[2];
+    V8 ov[2];
 #pragma unroll
     for (int p2 = 0; p2 < 2; ++p2) {
       const int orow = 8 * p2 + (lane >> 3);
-      ov[p2] = *reinterpret_cast<const bf16x8*>(ostg + orow * 128 + (((lane & 7) ^ (orow & 7)) << 4));
+      ov[p2] = *reinterpret_cast<const V8*>(ostg + orow * 128 + (((lane & 7) ^ (orow & 7)) << 4));
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (x + 3 <= x1) dma_chunk(x + 3);
@@ -865,7 +873,7 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
 #pragma unroll
     for (int p2 = 0; p2 < 2; ++p2) {
       const int orow = 8 * p2 + (lane >> 3);
-      *reinterpret_cast<bf16x8*>(ob + __umul24(i0 + 16 * wave + orow, ldo) + (lane & 7) * 8) = ov[p2];
+      *reinterpret_cast<V8*>(ob + __umul24(i0 + 16 * wave + orow, ldo) + (lane & 7) * 8) = ov[p2];
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1036,7 +1044,8 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
   RF_REQUIRE(gmax == 0 || gidx, "rf_band_attn_fwd: gidx required");
   if (B == 0 || Lp == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
-  if (dtype == RF_BF16) {
+  if (dtype == RF_BF16 || dtype == RF_F16) {
+    const bool h16 = dtype == RF_F16;
     RF_REQUIRE(half_w == 32, "rf_band_attn_fwd(bf16): window must be 64 (half 32), got half %d", half_w);
     RF_REQUIRE(Lp % 64 == 0, "rf_band_attn_fwd(bf16): Lp=%d must be a multiple of 64", Lp);
     RF_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0, "rf_band_attn_fwd(bf16): alignment");
@@ -1054,31 +1063,42 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
         attr = true;
       }
       RF_REQUIRE(lds <= 80000, "rf_band_attn_fwd(bf16): Lp=%d too long for the pipelined kernel", Lp);
-      if (g_knob[KNOB_BAND_PATH] == 1 && dr.thresh == 0) {
+      if (g_knob[KNOB_BAND_PATH] == 1 && dr.thresh == 0 && !h16) {
         k_band_attn_pipe<<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
                                                            (const bf16*)v, ld_qkv, flags, gidx, gmax,
                                                            (bf16*)out, ld_out);
       } else {
         static bool attr2 = false;
         if (!attr2) {
-          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    80000);
-          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    80000);
+          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2<bf16, false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80000);
+          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2<bf16, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80000);
+          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2<f16, false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80000);
+          (void)hipFuncSetAttribute((const void*)k_band_attn_pipe2<f16, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80000);
           attr2 = true;
         }
-        if (dr.thresh)
-          k_band_attn_pipe2<true><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
-                                                                   (const bf16*)v, ld_qkv, flags, gidx, gmax,
-                                                                   (bf16*)out, ld_out, dr);
-        else
-          k_band_attn_pipe2<false><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q, (const bf16*)k,
-                                                                    (const bf16*)v, ld_qkv, flags, gidx, gmax,
-                                                                    (bf16*)out, ld_out, dr);
+#define P2_(E, D) k_band_attn_pipe2<E, D><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const E*)q, (const E*)k, \
+                                                                       (const E*)v, ld_qkv, flags, gidx, gmax,   \
+                                                                       (E*)out, ld_out, dr)
+        if (h16) {
+          if (dr.thresh) P2_(f16, true);
+          else P2_(f16, false);
+        } else {
+          if (dr.thresh) P2_(bf16, true);
+          else P2_(bf16, false);
+        }
+#undef P2_
       }
     } else {
-      k_band_attn_bf16<<<(Lp / 64) * H * B, 256, 0, s>>>(Lp, (const bf16*)q, (const bf16*)k, (const bf16*)v,
-                                                         ld_qkv, flags, gidx, gmax, (bf16*)out, ld_out, H);
+      if (h16)
+        k_band_attn_bf16<f16><<<(Lp / 64) * H * B, 256, 0, s>>>(Lp, (const f16*)q, (const f16*)k, (const f16*)v,
+                                                                ld_qkv, flags, gidx, gmax, (f16*)out, ld_out, H);
+      else
+        k_band_attn_bf16<bf16><<<(Lp / 64) * H * B, 256, 0, s>>>(Lp, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                                                                 ld_qkv, flags, gidx, gmax, (bf16*)out, ld_out, H);
     }
   } else if (dtype == RF_F32) {
     RF_REQUIRE(half_w > 0, "rf_band_attn_fwd: bad half window");
@@ -1107,6 +1127,9 @@ extern "C" int rf_global_attn_fwd(int dtype, int B, int Lp, int H, int hd, const
     k_global_attn<bf16><<<grid, 256, lds, s>>>(Lp, (const bf16*)qg, ld_qg, (const bf16*)kg,
                                                (const bf16*)vg, ld_kv, flags, gidx, gmax,
                                                (bf16*)out, ld_out);
+  else if (dtype == RF_F16)
+    k_global_attn<f16><<<grid, 256, lds, s>>>(Lp, (const f16*)qg, ld_qg, (const f16*)kg, (const f16*)vg, ld_kv, flags,
+                                              gidx, gmax, (f16*)out, ld_out);
   else if (dtype == RF_F32)
     k_global_attn<float><<<grid, 256, lds, s>>>(Lp, (const float*)qg, ld_qg, (const float*)kg,
                                                 (const float*)vg, ld_kv, flags, gidx, gmax,

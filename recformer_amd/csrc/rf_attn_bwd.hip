@@ -18,6 +18,8 @@
 //                  their gradient from the host reduction).
 // Query rows that are padding or global (flag != 1) carry no local gradient: their dO is
 // treated as 0 (lse = +inf, delta = 0).
+#include <type_traits>
+
 #include "rf_common.h"
 
 namespace rf {
@@ -26,19 +28,24 @@ constexpr float BW_NEG_INF = -__builtin_inff();
 constexpr float BW_LOG2E = 1.4426950408889634f;
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_b;
-__device__ __forceinline__ bf16x4 trr(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_b*)p);
+template <typename E>
+__device__ __forceinline__ typename H16<E>::x4 trr(const char* p) {  // 16-bit transposed read (bit patterns)
+  return __builtin_bit_cast(typename H16<E>::x4, __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_b*)p));
 }
 __device__ __forceinline__ int bswz128(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
 __device__ __forceinline__ int bswz_el(int row, int col) {
   return row * 128 + (((col >> 3) ^ (row & 7)) << 4) + ((col & 7) << 1);
 }
-__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
-  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+template <typename V4>
+__device__ __forceinline__ auto cat8(V4 a, V4 b) {
+  typedef decltype(a[0]) E0;
+  typedef typename std::remove_cv<typename std::remove_reference<E0>::type>::type E;
+  return typename H16<E>::x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 // 8-row x 128-B DMA piece `pc` of a [rows][64 bf16] image: rows pc*8 + lane/8 of `base`
 // (row index clamped into [0, Lp)), source chunk swizzled so the image is XOR-swizzled.
-__device__ __forceinline__ void dma_rows(const bf16* base, int ld, int row0, int Lp, char* img, int pc,
+template <typename E>
+__device__ __forceinline__ void dma_rows(const E* base, int ld, int row0, int Lp, char* img, int pc,
                                          int lane) {
   const int row = pc * 8 + (lane >> 3);
   const int ch = (lane & 7) ^ (row & 7);
@@ -62,17 +69,21 @@ __device__ __forceinline__ void store_g4(float* p, f32x4 v) { *reinterpret_cast<
 __device__ __forceinline__ void store_g4(bf16* p, f32x4 v) {
   *reinterpret_cast<bf16x4*>(p) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
 }
+__device__ __forceinline__ void store_g4(f16* p, f32x4 v) {
+  *reinterpret_cast<f16x4*>(p) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+}
 
-template <typename GT>
-__global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* __restrict__ q,
-                                                     const bf16* __restrict__ k, const bf16* __restrict__ v,
-                                                     int ld, const bf16* __restrict__ o, int ldo,
-                                                     const bf16* __restrict__ dout, int ldd,
+template <typename E, typename GT>
+__global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const E* __restrict__ q,
+                                                     const E* __restrict__ k, const E* __restrict__ v,
+                                                     int ld, const E* __restrict__ o, int ldo,
+                                                     const E* __restrict__ dout, int ldd,
                                                      const uint8_t* __restrict__ flags,
                                                      const int32_t* __restrict__ gidx, int gmax,
                                                      GT* __restrict__ dq, int lddq, float* __restrict__ lse2,
                                                      float* __restrict__ delta, float* __restrict__ gds,
                                                      float* __restrict__ gpr, AttnDrop dr) {
+  typedef typename H16<E>::x8 V8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -83,10 +94,10 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* _
   const int g = lane >> 4, li = lane & 15;
   const int64_t rb = (int64_t)b * Lp;
   const int i0 = 64 * x;
-  const bf16* qh = q + rb * ld + h * 64;
-  const bf16* kh = k + rb * ld + h * 64;
-  const bf16* vh = v + rb * ld + h * 64;
-  const bf16* dh = dout + rb * ldd + h * 64;
+  const E* qh = q + rb * ld + h * 64;
+  const E* kh = k + rb * ld + h * 64;
+  const E* vh = v + rb * ld + h * 64;
+  const E* dh = dout + rb * ldd + h * 64;
   int* gp = reinterpret_cast<int*>(smem + BQ_GP);
   unsigned long long* mk = reinterpret_cast<unsigned long long*>(smem + BQ_MK);
   const int gt = gmax > 16 ? 2 : (gmax > 0 ? 1 : 0);
@@ -119,18 +130,18 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* _
   // this lane's query and its O fragment (delta = dO . O)
   const int myq = i0 + 16 * wave + li;
   const bool qv = flags[rb + myq] == 1;
-  bf16x8 of[2];
+  V8 of[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
-    of[s2] = *reinterpret_cast<const bf16x8*>(o + (rb + myq) * ldo + h * 64 + 32 * s2 + 8 * g);
+    of[s2] = *reinterpret_cast<const V8*>(o + (rb + myq) * ldo + h * 64 + 32 * s2 + 8 * g);
   wait_vmcnt0();
   __syncthreads();
 
-  bf16x8 qf[2], df[2];
+  V8 qf[2], df[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
-    qf[s2] = *reinterpret_cast<const bf16x8*>(smem + BQ_Q + bswz128(16 * wave + li, 4 * s2 + g));
-    df[s2] = qv ? *reinterpret_cast<const bf16x8*>(smem + BQ_DO + bswz128(16 * wave + li, 4 * s2 + g)) : bf16x8{};
+    qf[s2] = *reinterpret_cast<const V8*>(smem + BQ_Q + bswz128(16 * wave + li, 4 * s2 + g));
+    df[s2] = qv ? *reinterpret_cast<const V8*>(smem + BQ_DO + bswz128(16 * wave + li, 4 * s2 + g)) : V8{};
   }
   float dl = 0.f;
 #pragma unroll
@@ -149,10 +160,10 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* _
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const int off = bswz128(16 * wave + 16 * t + li, 4 * s2 + g);
-      st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(smem + BQ_K + off), qf[s2],
-                                                      st[t], 0, 0, 0);
-      dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(smem + BQ_V + off), df[s2],
-                                                      dp[t], 0, 0, 0);
+      st[t] = mfma16(*reinterpret_cast<const V8*>(smem + BQ_K + off), qf[s2],
+                                                      st[t]);
+      dp[t] = mfma16(*reinterpret_cast<const V8*>(smem + BQ_V + off), df[s2],
+                                                      dp[t]);
     }
   }
 #pragma unroll
@@ -163,10 +174,10 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* _
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int off = bswz128(16 * t + li, 4 * s2 + g);
-        sg[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(smem + BQ_KG + off),
-                                                        qf[s2], sg[t], 0, 0, 0);
-        dg[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(smem + BQ_VG + off),
-                                                        df[s2], dg[t], 0, 0, 0);
+        sg[t] = mfma16(*reinterpret_cast<const V8*>(smem + BQ_KG + off),
+                                                        qf[s2], sg[t]);
+        dg[t] = mfma16(*reinterpret_cast<const V8*>(smem + BQ_VG + off),
+                                                        df[s2], dg[t]);
       }
     }
   }
@@ -252,29 +263,29 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const bf16* _
   const int rr = 4 * g + (li >> 2);
 #pragma unroll
   for (int s2 = 0; s2 < 3; ++s2) {
-    bf16x8 pf;
+    V8 pf;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int t = 2 * s2 + (j >> 2);
-      pf[j] = (bf16)(t < 5 ? dp[t < 5 ? t : 4][j & 3] : 0.f);
+      pf[j] = (E)(t < 5 ? dp[t < 5 ? t : 4][j & 3] : 0.f);
     }
     const int ga = 16 * wave + 32 * s2, gb = s2 < 2 ? ga + 16 : ga;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const int col = 16 * dt + 4 * (li & 3);
-      const bf16x8 kf = cat8(trr(smem + BQ_K + bswz_el(ga + rr, col)), trr(smem + BQ_K + bswz_el(gb + rr, col)));
-      acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, pf, acc[dt], 0, 0, 0);
+      const V8 kf = cat8(trr<E>(smem + BQ_K + bswz_el(ga + rr, col)), trr<E>(smem + BQ_K + bswz_el(gb + rr, col)));
+      acc[dt] = mfma16(kf, pf, acc[dt]);
     }
   }
   if (gt > 0) {
-    bf16x8 pf;
+    V8 pf;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pf[j] = (bf16)dg[j >> 2][j & 3];
+    for (int j = 0; j < 8; ++j) pf[j] = (E)dg[j >> 2][j & 3];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const int col = 16 * dt + 4 * (li & 3);
-      const bf16x8 kf = cat8(trr(smem + BQ_KG + bswz_el(rr, col)), trr(smem + BQ_KG + bswz_el(16 + rr, col)));
-      acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, pf, acc[dt], 0, 0, 0);
+      const V8 kf = cat8(trr<E>(smem + BQ_KG + bswz_el(rr, col)), trr<E>(smem + BQ_KG + bswz_el(16 + rr, col)));
+      acc[dt] = mfma16(kf, pf, acc[dt]);
     }
   }
   GT* dqr = dq + (rb + myq) * lddq + h * 64 + 4 * g;
@@ -306,14 +317,15 @@ constexpr int BK_L = 49152;    // 128 float lse2
 constexpr int BK_D = 49664;    // 128 float delta
 constexpr int BK_LDS = 50176;
 
-template <typename GT>
-__global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* __restrict__ q,
-                                                      const bf16* __restrict__ k, const bf16* __restrict__ v,
-                                                      int ld, const bf16* __restrict__ dout, int ldd,
+template <typename E, typename GT>
+__global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const E* __restrict__ q,
+                                                      const E* __restrict__ k, const E* __restrict__ v,
+                                                      int ld, const E* __restrict__ dout, int ldd,
                                                       const uint8_t* __restrict__ flags,
                                                       const float* __restrict__ lse2,
                                                       const float* __restrict__ delta, GT* __restrict__ dk,
                                                       GT* __restrict__ dv, int lddkv, AttnDrop dr) {
+  typedef typename H16<E>::x8 V8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -324,10 +336,10 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
   const int g = lane >> 4, li = lane & 15;
   const int64_t rb = (int64_t)b * Lp;
   const int j0 = 64 * y;
-  const bf16* qh = q + rb * ld + h * 64;
-  const bf16* kh = k + rb * ld + h * 64;
-  const bf16* vh = v + rb * ld + h * 64;
-  const bf16* dh = dout + rb * ldd + h * 64;
+  const E* qh = q + rb * ld + h * 64;
+  const E* kh = k + rb * ld + h * 64;
+  const E* vh = v + rb * ld + h * 64;
+  const E* dh = dout + rb * ldd + h * 64;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     dma_rows(kh, ld, j0, Lp, smem + BK_K, 2 * wave + j, lane);
@@ -352,11 +364,11 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
   wait_vmcnt0();
   __syncthreads();
 
-  bf16x8 kb[2], vb[2];
+  V8 kb[2], vb[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
-    kb[s2] = *reinterpret_cast<const bf16x8*>(smem + BK_K + bswz128(16 * wave + li, 4 * s2 + g));
-    vb[s2] = *reinterpret_cast<const bf16x8*>(smem + BK_V + bswz128(16 * wave + li, 4 * s2 + g));
+    kb[s2] = *reinterpret_cast<const V8*>(smem + BK_K + bswz128(16 * wave + li, 4 * s2 + g));
+    vb[s2] = *reinterpret_cast<const V8*>(smem + BK_V + bswz128(16 * wave + li, 4 * s2 + g));
   }
   // S and dP for query window rows 16w + 16t + 4g + r (t < 5) against this lane's key
   f32x4 st[5], dp[5];
@@ -367,10 +379,10 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const int off = bswz128(16 * wave + 16 * t + li, 4 * s2 + g);
-      st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(smem + BK_Q + off), kb[s2],
-                                                      st[t], 0, 0, 0);
-      dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(smem + BK_DO + off), vb[s2],
-                                                      dp[t], 0, 0, 0);
+      st[t] = mfma16(*reinterpret_cast<const V8*>(smem + BK_Q + off), kb[s2],
+                                                      st[t]);
+      dp[t] = mfma16(*reinterpret_cast<const V8*>(smem + BK_DO + off), vb[s2],
+                                                      dp[t]);
     }
   }
   // band: query span index 16t + 4g + r in [li, li + 64]; P from the saved row lse (log2)
@@ -403,21 +415,21 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
   const int rr = 4 * g + (li >> 2);
 #pragma unroll
   for (int s2 = 0; s2 < 3; ++s2) {
-    bf16x8 pf, sf;
+    V8 pf, sf;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int t = 2 * s2 + (j >> 2);
-      pf[j] = (bf16)(t < 5 ? st[t < 5 ? t : 4][j & 3] : 0.f);
-      sf[j] = (bf16)(t < 5 ? dp[t < 5 ? t : 4][j & 3] : 0.f);
+      pf[j] = (E)(t < 5 ? st[t < 5 ? t : 4][j & 3] : 0.f);
+      sf[j] = (E)(t < 5 ? dp[t < 5 ? t : 4][j & 3] : 0.f);
     }
     const int ga = 16 * wave + 32 * s2, gb = s2 < 2 ? ga + 16 : ga;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const int col = 16 * dt + 4 * (li & 3);
-      const bf16x8 df = cat8(trr(smem + BK_DO + bswz_el(ga + rr, col)), trr(smem + BK_DO + bswz_el(gb + rr, col)));
-      const bf16x8 qf = cat8(trr(smem + BK_Q + bswz_el(ga + rr, col)), trr(smem + BK_Q + bswz_el(gb + rr, col)));
-      av[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df, pf, av[dt], 0, 0, 0);
-      ak[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf, sf, ak[dt], 0, 0, 0);
+      const V8 df = cat8(trr<E>(smem + BK_DO + bswz_el(ga + rr, col)), trr<E>(smem + BK_DO + bswz_el(gb + rr, col)));
+      const V8 qf = cat8(trr<E>(smem + BK_Q + bswz_el(ga + rr, col)), trr<E>(smem + BK_Q + bswz_el(gb + rr, col)));
+      av[dt] = mfma16(df, pf, av[dt]);
+      ak[dt] = mfma16(qf, sf, ak[dt]);
     }
   }
   GT* dkr = dk + (rb + myk) * lddkv + h * 64 + 4 * g;
@@ -433,33 +445,35 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const bf16* 
 
 using namespace rf;
 
-template <typename GT>
+template <typename E, typename GT>
 static void launch_band_bwd(int B, int Lp, int H, const void* q, const void* k, const void* v, int ld_qkv,
                             const void* o, int ld_o, const void* dout, int ld_do, const uint8_t* flags,
                             const int32_t* gidx, int gmax, GT* dq, GT* dk, GT* dv, int ld_grad, float* lse2,
                             float* delta, float* gds, float* gpr, const AttnDrop& dr, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_band_bwd_q<GT>, hipFuncAttributeMaxDynamicSharedMemorySize, BQ_LDS);
-    (void)hipFuncSetAttribute((const void*)k_band_bwd_kv<GT>, hipFuncAttributeMaxDynamicSharedMemorySize, BK_LDS);
+    (void)hipFuncSetAttribute((const void*)k_band_bwd_q<E, GT>, hipFuncAttributeMaxDynamicSharedMemorySize, BQ_LDS);
+    (void)hipFuncSetAttribute((const void*)k_band_bwd_kv<E, GT>, hipFuncAttributeMaxDynamicSharedMemorySize, BK_LDS);
     attr = true;
   }
   const int nblk = (Lp / 64) * H * B;
-  k_band_bwd_q<GT><<<nblk, 256, BQ_LDS, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
-                                             (const bf16*)o, ld_o, (const bf16*)dout, ld_do, flags, gidx, gmax, dq,
+  k_band_bwd_q<E, GT><<<nblk, 256, BQ_LDS, s>>>(Lp, H, (const E*)q, (const E*)k, (const E*)v, ld_qkv,
+                                             (const E*)o, ld_o, (const E*)dout, ld_do, flags, gidx, gmax, dq,
                                              ld_grad, lse2, delta, gds, gpr, dr);
-  k_band_bwd_kv<GT><<<nblk, 256, BK_LDS, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
-                                              (const bf16*)dout, ld_do, flags, lse2, delta, dk, dv, ld_grad, dr);
+  k_band_bwd_kv<E, GT><<<nblk, 256, BK_LDS, s>>>(Lp, H, (const E*)q, (const E*)k, (const E*)v, ld_qkv,
+                                              (const E*)dout, ld_do, flags, lse2, delta, dk, dv, ld_grad, dr);
 }
 
-extern "C" int rf_band_attn_bwd_drop(int grad_dtype, int B, int Lp, int H, int hd, int half_w, const void* q,
-                                     const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
+extern "C" int rf_band_attn_bwd_drop(int dtype, int grad_dtype, int B, int Lp, int H, int hd, int half_w,
+                                     const void* q, const void* k, const void* v, int ld_qkv, const void* o, int ld_o,
                                      const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx,
                                      int gmax, void* dq, void* dk, void* dv, int ld_grad, float* lse2, float* delta,
                                      float* gds, float* gpr, float p_drop, uint64_t seed, rf_stream_t stream) {
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_band_attn_bwd: operands must be bf16 or fp16 (got %d)", dtype);
+  RF_REQUIRE(grad_dtype == RF_F32 || grad_dtype == dtype,
+             "rf_band_attn_bwd: gradients fp32 or the operand type (got %d for %d)", grad_dtype, dtype);
   RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_band_attn_bwd: dropout p=%g outside [0, 1)", p_drop);
   const AttnDrop dr{seed, drop_thresh(p_drop), 1.0f / (1.0f - p_drop)};
-  RF_REQUIRE(grad_dtype == RF_F32 || grad_dtype == RF_BF16, "rf_band_attn_bwd: bad gradient dtype %d", grad_dtype);
   RF_REQUIRE(hd == 64 && half_w == 32, "rf_band_attn_bwd: head_dim 64 and window 64 only (got %d, %d)", hd,
              2 * half_w);
   RF_REQUIRE(B >= 0 && H > 0 && Lp >= 0 && gmax >= 0 && gmax <= 32, "rf_band_attn_bwd: bad shape");
@@ -471,12 +485,16 @@ extern "C" int rf_band_attn_bwd_drop(int grad_dtype, int B, int Lp, int H, int h
   RF_REQUIRE(gmax == 0 || (gidx && gds && gpr), "rf_band_attn_bwd: gidx / global outputs required");
   if (B == 0 || Lp == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
-  if (grad_dtype == RF_BF16)
-    launch_band_bwd<bf16>(B, Lp, H, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx, gmax, (bf16*)dq, (bf16*)dk,
-                          (bf16*)dv, ld_grad, lse2, delta, gds, gpr, dr, s);
-  else
-    launch_band_bwd<float>(B, Lp, H, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx, gmax, (float*)dq,
-                           (float*)dk, (float*)dv, ld_grad, lse2, delta, gds, gpr, dr, s);
+#define LB_(E, GT) launch_band_bwd<E, GT>(B, Lp, H, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx, gmax, (GT*)dq, \
+                                          (GT*)dk, (GT*)dv, ld_grad, lse2, delta, gds, gpr, dr, s)
+  if (dtype == RF_F16) {
+    if (grad_dtype == RF_F16) LB_(f16, f16);
+    else LB_(f16, float);
+  } else {
+    if (grad_dtype == RF_BF16) LB_(bf16, bf16);
+    else LB_(bf16, float);
+  }
+#undef LB_
   RF_LAUNCH_CHECK("rf_band_attn_bwd");
 }
 
@@ -485,8 +503,8 @@ extern "C" int rf_band_attn_bwd_dt(int grad_dtype, int B, int Lp, int H, int hd,
                                    const void* dout, int ld_do, const uint8_t* flags, const int32_t* gidx, int gmax,
                                    void* dq, void* dk, void* dv, int ld_grad, float* lse2, float* delta, float* gds,
                                    float* gpr, rf_stream_t stream) {
-  return rf_band_attn_bwd_drop(grad_dtype, B, Lp, H, hd, half_w, q, k, v, ld_qkv, o, ld_o, dout, ld_do, flags, gidx,
-                               gmax, dq, dk, dv, ld_grad, lse2, delta, gds, gpr, 0.f, 0, stream);
+  return rf_band_attn_bwd_drop(RF_BF16, grad_dtype, B, Lp, H, hd, half_w, q, k, v, ld_qkv, o, ld_o, dout, ld_do,
+                               flags, gidx, gmax, dq, dk, dv, ld_grad, lse2, delta, gds, gpr, 0.f, 0, stream);
 }
 
 extern "C" int rf_band_attn_bwd(int B, int Lp, int H, int hd, int half_w, const void* q, const void* k,

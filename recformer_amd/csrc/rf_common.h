@@ -66,6 +66,28 @@ template <> __device__ __forceinline__ float from_f32<float>(float x) { return x
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 template <> __device__ __forceinline__ f16 from_f32<f16>(float x) { return (f16)x; }
 
+// ---- 16-bit operand types: bf16 (autocast bfloat16) and fp16 (torch.cuda.amp default) ----------
+template <typename E> struct H16;
+template <> struct H16<bf16> {
+  typedef bf16x8 x8;
+  typedef bf16x4 x4;
+  typedef bf16x2 x2;
+  static constexpr bool bf = true;
+};
+template <> struct H16<f16> {
+  typedef f16x8 x8;
+  typedef f16x4 x4;
+  typedef f16x2 x2;
+  static constexpr bool bf = false;
+};
+// v_mfma_f32_16x16x32_{bf16,f16}: one instruction shape, the element type picks the opcode
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
 // erf with |error| <= 1.5e-7 (Abramowitz & Stegun 7.1.26): one v_rcp, one v_exp and a
 // degree-5 Horner chain — ~4x fewer VALU issues than the libm erff, which dominated the
 // FFN1 GEMM epilogue (it runs after the MFMA loop, so its VALU cost is not hidden).

@@ -60,7 +60,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, fl
   if (EPI == RF_EPI_BIAS_GELU_AUX)
     reinterpret_cast<TIN*>(const_cast<void*>(e.R))[(int64_t)row * e.ldr + col] = from_f32<TIN>(v);
   if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX)
-    v = (CF32 || sizeof(TIN) == 4) ? gelu_erf(v) : gelu_bf16out(v);
+    v = (CF32 || !std::is_same<TIN, bf16>::value) ? gelu_erf(v) : gelu_bf16out(v);  // fp16: exact form
   if (EPI == RF_EPI_BIAS_RESID) {
     if (RF32)
       v += reinterpret_cast<const float*>(e.R)[(int64_t)row * e.ldr + col];
@@ -99,12 +99,12 @@ __device__ __forceinline__ void load_bias16(const EpiArgs& e, int c0, float* b) 
 
 // 16 consecutive columns [c0, c0+16) of one output row: vector epilogue. `bv` is the bias
 // slice from load_bias16 (hoisted by the caller).
-template <int EPI, bool CF32, bool RF32>
+template <typename E, int EPI, bool CF32, bool RF32>
 __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, float* v, const float* bv) {
   if (row >= e.M) return;
   if (c0 + 16 > e.N) {  // ragged right edge: scalar path
 #pragma unroll
-    for (int k = 0; k < 16; ++k) epi_store<bf16, EPI, CF32, RF32>(e, row, c0 + k, v[k]);
+    for (int k = 0; k < 16; ++k) epi_store<E, EPI, CF32, RF32>(e, row, c0 + k, v[k]);
     return;
   }
   if (EPI == RF_EPI_COS) {
@@ -128,18 +128,18 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
     for (int k = 0; k < 16; ++k) v[k] *= e.col_scale;
   }
   if (EPI == RF_EPI_BIAS_GELU_AUX) {
-    bf16* z = reinterpret_cast<bf16*>(const_cast<void*>(e.R)) + (int64_t)row * e.ldr + c0;
+    E* z = reinterpret_cast<E*>(const_cast<void*>(e.R)) + (int64_t)row * e.ldr + c0;
 #pragma unroll
     for (int h8 = 0; h8 < 2; ++h8) {
-      bf16x8 x;
+      typename H16<E>::x8 x;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) x[k] = (bf16)v[8 * h8 + k];
-      *reinterpret_cast<bf16x8*>(z + 8 * h8) = x;
+      for (int k = 0; k < 8; ++k) x[k] = (E)v[8 * h8 + k];
+      *reinterpret_cast<typename H16<E>::x8*>(z + 8 * h8) = x;
     }
   }
   if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = CF32 ? gelu_erf(v[k]) : gelu_bf16out(v[k]);
+    for (int k = 0; k < 16; ++k) v[k] = (CF32 || !H16<E>::bf) ? gelu_erf(v[k]) : gelu_bf16out(v[k]);
   }
   if (EPI == RF_EPI_BIAS_RESID) {
     if (RF32) {
@@ -150,10 +150,10 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
         v[4 * q] += x.x; v[4 * q + 1] += x.y; v[4 * q + 2] += x.z; v[4 * q + 3] += x.w;
       }
     } else {
-      const bf16* r = reinterpret_cast<const bf16*>(e.R) + (int64_t)row * e.ldr + c0;
+      const E* r = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const bf16x8 x = *reinterpret_cast<const bf16x8*>(r + 8 * q);
+        const typename H16<E>::x8 x = *reinterpret_cast<const typename H16<E>::x8*>(r + 8 * q);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[8 * q + k] += (float)x[k];
       }
@@ -180,13 +180,13 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
     for (int q = 0; q < 4; ++q)
       *reinterpret_cast<f32x4*>(out + 4 * q) = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
   } else {
-    bf16* out = reinterpret_cast<bf16*>(e.C) + (int64_t)row * e.ldc + c0;
+    E* out = reinterpret_cast<E*>(e.C) + (int64_t)row * e.ldc + c0;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      bf16x8 x;
+      typename H16<E>::x8 x;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) x[k] = (bf16)v[8 * q + k];
-      *reinterpret_cast<bf16x8*>(out + 8 * q) = x;
+      for (int k = 0; k < 8; ++k) x[k] = (E)v[8 * q + k];
+      *reinterpret_cast<typename H16<E>::x8*>(out + 8 * q) = x;
     }
   }
 }
@@ -224,9 +224,9 @@ constexpr int gemm_min_waves(int bm, int bn, int wm, int wn, int bk, int nstage)
                     : (163840 / (nstage * (bm + bn) * bk * 2)) * ((bm / wm) * (bn / wn)) / 4);
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
+template <typename E, int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, gemm_min_waves(BM, BN, WM, WN, BK, NSTAGE))
-    k_gemm_bf16(int K, const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw,
+    k_gemm_bf16(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw,
                 EpiArgs e, int nTn) {
   using G = TileGeo<BK>;
   constexpr int NWN = BN / WN;
@@ -248,7 +248,8 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, gemm_min_waves(BM,
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / NWN, wn = wave % NWN;
 
-  const bf16* src[CPW];
+  typedef typename H16<E>::x8 V8;
+  const E* src[CPW];
   int dst[CPW];
 #pragma unroll
   for (int i = 0; i < CPW; ++i) {
@@ -283,27 +284,27 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, gemm_min_waves(BM,
     // the LDS->register stage). Slot (kt+3)%4 = (kt-1)%4 was last read (frag prefetch of tile
     // kt-1) in iteration kt-2 and drained by that wave's lgkmcnt(0) before iteration kt-1's
     // barrier.
-    auto read_frags = [&](int kt, bf16x8 (&a)[FM], bf16x8 (&b)[FN]) {
+    auto read_frags = [&](int kt, V8 (&a)[FM], V8 (&b)[FN]) {
       const char* as = smem + (kt & 3) * STAGE;
       const char* ws = as + A_BYTES;
       const int ch = lane >> 4;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * WM + i * 16 + (lane & 15);
-        a[i] = *reinterpret_cast<const bf16x8*>(as + r * G::ROWB + (G::slot(r, ch) << 4));
+        a[i] = *reinterpret_cast<const V8*>(as + r * G::ROWB + (G::slot(r, ch) << 4));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wn * WN + j * 16 + (lane & 15);
-        b[j] = *reinterpret_cast<const bf16x8*>(ws + r * G::ROWB + (G::slot(r, ch) << 4));
+        b[j] = *reinterpret_cast<const V8*>(ws + r * G::ROWB + (G::slot(r, ch) << 4));
       }
     };
-    auto mma = [&](const bf16x8 (&a)[FM], const bf16x8 (&b)[FN]) {
+    auto mma = [&](const V8 (&a)[FM], const V8 (&b)[FN]) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
     };
     auto sync_tile = [&](int kt) {  // tile kt landed in every wave's pieces
       const int ahead = nk - 1 - kt;  // tiles kt+1.. that may still be in flight (at most 1)
@@ -313,7 +314,7 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, gemm_min_waves(BM,
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     };
-    bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+    V8 a0[FM], b0[FN], a1[FM], b1[FN];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
       if (i < nk) stage(i, i);
@@ -357,22 +358,22 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, gemm_min_waves(BM,
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       const int ch = 4 * s + (lane >> 4);
-      bf16x8 a[FM], b[FN];
+      V8 a[FM], b[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * WM + i * 16 + (lane & 15);
-        a[i] = *reinterpret_cast<const bf16x8*>(as + r * G::ROWB + (G::slot(r, ch) << 4));
+        a[i] = *reinterpret_cast<const V8*>(as + r * G::ROWB + (G::slot(r, ch) << 4));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wn * WN + j * 16 + (lane & 15);
-        b[j] = *reinterpret_cast<const bf16x8*>(ws + r * G::ROWB + (G::slot(r, ch) << 4));
+        b[j] = *reinterpret_cast<const V8*>(ws + r * G::ROWB + (G::slot(r, ch) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
     }
   }
   }
@@ -402,7 +403,7 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, gemm_min_waves(BM,
       __builtin_amdgcn_wave_barrier();
       float bv[16];
       load_bias16<EPI>(e, n0 + wn * WN + j0 * 16 + cc, bv);
-      epi_row16<EPI, CF32, RF32>(e, m0 + wm * WM + i * 16 + rr, n0 + wn * WN + j0 * 16 + cc, v, bv);
+      epi_row16<E, EPI, CF32, RF32>(e, m0 + wm * WM + i * 16 + rr, n0 + wn * WN + j0 * 16 + cc, v, bv);
     }
   }
 }
@@ -511,13 +512,13 @@ __device__ __forceinline__ int wperm(int rho) {
 // LN beta for those columns (hoisted by the caller). Mirrors epi_row16 / epi_store.
 // CHECK = false: interior tile (no bounds tests, EPI_COS row norm `rsc` from LDS), so the
 // epilogue holds no global load and hipcc places no vmcnt wait between its stores.
-template <int EPI, bool CF32, bool RF32, int NV, bool CHECK = true>
+template <typename E, int EPI, bool CF32, bool RF32, int NV, bool CHECK = true>
 __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float* v, const float* bv,
                                         const float* gm, const float* bt, float rsc = 0.f) {
   if (CHECK && row >= e.M) return;
   if (CHECK && c0 + NV > e.N) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) epi_store<bf16, EPI, CF32, RF32>(e, row, c0 + k, v[k]);
+    for (int k = 0; k < NV; ++k) epi_store<E, EPI, CF32, RF32>(e, row, c0 + k, v[k]);
     return;
   }
   if (EPI == RF_EPI_COS) {
@@ -539,19 +540,19 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
     for (int k = 0; k < NV; ++k) v[k] *= e.col_scale;
   }
   if (EPI == RF_EPI_BIAS_GELU_AUX) {  // the pre-activation, bf16 (NV = 8 on this path)
-    bf16* z = reinterpret_cast<bf16*>(const_cast<void*>(e.R)) + (int64_t)row * e.ldr + c0;
+    E* z = reinterpret_cast<E*>(const_cast<void*>(e.R)) + (int64_t)row * e.ldr + c0;
     if (NV == 8) {
-      bf16x8 x;
+      typename H16<E>::x8 x;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) x[k] = (bf16)v[k];
-      *reinterpret_cast<bf16x8*>(z) = x;
+      for (int k = 0; k < 8; ++k) x[k] = (E)v[k];
+      *reinterpret_cast<typename H16<E>::x8*>(z) = x;
     } else {
 #pragma unroll
-      for (int k = 0; k < NV; ++k) z[k] = (bf16)v[k];
+      for (int k = 0; k < NV; ++k) z[k] = (E)v[k];
     }
   }
   if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
-    if (CF32) {
+    if (CF32 || !H16<E>::bf) {  // fp16 outputs: the exact form (the fitted one is sized to bf16)
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[k] = gelu_erf(v[k]);
     } else {
@@ -572,10 +573,10 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
         v[4 * q] += x.x; v[4 * q + 1] += x.y; v[4 * q + 2] += x.z; v[4 * q + 3] += x.w;
       }
     } else {
-      const bf16* r = reinterpret_cast<const bf16*>(e.R) + (int64_t)row * e.ldr + c0;
+      const E* r = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
 #pragma unroll
       for (int q = 0; q < NV / 4; ++q) {
-        const bf16x4 x = *reinterpret_cast<const bf16x4*>(r + 4 * q);
+        const typename H16<E>::x4 x = *reinterpret_cast<const typename H16<E>::x4*>(r + 4 * q);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[4 * q + k] += (float)x[k];
       }
@@ -599,23 +600,23 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
     for (int q = 0; q < NV / 4; ++q)
       *reinterpret_cast<f32x4*>(out + 4 * q) = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
   } else {
-    bf16* out = reinterpret_cast<bf16*>(e.C) + (int64_t)row * e.ldc + c0;
+    E* out = reinterpret_cast<E*>(e.C) + (int64_t)row * e.ldc + c0;
     if (NV == 8) {
-      bf16x8 x;
+      typename H16<E>::x8 x;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) x[k] = (bf16)v[k];
+      for (int k = 0; k < 8; ++k) x[k] = (E)v[k];
 #if !defined(RF_GEMM_PLAIN_STORE)
       // non-temporal: the tile's output is not re-read by this kernel; measured +0.8% per C2
       // step (tools/gpu/gemm_var.sh: qkv -4%, FFN -1.5%)
-      __builtin_nontemporal_store(x, reinterpret_cast<bf16x8*>(out));
+      __builtin_nontemporal_store(x, reinterpret_cast<typename H16<E>::x8*>(out));
 #else
-      *reinterpret_cast<bf16x8*>(out) = x;
+      *reinterpret_cast<typename H16<E>::x8*>(out) = x;
 #endif
     } else {
-      bf16x4 x;
+      typename H16<E>::x4 x;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) x[k] = (bf16)v[k];
-      *reinterpret_cast<bf16x4*>(out) = x;
+      for (int k = 0; k < 4; ++k) x[k] = (E)v[k];
+      *reinterpret_cast<typename H16<E>::x4*>(out) = x;
     }
   }
 }
@@ -679,10 +680,11 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 // K-iteration), so (vmcnt retiring in issue order) the next tile can start while the
 // epilogue's S stores are still draining: the prologue wait and the first P4 wait count them
 // as allowed-outstanding (interior tiles only, where S is exact).
-template <int EPI, bool CF32, bool RF32>
+template <typename E, int EPI, bool CF32, bool RF32>
 __global__ void __launch_bounds__(512, 1)
-    k_gemm_pp(int K, const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw, EpiArgs e,
+    k_gemm_pp(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e,
               int nTm, int nTn) {
+  typedef typename H16<E>::x8 V8;
   constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;  // fp32 output layout
   constexpr int S = OUT32 ? 32 : 16;                  // epilogue stores per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -735,7 +737,7 @@ __global__ void __launch_bounds__(512, 1)
     }
     char* dst = smem + ((t & 1) * 4 + half) * PP_HALF + wave * 2048;
     const bool isA = half < 2;
-    const bf16* base = isA ? A : W;
+    const E* base = isA ? A : W;
     const int ld = isA ? lda : ldw;
     const int lim = (isA ? e.M : e.N) - 1;
     const int r0 = (isA ? bm0 : bn0) + (half & 1) * 128;
@@ -776,7 +778,7 @@ __global__ void __launch_bounds__(512, 1)
   const int bBase = (2 + wc) * PP_HALF;                    // the whole W-half
 
   // quadrant (qm, qn) = 32 rows x 64 columns of the wave's 64 x 128 tile
-  bf16x8 a[2][2][2], b[2][4][2];
+  V8 a[2][2][2], b[2][4][2];
   f32x4 acc[4][8];
 
   auto read_a = [&](int buf, int qm) {
@@ -787,8 +789,8 @@ __global__ void __launch_bounds__(512, 1)
     const char* base = smem + buf * 4 * PP_HALF + aBase + qm * 32 * 128;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      a[qm][i][0] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + off0);
-      a[qm][i][1] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + off1);
+      a[qm][i][0] = *reinterpret_cast<const V8*>(base + i * 16 * 128 + off0);
+      a[qm][i][1] = *reinterpret_cast<const V8*>(base + i * 16 * 128 + off1);
     }
   };
   auto read_b = [&](int buf, int qn) {
@@ -799,8 +801,8 @@ __global__ void __launch_bounds__(512, 1)
     const char* base = smem + buf * 4 * PP_HALF + bBase + qn * 64 * 128;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      b[qn][j][0] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + off0);
-      b[qn][j][1] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + off1);
+      b[qn][j][0] = *reinterpret_cast<const V8*>(base + j * 16 * 128 + off0);
+      b[qn][j][1] = *reinterpret_cast<const V8*>(base + j * 16 * 128 + off1);
     }
   };
   auto mma = [&](int qm, int qn) {
@@ -811,7 +813,7 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[qm * 2 + i][qn * 4 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[qm][i][ks], b[qn][j][ks], acc[qm * 2 + i][qn * 4 + j], 0, 0, 0);
+              mfma16(a[qm][i][ks], b[qn][j][ks], acc[qm * 2 + i][qn * 4 + j]);
   };
   auto bar = [&]() {
     __builtin_amdgcn_s_barrier();
@@ -945,10 +947,10 @@ __global__ void __launch_bounds__(512, 1)
           const int row = erow + mf * 16 + r;
           const float rsc = EPI == RF_EPI_COS ? cb[256 + row - em0] : 0.f;
           if (OUT32) {
-            epi_seg<EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
-            epi_seg<EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
+            epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+            epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
           } else {
-            epi_seg<EPI, CF32, RF32, 8, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+            epi_seg<E, EPI, CF32, RF32, 8, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
           }
         }
     };
@@ -980,35 +982,35 @@ static int num_cus() {
   return n[dev];
 }
 
-template <int EPI, bool CF32, bool RF32>
+template <typename E, int EPI, bool CF32, bool RF32>
 static void launch_pp(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
                       hipStream_t s) {
   constexpr size_t lds = CV_OFF + 6 * 1024;  // ring + diagnostic stamp area + column vectors
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_pp<EPI, CF32, RF32>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_pp<E, EPI, CF32, RF32>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   const int nTm = (M + 255) / 256, nTn = (N + 255) / 256;
   const int grid = min(nTm * nTn, num_cus());
-  k_gemm_pp<EPI, CF32, RF32><<<grid, 512, lds, s>>>(K, (const bf16*)A, lda, (const bf16*)W, ldw, e, nTm, nTn);
+  k_gemm_pp<E, EPI, CF32, RF32><<<grid, 512, lds, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
+template <typename E, int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
 static void launch_bf16(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                         const EpiArgs& e, hipStream_t s) {
   constexpr int threads = (BM / WM) * (BN / WN) * 64;
   constexpr size_t lds = (size_t)NSTAGE * (BM + BN) * BK * 2;
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_bf16<BM, BN, WM, WN, BK, NSTAGE, EPI, CF32, RF32>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_bf16<E, BM, BN, WM, WN, BK, NSTAGE, EPI, CF32, RF32>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   const int nTm = (M + BM - 1) / BM, nTn = (N + BN - 1) / BN;
-  k_gemm_bf16<BM, BN, WM, WN, BK, NSTAGE, EPI, CF32, RF32><<<nTm * nTn, threads, lds, s>>>(
-      K, (const bf16*)A, lda, (const bf16*)W, ldw, e, nTn);
+  k_gemm_bf16<E, BM, BN, WM, WN, BK, NSTAGE, EPI, CF32, RF32><<<nTm * nTn, threads, lds, s>>>(
+      K, (const E*)A, lda, (const E*)W, ldw, e, nTn);
 }
 
 // Variant selector for A/B timing (knob gemm_variant): 5 -> 256^2 ping-pong (default), 1 -> 256^2
@@ -1028,28 +1030,59 @@ static bool pp_cols_ok(int M, int N, const EpiArgs& e) {
          (e.ra == nullptr || (M >= 4 && M % 4 == 0 && al16(e.ra)));
 }
 
-template <int EPI, bool CF32, bool RF32>
+template <typename E, int EPI, bool CF32, bool RF32>
 static void dispatch_tile(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                           const EpiArgs& e, hipStream_t s) {
   // 256x256 when the grid still covers the chip; 128x128 for skinny problems
   const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
   if (tiles256 >= 128) {
     switch (gemm_variant()) {
-      case 1: launch_bf16<256, 256, 128, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
-      case 2: launch_bf16<256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
-      case 3: launch_bf16<128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
-      case 4: launch_bf16<256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 1: launch_bf16<E, 256, 256, 128, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 2: launch_bf16<E, 256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 3: launch_bf16<E, 128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 4: launch_bf16<E, 256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 5:
         if (pp_cols_ok(M, N, e)) {
-          launch_pp<EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+          launch_pp<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
           break;
         }
-        launch_bf16<256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+        launch_bf16<E, 256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
         break;
-      default: launch_bf16<256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      default: launch_bf16<E, 256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
     }
   } else {
-    launch_bf16<128, 128, 64, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+    launch_bf16<E, 128, 128, 64, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+  }
+}
+
+// the 16-bit epilogue / io combinations rf_gemm accepts, for one operand type
+template <typename E>
+static void gemm16(int epilogue, bool cf, bool rf, int M, int N, int K, const void* A, int lda, const void* W,
+                   int ldw, const EpiArgs& e, hipStream_t s) {
+  switch (epilogue) {
+    case RF_EPI_NONE:
+      if (cf) dispatch_tile<E, RF_EPI_NONE, true, false>(M, N, K, A, lda, W, ldw, e, s);
+      else dispatch_tile<E, RF_EPI_NONE, false, false>(M, N, K, A, lda, W, ldw, e, s);
+      break;
+    case RF_EPI_BIAS:
+      if (cf) dispatch_tile<E, RF_EPI_BIAS, true, false>(M, N, K, A, lda, W, ldw, e, s);
+      else dispatch_tile<E, RF_EPI_BIAS, false, false>(M, N, K, A, lda, W, ldw, e, s);
+      break;
+    case RF_EPI_BIAS_GELU:
+      dispatch_tile<E, RF_EPI_BIAS_GELU, false, false>(M, N, K, A, lda, W, ldw, e, s);
+      break;
+    case RF_EPI_BIAS_GELU_AUX:
+      dispatch_tile<E, RF_EPI_BIAS_GELU_AUX, false, false>(M, N, K, A, lda, W, ldw, e, s);
+      break;
+    case RF_EPI_BIAS_RESID:
+      if (cf && rf) dispatch_tile<E, RF_EPI_BIAS_RESID, true, true>(M, N, K, A, lda, W, ldw, e, s);
+      else if (cf) dispatch_tile<E, RF_EPI_BIAS_RESID, true, false>(M, N, K, A, lda, W, ldw, e, s);
+      else if (rf) dispatch_tile<E, RF_EPI_BIAS_RESID, false, true>(M, N, K, A, lda, W, ldw, e, s);
+      else dispatch_tile<E, RF_EPI_BIAS_RESID, false, false>(M, N, K, A, lda, W, ldw, e, s);
+      break;
+    case RF_EPI_COS:
+      dispatch_tile<E, RF_EPI_COS, false, false>(M, N, K, A, lda, W, ldw, e, s);
+      break;
   }
 }
 
@@ -1065,8 +1098,8 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
   RF_REQUIRE(lda >= K && ldw >= K && ldc >= N, "rf_gemm: bad leading dims");
   RF_REQUIRE((epilogue >= RF_EPI_NONE && epilogue <= RF_EPI_COS) || epilogue == RF_EPI_BIAS_GELU_AUX,
              "rf_gemm: bad epilogue %d", epilogue);
-  RF_REQUIRE(epilogue != RF_EPI_BIAS_GELU_AUX || (dtype == RF_BF16 && resid && ldr >= N && !(io_flags & 3)),
-             "rf_gemm: EPI_BIAS_GELU_AUX needs bf16 and a bf16 pre-activation output (resid)");
+  RF_REQUIRE(epilogue != RF_EPI_BIAS_GELU_AUX || (dtype != RF_F32 && resid && ldr >= N && !(io_flags & 3)),
+             "rf_gemm: EPI_BIAS_GELU_AUX needs 16-bit operands and a pre-activation output (resid) of that type");
   RF_REQUIRE(epilogue == RF_EPI_NONE || epilogue == RF_EPI_COS || bias, "rf_gemm: bias required");
   RF_REQUIRE(epilogue != RF_EPI_BIAS_RESID || (resid && ldr >= N), "rf_gemm: residual required");
   RF_REQUIRE(epilogue != RF_EPI_COS || (ra && rw), "rf_gemm: norms required for EPI_COS");
@@ -1074,38 +1107,15 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
   EpiArgs e{M, N, bias, resid, ldr, C, ldc, scale_cols, col_scale, ra, rw,
             nullptr, nullptr, nullptr, nullptr, g_stamps, gemm_gn()};
   hipStream_t s = as_stream(stream);
-  if (dtype == RF_BF16) {
-    RF_REQUIRE(K % 64 == 0, "rf_gemm(bf16): K=%d must be a multiple of 64", K);
-    RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0, "rf_gemm(bf16): lda/ldw must be multiples of 8");
+  if (dtype == RF_BF16 || dtype == RF_F16) {
+    RF_REQUIRE(K % 64 == 0, "rf_gemm(16-bit): K=%d must be a multiple of 64", K);
+    RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0, "rf_gemm(16-bit): lda/ldw must be multiples of 8");
     RF_REQUIRE(ldc % 8 == 0 && (resid == nullptr || ldr % 8 == 0),
-               "rf_gemm(bf16): ldc/ldr must be multiples of 8 (16-B vector epilogue)");
-    RF_REQUIRE(scale_cols % 16 == 0, "rf_gemm(bf16): scale_cols must be a multiple of 16");
+               "rf_gemm(16-bit): ldc/ldr must be multiples of 8 (16-B vector epilogue)");
+    RF_REQUIRE(scale_cols % 16 == 0, "rf_gemm(16-bit): scale_cols must be a multiple of 16");
     const bool cf = io_flags & RF_IO_C_F32, rf = io_flags & RF_IO_R_F32;
-    switch (epilogue) {
-      case RF_EPI_NONE:
-        if (cf) dispatch_tile<RF_EPI_NONE, true, false>(M, N, K, A, lda, W, ldw, e, s);
-        else dispatch_tile<RF_EPI_NONE, false, false>(M, N, K, A, lda, W, ldw, e, s);
-        break;
-      case RF_EPI_BIAS:
-        if (cf) dispatch_tile<RF_EPI_BIAS, true, false>(M, N, K, A, lda, W, ldw, e, s);
-        else dispatch_tile<RF_EPI_BIAS, false, false>(M, N, K, A, lda, W, ldw, e, s);
-        break;
-      case RF_EPI_BIAS_GELU:
-        dispatch_tile<RF_EPI_BIAS_GELU, false, false>(M, N, K, A, lda, W, ldw, e, s);
-        break;
-      case RF_EPI_BIAS_GELU_AUX:
-        dispatch_tile<RF_EPI_BIAS_GELU_AUX, false, false>(M, N, K, A, lda, W, ldw, e, s);
-        break;
-      case RF_EPI_BIAS_RESID:
-        if (cf && rf) dispatch_tile<RF_EPI_BIAS_RESID, true, true>(M, N, K, A, lda, W, ldw, e, s);
-        else if (cf) dispatch_tile<RF_EPI_BIAS_RESID, true, false>(M, N, K, A, lda, W, ldw, e, s);
-        else if (rf) dispatch_tile<RF_EPI_BIAS_RESID, false, true>(M, N, K, A, lda, W, ldw, e, s);
-        else dispatch_tile<RF_EPI_BIAS_RESID, false, false>(M, N, K, A, lda, W, ldw, e, s);
-        break;
-      case RF_EPI_COS:
-        dispatch_tile<RF_EPI_COS, false, false>(M, N, K, A, lda, W, ldw, e, s);
-        break;
-    }
+    if (dtype == RF_F16) gemm16<f16>(epilogue, cf, rf, M, N, K, A, lda, W, ldw, e, s);
+    else gemm16<bf16>(epilogue, cf, rf, M, N, K, A, lda, W, ldw, e, s);
   } else if (dtype == RF_F32) {
     RF_REQUIRE(K % GF_K == 0, "rf_gemm(f32): K=%d must be a multiple of %d", K, GF_K);
     RF_REQUIRE(lda % 4 == 0 && ldw % 4 == 0, "rf_gemm(f32): lda/ldw must be multiples of 4");
@@ -1138,7 +1148,7 @@ extern "C" int rf_gemm_resid_ln(int dtype, int M, int N, int K, const void* A, i
     RF_REQUIRE(K % 64 == 0, "rf_gemm_resid_ln(bf16): K=%d must be a multiple of 64", K);
     RF_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0 && ldr % 8 == 0,
                "rf_gemm_resid_ln(bf16): leading dims must be multiples of 8");
-    dispatch_tile<RF_EPI_BIAS_RESID_LN, true, true>(M, N, K, A, lda, W, ldw, e, s);
+    dispatch_tile<bf16, RF_EPI_BIAS_RESID_LN, true, true>(M, N, K, A, lda, W, ldw, e, s);
   } else if (dtype == RF_F32) {
     RF_REQUIRE(K % GF_K == 0 && lda % 4 == 0 && ldw % 4 == 0, "rf_gemm_resid_ln(f32): alignment");
     const int nTm = (M + GF_M - 1) / GF_M, nTn = (N + GF_N - 1) / GF_N;

@@ -422,14 +422,14 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
 // stream); x (the backward's input) and the row stats are written. The keep mask is a counter
 // hash of (seed, element index) — regenerated by the backward, never stored.
 
-template <int VEC, int NCH>
-__global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const bf16* __restrict__ t, int ldt,
+template <typename E, int VEC, int NCH>
+__global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const E* __restrict__ t, int ldt,
                                                           const float* __restrict__ res, uint32_t thresh,
                                                           float keep_scale, uint64_t seed,
                                                           const float* __restrict__ lw, const float* __restrict__ lb,
                                                           float eps, float* __restrict__ xo, float* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                          bf16* __restrict__ y16) {
+                                                          E* __restrict__ y16) {
   constexpr int D = 64 * VEC * NCH;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const bf16* __re
   for (int c = 0; c < NCH; ++c) {
     const int e = c * 64 * VEC + lane * VEC;
     float tv[VEC], rv[VEC];
-    Vec<bf16, VEC>::load(t + (int64_t)row * ldt + e, tv);
+    Vec<E, VEC>::load(t + (int64_t)row * ldt + e, tv);
     Vec<float, VEC>::load(res + (int64_t)row * D + e, rv);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
@@ -473,7 +473,7 @@ __global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const bf16* __re
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o[j] = (xv[c][j] - mean) * rstd * w[j] + bb[j];
     Vec<float, VEC>::store(y + (int64_t)row * D + e, o);
-    if (y16) Vec<bf16, VEC>::store(y16 + (int64_t)row * D + e, o);  // the next GEMM's operand
+    if (y16) Vec<E, VEC>::store(y16 + (int64_t)row * D + e, o);  // the next GEMM's operand
   }
 }
 
@@ -487,15 +487,15 @@ constexpr int LNB_ROWS = 32;
 
 // With dt != null (the dropout + residual form above) it also writes the dense branch's
 // gradient dt = dx * keep * keep_scale in bf16 (the mask regenerated from the seed).
-template <int VEC, int NCH>
+template <typename E, int VEC, int NCH>
 __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __restrict__ dy,
                                                         const float* __restrict__ x, int ldx,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ rstd,
                                                         const float* __restrict__ w, float* __restrict__ dx,
-                                                        float* __restrict__ part, bf16* __restrict__ dt,
+                                                        float* __restrict__ part, E* __restrict__ dt,
                                                         uint32_t thresh, float keep_scale, uint64_t seed,
-                                                        const bf16* __restrict__ dy2) {
+                                                        const E* __restrict__ dy2) {
   constexpr int D = 64 * VEC * NCH;
   __shared__ float red[4][2][D];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -525,7 +525,7 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
       }
       if (dy2) {  // second consumer's gradient (bf16), summed as autograd would
         float d2[VEC];
-        Vec<bf16, VEC>::load(dy2 + (int64_t)row * D + e, d2);
+        Vec<E, VEC>::load(dy2 + (int64_t)row * D + e, d2);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) d[j] += d2[j];
       }
@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
 #pragma unroll
         for (int j = 0; j < VEC; ++j)
           od[j] = (thresh == 0 || drop_keep(seed, (uint64_t)row * D + e + j, thresh)) ? o[j] * keep_scale : 0.f;
-        Vec<bf16, VEC>::store(dt + (int64_t)row * D + e, od);
+        Vec<E, VEC>::store(dt + (int64_t)row * D + e, od);
       }
     }
   }
@@ -890,6 +890,10 @@ int rf_embed_ln_fwd(int table_dtype, int out_dtype, int M, int D, const int32_t*
     return launch_embed<float, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, nullptr, s);
   if (table_dtype == RF_BF16 && out_dtype == RF_BF16)
     return launch_embed<bf16, bf16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, nullptr, s);
+  if (table_dtype == RF_F32 && out_dtype == RF_F16)
+    return launch_embed<float, f16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, nullptr, s);
+  if (table_dtype == RF_F16 && out_dtype == RF_F16)
+    return launch_embed<f16, f16>(M, D, ids, pos, tt, ip, word_emb, pos_emb, type_emb, ipos_emb, ln_w, ln_b, eps, out, out32, nullptr, s);
   RF_REQUIRE(false, "rf_embed_ln_fwd: unsupported dtypes table=%d out=%d", table_dtype, out_dtype);
 }
 
@@ -914,6 +918,12 @@ int rf_add_layernorm_fwd(int x_dtype, int y_dtype, int M, int D, const void* x, 
     return launch_ln<float, float>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
   if (x_dtype == RF_BF16 && y_dtype == RF_F32)
     return launch_ln<bf16, float>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
+  if (x_dtype == RF_F16 && y_dtype == RF_F16)
+    return launch_ln<f16, f16>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
+  if (x_dtype == RF_F32 && y_dtype == RF_F16)
+    return launch_ln<float, f16>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
+  if (x_dtype == RF_F16 && y_dtype == RF_F32)
+    return launch_ln<f16, float>(M, D, x, ldx, res, w, b, eps, y, ldy, y32, mean, rstd, s);
   RF_REQUIRE(false, "rf_layernorm_fwd: bad dtypes %d/%d", x_dtype, y_dtype);
 }
 
@@ -977,6 +987,9 @@ int rf_scatter_add_rows(int dtype, int R, int D, const int32_t* rows, const void
   if (dtype == RF_BF16)
     k_scatter_add_rows<bf16><<<grid, 256, 0, s>>>(R, D, rows, (const bf16*)src0, (const bf16*)src1, ld_src,
                                                   (bf16*)dst0, (bf16*)dst1, ld_dst);
+  else if (dtype == RF_F16)
+    k_scatter_add_rows<f16><<<grid, 256, 0, s>>>(R, D, rows, (const f16*)src0, (const f16*)src1, ld_src, (f16*)dst0,
+                                                 (f16*)dst1, ld_dst);
   else if (dtype == RF_F32)
     k_scatter_add_rows<float><<<grid, 256, 0, s>>>(R, D, rows, (const float*)src0, (const float*)src1, ld_src,
                                                    (float*)dst0, (float*)dst1, ld_dst);
@@ -994,15 +1007,19 @@ int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, v
     RF_LAUNCH_CHECK("rf_colsum");
   }
   if (dtype == RF_BF16) colsum<bf16>(M, N, (const bf16*)x, ldx, (float*)workspace, out, nullptr, N, s);
+  else if (dtype == RF_F16) colsum<f16>(M, N, (const f16*)x, ldx, (float*)workspace, out, nullptr, N, s);
   else if (dtype == RF_F32) colsum<float>(M, N, (const float*)x, ldx, (float*)workspace, out, nullptr, N, s);
   else RF_REQUIRE(false, "rf_colsum: bad dtype %d", dtype);
   RF_LAUNCH_CHECK("rf_colsum");
 }
 
+extern "C++" {
+template <typename E>
 static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                        const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
-                       bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
-                       const bf16* dy2 = nullptr);
+                       E* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
+                       const E* dy2 = nullptr);
+}
 
 
 int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
@@ -1014,6 +1031,12 @@ int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, f
 int rf_drop_add_ln_fwd_dual(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
                             const float* w, const float* b, float eps, float* x, float* y, float* mean,
                             float* rstd, void* y16, rf_stream_t stream) {
+  return rf_drop_add_ln_fwd_t(RF_BF16, M, D, t, ldt, res, p, seed, w, b, eps, x, y, mean, rstd, y16, stream);
+}
+int rf_drop_add_ln_fwd_t(int dtype, int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
+                         const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,
+                         void* y16, rf_stream_t stream) {
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_drop_add_ln_fwd: dtype must be bf16 or fp16");
   RF_REQUIRE(M >= 0 && ldt >= D && p >= 0.f && p < 1.f, "rf_drop_add_ln_fwd: bad arguments");
   if (M == 0) return RF_OK;
   RF_REQUIRE(t && res && w && b && x && y && mean && rstd, "rf_drop_add_ln_fwd: null pointer");
@@ -1023,9 +1046,15 @@ int rf_drop_add_ln_fwd_dual(int M, int D, const void* t, int ldt, const float* r
   const float ks = 1.0f / (1.0f - p);
   dim3 grid((M + 3) / 4);
 #define L_(V, N)                                                                                   \
-  k_drop_add_ln_fwd<V, N><<<grid, 256, 0, s>>>(M, (const bf16*)t, ldt, res, th, ks, seed, w, b, eps, x, y, \
-                                               mean, rstd, (bf16*)y16)
-  RF_ROW_DISPATCH(D, L_);
+  k_drop_add_ln_fwd<E, V, N><<<grid, 256, 0, s>>>(M, (const E*)t, ldt, res, th, ks, seed, w, b, eps, x, y, \
+                                                  mean, rstd, (E*)y16)
+  if (dtype == RF_F16) {
+    typedef f16 E;
+    RF_ROW_DISPATCH(D, L_);
+  } else {
+    typedef bf16 E;
+    RF_ROW_DISPATCH(D, L_);
+  }
 #undef L_
   RF_LAUNCH_CHECK("rf_drop_add_ln_fwd");
 }
@@ -1040,22 +1069,34 @@ int rf_drop_add_ln_bwd(int M, int D, const float* dy, const float* x, const floa
 int rf_drop_add_ln_bwd_dual(int M, int D, const float* dy, const void* dy16, const float* x, const float* mean,
                             const float* rstd, const float* w, float p, uint64_t seed, float* dres, void* dt,
                             float* dw, float* db, void* workspace, rf_stream_t stream) {
+  return rf_drop_add_ln_bwd_t(RF_BF16, M, D, dy, dy16, x, mean, rstd, w, p, seed, dres, dt, dw, db, workspace,
+                              stream);
+}
+int rf_drop_add_ln_bwd_t(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
+                         const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
+                         void* dt, float* dw, float* db, void* workspace, rf_stream_t stream) {
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_drop_add_ln_bwd: dtype must be bf16 or fp16");
   RF_REQUIRE(M >= 0 && p >= 0.f && p < 1.f, "rf_drop_add_ln_bwd: bad arguments");
   RF_REQUIRE(M == 0 || dt, "rf_drop_add_ln_bwd: null dt");
-  return ln_bwd_impl(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (bf16*)dt, drop_thresh(p),
-                     1.0f / (1.0f - p), seed, stream, (const bf16*)dy16);
+  if (dtype == RF_F16)
+    return ln_bwd_impl<f16>(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (f16*)dt, drop_thresh(p),
+                            1.0f / (1.0f - p), seed, stream, (const f16*)dy16);
+  return ln_bwd_impl<bf16>(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (bf16*)dt, drop_thresh(p),
+                           1.0f / (1.0f - p), seed, stream, (const bf16*)dy16);
 }
 
 int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                      const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                      rf_stream_t stream) {
-  return ln_bwd_impl(M, D, dy, x, ldx, mean, rstd, w, dx, dw, db, workspace, nullptr, 0u, 1.f, 0ull, stream);
+  return ln_bwd_impl<bf16>(M, D, dy, x, ldx, mean, rstd, w, dx, dw, db, workspace, nullptr, 0u, 1.f, 0ull, stream);
 }
 
+extern "C++" {
+template <typename E>
 static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                        const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
-                       bf16* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
-                       const bf16* dy2) {
+                       E* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
+                       const E* dy2) {
   RF_REQUIRE(M >= 0 && ldx >= D, "rf_layernorm_bwd: bad shape");
   if (M == 0) return RF_OK;
   RF_REQUIRE((dy || dy2) && x && mean && rstd && w && dx && dw && db && workspace, "rf_layernorm_bwd: null pointer");
@@ -1063,11 +1104,12 @@ static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, c
   hipStream_t s = as_stream(stream);
   const int nb = (M + LNB_ROWS - 1) / LNB_ROWS;
   float* part = reinterpret_cast<float*>(workspace);
-#define L_(V, N) k_layernorm_bwd<V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, dy2)
+#define L_(V, N) k_layernorm_bwd<E, V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, dy2)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
   colsum<float>(nb, 2 * D, part, 2 * D, part + (size_t)nb * 2 * D, dw, db, D, s);  // [dw | db] columns
   RF_LAUNCH_CHECK("rf_layernorm_bwd");
+}
 }
 
 int rf_row_inv_norm(int dtype, int M, int D, const void* x, int ldx, float eps, float* out,
@@ -1101,6 +1143,8 @@ int rf_gather_global_rows(int dtype, int B, int Lp, int D, int gmax, const void*
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16)
     k_gather_rows<bf16><<<B * gmax, 256, 0, s>>>(Lp, D, gmax, (const bf16*)x, ldx, gidx, (bf16*)out);
+  else if (dtype == RF_F16)
+    k_gather_rows<f16><<<B * gmax, 256, 0, s>>>(Lp, D, gmax, (const f16*)x, ldx, gidx, (f16*)out);
   else if (dtype == RF_F32)
     k_gather_rows<float><<<B * gmax, 256, 0, s>>>(Lp, D, gmax, (const float*)x, ldx, gidx, (float*)out);
   else
@@ -1118,6 +1162,9 @@ int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, co
   if (dtype == RF_BF16)
     k_cos_cand<bf16><<<grid, 256, 0, s>>>(B, C, D, (const bf16*)z, ldz, rz, (const bf16*)items, ldi,
                                           ri, cand, inv_temp, scores);
+  else if (dtype == RF_F16)
+    k_cos_cand<f16><<<grid, 256, 0, s>>>(B, C, D, (const f16*)z, ldz, rz, (const f16*)items, ldi, ri, cand, inv_temp,
+                                         scores);
   else if (dtype == RF_F32)
     k_cos_cand<float><<<grid, 256, 0, s>>>(B, C, D, (const float*)z, ldz, rz, (const float*)items,
                                            ldi, ri, cand, inv_temp, scores);
@@ -1134,6 +1181,8 @@ int rf_cross_entropy_fwd(int dtype, int M, int N, const void* logits, int64_t ld
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16)
     k_cross_entropy<bf16><<<M, 256, 0, s>>>(N, (const bf16*)logits, ldx, labels, ignore_index, loss, argmax);
+  else if (dtype == RF_F16)
+    k_cross_entropy<f16><<<M, 256, 0, s>>>(N, (const f16*)logits, ldx, labels, ignore_index, loss, argmax);
   else if (dtype == RF_F32)
     k_cross_entropy<float><<<M, 256, 0, s>>>(N, (const float*)logits, ldx, labels, ignore_index, loss, argmax);
   else

@@ -226,10 +226,14 @@ LM_HEAD_MASKED_ONLY = True
 
 
 def _compute_dtype(param_dtype: torch.dtype) -> torch.dtype:
+    """The GEMM / attention operand type: the autocast dtype under torch.autocast (fp16 is the
+    default of torch.cuda.amp.autocast(), the reference's finetune.py:106-110; bf16 on request),
+    else the parameters' type (model.half() / model.to(bfloat16)), else fp32."""
     if torch.is_autocast_enabled("cuda"):
-        return torch.bfloat16
+        adt = torch.get_autocast_dtype("cuda")
+        return adt if adt in (torch.bfloat16, torch.float16) else torch.bfloat16
     if param_dtype in (torch.bfloat16, torch.float16):
-        return torch.bfloat16
+        return param_dtype
     return torch.float32
 
 
@@ -400,7 +404,8 @@ class RecformerModel(nn.Module):
         # reference's autocast run), the fp32 stream held split as (hi, lo) 16-bit planes whose
         # hi plane is the bf16 GEMM operand (ops.add_layernorm_split); fp32 path: everything fp32.
         mixed = dt != torch.float32
-        split = mixed and SPLIT_STREAM
+        # the split planes' hi half is a bf16 operand; fp16 keeps the fp32 stream plus an fp16 copy
+        split = mixed and SPLIT_STREAM and dt == torch.bfloat16
         nl = len(pk["layers"])
         if split:
             h, h_lo = ops.embed_ln_split(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
@@ -416,7 +421,9 @@ class RecformerModel(nn.Module):
         windows = cfg.window_per_layer()
         # global rows: the key/value-projection fold by default; `config.global_attention_fold
         # = False` keeps the reference's structure (k_g/v_g projected over all tokens).
-        fold = getattr(cfg, "global_attention_fold", True)
+        # (fp16: the unfolded form, key_global / value_global projected with the q|k|v GEMM — the
+        # fold kernels are bf16 / fp32)
+        fold = getattr(cfg, "global_attention_fold", True) and dt != torch.float16
         eps = cfg.layer_norm_eps
         gws = None
         for li, lw in enumerate(pk["layers"]):
@@ -520,7 +527,7 @@ class RecformerForSeqRec(nn.Module):
 
     def similarity_score(self, pooler_output, candidates=None):
         """models.py:539-545: (B,N) or (B,C) fp32 scores = cos / temp."""
-        dt = pooler_output.dtype if pooler_output.dtype in (torch.bfloat16, torch.float32) else torch.bfloat16
+        dt = pooler_output.dtype
         z = pooler_output.to(dt).contiguous()
         table, rnorm = self._items(dt)
         inv_t = 1.0 / self.config.temp

@@ -327,22 +327,23 @@ def drop_add_ln_fwd(t: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torc
     lib = _lib.load()
     _dev(t, res, w, b)
     M, D = t.shape
-    if t.dtype != torch.bfloat16 or res.dtype != torch.float32 or not res.is_contiguous():
-        raise TypeError("drop_add_ln_fwd: t bf16 (row-major), res contiguous fp32")
+    if t.dtype not in (torch.bfloat16, torch.float16) or res.dtype != torch.float32 or not res.is_contiguous():
+        raise TypeError("drop_add_ln_fwd: t bf16 / fp16 (row-major), res contiguous fp32")
     x = torch.empty(M, D, dtype=torch.float32, device=t.device)
     y = torch.empty_like(x)
     mean = torch.empty(M, dtype=torch.float32, device=t.device)
     rstd = torch.empty_like(mean)
-    y16 = torch.empty(M, D, dtype=torch.bfloat16, device=t.device) if want_bf16 else None
-    check(lib.rf_drop_add_ln_fwd_dual(M, D, _p(t), _rowmajor(t, "t"), _p(res), float(p), seed,
-                                      _p(w.float().contiguous()), _p(b.float().contiguous()), float(eps), _p(x),
-                                      _p(y), _p(mean), _p(rstd), _p(y16), _stream(t)), "rf_drop_add_ln_fwd")
+    y16 = torch.empty(M, D, dtype=t.dtype, device=t.device) if want_bf16 else None
+    check(lib.rf_drop_add_ln_fwd_t(dtype_code(t.dtype), M, D, _p(t), _rowmajor(t, "t"), _p(res), float(p), seed,
+                                   _p(w.float().contiguous()), _p(b.float().contiguous()), float(eps), _p(x),
+                                   _p(y), _p(mean), _p(rstd), _p(y16), _stream(t)), "rf_drop_add_ln_fwd")
     return (x, y, mean, rstd, y16) if want_bf16 else (x, y, mean, rstd)
 
 
-def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[torch.Tensor] = None):
-    """rf_drop_add_ln_bwd(_dual): (dres fp32, dt bf16, dw, db) for the gradient dy (fp32) of y plus,
-    when given, dy16 (bf16) of its bf16 copy; either may be None (not both)."""
+def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[torch.Tensor] = None,
+                    dtype: torch.dtype = torch.bfloat16):
+    """rf_drop_add_ln_bwd_t: (dres fp32, dt, dw, db) for the gradient dy (fp32) of y plus, when given,
+    dy16 of its 16-bit copy; either may be None (not both). dt and dy16 in `dtype` (bf16 / fp16)."""
     lib = _lib.load()
     _dev(x, mean, rstd, w)
     M, D = x.shape
@@ -350,16 +351,17 @@ def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[to
         raise ValueError("drop_add_ln_bwd: no gradient")
     dy = None if dy is None else dy.float().contiguous()
     if dy16 is not None:
-        if dy16.dtype != torch.bfloat16 or tuple(dy16.shape) != (M, D):
-            raise TypeError("drop_add_ln_bwd: dy16 must be a bf16 (M, D) tensor")
+        if dy16.dtype != dtype or tuple(dy16.shape) != (M, D):
+            raise TypeError(f"drop_add_ln_bwd: dy16 must be a {dtype} (M, D) tensor")
         dy16 = dy16.contiguous()
     dres = torch.empty(M, D, dtype=torch.float32, device=x.device)
-    dt = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
+    dt = torch.empty(M, D, dtype=dtype, device=x.device)
     dw = torch.empty(D, dtype=torch.float32, device=x.device)
     db = torch.empty_like(dw)
     ws = torch.empty(max(lib.rf_layernorm_bwd_workspace(M, D), 4), dtype=torch.uint8, device=x.device)
-    check(lib.rf_drop_add_ln_bwd_dual(M, D, _p(dy), _p(dy16), _p(x), _p(mean), _p(rstd), _p(w.float().contiguous()),
-                                      float(p), seed, _p(dres), _p(dt), _p(dw), _p(db), _p(ws), _stream(x)),
+    check(lib.rf_drop_add_ln_bwd_t(dtype_code(dtype), M, D, _p(dy), _p(dy16), _p(x), _p(mean), _p(rstd),
+                                   _p(w.float().contiguous()), float(p), seed, _p(dres), _p(dt), _p(dw), _p(db), _p(ws),
+                                   _stream(x)),
           "rf_drop_add_ln_bwd")
     return dres, dt, dw, db
 
@@ -399,9 +401,9 @@ def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, t
     gmax = gidx.shape[1]
     dev = q.device
     if dqkv is not None:
-        if (dqkv.dtype not in (torch.float32, torch.bfloat16) or not dqkv.is_contiguous()
+        if (dqkv.dtype not in (torch.float32, q.dtype) or not dqkv.is_contiguous()
                 or tuple(dqkv.shape) != (B * Lp, 3 * D)):
-            raise ValueError("band_attention_bwd: dqkv must be a contiguous fp32 or bf16 (B*Lp, 3*D) tensor")
+            raise ValueError("band_attention_bwd: dqkv must be a contiguous fp32 or q-dtype (B*Lp, 3*D) tensor")
         dq, dk, dv, ldg = dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], 3 * D
     else:
         dq = torch.empty(B * Lp, D, dtype=torch.float32, device=dev)
@@ -413,7 +415,7 @@ def band_attention_bwd(q, k, v, o, dout, flags, gidx, B: int, Lp: int, H: int, t
     gds = torch.empty(B, H, Lp, max(gmax, 1), dtype=torch.float32, device=dev) if gmax else None
     gpr = torch.empty_like(gds) if gmax else None
     with _region(tag):
-        rc = lib.rf_band_attn_bwd_drop(dtype_code(dq.dtype), B, Lp, H, 64, 32, _p(q), _p(k), _p(v), ld, _p(o),
+        rc = lib.rf_band_attn_bwd_drop(dtype_code(q.dtype), dtype_code(dq.dtype), B, Lp, H, 64, 32, _p(q), _p(k), _p(v), ld, _p(o),
                                        _rowmajor(o, "o"), _p(dout), _rowmajor(dout, "dout"), _p(flags),
                                        _p(gidx.contiguous()) if gmax else None, gmax, _p(dq), _p(dk), _p(dv), ldg,
                                        _p(lse2), _p(delta), _p(gds), _p(gpr), float(p_drop), int(seed), _stream(q))

@@ -176,6 +176,7 @@ class _DropAddLN(torch.autograd.Function):
         x, y, mean, rstd = out[:4]
         ctx.save_for_backward(x, mean, rstd, w)
         ctx.p, ctx.seed = p, seed
+        ctx.tdt = t.dtype
         ctx.set_materialize_grads(False)
         return (y, out[4]) if dual else y
 
@@ -184,7 +185,7 @@ class _DropAddLN(torch.autograd.Function):
         if dy is None and dy16 is None:
             return None, None, None, None, None, None, None, None
         x, mean, rstd, w = ctx.saved_tensors
-        dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16)
+        dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16, dtype=ctx.tdt)
         return dt, dres, dw, db, None, None, None, None
 
 
@@ -414,16 +415,18 @@ class _Attention(torch.autograd.Function):
             # backward of this case is the fp32 recompute as well)
             out = _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w,
                                    ctx.drop).to(q.dtype)
-        elif ctx.drop is not None:
+        elif ctx.drop is not None or q.dtype == torch.float16:
+            # global rows as torch ops (closed-form backward): under attention dropout (the hash
+            # mask) and for fp16 operands (the fold kernels are bf16 / fp32)
             out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w, p_drop=attn_p, seed=seed)
             if G > 0:
-                ctx.gz = _global_keep(gidx, B, Lp, H, attn_p, seed)
+                ctx.gz = _global_keep(gidx, B, Lp, H, attn_p, seed) if ctx.drop is not None else None
                 og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H, ctx.gz)
                 rows, keep = grows[:2] if grows is not None else _global_rows(gidx, B, Lp)
                 _put_global_rows(out, og, rows, keep, B, G)
         else:
             out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w)
-        if ctx.drop is None and G > 0:
+        if ctx.drop is None and q.dtype != torch.float16 and G > 0:
             if fold:
                 ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg,
                                           wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out)
@@ -443,13 +446,13 @@ class _Attention(torch.autograd.Function):
         D = qkv.shape[1] // 3
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         gmax = gidx.shape[1]
-        hip_local = q.dtype == torch.bfloat16 and half_w == 32 and D == 64 * H and gmax <= 32
+        hip_local = q.dtype in (torch.bfloat16, torch.float16) and half_w == 32 and D == 64 * H and gmax <= 32
         if not hip_local:
             return _Attention._backward_torch(ctx, dout)
         p_drop, seed = ctx.drop if ctx.drop is not None else (0.0, 0)
         # local branch on the HIP backward kernels (rf_attn_bwd.hip); global rows of dout belong
         # to the global branch only (their local output was overwritten)
-        d16 = dout.to(torch.bfloat16).contiguous()
+        d16 = dout.to(q.dtype).contiguous()
         # gradients written in the projection's dtype (bf16): no fp32 copy and cast per layer
         dqkv = torch.empty(B * Lp, 3 * D, dtype=qkv.dtype, device=q.device)
         dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H, dqkv=dqkv,
@@ -613,7 +616,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         gvalid = (gidx >= 0).reshape(-1, 1)
         grows = (rows, gvalid.view(-1), torch.where(gvalid.view(-1), rows, -1).to(torch.int32))
     # bf16 path: dropout + residual + LayerNorm as one HIP pass each way (_DropAddLN)
-    fused = dt == torch.bfloat16 and D in (64, 128, 256, 384, 512, 768, 1024)
+    fused = dt in (torch.bfloat16, torch.float16) and D in (64, 128, 256, 384, 512, 768, 1024)
     h16 = None  # bf16 copy of h32 written by the previous layer's LayerNorm (fused path)
     nl = len(model.encoder.layer)
     # the pass's dropout seeds (two LayerNorms per layer) in one draw from torch's CPU generator

@@ -25,7 +25,7 @@ def _tol(dt):
     return 1e-4 if dt == torch.float32 else 2e-2
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,N,K", [(64, 128, 64), (200, 200, 768), (1024, 768, 768), (320, 3840, 768), (256, 768, 3072)])
 @pytest.mark.parametrize("epi", [ops.RF_EPI_NONE, ops.RF_EPI_BIAS, ops.RF_EPI_BIAS_GELU, ops.RF_EPI_BIAS_RESID])
 def test_gemm_epilogues(dev, dt, M, N, K, epi):
@@ -86,7 +86,7 @@ def test_gemm_resid_ln(dev, dt):
     assert (out - ref).abs().max().item() <= (1e-4 if dt == torch.float32 else 1e-3) * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 def test_gemm_strided_views(dev, dt):
     """Column slices of a fused buffer as A (the q/k/v views) and as W (packed weights)."""
     big = _rand((256, 5 * 128), dev, dt, seed=5)
@@ -97,7 +97,7 @@ def test_gemm_strided_views(dev, dt):
     assert (out.float() - ref).abs().max().item() <= _tol(dt) * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("D", [128, 768])
 def test_layernorm(dev, dt, D):
     x = _rand((333, D), dev, dt, 3.0, seed=7) + 1.0
@@ -243,7 +243,7 @@ def _attn_case(dev, dt, B, Lp, H, lens, globals_, seed):
     return qkv, merged, flags, gidx, G
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", [
     dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
     dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
@@ -275,7 +275,7 @@ def test_band_and_global_attention(dev, dt, case):
     assert ctx.float().cpu()[pad_rows].abs().max().item() == 0.0 if pad_rows.any() else True
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 def test_cos_scores(dev, dt):
     z = _rand((37, 768), dev, dt, seed=30)
     E = _rand((1000, 768), dev, dt, seed=31)
@@ -326,7 +326,7 @@ def test_global_attention_fold(dev, dt, case):
             assert err <= (1e-4 if dt == torch.float32 else 2e-2), (b, g, err)
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N", [4, 1000, 50265])
 def test_cross_entropy(dev, dt, N):
     """rf_cross_entropy_fwd vs torch cross_entropy (mean over non-ignored, ignore -100) + argmax."""
@@ -519,7 +519,7 @@ def test_layernorm_bwd_matches_autograd(dev, M, D):
     assert (db - br.grad).abs().max().item() <= 1e-4 * br.grad.abs().max().item() + 1e-4
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,N", [(1, 5), (333, 768), (16384, 2304), (70, 3072), (65, 6)])
 def test_colsum(dev, dt, M, N):
     for x in (_rand((M, N + 8), dev, dt, seed=41)[:, :N], _rand((M, N + 3), dev, dt, seed=42)[:, :N]):
@@ -587,7 +587,7 @@ def test_drop_add_ln_dual(dev, D):
             assert torch.equal(u, v)
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32, torch.float16])
 def test_scatter_add_rows(dev, dt):
     """rf_scatter_add_rows: dst[rows[r]] += src[r] for two pairs, strided destinations (column
     views of one wide tensor), skipped rows (-1) and a repeated row, against index_add_."""
@@ -607,6 +607,37 @@ def test_scatter_add_rows(dev, dt):
     tol = 1e-5 if dt == torch.float32 else 1e-2  # repeated rows: addition order may differ
     assert float((wide.float() - ref.float()).abs().max()) <= tol * 8
     assert torch.equal(wide[:, :D], ref[:, :D])
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (8192, 768, 3072), (4100, 2304, 768)])
+@pytest.mark.parametrize("epi", [ops.RF_EPI_NONE, ops.RF_EPI_BIAS, ops.RF_EPI_BIAS_GELU, ops.RF_EPI_BIAS_RESID,
+                                 ops.RF_EPI_COS])
+def test_gemm_pingpong_16bit(dev, dt, M, N, K, epi):
+    """The 256x256 ping-pong kernel (grids >= 128 tiles) in bf16 and fp16 for every epilogue,
+    including a ragged M edge, against fp32 torch on the same operands."""
+    a = _rand((M, K), dev, dt, 0.5, seed=81)
+    w = _rand((N, K), dev, dt, 0.05, seed=82)
+    b = _rand((N,), dev, torch.float32, seed=83)
+    r = _rand((M, N), dev, dt, seed=84)
+    if epi == ops.RF_EPI_COS:
+        ra, rw = ops.row_inv_norm(a), ops.row_inv_norm(w)
+        out = ops.cos_scores(a, w, 20.0, z_rnorm=ra, items_rnorm=rw)
+        ref = F.normalize(a.float(), dim=-1) @ F.normalize(w.float(), dim=-1).t() * 20.0
+        assert (out - ref).abs().max().item() <= 2e-2
+        return
+    out = ops.gemm(a, w, b if epi else None, epi, resid=r if epi == ops.RF_EPI_BIAS_RESID else None,
+                   scale_cols=N // 3 // 16 * 16, col_scale=0.125)
+    ref = a.float() @ w.float().t()
+    if epi:
+        ref = ref + b
+    ref[:, :N // 3 // 16 * 16] *= 0.125
+    if epi == ops.RF_EPI_BIAS_GELU:
+        ref = F.gelu(ref)
+    if epi == ops.RF_EPI_BIAS_RESID:
+        ref = ref + r.float()
+    rel = (out.float() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+    assert rel <= (4e-3 if dt == torch.float16 else 2e-2), rel
 
 
 @pytest.mark.parametrize("M,N", [(4096, 3072), (1000, 3072), (300, 200)])

@@ -31,7 +31,7 @@ def _oracle_grads(sd0, cfg, batch, items, labels, temp):
     return float(loss.detach()), {k: v.grad for k, v in sd.items() if v.grad is not None}
 
 
-@pytest.mark.parametrize("mode", ["fp32", "autocast"])
+@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
 @pytest.mark.parametrize("name", ["c1_full", "c1_ragged"])
 def test_seqrec_full_softmax_grads(dev, mode, name):
     g = load_golden(name)
@@ -47,7 +47,8 @@ def test_seqrec_full_softmax_grads(dev, mode, name):
     model.config.finetune_negative_sample_size = 0
     model.init_item_embedding(items.clone())
     model = model.to(dev).train()
-    ctx = torch.autocast("cuda", dtype=torch.bfloat16) if mode == "autocast" else contextlib.nullcontext()
+    ctx = (torch.autocast("cuda", dtype=torch.bfloat16 if mode == "autocast" else torch.float16)
+           if mode != "fp32" else contextlib.nullcontext())
     with ctx:
         loss = model(**{k: v.to(dev) for k, v in batch.items()}, labels=labels.to(dev))
     loss.backward()
@@ -143,13 +144,14 @@ def test_pretrain_lm_head_masked_rows_only(dev, monkeypatch, train):
         assert float((ga - gb).abs().max()) <= 1e-4 * max(float(ga.abs().max()), 1e-6), k
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", [
     dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
     dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
     dict(B=1, Lp=128, H=1, lens=[128], globals_=()),
     dict(B=2, Lp=1024, H=12, lens=[1024, 700], globals_=((0, 0), (1, 0), (1, 5))),
 ])
-def test_band_attention_bwd_matches_autograd(dev, case):
+def test_band_attention_bwd_matches_autograd(dev, case, dt):
     """rf_band_attn_bwd (+ the per-sequence reduction of the global-key columns, as
     train._Attention.backward does it) against autograd through the fp32 recompute of the local
     branch (train._local_torch) on the same bf16 inputs; rows with flag != 1 get no gradient.
@@ -159,12 +161,12 @@ def test_band_attention_bwd_matches_autograd(dev, case):
     from tests.test_gpu_kernels import _attn_case
     B, Lp, H = case["B"], case["Lp"], case["H"]
     D = H * 64
-    qkv, merged, flags, gidx, G = _attn_case(dev, torch.bfloat16, B, Lp, H, case["lens"], case["globals_"], 11)
-    qkv[:, :D] = (qkv[:, :D].float() * 0.125).to(torch.bfloat16)  # pre-scaled, like the QKV GEMM output
+    qkv, merged, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, case["lens"], case["globals_"], 11)
+    qkv[:, :D] = (qkv[:, :D].float() * 0.125).to(dt)  # pre-scaled, like the QKV GEMM output
     q, k, v = (qkv[:, i * D:(i + 1) * D] for i in range(3))
     out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, 32)
     torch.manual_seed(1)
-    dout = torch.randn(B * Lp, D, device=dev).to(torch.bfloat16)
+    dout = torch.randn(B * Lp, D, device=dev).to(dt)
     dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, dout, flags, gidx, B, Lp, H)
     if G > 0:
         rows, keep = _global_rows(gidx, B, Lp)
@@ -327,7 +329,7 @@ def test_seqrec_training_with_attention_dropout(dev, name):
         assert cos >= lim or float(r.abs().max()) < 1e-6, (k, cos)
 
 
-@pytest.mark.parametrize("mode", ["fp32", "autocast"])
+@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
 def test_c2_finetune_grads_match_reference(dev, mode):
     """C3 at full model size: RecformerForSeqRec fwd + bwd at 12L/768d, L=1024, B=2 (ragged
     lengths 1024 / 700) on the HIP training path against the REAL reference's gradients
@@ -358,7 +360,8 @@ def test_c2_finetune_grads_match_reference(dev, mode):
     hdl = model.longformer.register_forward_hook(hook)
     batch = {k: v.to(dev) for k, v in batch_of(g12).items()}
     labels = torch.from_numpy(gz["labels"]).to(dev)
-    ctx = torch.autocast("cuda", dtype=torch.bfloat16) if mode == "autocast" else contextlib.nullcontext()
+    ctx = (torch.autocast("cuda", dtype=torch.bfloat16 if mode == "autocast" else torch.float16)
+           if mode != "fp32" else contextlib.nullcontext())
     with ctx:
         loss = model(**batch, labels=labels)
     loss.backward()
