@@ -3,8 +3,9 @@
 One step = RecformerForSeqRec.forward (no labels) over one batch of B synthetic user
 sequences already resident in HBM: fused prologue + embedding/LN, 12 Longformer layers
 (MFMA GEMMs, banded local + global attention, LayerNorms), CLS pooling and cosine scores
-against a 10,000-item catalog (BASELINE.json configs[1]). bf16 weights
-and activations, fp32 accumulation, random-init weights of the longformer-base shape.
+against a 10,000-item catalog (BASELINE.json configs[1]). fp32 parameters
+under torch.autocast(bf16) (the reference's mixed precision): bf16 GEMM / attention operands,
+fp32 accumulation, fp32 residual stream; random-init weights of the longformer-base shape.
 
 N GPUs (torchrun, one process per GPU): every rank encodes its own B sequences (weak
 scaling, no data-path collective: user sequences are independent); the
@@ -45,6 +46,8 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--catalog", type=int, default=10000)
     ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
+                    help="autocast dtype of the GEMM / attention operands (fp32 parameters)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0,
                     help="target CPU work for the baseline samples, split over the thread counts (0 disables)")
     ap.add_argument("--cpu-threads", type=str, default="all,omp",
@@ -245,13 +248,18 @@ def main():
     model.init_item_embedding(items)
     want_cpu = (rank == 0 and world == 1 and args.cpu_baseline_seconds > 0)
     sd_cpu = {k: v.clone() for k, v in model.longformer.state_dict().items()} if want_cpu else None
-    model = model.to(dev).to(torch.bfloat16)
+    # the reference's mixed-precision mode: fp32 parameters under torch.autocast (the mode whose
+    # parity is pinned at the north star's 1e-2, tests/test_gpu_model.py); the kernels read cached
+    # 16-bit copies of the weights, so the step does the same work as with 16-bit parameters
+    model = model.to(dev)
+    amp = {"bf16": torch.bfloat16, "fp16": torch.float16}[args.dtype]
 
     batch = synth_batch(B, L, cfg.vocab_size, seed=100 + rank, item_len=21)
     batch = {k: v.to(dev) for k, v in batch.items()}
 
     def step():
-        return model(**batch)
+        with torch.autocast("cuda", dtype=amp):
+            return model(**batch)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -336,7 +344,7 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "user-seq/s",
             "n_gpus": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded ids/types/item-pos, random-init weights of the 12L/768d shape)",
             "config": {"workload": "C2: RecformerForSeqRec encode+score, 12L/768d/H12, seq_len 1024, "
                                    "window 64, CLS global, 10k-item cosine scoring",
