@@ -63,10 +63,19 @@ __device__ __forceinline__ void load4(const bf16* p, float* x) {
   x[0] = (float)v[0]; x[1] = (float)v[1]; x[2] = (float)v[2]; x[3] = (float)v[3];
 }
 
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_g;
-__device__ __forceinline__ bf16x4 tr_read_g(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_g*)p);
+__device__ __forceinline__ void load4(const f16* p, float* x) {
+  const f16x4 v = *reinterpret_cast<const f16x4*>(p);
+  x[0] = (float)v[0]; x[1] = (float)v[1]; x[2] = (float)v[2]; x[3] = (float)v[3];
 }
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_g;
+template <typename E>
+__device__ __forceinline__ typename H16<E>::x4 tr_read_g(const char* p) {  // 16-bit bit patterns
+  return __builtin_bit_cast(typename H16<E>::x4, __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_g*)p));
+}
+// 16-bit plane type of the u planes for an element type (fp32 mode writes none)
+template <typename T> struct Plane16 { typedef T type; };
+template <> struct Plane16<float> { typedef bf16 type; };
 
 template <int N>
 __device__ __forceinline__ void wait_vm_n() {
@@ -84,6 +93,7 @@ __global__ void __launch_bounds__(256) k_gfold_u(int D, int H, int R, const T* _
                                                   int ld_qg, const T* __restrict__ wkg,
                                                   const int32_t* __restrict__ gidx, GfoldWs ws,
                                                   bool out_bf16) {
+  typedef typename Plane16<T>::type P16;
   __shared__ float qs[64];
   const int h = blockIdx.x, r = blockIdx.y;
   if (gidx[r] < 0) return;
@@ -104,16 +114,16 @@ __global__ void __launch_bounds__(256) k_gfold_u(int D, int H, int R, const T* _
       }
     }
     if (out_bf16) {
-      bf16* hi = ws.u16 + ((int64_t)r * 2 * GF_HP + h) * D + k;
-      bf16* lo = hi + (int64_t)GF_HP * D;
-      bf16x4 vh, vl;
+      P16* hi = reinterpret_cast<P16*>(ws.u16) + ((int64_t)r * 2 * GF_HP + h) * D + k;
+      P16* lo = hi + (int64_t)GF_HP * D;
+      typename H16<P16>::x4 vh, vl;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        vh[i] = (bf16)a[i];
-        vl[i] = (bf16)(a[i] - (float)vh[i]);
+        vh[i] = (P16)a[i];
+        vl[i] = (P16)(a[i] - (float)vh[i]);
       }
-      *reinterpret_cast<bf16x4*>(hi) = vh;
-      *reinterpret_cast<bf16x4*>(lo) = vl;
+      *reinterpret_cast<typename H16<P16>::x4*>(hi) = vh;
+      *reinterpret_cast<typename H16<P16>::x4*>(lo) = vl;
     } else if (h < H) {
       *reinterpret_cast<float4*>(ws.u32 + ((int64_t)r * H + h) * (D + 4) + k) = make_float4(a[0], a[1], a[2], a[3]);
     }
@@ -130,6 +140,7 @@ __global__ void __launch_bounds__(256) k_gfold_qu(int Lp, int D, int H, int gmax
                                                    const float* __restrict__ bqg, float q_scale,
                                                    const T* __restrict__ wkg, const int32_t* __restrict__ gidx,
                                                    GfoldWs ws, bool out_bf16) {
+  typedef typename Plane16<T>::type P16;
   __shared__ float hrow[1024];
   __shared__ float qs[64];
   const int h = blockIdx.x, r = blockIdx.y;
@@ -172,16 +183,16 @@ __global__ void __launch_bounds__(256) k_gfold_qu(int Lp, int D, int H, int gmax
       }
     }
     if (out_bf16) {
-      bf16* hi = ws.u16 + ((int64_t)r * 2 * GF_HP + h) * D + k;
-      bf16* lo = hi + (int64_t)GF_HP * D;
-      bf16x4 vh, vl;
+      P16* hi = reinterpret_cast<P16*>(ws.u16) + ((int64_t)r * 2 * GF_HP + h) * D + k;
+      P16* lo = hi + (int64_t)GF_HP * D;
+      typename H16<P16>::x4 vh, vl;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        vh[i] = (bf16)a[i];
-        vl[i] = (bf16)(a[i] - (float)vh[i]);
+        vh[i] = (P16)a[i];
+        vl[i] = (P16)(a[i] - (float)vh[i]);
       }
-      *reinterpret_cast<bf16x4*>(hi) = vh;
-      *reinterpret_cast<bf16x4*>(lo) = vl;
+      *reinterpret_cast<typename H16<P16>::x4*>(hi) = vh;
+      *reinterpret_cast<typename H16<P16>::x4*>(lo) = vl;
     } else if (h < H) {
       *reinterpret_cast<float4*>(ws.u32 + ((int64_t)r * H + h) * (D + 4) + k) = make_float4(a[0], a[1], a[2], a[3]);
     }
@@ -207,13 +218,15 @@ __device__ __forceinline__ int gimg(int row, int col) {
 // the 64-column segments of Wkg its u columns need; with `sep` that slice has its own LDS region
 // and its DMA goes out with Wqg's at the start (one wait), else it reuses the Wqg region after
 // the qg phase.
-template <int D>
-__global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, const bf16* __restrict__ hs,
-                                                        int ldh, const bf16* __restrict__ wqg,
+template <typename E, int D>
+__global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, const E* __restrict__ hs,
+                                                        int ldh, const E* __restrict__ wqg,
                                                         const float* __restrict__ bqg, float q_scale,
-                                                        const bf16* __restrict__ wkg,
+                                                        const E* __restrict__ wkg,
                                                         const int32_t* __restrict__ gidx, GfoldWs ws,
                                                         int sep) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NK = D / 32;
   constexpr int nseg = D >> 6;
@@ -229,17 +242,17 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
   const int r = r0 + 16 * wave + li;
   const int pos = r < R ? gidx[r] : -1;
 
-  bf16x8 a[NK];
+  V8 a[NK];
   if (pos >= 0) {
-    const bf16* hr = hs + ((int64_t)(r / gmax) * Lp + pos) * ldh + 8 * g;
+    const E* hr = hs + ((int64_t)(r / gmax) * Lp + pos) * ldh + 8 * g;
 #pragma unroll
-    for (int s = 0; s < NK; ++s) a[s] = *reinterpret_cast<const bf16x8*>(hr + 32 * s);
+    for (int s = 0; s < NK; ++s) a[s] = *reinterpret_cast<const V8*>(hr + 32 * s);
   } else {
 #pragma unroll
-    for (int s = 0; s < NK; ++s) a[s] = bf16x8{};
+    for (int s = 0; s < NK; ++s) a[s] = V8{};
   }
   // segments [s0, s1) of the head's 64-row weight slice into image `dst` (segment s at s - s0)
-  auto dma_head = [&](const bf16* w, char* dst, int s0, int s1) {
+  auto dma_head = [&](const E* w, char* dst, int s0, int s1) {
     for (int p = wave + 8 * s0; p < s1 * 8; p += 4) {
       const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
       const int chk = (lane & 7) ^ (row & 7);
@@ -258,18 +271,18 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
     for (int s = 0; s < NK; ++s)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(smem + gimg(16 * nt + li, 32 * s + 8 * g));
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b, acc[nt], 0, 0, 0);
+        const V8 b = *reinterpret_cast<const V8*>(smem + gimg(16 * nt + li, 32 * s + 8 * g));
+        acc[nt] = mfma16(a[s], b, acc[nt]);
       }
     // C[row 4g+i][d 16nt+li] -> qg^T image [d][row]
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int d = 16 * nt + li;
       const float bb = bqg[h * 64 + d];
-      bf16x4 v;
+      V4 v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (bf16)((acc[nt][i] + bb) * q_scale);
-      *reinterpret_cast<bf16x4*>(pimg + (d * 16 + 4 * g) * 2) = v;
+      for (int i = 0; i < 4; ++i) v[i] = (E)((acc[nt][i] + bb) * q_scale);
+      *reinterpret_cast<V4*>(pimg + (d * 16 + 4 * g) * 2) = v;
     }
   }
   __syncthreads();  // every wave is done with the Wqg image
@@ -281,18 +294,18 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
     wait_vmcnt0();
   }
   __syncthreads();
-  bf16x8 pb[2];
+  V8 pb[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int rb = 32 * s + 8 * g + q4;
-    const bf16x4 v0 = tr_read_g(pimg + (rb * 16 + 4 * p4) * 2);
-    const bf16x4 v1 = tr_read_g(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
-    pb[s] = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    const V4 v0 = tr_read_g<E>(pimg + (rb * 16 + 4 * p4) * 2);
+    const V4 v1 = tr_read_g<E>(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
+    pb[s] = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
   }
   const int rw = r0 + 16 * wave + li;  // C column n = li -> this wave's row li
   const bool wr = rw < R && gidx[rw] >= 0;
-  bf16* hi = ws.u16 + ((int64_t)rw * 2 * GF_HP + h) * D + 4 * g;
-  bf16* lo = hi + (int64_t)GF_HP * D;
+  E* hi = reinterpret_cast<E*>(ws.u16) + ((int64_t)rw * 2 * GF_HP + h) * D + 4 * g;
+  E* lo = hi + (int64_t)GF_HP * D;
   // column split (gridDim.z): this block writes u columns [z D / nz, (z + 1) D / nz)
   for (int ct = ct0; ct < ct0 + nct; ++ct) {
     const int c0 = 16 * ct, cl = c0 - 64 * sg0;  // column within the staged slice
@@ -300,10 +313,10 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int rb = 32 * s + 8 * g + q4;
-      const bf16x4 v0 = tr_read_g(kimg + gimg(rb, cl + 4 * p4));
-      const bf16x4 v1 = tr_read_g(kimg + gimg(rb + 4, cl + 4 * p4));
-      const bf16x8 wa = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, pb[s], acc, 0, 0, 0);
+      const V4 v0 = tr_read_g<E>(kimg + gimg(rb, cl + 4 * p4));
+      const V4 v1 = tr_read_g<E>(kimg + gimg(rb + 4, cl + 4 * p4));
+      const V8 wa = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      acc = mfma16(wa, pb[s], acc);
     }
     // C[col c0+4g+i][row li]
 #if defined(RF_GF_DIAG) && (RF_GF_DIAG & 1)
@@ -311,14 +324,14 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
 #else
     if (wr) {
 #endif
-      bf16x4 vh, vl;
+      V4 vh, vl;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        vh[i] = (bf16)acc[i];
-        vl[i] = (bf16)(acc[i] - (float)vh[i]);
+        vh[i] = (E)acc[i];
+        vl[i] = (E)(acc[i] - (float)vh[i]);
       }
-      *reinterpret_cast<bf16x4*>(hi + c0) = vh;
-      *reinterpret_cast<bf16x4*>(lo + c0) = vl;
+      *reinterpret_cast<V4*>(hi + c0) = vh;
+      *reinterpret_cast<V4*>(lo + c0) = vl;
     }
   }
 }
@@ -327,12 +340,14 @@ __global__ void __launch_bounds__(256) k_gfold_qu_mfma(int Lp, int R, int gmax, 
 // grid (H, ceil(R/64)). w_h[row] = sum_c exp(m_c - M) w_c / sum_c exp(m_c - M) l_c is formed in
 // registers from the fp32 chunk partials and split into hi + lo bf16 (MFMA B operand);
 // out[row][h*64+d] = Wvg[h*64+d] . w_h[row] + bvg, with the head's Wvg slice in LDS.
-template <int D>
+template <typename E, int D>
 __global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax, int nch,
-                                                         const bf16* __restrict__ wvg,
+                                                         const E* __restrict__ wvg,
                                                          const float* __restrict__ bvg,
                                                          const int32_t* __restrict__ gidx, GfoldWs ws,
-                                                         bf16* __restrict__ out, int ldo) {
+                                                         E* __restrict__ out, int ldo) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NK = D / 32;
   constexpr int nseg = D >> 6;
@@ -379,28 +394,28 @@ __global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax,
       w8[4] = fmaf(sc, x1.x, w8[4]); w8[5] = fmaf(sc, x1.y, w8[5]);
       w8[6] = fmaf(sc, x1.z, w8[6]); w8[7] = fmaf(sc, x1.w, w8[7]);
     }
-    bf16x8 bh, bl;
+    V8 bh, bl;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      bh[i] = (bf16)w8[i];
-      bl[i] = (bf16)(w8[i] - (float)bh[i]);
+      bh[i] = (E)w8[i];
+      bl[i] = (E)(w8[i] - (float)bh[i]);
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const bf16x8 wa = *reinterpret_cast<const bf16x8*>(smem + gimg(16 * nt + li, 32 * s + 8 * g));
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bh, acc[nt], 0, 0, 0);
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bl, acc[nt], 0, 0, 0);
+      const V8 wa = *reinterpret_cast<const V8*>(smem + gimg(16 * nt + li, 32 * s + 8 * g));
+      acc[nt] = mfma16(wa, bh, acc[nt]);
+      acc[nt] = mfma16(wa, bl, acc[nt]);
     }
   }
   // C[d 16nt+4g+i][row li]
   if (pos >= 0) {
-    bf16* o = out + ((int64_t)(r / gmax) * Lp + pos) * ldo + h * 64 + 4 * g;
+    E* o = out + ((int64_t)(r / gmax) * Lp + pos) * ldo + h * 64 + 4 * g;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      bf16x4 v;
+      V4 v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (bf16)(acc[nt][i] + bvg[h * 64 + 16 * nt + 4 * g + i]);
-      *reinterpret_cast<bf16x4*>(o + 16 * nt) = v;
+      for (int i = 0; i < 4; ++i) v[i] = (E)(acc[nt][i] + bvg[h * 64 + 16 * nt + 4 * g + i]);
+      *reinterpret_cast<V4*>(o + 16 * nt) = v;
     }
   }
 }
@@ -411,12 +426,14 @@ __global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax,
 // over that half are done — so the h stream overlaps the MFMA work instead of alternating
 // with it. Row validity comes from per-sub-chunk ballots taken in the prologue (no global
 // load inside the loop, whose hipcc wait would drain the DMA queue).
-template <int D>
+template <typename E, int D>
 __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
-                                                             const bf16* __restrict__ hs, int ldh,
+                                                             const E* __restrict__ hs, int ldh,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
                                                              GfoldWs ws, int H) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NK = D / 32;
   constexpr int nseg = D >> 6;
@@ -437,7 +454,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
   float* m_run = red + 128;
   float* alpha_s = red + 144;
   unsigned long long* vmask = reinterpret_cast<unsigned long long*>(red + 160);  // per sub-chunk
-  const bf16* hb = hs + (int64_t)b * Lp * ldh;
+  const E* hb = hs + (int64_t)b * Lp * ldh;
   const int row_begin = ch * GF_CH;
   const int row_end = min(row_begin + GF_CH, Lp);
   const int nsub = (row_end - row_begin + 63) >> 6;
@@ -453,14 +470,14 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     }
   };
   // u fragments (B operand of S^T = H.U^T): hi and lo planes; heads >= H score 0
-  bf16x8 uh[NK], ul[NK];
+  V8 uh[NK], ul[NK];
   {
-    const bf16* uhi = ws.u16 + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
-    const bf16* ulo = uhi + (int64_t)GF_HP * D;
+    const E* uhi = reinterpret_cast<const E*>(ws.u16) + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
+    const E* ulo = uhi + (int64_t)GF_HP * D;
 #pragma unroll
     for (int s2 = 0; s2 < NK; ++s2) {
-      uh[s2] = li < H ? *reinterpret_cast<const bf16x8*>(uhi + 32 * s2) : bf16x8{};
-      ul[s2] = li < H ? *reinterpret_cast<const bf16x8*>(ulo + 32 * s2) : bf16x8{};
+      uh[s2] = li < H ? *reinterpret_cast<const V8*>(uhi + 32 * s2) : V8{};
+      ul[s2] = li < H ? *reinterpret_cast<const V8*>(ulo + 32 * s2) : V8{};
     }
   }
   if (wave < nsub) {  // validity ballots of the (up to 4) 64-row sub-chunks
@@ -489,18 +506,18 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int s2 = 0; s2 < NK / 2; ++s2) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + gimg(arow, 32 * s2 + 8 * g));
-      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, uh[s2], st, 0, 0, 0);
-      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ul[s2], st, 0, 0, 0);
+      const V8 a = *reinterpret_cast<const V8*>(smem + gimg(arow, 32 * s2 + 8 * g));
+      st = mfma16(a, uh[s2], st);
+      st = mfma16(a, ul[s2], st);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // half B landed
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int s2 = NK / 2; s2 < NK; ++s2) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + gimg(arow, 32 * s2 + 8 * g));
-      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, uh[s2], st, 0, 0, 0);
-      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ul[s2], st, 0, 0, 0);
+      const V8 a = *reinterpret_cast<const V8*>(smem + gimg(arow, 32 * s2 + 8 * g));
+      st = mfma16(a, uh[s2], st);
+      st = mfma16(a, ul[s2], st);
     }
     const unsigned long long vm = vmask[sub];
     float mx = GF_NEG_INF;
@@ -519,12 +536,12 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     const float m_new = fmaxf(m_old, fmaxf(fmaxf(red[li], red[16 + li]), fmaxf(red[32 + li], red[48 + li])));
     const float mu = (m_new == GF_NEG_INF) ? 0.f : m_new;
     float ls = 0.f;
-    bf16* pt = reinterpret_cast<bf16*>(pimg);
+    E* pt = reinterpret_cast<E*>(pimg);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float p = __expf(st[q] - mu);
       ls += p;
-      pt[(16 * wave + 4 * g + q) * 16 + li] = (bf16)p;
+      pt[(16 * wave + 4 * g + q) * 16 + li] = (E)p;
     }
     ls += __shfl_xor(ls, 16, 64);
     ls += __shfl_xor(ls, 32, 64);
@@ -541,13 +558,13 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     float al[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) al[q] = alpha_s[4 * g + q];
-    bf16x8 pa[2];
+    V8 pa[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const int rb = 32 * s2 + 8 * g + q4;
-      const bf16x4 v0 = tr_read_g(pimg + (rb * 16 + 4 * p4) * 2);
-      const bf16x4 v1 = tr_read_g(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
-      pa[s2] = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const V4 v0 = tr_read_g<E>(pimg + (rb * 16 + 4 * p4) * 2);
+      const V4 v1 = tr_read_g<E>(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
+      pa[s2] = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -560,10 +577,10 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int rb = 32 * s2 + 8 * g + q4;
-          const bf16x4 v0 = tr_read_g(smem + gimg(rb, col));
-          const bf16x4 v1 = tr_read_g(smem + gimg(rb + 4, col));
-          const bf16x8 hb8 = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[s2], hb8, acc[i], 0, 0, 0);
+          const V4 v0 = tr_read_g<E>(smem + gimg(rb, col));
+          const V4 v1 = tr_read_g<E>(smem + gimg(rb + 4, col));
+          const V8 hb8 = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          acc[i] = mfma16(pa[s2], hb8, acc[i]);
         }
       }
       // every wave is done reading this half of the image: refill it with the next sub-chunk
@@ -591,12 +608,14 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
 }
 
 // Single-buffered form for D not a multiple of 128 (one 64-row DMA, then compute).
-template <int D>
+template <typename E, int D>
 __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
-                                                             const bf16* __restrict__ hs, int ldh,
+                                                             const E* __restrict__ hs, int ldh,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
                                                              GfoldWs ws, int H) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NK = D / 32;
   constexpr int nseg = D >> 6;
@@ -608,21 +627,21 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
   const int g = lane >> 4, li = lane & 15;
   const int q4 = li >> 2, p4 = li & 3;
   // u fragments (B operand of S^T = H.U^T): hi and lo planes, issued before the first DMA wait
-  bf16x8 uh[NK], ul[NK];
+  V8 uh[NK], ul[NK];
   {
-    const bf16* uhi = ws.u16 + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
-    const bf16* ulo = uhi + (int64_t)GF_HP * D;
+    const E* uhi = reinterpret_cast<const E*>(ws.u16) + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
+    const E* ulo = uhi + (int64_t)GF_HP * D;
 #pragma unroll
     for (int s = 0; s < NK; ++s) {  // heads >= H: zero scores (their u rows are not written)
-      uh[s] = li < H ? *reinterpret_cast<const bf16x8*>(uhi + 32 * s) : bf16x8{};
-      ul[s] = li < H ? *reinterpret_cast<const bf16x8*>(ulo + 32 * s) : bf16x8{};
+      uh[s] = li < H ? *reinterpret_cast<const V8*>(uhi + 32 * s) : V8{};
+      ul[s] = li < H ? *reinterpret_cast<const V8*>(ulo + 32 * s) : V8{};
     }
   }
   char* pimg = smem + nseg * 64 * 128;                         // P [64 rows][16 heads] bf16
   float* red = reinterpret_cast<float*>(pimg + 64 * 16 * 2);    // [max 4x16][sum 4x16][m 16][alpha 16]
   float* m_run = red + 128;
   float* alpha_s = red + 144;
-  const bf16* hb = hs + (int64_t)b * Lp * ldh;
+  const E* hb = hs + (int64_t)b * Lp * ldh;
   if (threadIdx.x < 16) m_run[threadIdx.x] = GF_NEG_INF;
   float l_run = 0.f;  // per head li (valid in wave 0, g == 0)
   f32x4 acc[nmt];
@@ -647,9 +666,9 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
     const int arow = 16 * wave + li;
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + gimg(arow, 32 * s + 8 * g));
-      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, uh[s], st, 0, 0, 0);
-      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ul[s], st, 0, 0, 0);
+      const V8 a = *reinterpret_cast<const V8*>(smem + gimg(arow, 32 * s + 8 * g));
+      st = mfma16(a, uh[s], st);
+      st = mfma16(a, ul[s], st);
     }
     float mx = GF_NEG_INF;
 #pragma unroll
@@ -667,12 +686,12 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
     const float m_new = fmaxf(m_old, fmaxf(fmaxf(red[li], red[16 + li]), fmaxf(red[32 + li], red[48 + li])));
     const float mu = (m_new == GF_NEG_INF) ? 0.f : m_new;
     float ls = 0.f;
-    bf16* pt = reinterpret_cast<bf16*>(pimg);
+    E* pt = reinterpret_cast<E*>(pimg);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float p = __expf(st[q] - mu);
       ls += p;
-      pt[(16 * wave + 4 * g + q) * 16 + li] = (bf16)p;
+      pt[(16 * wave + 4 * g + q) * 16 + li] = (E)p;
     }
     ls += __shfl_xor(ls, 16, 64);
     ls += __shfl_xor(ls, 32, 64);
@@ -689,13 +708,13 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
     float al[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) al[q] = alpha_s[4 * g + q];
-    bf16x8 pa[2];
+    V8 pa[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int rb = 32 * s + 8 * g + q4;
-      const bf16x4 v0 = tr_read_g(pimg + (rb * 16 + 4 * p4) * 2);
-      const bf16x4 v1 = tr_read_g(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
-      pa[s] = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const V4 v0 = tr_read_g<E>(pimg + (rb * 16 + 4 * p4) * 2);
+      const V4 v1 = tr_read_g<E>(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
+      pa[s] = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     }
 #pragma unroll
     for (int i = 0; i < nmt; ++i) {
@@ -705,10 +724,10 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int rb = 32 * s + 8 * g + q4;
-        const bf16x4 v0 = tr_read_g(smem + gimg(rb, col));
-        const bf16x4 v1 = tr_read_g(smem + gimg(rb + 4, col));
-        const bf16x8 hb8 = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[s], hb8, acc[i], 0, 0, 0);
+        const V4 v0 = tr_read_g<E>(smem + gimg(rb, col));
+        const V4 v1 = tr_read_g<E>(smem + gimg(rb + 4, col));
+        const V8 hb8 = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        acc[i] = mfma16(pa[s], hb8, acc[i]);
       }
     }
   }
@@ -880,34 +899,33 @@ static bool gfold_use_mfma(int R, bool qu) {
   return qu || R >= 256;  // qg/u: MFMA with a column split wins at any R (C2: 20 -> 12.5 us)
 }
 
-// partial + out stages shared by both entry points (u already in the workspace)
-static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
-                            const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax,
-                            GfoldWs ws, int nch, void* out, int ld_out, hipStream_t s, bool do_partial = true,
-                            bool do_out = true) {
+// partial + out stages of the 16-bit path (bf16 / fp16 operands)
+template <typename E>
+static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
+                              const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax, GfoldWs ws,
+                              int nch, void* out, int ld_out, hipStream_t s, bool do_partial, bool do_out) {
   const int R = B * gmax;
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
-  if (dtype == RF_BF16) {
     const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + 160 * sizeof(float) + 4 * 8;
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
 #define GP_(DD)                                                                                 \
   case DD:                                                                                      \
     if (DD % 128 == 0) {                                                                        \
-      (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<DD>,                          \
+      (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<E, DD>,                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
-      k_gfold_partial_bf16<DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const bf16*)h, ldh,  \
+      k_gfold_partial_bf16<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const E*)h, ldh,  \
                                                                 flags, gidx, ws, H);            \
     } else {                                                                                    \
-      (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16_1<DD>,                        \
+      (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16_1<E, DD>,                        \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
-      k_gfold_partial_bf16_1<DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const bf16*)h, ldh, \
+      k_gfold_partial_bf16_1<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const E*)h, ldh, \
                                                                   flags, gidx, ws, H);          \
     }                                                                                           \
     break;
     if (do_partial) switch (D) {
       GP_(64) GP_(128) GP_(192) GP_(256) GP_(384) GP_(512) GP_(768) GP_(1024)
       default:
-        RF_REQUIRE(false, "rf_global_attn_fold(bf16): unsupported hidden size %d", D);
+        RF_REQUIRE(false, "rf_global_attn_fold(16-bit): unsupported hidden size %d", D);
     }
 #undef GP_
     if (!do_out) {
@@ -915,17 +933,33 @@ static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* 
       const size_t lds_w = (size_t)D * 128;
 #define GO_(DD)                                                                                 \
   case DD:                                                                                      \
-    (void)hipFuncSetAttribute((const void*)k_gfold_out_mfma<DD>,                                \
+    (void)hipFuncSetAttribute((const void*)k_gfold_out_mfma<E, DD>,                                \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w);          \
-    k_gfold_out_mfma<DD><<<dim3(H, (R + 63) / 64), 256, lds_w, s>>>(Lp, R, gmax, nch, (const bf16*)wvg, \
-                                                                   bvg, gidx, ws, (bf16*)out, ld_out); \
+    k_gfold_out_mfma<E, DD><<<dim3(H, (R + 63) / 64), 256, lds_w, s>>>(Lp, R, gmax, nch, (const E*)wvg, \
+                                                                   bvg, gidx, ws, (E*)out, ld_out); \
     break;
       switch (D) { GO_(64) GO_(128) GO_(192) GO_(256) GO_(384) GO_(512) GO_(768) GO_(1024) }
 #undef GO_
     } else {
-      k_gfold_out<bf16><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const bf16*)wvg, bvg, gidx, ws,
-                                                        (bf16*)out, ld_out);
+      k_gfold_out<E><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const E*)wvg, bvg, gidx, ws,
+                                                        (E*)out, ld_out);
     }
+  return RF_OK;
+}
+
+// partial + out stages shared by both entry points (u already in the workspace)
+static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
+                            const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax,
+                            GfoldWs ws, int nch, void* out, int ld_out, hipStream_t s, bool do_partial = true,
+                            bool do_out = true) {
+  const int R = B * gmax;
+  const size_t lds_o = (size_t)(D + nch) * sizeof(float);
+  if (dtype == RF_BF16 || dtype == RF_F16) {
+    return dtype == RF_F16
+               ? fold_partial_out16<f16>(B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s,
+                                         do_partial, do_out)
+               : fold_partial_out16<bf16>(B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s,
+                                          do_partial, do_out);
   } else {
     const size_t lds_p = (size_t)(H * (D + 4) + H * GF_CHF) * sizeof(float);
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
@@ -951,18 +985,20 @@ extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, c
   RF_REQUIRE(D == H * 64, "rf_global_attn_fold_fwd: D=%d must be H*64", D);
   RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_fwd: at most %d heads", GF_HP);
   RF_REQUIRE(ldh >= D && ld_qg >= D && ld_out >= D, "rf_global_attn_fold_fwd: dims");
-  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F32, "rf_global_attn_fold_fwd: bad dtype %d", dtype);
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16 || dtype == RF_F32, "rf_global_attn_fold_fwd: bad dtype %d", dtype);
   if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
   RF_REQUIRE(workspace && gidx && flags, "rf_global_attn_fold_fwd: null workspace/gidx/flags");
-  RF_REQUIRE(dtype != RF_BF16 || ldh % 8 == 0, "rf_global_attn_fold_fwd(bf16): ldh must be a multiple of 8");
+  RF_REQUIRE(dtype == RF_F32 || ldh % 8 == 0, "rf_global_attn_fold_fwd(16-bit): ldh must be a multiple of 8");
   RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_fwd(f32): ldh must be a multiple of 4");
   const int R = B * gmax;
-  const int nch = (Lp + (dtype == RF_BF16 ? GF_CH : GF_CHF) - 1) / (dtype == RF_BF16 ? GF_CH : GF_CHF);
+  const int nch = (Lp + (dtype != RF_F32 ? GF_CH : GF_CHF) - 1) / (dtype != RF_F32 ? GF_CH : GF_CHF);
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16)
     k_gfold_u<bf16><<<dim3(GF_HP, R), 192, 0, s>>>(D, H, R, (const bf16*)qg, ld_qg, (const bf16*)wkg, gidx,
                                                     ws, true);
+  else if (dtype == RF_F16)
+    k_gfold_u<f16><<<dim3(GF_HP, R), 192, 0, s>>>(D, H, R, (const f16*)qg, ld_qg, (const f16*)wkg, gidx, ws, true);
   else
     k_gfold_u<float><<<dim3(H, R), 192, 0, s>>>(D, H, R, (const float*)qg, ld_qg, (const float*)wkg, gidx,
                                                  ws, false);
@@ -982,17 +1018,17 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
   RF_REQUIRE(D == H * 64 && D <= 1024, "rf_global_attn_fold_h: D=%d must be H*64 <= 1024", D);
   RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_h: at most %d heads", GF_HP);
   RF_REQUIRE(ldh >= D && ld_out >= D, "rf_global_attn_fold_h: dims");
-  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F32, "rf_global_attn_fold_h: bad dtype %d", dtype);
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16 || dtype == RF_F32, "rf_global_attn_fold_h: bad dtype %d", dtype);
   if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
   RF_REQUIRE(workspace && gidx && flags && wqg && bqg, "rf_global_attn_fold_h: null pointer");
-  RF_REQUIRE(dtype != RF_BF16 || ldh % 8 == 0, "rf_global_attn_fold_h(bf16): ldh must be a multiple of 8");
+  RF_REQUIRE(dtype == RF_F32 || ldh % 8 == 0, "rf_global_attn_fold_h(16-bit): ldh must be a multiple of 8");
   RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_h(f32): ldh must be a multiple of 4");
   const int R = B * gmax;
-  const int nch = (Lp + (dtype == RF_BF16 ? GF_CH : GF_CHF) - 1) / (dtype == RF_BF16 ? GF_CH : GF_CHF);
+  const int nch = (Lp + (dtype != RF_F32 ? GF_CH : GF_CHF) - 1) / (dtype != RF_F32 ? GF_CH : GF_CHF);
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
   if (!(stage & 1)) {
-  } else if (dtype == RF_BF16 && gfold_use_mfma(R, true)) {
+  } else if (dtype != RF_F32 && gfold_use_mfma(R, true)) {
     RF_REQUIRE(D % 64 == 0 && D <= 1024, "rf_global_attn_fold_h: D=%d", D);
     // few row tiles: split u's columns over more blocks (each recomputes its tile's qg)
     int qsplit = 1;
@@ -1005,17 +1041,26 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
     const size_t lds_q = (size_t)D * 128 + (sep ? (size_t)nslice * 8192 : 0) + 4 * 2048;
 #define GQ_(DD)                                                                                   \
   case DD:                                                                                        \
-    (void)hipFuncSetAttribute((const void*)k_gfold_qu_mfma<DD>,                                   \
+    (void)hipFuncSetAttribute((const void*)k_gfold_qu_mfma<E, DD>,                                \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q);            \
-    k_gfold_qu_mfma<DD><<<dim3(H, (R + 63) / 64, qsplit), 256, lds_q, s>>>(Lp, R, gmax, (const bf16*)h, ldh, \
-                                                                  (const bf16*)wqg, bqg, q_scale,  \
-                                                                  (const bf16*)wkg, gidx, ws, sep); \
+    k_gfold_qu_mfma<E, DD><<<dim3(H, (R + 63) / 64, qsplit), 256, lds_q, s>>>(Lp, R, gmax, (const E*)h, ldh, \
+                                                                     (const E*)wqg, bqg, q_scale,  \
+                                                                     (const E*)wkg, gidx, ws, sep); \
     break;
-    switch (D) { GQ_(64) GQ_(128) GQ_(192) GQ_(256) GQ_(384) GQ_(512) GQ_(768) GQ_(1024) default: break; }
+    if (dtype == RF_F16) {
+      typedef f16 E;
+      switch (D) { GQ_(64) GQ_(128) GQ_(192) GQ_(256) GQ_(384) GQ_(512) GQ_(768) GQ_(1024) default: break; }
+    } else {
+      typedef bf16 E;
+      switch (D) { GQ_(64) GQ_(128) GQ_(192) GQ_(256) GQ_(384) GQ_(512) GQ_(768) GQ_(1024) default: break; }
+    }
 #undef GQ_
   } else if (dtype == RF_BF16)
     k_gfold_qu<bf16><<<dim3(GF_HP, R), 256, 0, s>>>(Lp, D, H, gmax, (const bf16*)h, ldh, (const bf16*)wqg, bqg,
                                                      q_scale, (const bf16*)wkg, gidx, ws, true);
+  else if (dtype == RF_F16)
+    k_gfold_qu<f16><<<dim3(GF_HP, R), 256, 0, s>>>(Lp, D, H, gmax, (const f16*)h, ldh, (const f16*)wqg, bqg, q_scale,
+                                                    (const f16*)wkg, gidx, ws, true);
   else
     k_gfold_qu<float><<<dim3(H, R), 256, 0, s>>>(Lp, D, H, gmax, (const float*)h, ldh, (const float*)wqg, bqg,
                                                   q_scale, (const float*)wkg, gidx, ws, false);

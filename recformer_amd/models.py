@@ -421,9 +421,7 @@ class RecformerModel(nn.Module):
         windows = cfg.window_per_layer()
         # global rows: the key/value-projection fold by default; `config.global_attention_fold
         # = False` keeps the reference's structure (k_g/v_g projected over all tokens).
-        # (fp16: the unfolded form, key_global / value_global projected with the q|k|v GEMM — the
-        # fold kernels are bf16 / fp32)
-        fold = getattr(cfg, "global_attention_fold", True) and dt != torch.float16
+        fold = getattr(cfg, "global_attention_fold", True)
         eps = cfg.layer_norm_eps
         gws = None
         for li, lw in enumerate(pk["layers"]):

@@ -415,18 +415,17 @@ class _Attention(torch.autograd.Function):
             # backward of this case is the fp32 recompute as well)
             out = _attention_torch(q, k, v, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w,
                                    ctx.drop).to(q.dtype)
-        elif ctx.drop is not None or q.dtype == torch.float16:
-            # global rows as torch ops (closed-form backward): under attention dropout (the hash
-            # mask) and for fp16 operands (the fold kernels are bf16 / fp32)
+        elif ctx.drop is not None:
+            # global rows under attention dropout (the hash mask) as torch ops; closed-form backward
             out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w, p_drop=attn_p, seed=seed)
             if G > 0:
-                ctx.gz = _global_keep(gidx, B, Lp, H, attn_p, seed) if ctx.drop is not None else None
+                ctx.gz = _global_keep(gidx, B, Lp, H, attn_p, seed)
                 og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H, ctx.gz)
                 rows, keep = grows[:2] if grows is not None else _global_rows(gidx, B, Lp)
                 _put_global_rows(out, og, rows, keep, B, G)
         else:
             out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w)
-        if ctx.drop is None and q.dtype != torch.float16 and G > 0:
+        if ctx.drop is None and G > 0:
             if fold:
                 ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg,
                                           wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out)

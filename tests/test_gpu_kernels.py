@@ -288,7 +288,7 @@ def test_cos_scores(dev, dt):
     assert (sc - refc).abs().max().item() <= (1e-4 if dt == torch.float32 else 2e-2)
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", [
     dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
     dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
@@ -348,7 +348,7 @@ def test_cross_entropy(dev, dt, N):
     assert abs(float(ops.cross_entropy(xp[:, :N], lab)) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", [
     dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
     dict(B=2, Lp=1024, H=12, lens=[1024, 333], globals_=((0, 0), (1, 0))),
@@ -378,7 +378,7 @@ def test_global_attention_fold_from_h(dev, dt, case):
     assert ctx_a.abs().sum().item() > 0
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,Lp,H", [(3, 192, 3), (4, 1024, 12), (300, 64, 12)])
 def test_global_fold_h_stages_match_one_call(dev, dt, B, Lp, H):
     """rf_global_attn_fold_h_stage(1) then (2) — as the encoder runs it, with h overwritten in
