@@ -60,7 +60,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, fl
   if (EPI == RF_EPI_BIAS_GELU_AUX)
     reinterpret_cast<TIN*>(const_cast<void*>(e.R))[(int64_t)row * e.ldr + col] = from_f32<TIN>(v);
   if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX)
-    v = (CF32 || !std::is_same<TIN, bf16>::value) ? gelu_erf(v) : gelu_bf16out(v);  // fp16: exact form
+    v = (CF32 || sizeof(TIN) == 4) ? gelu_erf(v) : gelu_bf16out(v);  // 16-bit outputs: the fitted form
   if (EPI == RF_EPI_BIAS_RESID) {
     if (RF32)
       v += reinterpret_cast<const float*>(e.R)[(int64_t)row * e.ldr + col];
@@ -139,7 +139,7 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
   }
   if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = (CF32 || !H16<E>::bf) ? gelu_erf(v[k]) : gelu_bf16out(v[k]);
+    for (int k = 0; k < 16; ++k) v[k] = CF32 ? gelu_erf(v[k]) : gelu_bf16out(v[k]);
   }
   if (EPI == RF_EPI_BIAS_RESID) {
     if (RF32) {
@@ -552,7 +552,7 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
     }
   }
   if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
-    if (CF32 || !H16<E>::bf) {  // fp16 outputs: the exact form (the fitted one is sized to bf16)
+    if (CF32) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[k] = gelu_erf(v[k]);
     } else {

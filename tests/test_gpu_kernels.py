@@ -408,13 +408,13 @@ def test_global_fold_h_stages_match_one_call(dev, dt, B, Lp, H):
         ops.global_attention_fold_h_stage(2, ws, h_keep, *args)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,Lp,H", [(300, 64, 12), (70, 192, 3), (5, 1024, 12)])
-def test_global_fold_mfma_matches_gemv(dev, monkeypatch, B, Lp, H):
+def test_global_fold_mfma_matches_gemv(dev, monkeypatch, B, Lp, H, dt):
     """The 64-row MFMA qg/u and out kernels (chosen for >= 256 global rows, e.g. a catalog of
     short item sequences) against the per-row GEMV kernels (pinned to the torch reference by
     test_band_and_global_attention) on the same inputs: ragged lengths, sequences without a
     global token (gidx -1), several globals per sequence and a partial last 64-row tile."""
-    dt = torch.bfloat16
     D = H * 64
     g = torch.Generator().manual_seed(B)
     lens = [int(x) for x in torch.randint(1, Lp + 1, (B,), generator=g)]
