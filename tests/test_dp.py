@@ -191,3 +191,61 @@ def test_pretrain_contrastive_dp_world2_matches_single_process(bucketed):
     for g, r in zip(grads, ref_grads):
         assert torch.allclose(g * 2, r, atol=1e-5, rtol=1e-5)
     assert n >= 2
+
+
+def _combine_worker(rank, ws, port, out_q):
+    """One rank's shard result for C5 retrieval (what rf_score_rank + rf_topk_* produce on the
+    device): counts over its catalog shard and its top-k with global ids; combined over ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from recformer_amd.ranker import combine_shards
+        parts = _shard_parts(rank, ws)
+        out = combine_shards(parts, 5)
+        out_q.put((rank, {k: (v.clone() if torch.is_tensor(v) else v) for k, v in out.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _scores():
+    g = torch.Generator().manual_seed(3)
+    s = torch.round(torch.randn(6, 40, generator=g) * 4) / 4  # ties across shard boundaries
+    lab = torch.tensor([0, 39, 17, 20, 5, 33])
+    return s, lab
+
+
+def _shard_parts(rank, ws):
+    from recformer_amd.ranker import merge_topk
+    s, lab = _scores()
+    a, b = dp.shard_range(s.shape[1], rank, ws)
+    sl = s.gather(1, lab[:, None])
+    sh = s[:, a:b]
+    ids = torch.arange(a, b, dtype=torch.int32).expand(s.shape[0], b - a)
+    v, i = merge_topk(sh, ids, 5)
+    return {"gt": (sh > sl).sum(1).to(torch.int32), "valid": torch.full((s.shape[0],), b - a, dtype=torch.int32),
+            "sexp": torch.exp(sh - 20.0).sum(1), "topv": v, "topi": i, "shift": 20.0}
+
+
+def test_retrieval_combine_world2_matches_one_shard():
+    """world-2 gloo: each rank's catalog-shard counts and top-k (ties across the shard boundary),
+    combined by ranker.combine_shards (all-reduce of counts / exp-sums, all-gather + merge of the
+    top-k), equal the single-shard result on every rank."""
+    from recformer_amd.ranker import merge_topk
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_combine_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    s, lab = _scores()
+    ref_v, ref_i = merge_topk(s, torch.arange(40, dtype=torch.int32).expand(6, 40), 5)
+    for r in (0, 1):
+        out = got[r]
+        assert torch.equal(out["gt"], (s > s.gather(1, lab[:, None])).sum(1).to(torch.int32))
+        assert torch.equal(out["valid"], torch.full((6,), 40, dtype=torch.int32))
+        assert torch.allclose(out["sexp"], torch.exp(s - 20.0).sum(1), rtol=1e-6)
+        assert torch.equal(out["topv"], ref_v) and torch.equal(out["topi"], ref_i)
