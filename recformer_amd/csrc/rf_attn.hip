@@ -880,6 +880,108 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
 }
 
 // ------------------------------------------------------------------------------------
+// Short sequences (Lp <= 64, a multiple of 16: catalog items of <s> + up to 63 tokens, padded to
+// a multiple of 16 instead of the 64-token window; finetune.py:38-63): every key of the sequence
+// is in one 64-row tile, so one workgroup per (sequence, head) scores all of them. Same contract
+// as the band kernels: a local query i sees keys j with flag 1 and |i - j| <= 32, plus every global
+// key (flag 2, local K/V); padded query rows are written as 0. Keys / values DMA'd to LDS, Q^T
+// fragments straight from HBM; S^T = K Q^T and O^T = V^T P^T on MFMA.
+constexpr int AS_K = 0, AS_V = 8192, AS_FL = 16384, AS_LDS = 16448;
+
+template <typename E>
+__global__ void __launch_bounds__(256) k_attn_short(int Lp, int H, const E* __restrict__ q, const E* __restrict__ k,
+                                                    const E* __restrict__ v, int ld, const uint8_t* __restrict__ flags,
+                                                    E* __restrict__ out, int ldo) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
+  __shared__ __attribute__((aligned(16))) char smem[AS_LDS];
+  const int bh = blockIdx.x, h = bh % H, b = bh / H;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t rb = (int64_t)b * Lp;
+  const int hoff = h * 64;
+  uint8_t* fl = reinterpret_cast<uint8_t*>(smem + AS_FL);
+  // K / V rows 0..63 (clamped into the sequence; rows >= Lp are masked): 2 pieces of 8 rows per wave
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 16 * wave + 8 * j + (lane >> 3);
+    const int ch = (lane & 7) ^ (row & 7);
+    const int64_t off = (rb + min(row, Lp - 1)) * ld + hoff + ch * 8;
+    glds16(k + off, smem + AS_K + (16 * wave + 8 * j) * 128);
+    glds16(v + off, smem + AS_V + (16 * wave + 8 * j) * 128);
+  }
+  if (threadIdx.x < 64) fl[threadIdx.x] = (int)threadIdx.x < Lp ? flags[rb + threadIdx.x] : 0;
+  const int myq = 16 * wave + li;
+  const int qr = min(myq, Lp - 1);
+  V8 qf[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) qf[s2] = *reinterpret_cast<const V8*>(q + (rb + qr) * ld + hoff + 32 * s2 + 8 * g);
+  wait_vmcnt0();
+  __syncthreads();
+  if (16 * wave >= Lp) return;  // whole wave past the sequence (after the barrier)
+  f32x4 st[4];
+  float mx = RF_NEG_INF;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      st[t] = mfma16(*reinterpret_cast<const V8*>(smem + AS_K + swz128(16 * t + li, 4 * s2 + g)), qf[s2], st[t]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kj = 16 * t + 4 * g + r;
+      const int f = kj < Lp ? fl[kj] : 0;
+      const bool ok = (f == 1 && abs(kj - myq) <= 32) || f == 2;
+      st[t][r] = ok ? st[t][r] : RF_NEG_INF;
+      mx = fmaxf(mx, st[t][r]);
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float nmu = (mx == RF_NEG_INF) ? 0.f : -mx * LOG2E;
+  float lsum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      st[t][r] = __builtin_amdgcn_exp2f(fmaf(st[t][r], LOG2E, nmu));
+      lsum += st[t][r];
+    }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int rr = 4 * g + (li >> 2);
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    V8 pf;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pf[j] = (E)st[2 * s2 + (j >> 2)][j & 3];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int col = 16 * dt + 4 * (li & 3);
+      const V4 v0 = tr_read<E>(smem + AS_V, swz_el(32 * s2 + rr, col));
+      const V4 v1 = tr_read<E>(smem + AS_V, swz_el(32 * s2 + 16 + rr, col));
+      const V8 vf = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      o[dt] = mfma16(vf, pf, o[dt]);
+    }
+  }
+  if (myq >= Lp) return;
+  const bool qvalid = fl[myq] != 0;
+  const float inv = (qvalid && lsum > 0.f) ? 1.0f / lsum : 0.f;
+  E* orow = out + (rb + myq) * ldo + hoff + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    V4 w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w[r] = (E)(o[dt][r] * inv);
+    *reinterpret_cast<V4*>(orow + 16 * dt) = w;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Local branch, generic element type, VALU (fp32 parity path; any even window).
 // One wave per (query, head): lanes own keys; scores reduced with wave shuffles.
 template <typename T>
@@ -1047,10 +1149,20 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
   if (dtype == RF_BF16 || dtype == RF_F16) {
     const bool h16 = dtype == RF_F16;
     RF_REQUIRE(half_w == 32, "rf_band_attn_fwd(bf16): window must be 64 (half 32), got half %d", half_w);
-    RF_REQUIRE(Lp % 64 == 0, "rf_band_attn_fwd(bf16): Lp=%d must be a multiple of 64", Lp);
+    RF_REQUIRE(Lp % 64 == 0 || (Lp < 64 && Lp % 16 == 0 && dr.thresh == 0),
+               "rf_band_attn_fwd(16-bit): Lp=%d must be a multiple of 64, or < 64 and a multiple of 16 "
+               "(short sequences; no dropout)", Lp);
     RF_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0, "rf_band_attn_fwd(bf16): alignment");
     RF_REQUIRE(dr.thresh == 0 || gmax <= 32, "rf_band_attn_fwd(bf16): dropout needs gmax <= 32 (got %d)", gmax);
-    if (gmax <= 32 && (g_knob[KNOB_BAND_PATH] != 2 || dr.thresh)) {
+    if (Lp < 64) {
+      RF_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0, "rf_band_attn_fwd(short): alignment");
+      if (h16)
+        k_attn_short<f16><<<H * B, 256, 0, s>>>(Lp, H, (const f16*)q, (const f16*)k, (const f16*)v, ld_qkv, flags,
+                                                 (f16*)out, ld_out);
+      else
+        k_attn_short<bf16><<<H * B, 256, 0, s>>>(Lp, H, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv, flags,
+                                                  (bf16*)out, ld_out);
+    } else if (gmax <= 32 && (g_knob[KNOB_BAND_PATH] != 2 || dr.thresh)) {
       // pipelined: runs of qpb query blocks per workgroup, >= ~3 workgroups per CU slot
       const int nqb = Lp / 64;
       int qpb = nqb >= 16 ? (nqb + 1) / 2 : nqb;

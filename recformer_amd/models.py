@@ -217,6 +217,10 @@ def _cos_train(z: torch.Tensor, items: torch.Tensor, temp: float) -> torch.Tenso
 # bf16 path: keep the fp32 residual stream as split (hi, lo) 16-bit planes;
 # False = a plain fp32 tensor plus a separate bf16 GEMM operand (A/B tools, tests).
 SPLIT_STREAM = True
+# sequences shorter than the 64-token window (catalog items: <s> + <= 63 tokens, finetune.py:38-63)
+# padded to a multiple of 16 instead of 64 (rf_band_attn_fwd's short-sequence kernel): the valid
+# rows' outputs are the same (padding is masked), with up to 3/4 fewer rows through every GEMM
+SHORT_SEQ = True
 # run the global fold's pass over h before the qkv GEMM (rf_global_attn_fold_h_stage)
 FOLD_EARLY = True
 # training: RecformerForPretraining's four encoder passes share one autograd cast per weight
@@ -384,6 +388,9 @@ class RecformerModel(nn.Module):
         B, L = input_ids.shape
         W = self._window()
         Lp = L + (W - L % W) % W
+        windows_all = cfg.window_per_layer()
+        if SHORT_SEQ and L < W and W == 64 and all(w == 64 for w in windows_all):
+            Lp = max(16, (L + 15) // 16 * 16)
         D, H = cfg.hidden_size, cfg.num_attention_heads
         hd = D // H
         dt = _compute_dtype(self.dtype)

@@ -186,3 +186,41 @@ def test_c2_full_size_properties(dev):
     assert (s_perm - s[perm]).abs().max().item() <= 1e-4
     assert (s_one - s[[0, 17, 63]]).abs().max().item() <= 1e-4
     assert (s.max(1).values <= 1.0 / cfg.temp + 1e-3).all()  # |cos| <= 1
+
+
+@pytest.fixture(scope="module")
+def catalog_case():
+    """A catalog-shaped batch (C5 / finetune.py:38-63 item encoding): 260 items of <s> + 32
+    attribute tokens (L = 33), one global CLS row each (>= 256 global rows: the MFMA fold path),
+    12L/768d weights; the oracle's fp32 outputs (oracle/restatement.py, pinned to the reference)."""
+    from oracle import restatement as R
+    from recformer_amd.synth import synth_batch
+    torch.set_num_threads(16)
+    m = hashed_model(BASE, seed=2)
+    b = synth_batch(260, 33, BASE["vocab_size"], seed=77, item_len=32)
+    b["attention_mask"][7, 20:] = 0  # a few ragged items
+    b["attention_mask"][100, 5:] = 0
+    h, p = R.model_forward(m.state_dict(), m.config, **b)
+    return m, b, h, p
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
+@pytest.mark.parametrize("short", [True, False])
+def test_catalog_batch_vs_oracle(dev, catalog_case, monkeypatch, mode, short):
+    """Catalog encoding end to end against the oracle: the short-sequence path (L = 33 padded to
+    48, rf_band_attn_fwd's Lp < 64 kernel; models.SHORT_SEQ) and the window-padded one (Lp = 64)."""
+    from recformer_amd import models
+    monkeypatch.setattr(models, "SHORT_SEQ", short)
+    m, b, h_ref, p_ref = catalog_case
+    import copy
+    model, ctx = _prep(copy.deepcopy(m), dev, mode)
+    with torch.no_grad(), ctx:
+        out = model(**{k: v.to(dev) for k, v in b.items()})
+    assert out.last_hidden_state.shape == h_ref.shape
+    valid = b["attention_mask"].bool()
+    e = errs(out.last_hidden_state[valid.to(dev)], h_ref[valid])
+    ep = errs(out.pooler_output, p_ref)
+    if mode == "fp32":
+        assert e["max"] <= 1e-3 and ep["max"] <= 1e-3, (e, ep)
+    else:
+        _check_e2e(mode, e, out.pooler_output, p_ref)
