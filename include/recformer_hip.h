@@ -244,6 +244,19 @@ int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, const void* 
                             const void* wvg, const float* bvg, const uint8_t* flags,
                             const int32_t* gidx, int gmax, void* workspace, void* out,
                             int ld_out, rf_stream_t stream);
+/* The same with attention-probability dropout on the global rows (training; TF:1036-1037):
+ * w_h = sum_j z_j p_j h_j and the value bias weighted by sum_j z_j p_j, with z the keep mask x
+ * 1/(1-p) of row (b*H + h)*Lp + gidx[b,g], key j (rf_common.h drop_keep). 16-bit dtypes only;
+ * p_drop = 0 is rf_global_attn_fold_fwd. */
+int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int H, const void* qg, int ld_qg,
+                                 const void* h, int ldh, const void* wkg, const float* bkg,
+                                 const void* wvg, const float* bvg, const uint8_t* flags,
+                                 const int32_t* gidx, int gmax, void* workspace, void* out,
+                                 int ld_out, float p_drop, uint64_t seed, rf_stream_t stream);
+/* That mask for the backward: z (B, H, gmax, Lp) fp32, z[b,h,g,l] = keep x 1/(1-p) of row
+ * (b*H + h)*Lp + max(gidx[b,g], 0), key l. */
+int rf_attn_global_keep(int B, int H, int Lp, const int32_t* gidx, int gmax, float p_drop,
+                        uint64_t seed, float* z, rf_stream_t stream);
 
 /* The same, starting from the layer input: qg_h = (Wqg_h h_g + bqg_h) * q_scale for each global
  * row's hidden vector h_g (query_global, TF:972-982, rounded to dtype like a GEMM output), then

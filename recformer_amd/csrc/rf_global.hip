@@ -27,12 +27,15 @@ constexpr float GF_NEG_INF = -__builtin_inff();
 constexpr int GF_CH = 256;    // rows per chunk (bf16 kernel walks it in 64-row sub-chunks)
 constexpr int GF_CHF = 64;    // rows per chunk of the fp32 VALU kernel
 constexpr int GF_HP = 16;     // heads padded to one MFMA column tile (H <= 16)
+constexpr int GF_RED_LD = 176;  // partial kernels' LDS reduction area: dropped sums at red + 176
+constexpr int GF_RED_FLOATS = GF_RED_LD + 64;
 
 struct GfoldWs {
   bf16* u16;     // [R][2 planes hi/lo][16][D]
   float* u32;    // [R][H][D+4]
   float* m;      // [R][nch][16]
   float* l;      // [R][nch][16]
+  float* ld;     // [R][nch][16]  sum of the dropped probabilities (attention dropout only)
   float* w;      // [R][nch][16][D]
 };
 
@@ -45,13 +48,14 @@ inline GfoldWs gfold_carve(void* ws, int R, int nch, int H, int D) {
   w.u32 = (float*)p; p += align256((size_t)R * H * (D + 4) * 4);
   w.m = (float*)p; p += align256((size_t)R * nch * GF_HP * 4);
   w.l = (float*)p; p += align256((size_t)R * nch * GF_HP * 4);
+  w.ld = (float*)p; p += align256((size_t)R * nch * GF_HP * 4);
   w.w = (float*)p;
   return w;
 }
 
 inline size_t gfold_bytes(int R, int nch, int H, int D) {
   return align256((size_t)R * 2 * GF_HP * D * 2) + align256((size_t)R * H * (D + 4) * 4) +
-         2 * align256((size_t)R * nch * GF_HP * 4) + (size_t)R * nch * D * GF_HP * 4;
+         3 * align256((size_t)R * nch * GF_HP * 4) + (size_t)R * nch * D * GF_HP * 4;
 }
 
 __device__ __forceinline__ void load4(const float* p, float* x) {
@@ -345,7 +349,7 @@ __global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax,
                                                          const E* __restrict__ wvg,
                                                          const float* __restrict__ bvg,
                                                          const int32_t* __restrict__ gidx, GfoldWs ws,
-                                                         E* __restrict__ out, int ldo) {
+                                                         E* __restrict__ out, int ldo, bool drop) {
   typedef typename H16<E>::x8 V8;
   typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -364,12 +368,16 @@ __global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax,
   const int rr = pos >= 0 ? r : 0;  // rows without a global token read row 0's partials, unused
   float mx = GF_NEG_INF;
   for (int c = 0; c < nch; ++c) mx = fmaxf(mx, ws.m[((int64_t)rr * nch + c) * GF_HP + h]);
-  float lsum = 0.f;
+  float lsum = 0.f, dsum = 0.f;
   for (int c = 0; c < nch; ++c) {
     const float mc = ws.m[((int64_t)rr * nch + c) * GF_HP + h];
-    lsum += (mc == GF_NEG_INF ? 0.f : __expf(mc - mx)) * ws.l[((int64_t)rr * nch + c) * GF_HP + h];
+    const float sc = mc == GF_NEG_INF ? 0.f : __expf(mc - mx);
+    lsum += sc * ws.l[((int64_t)rr * nch + c) * GF_HP + h];
+    if (drop) dsum += sc * ws.ld[((int64_t)rr * nch + c) * GF_HP + h];
   }
   const float inv = lsum > 0.f ? 1.0f / lsum : 0.f;
+  // the value bias enters with the weight sum_j p'_j (1 without dropout: the p_j sum to 1)
+  const float bw = drop ? dsum * inv : 1.f;
   wait_vmcnt0();
   __syncthreads();
   f32x4 acc[4];
@@ -414,7 +422,8 @@ __global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax,
     for (int nt = 0; nt < 4; ++nt) {
       V4 v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (E)(acc[nt][i] + bvg[h * 64 + 16 * nt + 4 * g + i]);
+      for (int i = 0; i < 4; ++i) v[i] = (E)(acc[nt][i] + (drop ? bvg[h * 64 + 16 * nt + 4 * g + i] * bw
+                                                                 : bvg[h * 64 + 16 * nt + 4 * g + i]));
       *reinterpret_cast<V4*>(o + 16 * nt) = v;
     }
   }
@@ -431,7 +440,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
                                                              const E* __restrict__ hs, int ldh,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
-                                                             GfoldWs ws, int H) {
+                                                             GfoldWs ws, int H, AttnDrop dr) {
   typedef typename H16<E>::x8 V8;
   typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -490,7 +499,8 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // u fragments and flags, before the DMA stream
   dma_half(row_begin, 0);
   dma_half(row_begin, 1);
-  float l_run = 0.f;  // per head li (valid in wave 0, g == 0)
+  float l_run = 0.f, ld_run = 0.f;  // per head li (valid in wave 0, g == 0)
+  const uint64_t drow = ((uint64_t)b * H + li) * Lp + (uint64_t)max(gidx[r], 0);  // dropout mask row
   f32x4 acc[nmt];
 #pragma unroll
   for (int i = 0; i < nmt; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -535,21 +545,33 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     const float m_old = m_run[li];
     const float m_new = fmaxf(m_old, fmaxf(fmaxf(red[li], red[16 + li]), fmaxf(red[32 + li], red[48 + li])));
     const float mu = (m_new == GF_NEG_INF) ? 0.f : m_new;
-    float ls = 0.f;
+    float ls = 0.f, lsd = 0.f;
     E* pt = reinterpret_cast<E*>(pimg);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float p = __expf(st[q] - mu);
+      float p = __expf(st[q] - mu);
       ls += p;
+      if (dr.thresh) {  // TF:1036-1037: W and the value-bias weight use the dropped probabilities
+        p *= attn_keep_scale(dr, drow, Lp, j0 + 16 * wave + 4 * g + q);
+        lsd += p;
+      }
       pt[(16 * wave + 4 * g + q) * 16 + li] = (E)p;
     }
     ls += __shfl_xor(ls, 16, 64);
     ls += __shfl_xor(ls, 32, 64);
     if (g == 0) red[64 + wave * 16 + li] = ls;
+    if (dr.thresh) {
+      lsd += __shfl_xor(lsd, 16, 64);
+      lsd += __shfl_xor(lsd, 32, 64);
+      if (g == 0) red[GF_RED_LD + wave * 16 + li] = lsd;
+    }
     __syncthreads();  // P, sums and every wave's read of m_run are done
     if (wave == 0 && g == 0) {
       const float a = __expf(m_old - mu);  // 0 when m_old = -inf
       l_run = l_run * a + red[64 + li] + red[80 + li] + red[96 + li] + red[112 + li];
+      if (dr.thresh)
+        ld_run = ld_run * a + red[GF_RED_LD + li] + red[GF_RED_LD + 16 + li] + red[GF_RED_LD + 32 + li] +
+                 red[GF_RED_LD + 48 + li];
       alpha_s[li] = a;
       m_run[li] = m_new;
     }
@@ -593,6 +615,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
   if (wave == 0 && g == 0) {
     ws.m[((int64_t)r * nch + ch) * GF_HP + li] = m_run[li];
     ws.l[((int64_t)r * nch + ch) * GF_HP + li] = l_run;
+    if (dr.thresh) ws.ld[((int64_t)r * nch + ch) * GF_HP + li] = ld_run;
   }
   float* wout = ws.w + ((int64_t)r * nch + ch) * GF_HP * D;
 #pragma unroll
@@ -613,7 +636,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
                                                              const E* __restrict__ hs, int ldh,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
-                                                             GfoldWs ws, int H) {
+                                                             GfoldWs ws, int H, AttnDrop dr) {
   typedef typename H16<E>::x8 V8;
   typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -643,7 +666,8 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
   float* alpha_s = red + 144;
   const E* hb = hs + (int64_t)b * Lp * ldh;
   if (threadIdx.x < 16) m_run[threadIdx.x] = GF_NEG_INF;
-  float l_run = 0.f;  // per head li (valid in wave 0, g == 0)
+  float l_run = 0.f, ld_run = 0.f;  // per head li (valid in wave 0, g == 0)
+  const uint64_t drow = ((uint64_t)b * H + li) * Lp + (uint64_t)max(gidx[r], 0);  // dropout mask row
   f32x4 acc[nmt];
 #pragma unroll
   for (int i = 0; i < nmt; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -685,21 +709,33 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
     const float m_old = m_run[li];
     const float m_new = fmaxf(m_old, fmaxf(fmaxf(red[li], red[16 + li]), fmaxf(red[32 + li], red[48 + li])));
     const float mu = (m_new == GF_NEG_INF) ? 0.f : m_new;
-    float ls = 0.f;
+    float ls = 0.f, lsd = 0.f;
     E* pt = reinterpret_cast<E*>(pimg);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float p = __expf(st[q] - mu);
+      float p = __expf(st[q] - mu);
       ls += p;
+      if (dr.thresh) {  // TF:1036-1037: W and the value-bias weight use the dropped probabilities
+        p *= attn_keep_scale(dr, drow, Lp, j0 + 16 * wave + 4 * g + q);
+        lsd += p;
+      }
       pt[(16 * wave + 4 * g + q) * 16 + li] = (E)p;
     }
     ls += __shfl_xor(ls, 16, 64);
     ls += __shfl_xor(ls, 32, 64);
     if (g == 0) red[64 + wave * 16 + li] = ls;
+    if (dr.thresh) {
+      lsd += __shfl_xor(lsd, 16, 64);
+      lsd += __shfl_xor(lsd, 32, 64);
+      if (g == 0) red[GF_RED_LD + wave * 16 + li] = lsd;
+    }
     __syncthreads();  // P, sums and every wave's read of m_run are done
     if (wave == 0 && g == 0) {
       const float a = __expf(m_old - mu);  // 0 when m_old = -inf
       l_run = l_run * a + red[64 + li] + red[80 + li] + red[96 + li] + red[112 + li];
+      if (dr.thresh)
+        ld_run = ld_run * a + red[GF_RED_LD + li] + red[GF_RED_LD + 16 + li] + red[GF_RED_LD + 32 + li] +
+                 red[GF_RED_LD + 48 + li];
       alpha_s[li] = a;
       m_run[li] = m_new;
     }
@@ -734,6 +770,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
   if (wave == 0 && g == 0) {
     ws.m[((int64_t)r * nch + ch) * GF_HP + li] = m_run[li];
     ws.l[((int64_t)r * nch + ch) * GF_HP + li] = l_run;
+    if (dr.thresh) ws.ld[((int64_t)r * nch + ch) * GF_HP + li] = ld_run;
   }
   float* wout = ws.w + ((int64_t)r * nch + ch) * GF_HP * D;
 #pragma unroll
@@ -828,10 +865,10 @@ __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int gmax, int 
                                                     const T* __restrict__ wvg,
                                                     const float* __restrict__ bvg,
                                                     const int32_t* __restrict__ gidx, GfoldWs ws,
-                                                    T* __restrict__ out, int ldo) {
+                                                    T* __restrict__ out, int ldo, bool drop) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];  // D floats + nch scales
   float* scl = wsm + D;
-  __shared__ float lsum_s;
+  __shared__ float lsum_s, dsum_s;
   const int h = blockIdx.x, r = blockIdx.y;
   const int pos = gidx[r];
   if (pos < 0) return;
@@ -841,18 +878,24 @@ __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int gmax, int 
     float mx = GF_NEG_INF;
     for (int c = t; c < nch; c += 64) mx = fmaxf(mx, ws.m[((int64_t)r * nch + c) * GF_HP + h]);
     mx = wave_max(mx);
-    float ls = 0.f;
+    float ls = 0.f, ds = 0.f;
     for (int c = t; c < nch; c += 64) {
       const float mc = ws.m[((int64_t)r * nch + c) * GF_HP + h];
       const float sc = (mc == GF_NEG_INF) ? 0.f : __expf(mc - mx);
       scl[c] = sc;
       ls += sc * ws.l[((int64_t)r * nch + c) * GF_HP + h];
+      if (drop) ds += sc * ws.ld[((int64_t)r * nch + c) * GF_HP + h];
     }
     ls = wave_sum(ls);
-    if (t == 0) lsum_s = ls;
+    if (drop) ds = wave_sum(ds);
+    if (t == 0) {
+      lsum_s = ls;
+      dsum_s = ds;
+    }
   }
   __syncthreads();
   const float inv = lsum_s > 0.f ? 1.0f / lsum_s : 0.f;
+  const float bw = drop ? dsum_s * inv : 1.f;  // value-bias weight sum_j p'_j (see k_gfold_out_mfma)
   for (int k = t; k < D; k += 256) {
     float a = 0.f;
     for (int c = 0; c < nch; ++c) a = fmaf(scl[c], ws.w[(((int64_t)r * nch + c) * GF_HP + h) * D + k], a);
@@ -874,7 +917,8 @@ __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int gmax, int 
     }
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
-    if (part == 0) out[((int64_t)b * Lp + pos) * ldo + h * 64 + d] = from_f32<T>(a + bvg[h * 64 + d]);
+    if (part == 0)
+      out[((int64_t)b * Lp + pos) * ldo + h * 64 + d] = from_f32<T>(a + (drop ? bvg[h * 64 + d] * bw : bvg[h * 64 + d]));
   }
 }
 
@@ -903,10 +947,11 @@ static bool gfold_use_mfma(int R, bool qu) {
 template <typename E>
 static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
                               const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax, GfoldWs ws,
-                              int nch, void* out, int ld_out, hipStream_t s, bool do_partial, bool do_out) {
+                              int nch, void* out, int ld_out, hipStream_t s, bool do_partial, bool do_out,
+                              AttnDrop dr) {
   const int R = B * gmax;
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
-    const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + 160 * sizeof(float) + 4 * 8;
+    const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + GF_RED_FLOATS * sizeof(float);
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
 #define GP_(DD)                                                                                 \
   case DD:                                                                                      \
@@ -914,12 +959,12 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<E, DD>,                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
       k_gfold_partial_bf16<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const E*)h, ldh,  \
-                                                                flags, gidx, ws, H);            \
+                                                                flags, gidx, ws, H, dr);        \
     } else {                                                                                    \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16_1<E, DD>,                        \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
       k_gfold_partial_bf16_1<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const E*)h, ldh, \
-                                                                  flags, gidx, ws, H);          \
+                                                                  flags, gidx, ws, H, dr);      \
     }                                                                                           \
     break;
     if (do_partial) switch (D) {
@@ -936,13 +981,14 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
     (void)hipFuncSetAttribute((const void*)k_gfold_out_mfma<E, DD>,                                \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w);          \
     k_gfold_out_mfma<E, DD><<<dim3(H, (R + 63) / 64), 256, lds_w, s>>>(Lp, R, gmax, nch, (const E*)wvg, \
-                                                                   bvg, gidx, ws, (E*)out, ld_out); \
+                                                                   bvg, gidx, ws, (E*)out, ld_out, \
+                                                                   dr.thresh != 0);                 \
     break;
       switch (D) { GO_(64) GO_(128) GO_(192) GO_(256) GO_(384) GO_(512) GO_(768) GO_(1024) }
 #undef GO_
     } else {
       k_gfold_out<E><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const E*)wvg, bvg, gidx, ws,
-                                                        (E*)out, ld_out);
+                                                        (E*)out, ld_out, dr.thresh != 0);
     }
   return RF_OK;
 }
@@ -951,15 +997,15 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
 static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
                             const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax,
                             GfoldWs ws, int nch, void* out, int ld_out, hipStream_t s, bool do_partial = true,
-                            bool do_out = true) {
+                            bool do_out = true, AttnDrop dr = AttnDrop{0, 0, 1.f}) {
   const int R = B * gmax;
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
   if (dtype == RF_BF16 || dtype == RF_F16) {
     return dtype == RF_F16
                ? fold_partial_out16<f16>(B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s,
-                                         do_partial, do_out)
+                                         do_partial, do_out, dr)
                : fold_partial_out16<bf16>(B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s,
-                                          do_partial, do_out);
+                                          do_partial, do_out, dr);
   } else {
     const size_t lds_p = (size_t)(H * (D + 4) + H * GF_CHF) * sizeof(float);
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
@@ -969,18 +1015,21 @@ static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* 
       k_gfold_partial_f32<<<dim3(nch, R), 256, lds_p, s>>>(Lp, D, H, gmax, (const float*)h, ldh, flags, gidx, ws);
     if (do_out)
       k_gfold_out<float><<<dim3(H, R), 256, lds_o, s>>>(Lp, D, gmax, nch, (const float*)wvg, bvg, gidx, ws,
-                                                       (float*)out, ld_out);
+                                                       (float*)out, ld_out, false);
   }
   return RF_OK;
 }
 
-extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, const void* qg,
-                                       int ld_qg, const void* h, int ldh, const void* wkg,
-                                       const float* bkg, const void* wvg, const float* bvg,
-                                       const uint8_t* flags, const int32_t* gidx, int gmax,
-                                       void* workspace, void* out, int ld_out,
-                                       rf_stream_t stream) {
+extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int H, const void* qg,
+                                            int ld_qg, const void* h, int ldh, const void* wkg,
+                                            const float* bkg, const void* wvg, const float* bvg,
+                                            const uint8_t* flags, const int32_t* gidx, int gmax,
+                                            void* workspace, void* out, int ld_out, float p_drop,
+                                            uint64_t seed, rf_stream_t stream) {
   (void)bkg;  // softmax-invariant (see header comment)
+  RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_global_attn_fold_fwd: p_drop %f not in [0, 1)", p_drop);
+  RF_REQUIRE(p_drop == 0.f || dtype != RF_F32, "rf_global_attn_fold_fwd: attention dropout needs 16-bit operands");
+  const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f};
   RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0, "rf_global_attn_fold_fwd: bad shape");
   RF_REQUIRE(D == H * 64, "rf_global_attn_fold_fwd: D=%d must be H*64", D);
   RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_fwd: at most %d heads", GF_HP);
@@ -1002,9 +1051,41 @@ extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, c
   else
     k_gfold_u<float><<<dim3(H, R), 192, 0, s>>>(D, H, R, (const float*)qg, ld_qg, (const float*)wkg, gidx,
                                                  ws, false);
-  const int rc = fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s);
+  const int rc =
+      fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s, true, true, dr);
   if (rc != RF_OK) return rc;
   RF_LAUNCH_CHECK("rf_global_attn_fold_fwd");
+}
+
+extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, const void* qg, int ld_qg,
+                                       const void* h, int ldh, const void* wkg, const float* bkg, const void* wvg,
+                                       const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax,
+                                       void* workspace, void* out, int ld_out, rf_stream_t stream) {
+  return rf_global_attn_fold_fwd_drop(dtype, B, Lp, D, H, qg, ld_qg, h, ldh, wkg, bkg, wvg, bvg, flags, gidx, gmax,
+                                      workspace, out, ld_out, 0.f, 0, stream);
+}
+
+// Attention-dropout scale of the global query rows (TF:1036-1037) for the training backward:
+// z[((b H + h) gmax + g) Lp + l] = keep(row (b H + h) Lp + gidx[b][g], key l) / (1 - p); an empty
+// slot (gidx < 0) uses position 0 (its gradient is zero). recformer_amd/train.py _global_keep.
+__global__ void k_attn_global_keep(int B, int H, int Lp, int gmax, const int32_t* __restrict__ gidx, AttnDrop dr,
+                                   float* __restrict__ z) {
+  const int bhg = blockIdx.y;  // (b H + h) gmax + g
+  const int g = bhg % gmax, bh = bhg / gmax, b = bh / H;
+  const uint64_t row = (uint64_t)bh * Lp + (uint64_t)max(gidx[b * gmax + g], 0);
+  for (int l = blockIdx.x * blockDim.x + threadIdx.x; l < Lp; l += gridDim.x * blockDim.x)
+    z[(int64_t)bhg * Lp + l] = attn_keep_scale(dr, row, Lp, l);
+}
+
+extern "C" int rf_attn_global_keep(int B, int H, int Lp, const int32_t* gidx, int gmax, float p_drop, uint64_t seed,
+                                   float* z, rf_stream_t stream) {
+  RF_REQUIRE(B >= 0 && H > 0 && Lp >= 0 && gmax >= 0, "rf_attn_global_keep: bad shape");
+  RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_attn_global_keep: p_drop %f not in [0, 1)", p_drop);
+  if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
+  RF_REQUIRE(gidx && z, "rf_attn_global_keep: null pointer");
+  const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f};
+  k_attn_global_keep<<<dim3((Lp + 255) / 256, B * H * gmax), 256, 0, as_stream(stream)>>>(B, H, Lp, gmax, gidx, dr, z);
+  RF_LAUNCH_CHECK("rf_attn_global_keep");
 }
 
 extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, int D, int H, const void* h,

@@ -488,9 +488,10 @@ def global_attention(qg, kg, vg, flags, gidx, B: int, Lp: int, H: int, out: torc
 
 
 def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int,
-                          out: torch.Tensor, tag: Optional[str] = None):
-    """Global query rows through the key/value-projection fold (rf_global_attn_fold_fwd):
-    overwrites ctx rows at the global positions."""
+                          out: torch.Tensor, tag: Optional[str] = None, p_drop: float = 0.0, seed: int = 0):
+    """Global query rows through the key/value-projection fold (rf_global_attn_fold_fwd_drop):
+    overwrites ctx rows at the global positions; p_drop > 0: attention-probability dropout with
+    the counter-hash mask of `seed` (16-bit dtypes)."""
     lib = _lib.load()
     gmax = gidx.shape[1]
     if gmax == 0:
@@ -503,12 +504,25 @@ def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: in
         if not t.is_contiguous() or t.dtype != h.dtype:
             raise ValueError("global_attention_fold: weights must be contiguous in the compute dtype")
     with _region(tag):
-        rc = lib.rf_global_attn_fold_fwd(dtype_code(h.dtype), B, Lp, D, H, _p(qg), _rowmajor(qg, "qg"),
-                                         _p(h), _rowmajor(h, "h"), _p(wkg), _p(bkg), _p(wvg), _p(bvg),
-                                         _p(flags), _p(gidx.contiguous()), gmax, _p(ws), _p(out),
-                                         _rowmajor(out, "out"), _stream(out))
-    check(rc, "rf_global_attn_fold_fwd")
+        rc = lib.rf_global_attn_fold_fwd_drop(dtype_code(h.dtype), B, Lp, D, H, _p(qg), _rowmajor(qg, "qg"),
+                                              _p(h), _rowmajor(h, "h"), _p(wkg), _p(bkg), _p(wvg), _p(bvg),
+                                              _p(flags), _p(gidx.contiguous()), gmax, _p(ws), _p(out),
+                                              _rowmajor(out, "out"), float(p_drop), int(seed) & (2**64 - 1),
+                                              _stream(out))
+    check(rc, "rf_global_attn_fold_fwd_drop")
     return out
+
+
+def attn_global_keep(gidx, B: int, Lp: int, H: int, p_drop: float, seed: int) -> torch.Tensor:
+    """(B, H, gmax, Lp) fp32 attention-dropout scale of the global query rows (rf_attn_global_keep;
+    the mask rf_global_attn_fold_fwd_drop applies)."""
+    gmax = gidx.shape[1]
+    z = torch.empty(B, H, gmax, Lp, dtype=torch.float32, device=gidx.device)
+    g32 = gidx.to(torch.int32).contiguous()
+    rc = _lib.load().rf_attn_global_keep(B, H, Lp, _p(g32), gmax, float(p_drop), int(seed) & (2**64 - 1), _p(z),
+                                         _stream(z))
+    check(rc, "rf_attn_global_keep")
+    return z
 
 
 def global_attention_fold_h(h, wqg, bqg, q_scale: float, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int,

@@ -399,8 +399,8 @@ def _put_global_rows(out, og, rows, keep, B: int, G: int):
 class _Attention(torch.autograd.Function):
     """Takes the fused (B*Lp, 3D) q|k|v projection and returns its gradient as one tensor (no
     per-slice zero-fill + accumulate in autograd). attn_p > 0: attention-probability dropout
-    (TF:585-586 local rows on the band kernels, TF:1036-1037 global rows as torch ops) with the
-    counter-hash mask of `seed`, regenerated in the backward."""
+    (TF:585-586 local rows on the band kernels, TF:1036-1037 global rows on the fold kernels)
+    with the counter-hash mask of `seed`, regenerated in the backward."""
 
     @staticmethod
     def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold, grows=None,
@@ -418,7 +418,13 @@ class _Attention(torch.autograd.Function):
         elif ctx.drop is not None:
             # global rows under attention dropout (the hash mask) as torch ops; closed-form backward
             out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w, p_drop=attn_p, seed=seed)
-            if G > 0:
+            if G > 0 and fold and q.dtype != torch.float32:
+                # the fold kernels with the same mask (rf_global_attn_fold_fwd_drop); the mask
+                # itself for the closed-form backward from one kernel (rf_attn_global_keep)
+                ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg,
+                                          wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out, p_drop=attn_p, seed=seed)
+                ctx.gz = ops.attn_global_keep(gidx, B, Lp, H, attn_p, seed)
+            elif G > 0:
                 ctx.gz = _global_keep(gidx, B, Lp, H, attn_p, seed)
                 og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H, ctx.gz)
                 rows, keep = grows[:2] if grows is not None else _global_rows(gidx, B, Lp)

@@ -270,6 +270,46 @@ def test_band_attention_dropout_bwd(dev, case):
         assert err <= 2e-2 * max(float(r.abs().max()), 1e-6), (name, err, float(r.abs().max()))
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", _DROP_CASES)
+def test_global_fold_dropout(dev, dt, case):
+    """Global query rows under attention-probability dropout (TF:1036-1037) on the fold kernels
+    (rf_global_attn_fold_fwd_drop) against the fp32 torch fold with the same mask
+    (train._global_torch); the mask kernel (rf_attn_global_keep) equals train._global_keep
+    bit for bit; p = 0 is the plain fold."""
+    from recformer_amd.train import _global_keep, _global_torch
+    from tests.test_gpu_kernels import _attn_case, _rand
+    B, Lp, H = case["B"], case["Lp"], case["H"]
+    D = H * 64
+    _, merged, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, case["lens"], case["globals_"], 3)
+    h = _rand((B * Lp, D), dev, dt, 1.0, seed=40)
+    wkg = _rand((D, D), dev, dt, 0.05, seed=41)
+    wvg = _rand((D, D), dev, dt, 0.05, seed=42)
+    bkg = _rand((D,), dev, torch.float32, 0.1, seed=43)
+    bvg = _rand((D,), dev, torch.float32, 0.5, seed=44)
+    qg = _rand((B * G, D), dev, dt, 1.0, seed=45)
+    p, seed = 0.1, 20241016
+    z = ops.attn_global_keep(gidx, B, Lp, H, p, seed)
+    assert torch.equal(z, _global_keep(gidx, B, Lp, H, p, seed))
+    kept = float((z > 0).float().mean())
+    assert abs(kept - 0.9) < 0.02, kept
+    ctx = torch.zeros(B * Lp, D, dtype=dt, device=dev)
+    ops.global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, ctx, p_drop=p, seed=seed)
+    ref = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H, z)
+    plain = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H)
+    rows = (torch.arange(B, device=dev)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
+    keep = (gidx >= 0).reshape(-1)
+    got = ctx[rows].float()
+    err = float((got - ref)[keep].abs().max())
+    assert err <= 2e-2, err
+    assert float((ref - plain)[keep].abs().max()) > 10 * err  # the mask matters at this tolerance
+    ctx0 = torch.zeros_like(ctx)
+    ctx1 = torch.zeros_like(ctx)
+    ops.global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, ctx0, p_drop=0.0, seed=seed)
+    ops.global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, ctx1)
+    assert torch.equal(ctx0, ctx1)
+
+
 def _drop_model(dev, p_att, p_hid, seed=1):
     lf = hashed_model(dict(C1, hidden_dropout_prob=p_hid, attention_probs_dropout_prob=p_att), seed=seed)
     model = RecformerForSeqRec(lf.config)

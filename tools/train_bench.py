@@ -1,7 +1,8 @@
 """C3 finetune-step throughput (BASELINE configs[2]): RecformerForSeqRec forward + backward +
 AdamW step under bf16 autocast, 12L/768d, B sequences x L=1024 per step, 10k-item catalog,
-full softmax (finetune.sh) or sampled (--negatives k). Dropout on hidden layers (0.1) and off
-on attention probabilities (not implemented on the training path).
+full softmax (finetune.sh) or sampled (--negatives k). Dropout 0.1 on hidden layers and on
+attention probabilities (the longformer-base config finetune.py loads; --attn-dropout 0 to turn
+the latter off).
 
     python tools/train_bench.py [--batch 16] [--steps 5] [--negatives 0]
 """
@@ -25,6 +26,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--negatives", type=int, default=0)
     ap.add_argument("--catalog", type=int, default=10000)
+    ap.add_argument("--attn-dropout", type=float, default=0.1)
+    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16")
     ap.add_argument("--no-dw-split", action="store_true", help="A/B: weight gradients as one GEMM each")
     ap.add_argument("--no-fused-gelu", action="store_true", help="A/B: FFN1 GEMM then F.gelu")
     a = ap.parse_args()
@@ -35,7 +38,7 @@ def main():
         from recformer_amd import train
         train.DW_SPLIT_K = False
     dev = torch.device("cuda")
-    cfg = RecformerConfig(**dict(BASE, item_num=a.catalog, attention_probs_dropout_prob=0.0,
+    cfg = RecformerConfig(**dict(BASE, item_num=a.catalog, attention_probs_dropout_prob=a.attn_dropout,
                                  finetune_negative_sample_size=a.negatives))
     torch.manual_seed(0)
     model = RecformerForSeqRec(cfg)
@@ -45,11 +48,19 @@ def main():
     batch = {k: v.to(dev) for k, v in synth_batch(a.batch, 1024, cfg.vocab_size, seed=7, item_len=21).items()}
     labels = torch.randint(0, a.catalog, (a.batch,), device=dev)
 
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
+    scaler = torch.amp.GradScaler("cuda") if a.dtype == "fp16" else None
+
     def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=dt):
             loss = model(**batch, labels=labels)
-        loss.backward()
-        opt.step()
+        if scaler is not None:  # finetune.py:106-116 (fp16 autocast + GradScaler)
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+        else:
+            loss.backward()
+            opt.step()
         opt.zero_grad(set_to_none=True)
         return loss
 
@@ -60,10 +71,11 @@ def main():
     for _ in range(a.steps):
         loss = step()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    print(json.dumps({"workload": "C3 finetune step (fwd+bwd+AdamW), 12L/768d, L=1024, bf16 autocast",
+    el = time.perf_counter() - t0
+    print(json.dumps({"workload": f"C3 finetune step (fwd+bwd+AdamW), 12L/768d, L=1024, {a.dtype} autocast, "
+                                  f"attention dropout {a.attn_dropout}",
                       "batch": a.batch, "negatives": a.negatives, "catalog": a.catalog,
-                      "ms_per_step": round(1e3 * dt / a.steps, 2), "seq_per_s": round(a.batch * a.steps / dt, 2),
+                      "ms_per_step": round(1e3 * el / a.steps, 2), "seq_per_s": round(a.batch * a.steps / el, 2),
                       "loss": float(loss.detach()),
                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}))
 
