@@ -47,8 +47,8 @@ inline hipStream_t as_stream(rf_stream_t s) { return reinterpret_cast<hipStream_
 // Launch-path choices measured once and compiled in as defaults; tools/ switch them through
 // rf_debug_set_knob (one host call, no environment lookups on any launch).
 enum Knob {
-  KNOB_GEMM_GN = 0,     // ping-pong GEMM raster: column-group width (4)
-  KNOB_GEMM_VARIANT,    // bf16 GEMM kernel family (5 = ping-pong)
+  KNOB_GEMM_GN = 0,     // ping-pong GEMM raster: column-group width (6)
+  KNOB_GEMM_VARIANT,    // bf16 GEMM kernel family (6 = four-wave, 5 = ping-pong, 7 = four-wave BK32 ring)
   KNOB_BAND_QPB,        // band attention query blocks per workgroup (0 = auto)
   KNOB_BAND_PATH,       // band attention kernel: 0 pipe2, 1 pipe (v1), 2 one-shot
   KNOB_GFOLD_PATH,      // global fold GEMV/MFMA choice: 0 auto, 1 GEMV, 2 MFMA

@@ -997,6 +997,495 @@ static void launch_pp(int M, int N, int K, const void* A, int lda, const void* W
   k_gemm_pp<E, EPI, CF32, RF32><<<grid, 512, lds, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
 }
 
+// ---- 4-wave 256x256 GEMM: one wave per SIMD, 128x128 accumulator block per wave ----------------
+// The alternative main loop to the ping-pong (knob gemm_variant 6): 4 waves (2 x 2), each owning a
+// 128 x 128 block of the tile (256 accumulator registers), so a K-tile costs 32 ds_read_b128 per wave
+// (128 KiB per CU, vs 192 KiB for 8 waves of 64 x 128) against 128 MFMAs. One continuous MFMA stream
+// per SIMD with the LDS reads and the operand DMA interleaved into it (no second wave to alternate
+// with): each K-tile is two phases of 64 MFMAs — phase A on the ks = 0 fragments while the ks = 1
+// fragments of the same K-tile are read, phase B on ks = 1 while the next K-tile's ks = 0 fragments
+// are read and the K-tile after that is DMA'd into the buffer this one just released. One barrier
+// per K-tile (between the phases) publishes the next K-tile and releases the current buffer. Same
+// LDS image (XOR-swizzled 128-B rows), W-row permutation and epilogue as the ping-pong kernel; the
+// next tile's first two K-tiles are fetched across the tile boundary (virtual K-tiles nk, nk+1).
+constexpr int W4_BUF = 4 * PP_HALF;          // one K-tile: A rows 0-127, 128-255, W rows 0-127, 128-255
+constexpr int W4_CV = 2 * W4_BUF;            // column vectors [parity][3][1 KiB]
+constexpr int W4_LDS = W4_CV + 6 * 1024;
+
+template <typename E, int EPI, bool CF32, bool RF32>
+__global__ void __launch_bounds__(256, 1)
+    k_gemm_w4(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e,
+              int nTm, int nTn) {
+  typedef typename H16<E>::x8 V8;
+  constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;
+  constexpr int S = OUT32 ? 64 : 32;  // epilogue stores per wave (interior tile)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles = nTm * nTn;
+  int v = blockIdx.x;
+  if (v >= tiles) return;
+  const int GN = e.gn > 0 ? min(e.gn, nTn) : nTn;
+  auto tile_origin = [&](int vv, int& om0, int& on0) {
+    const int wg = xcd_remap(vv, tiles);
+    const int g = wg / (nTm * GN);
+    const int gw = min(GN, nTn - g * GN);
+    const int rem = wg - g * nTm * GN;
+    const int tm = rem / gw;
+    om0 = tm * 256;
+    on0 = (g * GN + rem - tm * gw) * 256;
+  };
+  int m0, n0, nm0 = 0, nn0 = 0;
+  tile_origin(v, m0, n0);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;  // A half (rows 128 wr..) and W half (columns 128 wc..)
+  const int nk = K >> 6;
+  // Operand DMA through buffer resources (buffer_load ... lds): rows past M / N read as zeros
+  // (num_records), the per-piece row step and the K-tile offset are scalars (soffset), so a piece
+  // costs no VALU. Wave w stages rows [64(w&1), +64) of A-half w>>1 and of W-half w>>1 as 8 pieces
+  // of 8 rows; lane: row 8p + lane/8 of the piece, 16-B chunk (lane&7)^(row&7). W rows permuted
+  // by wperm (whole-line epilogue stores): W row of piece p = 8(l>>3) + 4(w&1) + 64(p&1) + (p>>1)
+  // (16-bit out) or 64(w&1) + 4(l>>3) + 32(p&1) + (p>>1) (fp32 out), relative to the half.
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)min((int64_t)e.M * lda * 2, (int64_t)0x7FFFFFFF), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)min((int64_t)e.N * ldw * 2, (int64_t)0x7FFFFFFF), 0x00020000);
+  const int half = wave >> 1;
+  const int pch = ((lane & 7) ^ (lane >> 3)) * 8;                      // element offset of the chunk
+  const int arow_l = half * 128 + (wave & 1) * 64 + (lane >> 3);      // + 8p
+  const int wrow_l = half * 128 + (OUT32 ? 64 * (wave & 1) + 4 * (lane >> 3) : 8 * (lane >> 3) + 4 * (wave & 1));
+  auto voffA = [&](int bm0) { return ((bm0 + arow_l) * lda + pch) * 2; };
+  auto voffW = [&](int bn0) { return ((bn0 + wrow_l) * ldw + pch) * 2; };
+  int vA = voffA(m0), vW = voffW(n0), vAn = vA, vWn = vW;
+  auto launder = [&]() { asm volatile("" : "+v"(vA), "+v"(vW), "+v"(vAn), "+v"(vWn)); };
+  bool pf = false;  // the next tile exists: virtual K-tiles nk, nk+1 are its K-tiles 0, 1
+  // piece p (0-7 A, 8-15 W) of virtual K-tile kv (>= nk: the next tile's K-tile kv - nk) into buffer buf
+  auto dma_piece = [&](int kv, int buf, int p) {
+    const bool nxt = kv >= nk;
+    const int kt = nxt ? kv - nk : kv;
+    const bool isA = p < 8;
+    const int pp = p & 7;
+    char* dst = smem + buf * W4_BUF + (isA ? half : 2 + half) * PP_HALF + ((wave & 1) * 64 + 8 * pp) * 128;
+    const int rstep = isA ? 8 * pp : (OUT32 ? 32 * (pp & 1) + (pp >> 1) : 64 * (pp & 1) + (pp >> 1));
+    const int soff = kt * 128 + rstep * (isA ? lda : ldw) * 2;
+    const int vo = isA ? (nxt ? vAn : vA) : (nxt ? vWn : vW);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsW, (__attribute__((address_space(3))) void*)dst, 16, vo,
+                                             soff, 0, 0);
+  };
+  auto dma_cols = [&](int tm0, int tn0, int par) {
+    if (EPI == RF_EPI_NONE) return;
+    const int vec = wave % 3;
+    const float* src = EPI == RF_EPI_COS ? e.rw : e.bias;
+    int idx = min(tn0 + 4 * lane, e.N - 4);
+    if (EPI == RF_EPI_BIAS_RESID_LN && vec == 1) src = e.lgamma;
+    if (EPI == RF_EPI_BIAS_RESID_LN && vec == 2) src = e.lbeta;
+    if (EPI == RF_EPI_COS && vec == 1) {
+      src = e.ra;
+      idx = min(tm0 + 4 * lane, e.M - 4);
+    }
+    glds16(src + idx, smem + W4_CV + (par * 3 + vec) * 1024);
+  };
+  const int lr = lane & 15;
+  const int off0 = lr * 128 + (((lane >> 4) ^ (lane & 7)) << 4);
+  const int off1 = lr * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
+  const int aOff = wr * PP_HALF, bOff = (2 + wc) * PP_HALF;
+  V8 a0[8], b0[8], a1[8], b1[8];
+  f32x4 acc[8][8];
+  auto read0 = [&](int buf, int idx) {  // ks = 0 fragment idx (0-7 A, 8-15 W)
+    const char* base = smem + buf * W4_BUF + (idx < 8 ? aOff : bOff) + (idx & 7) * 16 * 128 + off0;
+    if (idx < 8) a0[idx] = *reinterpret_cast<const V8*>(base);
+    else b0[idx - 8] = *reinterpret_cast<const V8*>(base);
+  };
+  auto read1 = [&](int buf, int idx) {
+    const char* base = smem + buf * W4_BUF + (idx < 8 ? aOff : bOff) + (idx & 7) * 16 * 128 + off1;
+    if (idx < 8) a1[idx] = *reinterpret_cast<const V8*>(base);
+    else b1[idx - 8] = *reinterpret_cast<const V8*>(base);
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: K-tiles 0, 1 of the first tile, its column vectors
+  dma_cols(m0, n0, 0);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) dma_piece(0, 0, p);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) dma_piece(1, 1, p);
+  wait_vmcnt<16>();
+  bar();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) read0(0, i);
+  int kb = 0;      // LDS buffer of the current K-tile (running parity across tiles)
+  int tix = 0;     // tile counter (column-vector parity)
+  int relax = 0;   // epilogue stores of the previous (interior) tile still counted in vmcnt
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool has_next = v + (int)gridDim.x < tiles;
+    pf = has_next;
+    if (has_next) {
+      tile_origin(v + gridDim.x, nm0, nn0);
+    } else {
+      nm0 = m0;
+      nn0 = n0;
+    }
+    vAn = voffA(nm0);
+    vWn = voffW(nn0);
+    for (int t = 0; t < nk; ++t) {
+      launder();
+      // ---- phase A: ks = 0 MFMAs of K-tile t; ks = 1 fragments of K-tile t from LDS ----
+#pragma unroll
+      for (int i = 0; i < 16; ++i) read1(kb, i);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+      }
+      // ---- mid-sync: this wave's reads of buffer kb done; K-tile t+1 (buffer kb^1) landed ----
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t == 0 && relax) wait_vmcnt<(S < 63 ? S : 63)>();  // the previous tile's stores may stay in flight
+      else wait_vmcnt<0>();
+      bar();
+      // ---- phase B: ks = 1 MFMAs; K-tile t+1's ks = 0 fragments; DMA of K-tile t+2 into kb ----
+      // unconditional (branch-free phase): past the last tile the reads and the DMA (of the last
+      // tile's own rows, into the buffer nothing reads any more) are harmless
+      // (DMAs first: the LDS reads may not move above an LDS-DMA write the compiler cannot tell
+      // apart from them, so this order lets both interleave with the MFMAs)
+#pragma unroll
+      for (int p = 0; p < 16; ++p) dma_piece(t + 2, kb, p);
+      // the next tile's column vectors into the other parity slot (last read by the previous
+      // tile's epilogue, before this tile's first barrier); repeated per K-tile to stay branch-free
+      dma_cols(nm0, nn0, (tix + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) read0(kb ^ 1, i);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+#pragma unroll
+      for (int g = 0; g < 17; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 DMA piece
+      }
+#pragma unroll
+      for (int g = 0; g < 15; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      kb ^= 1;
+    }
+    // epilogue straight from the accumulators (as k_gemm_pp): lane (c = l&15, g = l>>4) holds rows
+    // 4g + r of each 16-row block i and the columns [8c, 8c+8) (16-bit) / [4c, 4c+4) u [64+4c, ..)
+    const bool interior = (m0 + 256 <= e.M) && (n0 + 256 <= e.N);
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const int erow = m0 + wr * 128 + 4 * (el >> 4);
+    const int ecol = n0 + wc * 128 + (OUT32 ? 4 : 8) * (el & 15);
+    float bv[8], gm[8], bt[8];
+    const float* cb = reinterpret_cast<const float*>(smem + W4_CV + (tix & 1) * 3 * 1024);
+    {
+      const int co = ecol - n0;
+      if (OUT32) {
+        lds_cols<EPI, 4>(cb, co, bv, gm, bt);
+        lds_cols<EPI, 4>(cb, co + 64, bv + 4, gm + 4, bt + 4);
+      } else {
+        lds_cols<EPI, 8>(cb, co, bv, gm, bt);
+      }
+    }
+    const int em0 = m0;
+    auto epilogue = [&](auto check) {
+      constexpr bool CK = decltype(check)::value;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float vv[8];
+#pragma unroll
+          for (int f = 0; f < 8; ++f) vv[f] = acc[i][f][r];
+          const int row = erow + i * 16 + r;
+          const float rsc = EPI == RF_EPI_COS ? cb[256 + row - em0] : 0.f;
+          if (OUT32) {
+            epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+            epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
+          } else {
+            epi_seg<E, EPI, CF32, RF32, 8, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+          }
+        }
+    };
+    if (interior) epilogue(std::false_type{});
+    else epilogue(std::true_type{});
+    asm volatile("" ::: "memory");
+    ++tix;
+    if (!has_next) break;
+    v += gridDim.x;
+    m0 = nm0;
+    n0 = nn0;
+    vA = vAn;
+    vW = vWn;
+    relax = interior ? S : 0;
+  }
+  wait_vmcnt<0>();
+}
+
+template <typename E, int EPI, bool CF32, bool RF32>
+static void launch_w4(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
+                      hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_w4<E, EPI, CF32, RF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)W4_LDS);
+    attr_set = true;
+  }
+  const int nTm = (M + 255) / 256, nTn = (N + 255) / 256;
+  const int grid = min(nTm * nTn, num_cus());
+  k_gemm_w4<E, EPI, CF32, RF32><<<grid, 256, W4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
+}
+
+// ---- 4-wave 256x256 GEMM on a 4-deep BK = 32 ring (knob gemm_variant 7) ----------------------------
+// As k_gemm_w4 (one wave per SIMD, 128 x 128 accumulators per wave), but the K loop walks 32-wide
+// K-tiles through a 4-slot LDS ring: iteration g runs the 64 MFMAs of K-tile g from one register set
+// while the 16 ds_read_b128 of K-tile g+1 fill the other and the 8 DMA pieces of K-tile g+4 go into
+// the slot K-tile g just left (read into registers during iteration g-1, released by its barrier).
+// So every DMA has three iterations (~3 x 64 MFMAs) to land, the DMA and LDS reads spread evenly
+// over the MFMA stream (8 + 16 per 64), and one barrier per iteration publishes K-tile g+2 and
+// releases slot g+1. LDS image: 64-B rows, chunk slot c ^ ((-(r>>2)) & 3) (TileGeo<32>); W rows
+// permuted by wperm like the ping-pong kernel, so the epilogue is the same.
+constexpr int R4_STAGE = 2 * 256 * 64;       // A 256 x 32 + W 256 x 32 (16-bit)
+constexpr int R4_CV = 4 * R4_STAGE;          // column vectors [parity][3][1 KiB], then a dummy slot
+constexpr int R4_LDS = R4_CV + 7 * 1024;
+
+template <typename E, int EPI, bool CF32, bool RF32>
+__global__ void __launch_bounds__(256, 1)
+    k_gemm_w4r(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e,
+               int nTm, int nTn) {
+  typedef typename H16<E>::x8 V8;
+  constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;
+  constexpr int S = OUT32 ? 64 : 32;   // epilogue stores per wave (interior tile)
+  constexpr int PER = 9;               // VMEM ops per iteration: 8 operand pieces + 1 column vector
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles = nTm * nTn;
+  int v = blockIdx.x;
+  if (v >= tiles) return;
+  const int GN = e.gn > 0 ? min(e.gn, nTn) : nTn;
+  auto tile_origin = [&](int vv, int& om0, int& on0) {
+    const int wg = xcd_remap(vv, tiles);
+    const int g = wg / (nTm * GN);
+    const int gw = min(GN, nTn - g * GN);
+    const int rem = wg - g * nTm * GN;
+    const int tm = rem / gw;
+    om0 = tm * 256;
+    on0 = (g * GN + rem - tm * gw) * 256;
+  };
+  int m0, n0, nm0, nn0;
+  tile_origin(v, m0, n0);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nk = K >> 5;  // 32-wide K-tiles (even: K % 64 == 0)
+  // DMA: wave w stages rows [64w, 64w + 64) of the A image and of the W image as 4 pieces of 16 rows
+  // each; lane: row 16p + l/4 of the piece, chunk slot l&3 holding source chunk (l&3) ^ ((-(l>>4))&3).
+  // W image row rho (0..255) holds W row 128(rho>>7) + wperm(rho & 127): 16-bit out
+  // 8(l>>2) + 4(w&1) + p, fp32 out 64(w&1) + 4(l>>2) + p, relative to the half.
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)A, (short)0, (int)min((int64_t)e.M * lda * 2, (int64_t)0x7FFFFFFF), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)W, (short)0, (int)min((int64_t)e.N * ldw * 2, (int64_t)0x7FFFFFFF), 0x00020000);
+  const int sch = ((lane & 3) ^ ((-(lane >> 4)) & 3)) * 8;  // source chunk (elements)
+  const int arow_l = 64 * wave + (lane >> 2);
+  const int wrow_l = 128 * (wave >> 1) + (OUT32 ? 64 * (wave & 1) + 4 * (lane >> 2) : 8 * (lane >> 2) + 4 * (wave & 1));
+  auto voffA = [&](int bm0) { return ((bm0 + arow_l) * lda + sch) * 2; };
+  auto voffW = [&](int bn0) { return ((bn0 + wrow_l) * ldw + sch) * 2; };
+  int vA = voffA(m0), vW = voffW(n0), vAn = vA, vWn = vW;
+  // the 8 pieces of virtual K-tile kv (>= nk: the next output tile's K-tile kv - nk) into ring slot
+  // `slot`, then one column-vector piece (cols of the next tile into parity slot cpar, or the dummy)
+  auto dma_tile = [&](int kv, int slot) {
+    const bool nxt = kv >= nk;
+    const int kt = nxt ? kv - nk : kv;
+    const int va = nxt ? vAn : vA, vw = nxt ? vWn : vW;
+    char* base = smem + slot * R4_STAGE + wave * 64 * 64;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(base + p * 1024), 16,
+                                               va, kt * 64 + 16 * p * lda * 2, 0, 0);
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (__attribute__((address_space(3))) void*)(base + 256 * 64 + p * 1024),
+                                               16, vw, kt * 64 + p * ldw * 2, 0, 0);
+  };
+  auto dma_cols = [&](int tm0, int tn0, int dst_off) {
+    const int vec = wave % 3;
+    const float* src = EPI == RF_EPI_COS ? e.rw : (e.bias != nullptr ? e.bias : reinterpret_cast<const float*>(A));
+    int idx = min(tn0 + 4 * lane, e.N - 4);
+    if (EPI == RF_EPI_BIAS_RESID_LN && vec == 1) src = e.lgamma;
+    if (EPI == RF_EPI_BIAS_RESID_LN && vec == 2) src = e.lbeta;
+    if (EPI == RF_EPI_COS && vec == 1) {
+      src = e.ra;
+      idx = min(tm0 + 4 * lane, e.M - 4);
+    }
+    if (EPI == RF_EPI_NONE) idx = 0;  // a harmless piece (keeps the per-iteration VMEM count fixed)
+    glds16(src + idx, smem + dst_off + (dst_off == R4_CV + 6 * 1024 ? 0 : vec * 1024));
+  };
+  const int lr = lane & 15, ch = lane >> 4;
+  const int aRd = (wr * 128 + lr) * 64 + ((ch ^ ((-(lr >> 2)) & 3)) << 4);
+  const int bRd = 256 * 64 + (wc * 128 + lr) * 64 + ((ch ^ ((-(lr >> 2)) & 3)) << 4);
+  V8 a0[8], b0[8], a1[8], b1[8];
+  f32x4 acc[8][8];
+  // (16-row blocks keep the row's low bits, so one swizzle offset serves all 8 fragments)
+  auto rd = [&](V8 (&a)[8], V8 (&b)[8], int slot, int idx) {
+    const char* base = smem + slot * R4_STAGE + (idx & 7) * 16 * 64;
+    if (idx < 8) a[idx] = *reinterpret_cast<const V8*>(base + aRd);
+    else b[idx - 8] = *reinterpret_cast<const V8*>(base + bRd);
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto launder = [&]() { asm volatile("" : "+v"(vA), "+v"(vW), "+v"(vAn), "+v"(vWn)); };
+
+  // one iteration: MFMAs of K-tile t from (xa, xb), reads of K-tile t+1 into (ya, yb), DMA of t+4
+  auto iter = [&](V8 (&xa)[8], V8 (&xb)[8], V8 (&ya)[8], V8 (&yb)[8], int t, int g, int cdst) {
+    dma_tile(t + 4, g & 3);
+    dma_cols(nm0, nn0, cdst);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rd(ya, yb, (g + 1) & 3, i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(xa[i], xb[j], acc[i][j]);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 DMA piece
+    }
+#pragma unroll
+    for (int q = 0; q < 15; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // 3 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 LDS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+  };
+
+  // prologue: K-tiles 0..3 of the first tile (+ its column vectors, 9 VMEM ops per K-tile)
+  nm0 = m0;
+  nn0 = n0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    dma_tile(k, k);
+    dma_cols(m0, n0, R4_CV);
+  }
+  wait_vmcnt<2 * PER>();  // K-tiles 0, 1 landed
+  bar();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) rd(a0, b0, 0, i);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bar();  // every wave has read slot 0 before iteration 0 refills it
+  int g = 0;       // running K-tile counter (ring slot, register-set parity) across tiles
+  int tix = 0;     // output-tile counter (column-vector parity)
+  int relax = 0;   // epilogue stores of the previous (interior) tile counted in vmcnt
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool has_next = v + (int)gridDim.x < tiles;
+    if (has_next) tile_origin(v + gridDim.x, nm0, nn0);
+    else {
+      nm0 = m0;
+      nn0 = n0;
+    }
+    vAn = voffA(nm0);
+    vWn = voffW(nn0);
+    const int cslot = R4_CV + ((tix + 1) & 1) * 3 * 1024;
+    for (int t = 0; t < nk; t += 2) {
+      launder();
+      // iteration 0 of a tile writes the dummy slot: a slower wave may still read the other
+      // parity slot in the previous tile's epilogue
+      iter(a0, b0, a1, b1, t, g, t == 0 ? R4_CV + 6 * 1024 : cslot);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t == 0 && relax) wait_vmcnt<(2 * PER + S < 63 ? 2 * PER + S : 63)>();
+      else wait_vmcnt<2 * PER>();
+      bar();
+      iter(a1, b1, a0, b0, t + 1, g + 1, cslot);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t == 0 && relax) wait_vmcnt<(2 * PER + S < 63 ? 2 * PER + S : 63)>();
+      else wait_vmcnt<2 * PER>();
+      bar();
+      g += 2;
+    }
+    // epilogue straight from the accumulators (as k_gemm_pp / k_gemm_w4)
+    const bool interior = (m0 + 256 <= e.M) && (n0 + 256 <= e.N);
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const int erow = m0 + wr * 128 + 4 * (el >> 4);
+    const int ecol = n0 + wc * 128 + (OUT32 ? 4 : 8) * (el & 15);
+    float bv[8], gm[8], bt[8];
+    const float* cb = reinterpret_cast<const float*>(smem + R4_CV + (tix & 1) * 3 * 1024);
+    {
+      const int co = ecol - n0;
+      if (OUT32) {
+        lds_cols<EPI, 4>(cb, co, bv, gm, bt);
+        lds_cols<EPI, 4>(cb, co + 64, bv + 4, gm + 4, bt + 4);
+      } else {
+        lds_cols<EPI, 8>(cb, co, bv, gm, bt);
+      }
+    }
+    const int em0 = m0;
+    auto epilogue = [&](auto check) {
+      constexpr bool CK = decltype(check)::value;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float vv[8];
+#pragma unroll
+          for (int f = 0; f < 8; ++f) vv[f] = acc[i][f][r];
+          const int row = erow + i * 16 + r;
+          const float rsc = EPI == RF_EPI_COS ? cb[256 + row - em0] : 0.f;
+          if (OUT32) {
+            epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+            epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
+          } else {
+            epi_seg<E, EPI, CF32, RF32, 8, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+          }
+        }
+    };
+    if (interior) epilogue(std::false_type{});
+    else epilogue(std::true_type{});
+    asm volatile("" ::: "memory");
+    ++tix;
+    if (!has_next) break;
+    v += gridDim.x;
+    m0 = nm0;
+    n0 = nn0;
+    vA = vAn;
+    vW = vWn;
+    relax = interior ? S : 0;
+  }
+  wait_vmcnt<0>();
+}
+
+template <typename E, int EPI, bool CF32, bool RF32>
+static void launch_w4r(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
+                       hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_w4r<E, EPI, CF32, RF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)R4_LDS);
+    attr_set = true;
+  }
+  const int nTm = (M + 255) / 256, nTn = (N + 255) / 256;
+  const int grid = min(nTm * nTn, num_cus());
+  k_gemm_w4r<E, EPI, CF32, RF32><<<grid, 256, R4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
+}
+
 template <typename E, int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
 static void launch_bf16(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                         const EpiArgs& e, hipStream_t s) {
@@ -1013,11 +1502,15 @@ static void launch_bf16(int M, int N, int K, const void* A, int lda, const void*
       K, (const E*)A, lda, (const E*)W, ldw, e, nTn);
 }
 
-// Variant selector for A/B timing (knob gemm_variant): 5 -> 256^2 ping-pong (default), 1 -> 256^2
-// BK64 x2, 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 -> 256x128 / 128^2 tiles.
+// Variant selector for A/B timing (knob gemm_variant): 6 -> 256^2 four-wave (default; tools/gemm_gn.py
+// with the bench epilogues, same box: qkv 211 -> 201 us, out-proj 73 -> 71, FFN1 316 -> 300, FFN2
+// 262 -> 260 vs the ping-pong), 5 -> 256^2 ping-pong, 7 -> four-wave on a BK32 ring (slower: 217 /
+// 77 / 315 / 275 us), 1 -> 256^2 BK64 x2, 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 ->
+// 256x128 / 128^2 tiles.
 static unsigned long long* g_stamps = nullptr;  // set by rf_debug_gemm_stamps (tools only)
 
-static int gemm_gn() { return g_knob[KNOB_GEMM_GN]; }  // 4 beats the full-width raster by ~4% (FFN1)
+// column groups of 6 tiles: qkv -2.7%, FFN1/FFN2 -1% vs 4 (tools/gemm_gn.py); full width loses on FFN1
+static int gemm_gn() { return g_knob[KNOB_GEMM_GN]; }
 
 static int gemm_variant() { return g_knob[KNOB_GEMM_VARIANT]; }
 
@@ -1041,6 +1534,20 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
       case 2: launch_bf16<E, 256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 3: launch_bf16<E, 128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 4: launch_bf16<E, 256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 7:
+        if (pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
+            (int64_t)N * ldw * 2 < 0x7FFFFFFF) {
+          launch_w4r<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+          break;
+        }
+        [[fallthrough]];
+      case 6:
+        if (pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
+            (int64_t)N * ldw * 2 < 0x7FFFFFFF) {
+          launch_w4<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+          break;
+        }
+        [[fallthrough]];
       case 5:
         if (pp_cols_ok(M, N, e)) {
           launch_pp<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
