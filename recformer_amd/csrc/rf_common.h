@@ -48,7 +48,7 @@ inline hipStream_t as_stream(rf_stream_t s) { return reinterpret_cast<hipStream_
 // rf_debug_set_knob (one host call, no environment lookups on any launch).
 enum Knob {
   KNOB_GEMM_GN = 0,     // ping-pong GEMM raster: column-group width (6)
-  KNOB_GEMM_VARIANT,    // bf16 GEMM kernel family (6 = four-wave, 5 = ping-pong, 7 = four-wave BK32 ring)
+  KNOB_GEMM_VARIANT,    // bf16 GEMM kernel family (8 = four-wave interleaved, 6 = four-wave, 5 = ping-pong, 7 = BK32 ring)
   KNOB_BAND_QPB,        // band attention query blocks per workgroup (0 = auto)
   KNOB_BAND_PATH,       // band attention kernel: 0 pipe2, 1 pipe (v1), 2 one-shot
   KNOB_GFOLD_PATH,      // global fold GEMV/MFMA choice: 0 auto, 1 GEMV, 2 MFMA
@@ -128,6 +128,32 @@ __device__ __forceinline__ f32x2 gelu2_bf16out(f32x2 x) {
   const f32x2 t = x * p;
   const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.0f;
   return x * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
+// gelu_bf16out on 4 pairs, one stage at a time across the pairs (the same operations per value, so
+// bit-identical): the four chains interleave, so the transcendental and packed-op hazards fill with
+// the other chains' instructions instead of s_nop (the per-pair form compiled to a serial chain).
+__device__ __forceinline__ void gelu8_bf16out(f32x2 (&x)[4]) {
+  f32x2 x2[4], t[4], d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x2[k] = __builtin_elementwise_min(x[k] * x[k], (f32x2){64.0f, 64.0f});
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    t[k] = __builtin_elementwise_fma((f32x2){0.0010142630552196598f, 0.0010142630552196598f}, x2[k],
+                                     (f32x2){-0.1067757240026454f, -0.1067757240026454f});
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    t[k] = __builtin_elementwise_fma(t[k], x2[k], (f32x2){-2.3011213394567367f, -2.3011213394567367f});
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = x[k] * t[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = (f32x2){__builtin_amdgcn_exp2f(t[k].x), __builtin_amdgcn_exp2f(t[k].y)};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = d[k] + 1.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = (f32x2){__builtin_amdgcn_rcpf(d[k].x), __builtin_amdgcn_rcpf(d[k].y)};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = x[k] * d[k];
 }
 
 // ---- split fp32 residual stream ------------------------------------------------

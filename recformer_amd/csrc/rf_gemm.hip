@@ -555,6 +555,16 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
     if (CF32) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[k] = gelu_erf(v[k]);
+    } else if (NV == 8) {
+      f32x2 y[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) y[k] = (f32x2){v[2 * k], v[2 * k + 1]};
+      gelu8_bf16out(y);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[2 * k] = y[k].x;
+        v[2 * k + 1] = y[k].y;
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < NV; k += 2) {
@@ -1012,7 +1022,7 @@ constexpr int W4_BUF = 4 * PP_HALF;          // one K-tile: A rows 0-127, 128-25
 constexpr int W4_CV = 2 * W4_BUF;            // column vectors [parity][3][1 KiB]
 constexpr int W4_LDS = W4_CV + 6 * 1024;
 
-template <typename E, int EPI, bool CF32, bool RF32>
+template <typename E, int EPI, bool CF32, bool RF32, bool IL>
 __global__ void __launch_bounds__(256, 1)
     k_gemm_w4(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e,
               int nTm, int nTn) {
@@ -1119,10 +1129,6 @@ __global__ void __launch_bounds__(256, 1)
   int tix = 0;     // tile counter (column-vector parity)
   int relax = 0;   // epilogue stores of the previous (interior) tile still counted in vmcnt
   for (;;) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const bool has_next = v + (int)gridDim.x < tiles;
     pf = has_next;
     if (has_next) {
@@ -1133,53 +1139,102 @@ __global__ void __launch_bounds__(256, 1)
     }
     vAn = voffA(nm0);
     vWn = voffW(nn0);
-    for (int t = 0; t < nk; ++t) {
-      launder();
-      // ---- phase A: ks = 0 MFMAs of K-tile t; ks = 1 fragments of K-tile t from LDS ----
+    // ---- phase A: ks = 0 MFMAs of K-tile t; ks = 1 fragments of K-tile t from LDS ----
+    auto phaseA = [&](auto zero) {
+      // W fragments first: phase B's MFMA order (i outer, j inner) needs all of b1 and a1[0] first
 #pragma unroll
-      for (int i = 0; i < 16; ++i) read1(kb, i);
+      for (int i = 0; i < 16; ++i) read1(kb, (i + 8) & 15);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = mfma16(a0[i], b0[j], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j]);
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
       }
-      // ---- mid-sync: this wave's reads of buffer kb done; K-tile t+1 (buffer kb^1) landed ----
+    };
+    // ---- mid-sync: this wave's reads of buffer kb done; K-tile t+1 (buffer kb^1) landed ----
+    auto midsync = [&](int t) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (t == 0 && relax) wait_vmcnt<(S < 63 ? S : 63)>();  // the previous tile's stores may stay in flight
       else wait_vmcnt<0>();
       bar();
-      // ---- phase B: ks = 1 MFMAs; K-tile t+1's ks = 0 fragments; DMA of K-tile t+2 into kb ----
-      // unconditional (branch-free phase): past the last tile the reads and the DMA (of the last
-      // tile's own rows, into the buffer nothing reads any more) are harmless
-      // (DMAs first: the LDS reads may not move above an LDS-DMA write the compiler cannot tell
-      // apart from them, so this order lets both interleave with the MFMAs)
+    };
+    // ---- phase B: ks = 1 MFMAs; K-tile t+1's ks = 0 fragments; DMA of K-tile t+2 into kb ----
+    // unconditional (branch-free phase): past the last tile the reads and the DMA (of the last
+    // tile's own rows, into the buffer nothing reads any more) are harmless. The LDS reads may not
+    // move above an LDS-DMA write the compiler cannot tell apart from them, so program order
+    // alternates them (IL) or puts the DMAs first, and the groups follow that order.
+    auto phaseB = [&](int t) {
+      if (IL) {
 #pragma unroll
-      for (int p = 0; p < 16; ++p) dma_piece(t + 2, kb, p);
+        for (int p = 0; p < 16; ++p) {
+          dma_piece(t + 2, kb, p);
+          read0(kb ^ 1, (p + 8) & 15);  // b0 first (phase A's MFMA order)
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < 16; ++p) dma_piece(t + 2, kb, p);
+      }
       // the next tile's column vectors into the other parity slot (last read by the previous
       // tile's epilogue, before this tile's first barrier); repeated per K-tile to stay branch-free
       dma_cols(nm0, nn0, (tix + 1) & 1);
+      if (!IL) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) read0(kb ^ 1, i);
+        for (int i = 0; i < 16; ++i) read0(kb ^ 1, i);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+      if (IL) {
 #pragma unroll
-      for (int g = 0; g < 17; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 DMA piece
-      }
+        for (int g = 0; g < 16; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 DMA piece
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+      } else {
 #pragma unroll
-      for (int g = 0; g < 15; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        for (int g = 0; g < 17; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 DMA piece
+        }
+#pragma unroll
+        for (int g = 0; g < 15; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       kb ^= 1;
+    };
+    if (IL) {  // the first phase A initialises the accumulators (MFMA with a zero C operand)
+      launder();
+      phaseA(std::true_type{});
+      for (int t = 0; t + 1 < nk; ++t) {
+        midsync(t);
+        phaseB(t);
+        launder();
+        phaseA(std::false_type{});
+      }
+      midsync(nk - 1);
+      phaseB(nk - 1);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < nk; ++t) {
+        launder();
+        phaseA(std::false_type{});
+        midsync(t);
+        phaseB(t);
+      }
     }
     // epilogue straight from the accumulators (as k_gemm_pp): lane (c = l&15, g = l>>4) holds rows
     // 4g + r of each 16-row block i and the columns [8c, 8c+8) (16-bit) / [4c, 4c+4) u [64+4c, ..)
@@ -1234,18 +1289,18 @@ __global__ void __launch_bounds__(256, 1)
   wait_vmcnt<0>();
 }
 
-template <typename E, int EPI, bool CF32, bool RF32>
+template <typename E, int EPI, bool CF32, bool RF32, bool IL>
 static void launch_w4(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
                       hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_w4<E, EPI, CF32, RF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)W4_LDS);
+    (void)hipFuncSetAttribute((const void*)k_gemm_w4<E, EPI, CF32, RF32, IL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)W4_LDS);
     attr_set = true;
   }
   const int nTm = (M + 255) / 256, nTn = (N + 255) / 256;
   const int grid = min(nTm * nTn, num_cus());
-  k_gemm_w4<E, EPI, CF32, RF32><<<grid, 256, W4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
+  k_gemm_w4<E, EPI, CF32, RF32, IL><<<grid, 256, W4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
 }
 
 // ---- 4-wave 256x256 GEMM on a 4-deep BK = 32 ring (knob gemm_variant 7) ----------------------------
@@ -1502,11 +1557,13 @@ static void launch_bf16(int M, int N, int K, const void* A, int lda, const void*
       K, (const E*)A, lda, (const E*)W, ldw, e, nTn);
 }
 
-// Variant selector for A/B timing (knob gemm_variant): 6 -> 256^2 four-wave (default; tools/gemm_gn.py
-// with the bench epilogues, same box: qkv 211 -> 201 us, out-proj 73 -> 71, FFN1 316 -> 300, FFN2
-// 262 -> 260 vs the ping-pong), 5 -> 256^2 ping-pong, 7 -> four-wave on a BK32 ring (slower: 217 /
-// 77 / 315 / 275 us), 1 -> 256^2 BK64 x2, 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 ->
-// 256x128 / 128^2 tiles.
+// Variant selector for A/B timing (knob gemm_variant), tools/gemm_gn.py with the bench epilogues:
+//   8 (default) four-wave, phase B DMA and LDS reads alternating, zero-C first MFMAs, W fragments
+//     read first; with the stage-wise GELU: qkv 198, out-proj 68.5, FFN1 285, FFN2 247 us
+//   6 four-wave, phase B DMAs then reads, accumulators zeroed per tile: 204 / 74 / 303 / 264 us
+//   5 ping-pong (8 waves): 220 / 77 / 321 / 264 us
+//   7 four-wave on a BK32 4-slot ring, one barrier per 64 MFMAs (slower than 6: 217 / 77 / 315 / 275)
+//   1 -> 256^2 BK64 x2, 0 -> 256^2 BK32 x4 register-pipelined ring, 2/3/4 -> 256x128 / 128^2 tiles.
 static unsigned long long* g_stamps = nullptr;  // set by rf_debug_gemm_stamps (tools only)
 
 // column groups of 6 tiles: qkv -2.7%, FFN1/FFN2 -1% vs 4 (tools/gemm_gn.py); full width loses on FFN1
@@ -1534,6 +1591,13 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
       case 2: launch_bf16<E, 256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 3: launch_bf16<E, 128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
       case 4: launch_bf16<E, 256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 8:
+        if (pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
+            (int64_t)N * ldw * 2 < 0x7FFFFFFF) {
+          launch_w4<E, EPI, CF32, RF32, true>(M, N, K, A, lda, W, ldw, e, s);
+          break;
+        }
+        [[fallthrough]];
       case 7:
         if (pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
             (int64_t)N * ldw * 2 < 0x7FFFFFFF) {
@@ -1544,7 +1608,7 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
       case 6:
         if (pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
             (int64_t)N * ldw * 2 < 0x7FFFFFFF) {
-          launch_w4<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+          launch_w4<E, EPI, CF32, RF32, false>(M, N, K, A, lda, W, ldw, e, s);
           break;
         }
         [[fallthrough]];

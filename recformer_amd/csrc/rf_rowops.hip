@@ -12,7 +12,7 @@
 namespace rf {
 
 static thread_local char g_err[512];
-int g_knob[KNOB_COUNT] = {6, 6, 0, 0, 0, 8};
+int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8};
 
 void set_error(const char* fmt, ...) {
   va_list ap;
