@@ -29,9 +29,17 @@ def tagger():
 
     def tag(name, grid):
         m = re.search(r"k_gemm_bf16<(\d+), (\d+), \d+, \d+, \d+, \d+, (\d+),", name)
-        mp = re.search(r"k_gemm_pp<(\d+),", name)
+        # 256^2 persistent kernels (ping-pong / four-wave): mangled (..Li<epi>E..) or demangled with
+        # the epilogue as the first integer argument; rocprofv3 garbles some demangled names of the
+        # 16-bit-templated kernels ("<bool _Accum, int, E, ...>"), which are bias epilogues here
+        mm = re.search(r"k_gemm_(?:pp|w4r?)I(?:DF16b|DF16_|f)Li(\d+)E", name)
+        md = re.search(r"k_gemm_(?:pp|w4r?)<(\d+)?", name)
+        mp = mm or md
         if m or mp:
-            bm, epi = (int(m.group(1)), int(m.group(3))) if m else (256, int(mp.group(1)))
+            if m:
+                bm, epi = int(m.group(1)), int(m.group(3))
+            else:
+                bm, epi = 256, int(mp.group(1)) if mp.group(1) else 1
             if epi == 5:  # residual + LN recompute epilogue (training / older runs)
                 t = "gemm_ffn2" if last[0] == "gemm_ffn1" else "gemm_out"
             elif epi == 1 and bm == 128:
