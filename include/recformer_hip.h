@@ -300,6 +300,12 @@ int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, co
  * argmax[m] (first maximum, torch.argmax) for cl_correct_num (models.py:497). ldx in elements. */
 int rf_cross_entropy_fwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,
                          int64_t ignore_index, float* loss, int32_t* argmax, rf_stream_t stream);
+/* Its gradient w.r.t. the logits for the mean loss (the LM-head decoder's backward, models.py:499-510):
+ * dlogits[m, c] = (softmax(x_m)[c] - [c == labels[m]]) * grad_scale[0] (device scalar: upstream
+ * gradient / counted rows), 0 for rows labelled ignore_index; dlogits in the logits' dtype. */
+int rf_cross_entropy_bwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,
+                         int64_t ignore_index, const float* grad_scale, void* dlogits, int64_t ldd,
+                         rf_stream_t stream);
 
 /* Ranker (utils.py:76-108) counts over a block of fp32 scores (M rows x N columns, ld):
  * gt[m] += #{n: s[m,n] > s_label[m]} (the strict rank), valid[m] += #{n: s[m,n] > -max_val}

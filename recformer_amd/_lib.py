@@ -90,6 +90,8 @@ SIGNATURES = {
     "rf_topk_dense": (c_int, [c_int, c_int, P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int32, c_int, P, P, P]),
     "rf_topk_merge": (c_int, [c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, P, P]),
     "rf_cross_entropy_fwd": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, ctypes.c_int64, P, P, P]),
+    "rf_cross_entropy_bwd": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, ctypes.c_int64, P, P,
+                                     ctypes.c_int64, P]),
 }
 
 _LIB: Optional[ctypes.CDLL] = None

@@ -1067,9 +1067,11 @@ __global__ void __launch_bounds__(256, 1)
   auto voffW = [&](int bn0) { return ((bn0 + wrow_l) * ldw + pch) * 2; };
   int vA = voffA(m0), vW = voffW(n0), vAn = vA, vWn = vW;
   auto launder = [&]() { asm volatile("" : "+v"(vA), "+v"(vW), "+v"(vAn), "+v"(vWn)); };
-  bool pf = false;  // the next tile exists: virtual K-tiles nk, nk+1 are its K-tiles 0, 1
   // piece p (0-7 A, 8-15 W) of virtual K-tile kv (>= nk: the next tile's K-tile kv - nk) into buffer buf
   auto dma_piece = [&](int kv, int buf, int p) {
+#if defined(RF_W4_DIAG) && (RF_W4_DIAG & 2)  // timing diagnostic: no operand DMA in the K-loop
+    if (kv >= 2) return;
+#endif
     const bool nxt = kv >= nk;
     const int kt = nxt ? kv - nk : kv;
     const bool isA = p < 8;
@@ -1101,11 +1103,19 @@ __global__ void __launch_bounds__(256, 1)
   V8 a0[8], b0[8], a1[8], b1[8];
   f32x4 acc[8][8];
   auto read0 = [&](int buf, int idx) {  // ks = 0 fragment idx (0-7 A, 8-15 W)
+#if defined(RF_W4_DIAG) && (RF_W4_DIAG & 4)  // timing diagnostic: no LDS operand reads
+    if (idx < 8) asm volatile("" : "=v"(a0[idx])); else asm volatile("" : "=v"(b0[idx - 8]));
+    return;
+#endif
     const char* base = smem + buf * W4_BUF + (idx < 8 ? aOff : bOff) + (idx & 7) * 16 * 128 + off0;
     if (idx < 8) a0[idx] = *reinterpret_cast<const V8*>(base);
     else b0[idx - 8] = *reinterpret_cast<const V8*>(base);
   };
   auto read1 = [&](int buf, int idx) {
+#if defined(RF_W4_DIAG) && (RF_W4_DIAG & 4)
+    if (idx < 8) asm volatile("" : "=v"(a1[idx])); else asm volatile("" : "=v"(b1[idx - 8]));
+    return;
+#endif
     const char* base = smem + buf * W4_BUF + (idx < 8 ? aOff : bOff) + (idx & 7) * 16 * 128 + off1;
     if (idx < 8) a1[idx] = *reinterpret_cast<const V8*>(base);
     else b1[idx - 8] = *reinterpret_cast<const V8*>(base);
@@ -1129,8 +1139,7 @@ __global__ void __launch_bounds__(256, 1)
   int tix = 0;     // tile counter (column-vector parity)
   int relax = 0;   // epilogue stores of the previous (interior) tile still counted in vmcnt
   for (;;) {
-    const bool has_next = v + (int)gridDim.x < tiles;
-    pf = has_next;
+    const bool has_next = v + (int)gridDim.x < tiles;  // virtual K-tiles nk, nk+1 = its K-tiles 0, 1
     if (has_next) {
       tile_origin(v + gridDim.x, nm0, nn0);
     } else {
@@ -1160,7 +1169,9 @@ __global__ void __launch_bounds__(256, 1)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (t == 0 && relax) wait_vmcnt<(S < 63 ? S : 63)>();  // the previous tile's stores may stay in flight
       else wait_vmcnt<0>();
+#if !(defined(RF_W4_DIAG) && (RF_W4_DIAG & 1))  // timing diagnostic: no barrier (wrong results)
       bar();
+#endif
     };
     // ---- phase B: ks = 1 MFMAs; K-tile t+1's ks = 0 fragments; DMA of K-tile t+2 into kb ----
     // unconditional (branch-free phase): past the last tile the reads and the DMA (of the last

@@ -24,7 +24,10 @@
 namespace rf {
 
 constexpr float GF_NEG_INF = -__builtin_inff();
-constexpr int GF_CH = 256;    // rows per chunk (bf16 kernel walks it in 64-row sub-chunks)
+#ifndef RF_GF_CH
+#define RF_GF_CH 256
+#endif
+constexpr int GF_CH = RF_GF_CH;  // rows per chunk (bf16 kernel walks it in 64-row sub-chunks)
 constexpr int GF_CHF = 64;    // rows per chunk of the fp32 VALU kernel
 constexpr int GF_HP = 16;     // heads padded to one MFMA column tile (H <= 16)
 constexpr int GF_RED_LD = 176;  // partial kernels' LDS reduction area: dropped sums at red + 176

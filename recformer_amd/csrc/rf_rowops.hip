@@ -770,6 +770,47 @@ __global__ void __launch_bounds__(256) k_cross_entropy(int N, const T* __restric
   }
 }
 
+// Gradient of the mean cross entropy w.r.t. the logits (the backward of models.py:499-510's
+// CrossEntropyLoss after the LM-head decoder): dx[c] = (softmax(x)[c] - [c == label]) * gs[0], 0 for
+// ignored rows; gs = upstream gradient / number of counted rows, on the device (no host read).
+// One block per row: max, then sum of exp(x - max), then the write — fp32 math, output in the
+// logits' dtype (the decoder GEMMs' operand), so no fp32 probability matrix is materialised.
+template <typename T>
+__global__ void __launch_bounds__(256) k_cross_entropy_bwd(int N, const T* __restrict__ x, int64_t ldx,
+                                                            const int64_t* __restrict__ labels, int64_t ignore,
+                                                            const float* __restrict__ gs, T* __restrict__ dx,
+                                                            int64_t ldd) {
+  __shared__ float sm[4], ss[4];
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const T* xr = x + (int64_t)row * ldx;
+  T* dr = dx + (int64_t)row * ldd;
+  const int64_t lab = labels[row];
+  if (lab == ignore) {
+    for (int c = t; c < N; c += 256) dr[c] = from_f32<T>(0.f);
+    return;
+  }
+  float m = -__builtin_inff();
+  for (int c = t; c < N; c += 256) m = fmaxf(m, to_f32(xr[c]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) sm[wave] = m;
+  __syncthreads();
+  const float M = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+  const float mu = M == -__builtin_inff() ? 0.f : M;
+  float l = 0.f;
+  for (int c = t; c < N; c += 256) l += __expf(to_f32(xr[c]) - mu);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+  if (lane == 0) ss[wave] = l;
+  __syncthreads();
+  const float g = gs[0];
+  const float sc = g / (ss[0] + ss[1] + ss[2] + ss[3]);
+  for (int c = t; c < N; c += 256) {
+    const float p = __expf(to_f32(xr[c]) - mu) * sc;
+    dr[c] = from_f32<T>(c == lab ? p - g : p);
+  }
+}
+
 // Ranker counts (utils.py:76-108) over a block of fp32 scores: per row b,
 //   gt[b]    += #{n : s[b,n] > s_label[b]}   (rank, strict — predicts < scores)
 //   valid[b] += #{n : s[b,n] > -max_val}     (valid_length)
@@ -1171,6 +1212,26 @@ int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, co
   else
     RF_REQUIRE(false, "rf_cos_score_cand: bad dtype %d", dtype);
   RF_LAUNCH_CHECK("rf_cos_score_cand");
+}
+
+int rf_cross_entropy_bwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,
+                        int64_t ignore_index, const float* grad_scale, void* dlogits, int64_t ldd, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && N > 0 && ldx >= N && ldd >= N, "rf_cross_entropy_bwd: bad shape");
+  if (M == 0) return RF_OK;
+  RF_REQUIRE(logits && labels && grad_scale && dlogits, "rf_cross_entropy_bwd: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_BF16)
+    k_cross_entropy_bwd<bf16><<<M, 256, 0, s>>>(N, (const bf16*)logits, ldx, labels, ignore_index, grad_scale,
+                                                (bf16*)dlogits, ldd);
+  else if (dtype == RF_F16)
+    k_cross_entropy_bwd<f16><<<M, 256, 0, s>>>(N, (const f16*)logits, ldx, labels, ignore_index, grad_scale,
+                                               (f16*)dlogits, ldd);
+  else if (dtype == RF_F32)
+    k_cross_entropy_bwd<float><<<M, 256, 0, s>>>(N, (const float*)logits, ldx, labels, ignore_index, grad_scale,
+                                                 (float*)dlogits, ldd);
+  else
+    RF_REQUIRE(false, "rf_cross_entropy_bwd: bad dtype %d", dtype);
+  RF_LAUNCH_CHECK("rf_cross_entropy_bwd");
 }
 
 int rf_cross_entropy_fwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,

@@ -225,6 +225,9 @@ SHORT_SEQ = True
 FOLD_EARLY = True
 # training: RecformerForPretraining's four encoder passes share one autograd cast per weight
 SHARE_TRAIN_CASTS = True
+# pretraining training: the LM-head decoder + masked-LM cross entropy on the HIP kernels
+# (train._DecoderCE) for 16-bit compute; False = torch ops (F.linear + F.cross_entropy)
+DECODER_CE_HIP = True
 # pretraining: the LM head runs on the masked (labelled) rows only (_mlm_rows)
 LM_HEAD_MASKED_ONLY = True
 
@@ -714,8 +717,15 @@ def _pretrain_train_losses(self, z1, z2, outputs_a, mlm_a, lab_a, mlm_b, lab_b, 
             x = F.gelu(F.linear(hid, head.dense.weight, head.dense.bias))
             x = F.layer_norm(x, (x.shape[-1],), head.layer_norm.weight, head.layer_norm.bias,
                              self.config.layer_norm_eps)
-            scores = F.linear(x, head.decoder.weight, head.bias)
-            loss = loss + self.config.mlm_weight * F.cross_entropy(scores.reshape(-1, self.config.vocab_size), lab)
+            dt = _compute_dtype(self.longformer.dtype)
+            if x.is_cuda and dt != torch.float32 and DECODER_CE_HIP:
+                # decoder GEMM + CE + its backward on the HIP kernels (train._DecoderCE)
+                from .train import decoder_ce
+                mlm = decoder_ce(x.to(dt), head.decoder.weight, head.bias, lab)
+            else:
+                scores = F.linear(x, head.decoder.weight, head.bias)
+                mlm = F.cross_entropy(scores.reshape(-1, self.config.vocab_size), lab)
+            loss = loss + self.config.mlm_weight * mlm
     return RecformerPretrainingOutput(loss=loss, logits=cos_sim, cl_correct_num=correct_num,
                                       cl_total_num=batch_size, hidden_states=outputs_a.hidden_states,
                                       attentions=outputs_a.attentions, global_attentions=outputs_a.global_attentions)

@@ -633,6 +633,25 @@ def cos_scores_cand(z: torch.Tensor, items: torch.Tensor, cand: torch.Tensor, in
     return out
 
 
+def cross_entropy_bwd(logits: torch.Tensor, labels: torch.Tensor, grad_scale: torch.Tensor,
+                      ignore_index: int = -100) -> torch.Tensor:
+    """rf_cross_entropy_bwd: d(mean CE)/d(logits) = (softmax - onehot) * grad_scale (a one-element
+    fp32 device tensor: upstream gradient / counted rows), zero rows for ignore_index; same dtype
+    and shape as logits."""
+    lib = _lib.load()
+    _dev(logits, labels, grad_scale)
+    M, N = logits.shape
+    labels = labels.reshape(-1).to(torch.int64).contiguous()
+    if labels.numel() != M:
+        raise ValueError(f"cross_entropy_bwd: {labels.numel()} labels for {M} rows")
+    gs = grad_scale.reshape(-1).to(torch.float32).contiguous()
+    out = torch.empty(M, N, dtype=logits.dtype, device=logits.device)
+    check(lib.rf_cross_entropy_bwd(dtype_code(logits.dtype), M, N, _p(logits), _rowmajor(logits, "logits"),
+                                   _p(labels), int(ignore_index), _p(gs), _p(out), N, _stream(out)),
+          "rf_cross_entropy_bwd")
+    return out
+
+
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100,
                   reduction: str = "mean", want_argmax: bool = False):
     """torch.nn.functional.cross_entropy over rows of a (M, N) fp32/bf16 logits view, in fp32 on

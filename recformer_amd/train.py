@@ -136,6 +136,40 @@ class _GemmGelu(torch.autograd.Function):
         return da, dw, None, db
 
 
+class _DecoderCE(torch.autograd.Function):
+    """LongformerLMHead.decoder + the masked-LM CrossEntropyLoss (TF:1283-1285, models.py:499-510)
+    for 16-bit compute: logits on rf_gemm in the compute dtype, the loss rows on
+    rf_cross_entropy_fwd (fp32 log-sum-exp), and in the backward d(loss)/d(logits) written in the
+    compute dtype by one kernel (rf_cross_entropy_bwd: softmax - one-hot, scaled on the device), so
+    no fp32 log-softmax / probability matrix of (rows x vocab) is materialised; dX and dW from it
+    as for every other Linear (dW in fp32 for the master weight)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, labels, ignore_index: int):
+        w16 = w.detach().to(x.dtype).contiguous()
+        logits = ops.gemm(x.contiguous(), w16, b.detach().float().contiguous(), ops.RF_EPI_BIAS)
+        rows = ops.cross_entropy(logits, labels, ignore_index, reduction="none")
+        n = (labels.reshape(-1) != ignore_index).sum().to(torch.float32)
+        ctx.save_for_backward(x, w16, logits, labels, n)
+        ctx.ign = ignore_index
+        ctx.wdt = w.dtype
+        return rows.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w16, logits, labels, n = ctx.saved_tensors
+        dlog = ops.cross_entropy_bwd(logits, labels, (g.float() / n).reshape(1), ctx.ign)
+        dx = dlog @ w16 if ctx.needs_input_grad[0] else None
+        dw = _weight_grad(dlog, x.contiguous()).to(ctx.wdt) if ctx.needs_input_grad[1] else None
+        db = ops.colsum(dlog) if ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None
+
+
+def decoder_ce(x, w, b, labels, ignore_index: int = -100):
+    """Mean cross entropy of x.W^T + b against labels (16-bit x; see _DecoderCE)."""
+    return _DecoderCE.apply(x, w, b, labels.reshape(-1), ignore_index)
+
+
 def _ln_backward(dy, x, mean, rstd, w):
     if x.dtype == torch.float32 and x.is_cuda:  # one HIP pass (rf_layernorm_bwd)
         return ops.layernorm_bwd(dy.float(), x, mean, rstd, w)

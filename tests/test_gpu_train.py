@@ -445,3 +445,55 @@ def test_c2_finetune_grads_match_reference(dev, mode):
                 assert cos >= lim, (n, cos)
         checked += 1
     assert checked + zero == len(gz["names"]) == 270 and zero == 29
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N", [1000, 50265])
+def test_cross_entropy_bwd(dev, dt, N):
+    """rf_cross_entropy_bwd = autograd of F.cross_entropy (mean over non-ignored rows, fp32 math) on
+    the same logits, scaled by an upstream gradient held on the device; ignored rows are zero."""
+    from recformer_amd import ops
+    torch.manual_seed(N)
+    M = 29
+    x = (torch.randn(M, N, device=dev) * 3).to(dt)
+    lab = torch.randint(0, N, (M,), device=dev)
+    lab[::4] = -100
+    xr = x.float().requires_grad_(True)
+    loss = F.cross_entropy(xr, lab, ignore_index=-100)
+    (gr,) = torch.autograd.grad(loss * 1.7, xr)
+    n = (lab != -100).sum().float()
+    got = ops.cross_entropy_bwd(x, lab, (torch.tensor(1.7, device=dev) / n).reshape(1))
+    assert got.dtype == dt and got.shape == x.shape
+    tol = 1e-6 if dt == torch.float32 else 4e-3 * float(gr.abs().max())
+    assert float((got.float() - gr).abs().max()) <= tol
+    assert float(got[::4].float().abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_pretrain_decoder_ce_hip_matches_torch(dev, monkeypatch, dt):
+    """Pretraining under autocast with the LM-head decoder + masked-LM CE on the HIP kernels
+    (models.DECODER_CE_HIP, train._DecoderCE) gives the loss and gradients of the torch ops
+    (F.linear under autocast + F.cross_entropy): loss within 1e-3, gradient cosine >= 0.999."""
+    from recformer_amd import models
+    from tests.common import hashed_pretrain, pretrain_inputs
+    g = load_golden("c1_pretrain")
+    m = hashed_pretrain(CFG).to(dev).train()
+    kw = {k: v.to(dev) for k, v in pretrain_inputs(g).items()}
+    res = {}
+    for hip in (False, True):
+        monkeypatch.setattr(models, "DECODER_CE_HIP", hip)
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=dt):
+            out = m(**kw)
+        out.loss.backward()
+        res[hip] = (float(out.loss), {k: p.grad.float().clone() for k, p in m.named_parameters() if p.grad is not None})
+    assert res[True][0] == pytest.approx(res[False][0], rel=1e-3, abs=1e-3)
+    assert res[True][1].keys() == res[False][1].keys()
+    gmax = max(float(v.abs().max()) for v in res[False][1].values())
+    for k, ga in res[False][1].items():
+        gb = res[True][1][k]
+        # key biases: the softmax cancels them, their gradient is rounding noise in both runs
+        if float(ga.abs().max()) < 1e-3 * gmax:
+            continue
+        cos = F.cosine_similarity(ga.reshape(1, -1), gb.reshape(1, -1)).item()
+        assert cos >= 0.999, (k, cos)
