@@ -1080,8 +1080,14 @@ __global__ void __launch_bounds__(256, 1)
     const int rstep = isA ? 8 * pp : (OUT32 ? 32 * (pp & 1) + (pp >> 1) : 64 * (pp & 1) + (pp >> 1));
     const int soff = kt * 128 + rstep * (isA ? lda : ldw) * 2;
     const int vo = isA ? (nxt ? vAn : vA) : (nxt ? vWn : vW);
+#if defined(RF_W4_DIAG) && (RF_W4_DIAG & 8)  // timing diagnostic: every DMA reads K-tile 0 (L2-hot)
+    const int soffd = rstep * (isA ? lda : ldw) * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsW, (__attribute__((address_space(3))) void*)dst, 16, vo,
+                                             kv < 2 ? soff : soffd, 0, 0);
+#else
     __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsW, (__attribute__((address_space(3))) void*)dst, 16, vo,
                                              soff, 0, 0);
+#endif
   };
   auto dma_cols = [&](int tm0, int tn0, int par) {
     if (EPI == RF_EPI_NONE) return;

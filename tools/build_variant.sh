@@ -7,7 +7,7 @@ name=$1; src=$2; shift 2
 cd "$(dirname "$0")/../recformer_amd/csrc"
 mkdir -p build/var ../../tools/var
 objs=""
-for f in rf_rowops rf_gemm rf_attn rf_attn_bwd rf_global; do
+for f in rf_rowops rf_gemm rf_attn rf_attn_bwd rf_global rf_retrieval; do
   if [ "$f.hip" = "$src" ]; then
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function "$@" -c $src -o build/var/${f}_$name.o
     objs="$objs build/var/${f}_$name.o"
