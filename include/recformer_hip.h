@@ -40,8 +40,10 @@ enum {
   RF_EPI_BIAS_RESID = 3, /* C = A.W^T + b + R          (TF:1068-1071 / 1127-1130, pre-LN) */
   RF_EPI_COS = 4,        /* C(f32) = A.W^T * ra[m] * rw[n] * scale (Similarity, models.py:358-369) */
   RF_EPI_BIAS_RESID_LN = 5, /* C(f32) = A.W^T + b + LN(R): rf_gemm_resid_ln only */
-  RF_EPI_BIAS_GELU_AUX = 6  /* C = gelu_erf(A.W^T + b) and R (bf16, written) = A.W^T + b: the
+  RF_EPI_BIAS_GELU_AUX = 6, /* C = gelu_erf(A.W^T + b) and R (bf16, written) = A.W^T + b: the
                                pre-activation the training path's GELU backward reads */
+  RF_EPI_DGELU = 7          /* C = (A.W^T) * gelu_erf'(R), R the 16-bit pre-activation, no bias: the
+                               GELU backward fused into the dA GEMM of the next Linear (TF:1113-1116) */
 };
 
 const char* rf_last_error(void);

@@ -17,6 +17,7 @@ RF_F32, RF_BF16, RF_F16 = 0, 1, 2
 RF_IO_C_F32, RF_IO_R_F32 = 1, 2
 RF_EPI_NONE, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF_EPI_COS = 0, 1, 2, 3, 4
 RF_EPI_BIAS_GELU_AUX = 6
+RF_EPI_DGELU = 7
 
 # symbol -> (restype, argtypes); must match include/recformer_hip.h exactly
 P = c_void_p

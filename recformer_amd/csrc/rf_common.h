@@ -105,6 +105,12 @@ __device__ __forceinline__ float erf_fast(float x) {
 // exact-erf GELU (transformers ACT2FN['gelu'] = x * Phi(x), TF:1115), |error| < 1e-6 |x|
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
+// derivative of the exact-erf GELU, d/dz [z Phi(z)] = Phi(z) + z phi(z), as torch's gelu_backward
+// (approximate='none') computes it in fp32
+__device__ __forceinline__ float dgelu_erf(float z) {
+  return 0.5f * (1.0f + erf_fast(z * 0.70710678118654752f)) + z * 0.3989422804014327f * __expf(-0.5f * z * z);
+}
+
 // GELU for 16-bit outputs: x * sigmoid(x (a + b x^2 + c x^4)) with (a, b, c) fitted minimax to
 // the exact-erf GELU, x^2 clamped at 64; |error| <= 2.6e-5 absolute on all of R (fp32): below the
 // bf16 rounding of the stored value, and below fp16's for |y| >= 0.03 (smaller outputs differ by

@@ -55,6 +55,14 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int row, int col, fl
     reinterpret_cast<float*>(e.C)[(int64_t)row * e.ldc + col] = v * (e.ra[row] * e.col_scale) * e.rw[col];
     return;
   }
+  if (EPI == RF_EPI_DGELU) {  // GELU backward: dz = du * gelu'(z), R = z (16-bit)
+    v *= dgelu_erf(to_f32(reinterpret_cast<const TIN*>(e.R)[(int64_t)row * e.ldr + col]));
+    if (CF32)
+      reinterpret_cast<float*>(e.C)[(int64_t)row * e.ldc + col] = v;
+    else
+      reinterpret_cast<TIN*>(e.C)[(int64_t)row * e.ldc + col] = from_f32<TIN>(v);
+    return;
+  }
   if (EPI != RF_EPI_NONE) v += e.bias[col];
   if (col < e.scale_cols) v *= e.col_scale;
   if (EPI == RF_EPI_BIAS_GELU_AUX)
@@ -85,7 +93,7 @@ constexpr int EPI_LD = 68;  // fp32 staging row stride (floats): conflict-free w
 // bias[c0, c0+16) as 4 float4 loads (zeros for EPI_NONE / EPI_COS or a ragged right edge)
 template <int EPI>
 __device__ __forceinline__ void load_bias16(const EpiArgs& e, int c0, float* b) {
-  if (EPI == RF_EPI_NONE || EPI == RF_EPI_COS || c0 + 16 > e.N) {
+  if (EPI == RF_EPI_NONE || EPI == RF_EPI_COS || EPI == RF_EPI_DGELU || c0 + 16 > e.N) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) b[k] = 0.f;
     return;
@@ -118,7 +126,11 @@ __device__ __forceinline__ void epi_row16(const EpiArgs& e, int row, int c0, flo
     }
     return;
   }
-  if (EPI != RF_EPI_NONE) {
+  if (EPI == RF_EPI_DGELU) {
+    const E* z = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] *= dgelu_erf(to_f32(z[k]));
+  } else if (EPI != RF_EPI_NONE) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] += bv[k];
   }
@@ -531,7 +543,17 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
                 v[4 * q + 3] * sc * bv[4 * q + 3]};
     return;
   }
-  if (EPI != RF_EPI_NONE) {
+  if (EPI == RF_EPI_DGELU) {
+    const E* z = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
+    if (NV == 8) {
+      const typename H16<E>::x8 x = *reinterpret_cast<const typename H16<E>::x8*>(z);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= dgelu_erf((float)x[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] *= dgelu_erf(to_f32(z[k]));
+    }
+  } else if (EPI != RF_EPI_NONE) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] += bv[k];
   }
@@ -640,7 +662,7 @@ __device__ __forceinline__ void load_cols(const EpiArgs& e, int c0, float* bv, f
     float4 b = make_float4(0.f, 0.f, 0.f, 0.f), g = b, t = b;
     if (in) {
       if (EPI == RF_EPI_COS) b = *reinterpret_cast<const float4*>(e.rw + c0 + 4 * q);
-      else if (EPI != RF_EPI_NONE) b = *reinterpret_cast<const float4*>(e.bias + c0 + 4 * q);
+      else if (EPI != RF_EPI_NONE && EPI != RF_EPI_DGELU) b = *reinterpret_cast<const float4*>(e.bias + c0 + 4 * q);
       if (EPI == RF_EPI_BIAS_RESID_LN) {
         g = *reinterpret_cast<const float4*>(e.lgamma + c0 + 4 * q);
         t = *reinterpret_cast<const float4*>(e.lbeta + c0 + 4 * q);
@@ -763,7 +785,7 @@ __global__ void __launch_bounds__(512, 1)
   // counted waits stay uniform. Source columns are clamped into [0, N): the ragged last
   // column tile's out-of-range segments take the scalar epi_store path, never these values.
   auto dma_cols = [&](int tm0, int tn0, int par) {
-    if (EPI == RF_EPI_NONE) return;
+    if (EPI == RF_EPI_NONE || EPI == RF_EPI_DGELU) return;
     const int vec = wave % 3;
     const float* src = EPI == RF_EPI_COS ? e.rw : e.bias;
     int idx = min(tn0 + 4 * lane, e.N - 4);
@@ -1090,7 +1112,7 @@ __global__ void __launch_bounds__(256, 1)
 #endif
   };
   auto dma_cols = [&](int tm0, int tn0, int par) {
-    if (EPI == RF_EPI_NONE) return;
+    if (EPI == RF_EPI_NONE || EPI == RF_EPI_DGELU) return;
     const int vec = wave % 3;
     const float* src = EPI == RF_EPI_COS ? e.rw : e.bias;
     int idx = min(tn0 + 4 * lane, e.N - 4);
@@ -1393,7 +1415,8 @@ __global__ void __launch_bounds__(256, 1)
   };
   auto dma_cols = [&](int tm0, int tn0, int dst_off) {
     const int vec = wave % 3;
-    const float* src = EPI == RF_EPI_COS ? e.rw : (e.bias != nullptr ? e.bias : reinterpret_cast<const float*>(A));
+    const float* src = EPI == RF_EPI_COS ? e.rw : (e.bias != nullptr && EPI != RF_EPI_DGELU ? e.bias
+                                                                                              : reinterpret_cast<const float*>(A));
     int idx = min(tn0 + 4 * lane, e.N - 4);
     if (EPI == RF_EPI_BIAS_RESID_LN && vec == 1) src = e.lgamma;
     if (EPI == RF_EPI_BIAS_RESID_LN && vec == 2) src = e.lbeta;
@@ -1401,7 +1424,7 @@ __global__ void __launch_bounds__(256, 1)
       src = e.ra;
       idx = min(tm0 + 4 * lane, e.M - 4);
     }
-    if (EPI == RF_EPI_NONE) idx = 0;  // a harmless piece (keeps the per-iteration VMEM count fixed)
+    if (EPI == RF_EPI_NONE || EPI == RF_EPI_DGELU) idx = 0;  // a harmless piece (fixed VMEM count)
     glds16(src + idx, smem + dst_off + (dst_off == R4_CV + 6 * 1024 ? 0 : vec * 1024));
   };
   const int lr = lane & 15, ch = lane >> 4;
@@ -1662,6 +1685,9 @@ static void gemm16(int epilogue, bool cf, bool rf, int M, int N, int K, const vo
     case RF_EPI_BIAS_GELU_AUX:
       dispatch_tile<E, RF_EPI_BIAS_GELU_AUX, false, false>(M, N, K, A, lda, W, ldw, e, s);
       break;
+    case RF_EPI_DGELU:
+      dispatch_tile<E, RF_EPI_DGELU, false, false>(M, N, K, A, lda, W, ldw, e, s);
+      break;
     case RF_EPI_BIAS_RESID:
       if (cf && rf) dispatch_tile<E, RF_EPI_BIAS_RESID, true, true>(M, N, K, A, lda, W, ldw, e, s);
       else if (cf) dispatch_tile<E, RF_EPI_BIAS_RESID, true, false>(M, N, K, A, lda, W, ldw, e, s);
@@ -1684,11 +1710,15 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
                        const float* rw, rf_stream_t stream) {
   RF_REQUIRE(M >= 0 && N > 0 && K > 0, "rf_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   RF_REQUIRE(lda >= K && ldw >= K && ldc >= N, "rf_gemm: bad leading dims");
-  RF_REQUIRE((epilogue >= RF_EPI_NONE && epilogue <= RF_EPI_COS) || epilogue == RF_EPI_BIAS_GELU_AUX,
+  RF_REQUIRE((epilogue >= RF_EPI_NONE && epilogue <= RF_EPI_COS) || epilogue == RF_EPI_BIAS_GELU_AUX ||
+                 epilogue == RF_EPI_DGELU,
              "rf_gemm: bad epilogue %d", epilogue);
+  RF_REQUIRE(epilogue != RF_EPI_DGELU || (dtype != RF_F32 && resid && ldr >= N && !(io_flags & 3)),
+             "rf_gemm: EPI_DGELU needs 16-bit operands and the pre-activation (resid) of that type");
   RF_REQUIRE(epilogue != RF_EPI_BIAS_GELU_AUX || (dtype != RF_F32 && resid && ldr >= N && !(io_flags & 3)),
              "rf_gemm: EPI_BIAS_GELU_AUX needs 16-bit operands and a pre-activation output (resid) of that type");
-  RF_REQUIRE(epilogue == RF_EPI_NONE || epilogue == RF_EPI_COS || bias, "rf_gemm: bias required");
+  RF_REQUIRE(epilogue == RF_EPI_NONE || epilogue == RF_EPI_COS || epilogue == RF_EPI_DGELU || bias,
+             "rf_gemm: bias required");
   RF_REQUIRE(epilogue != RF_EPI_BIAS_RESID || (resid && ldr >= N), "rf_gemm: residual required");
   RF_REQUIRE(epilogue != RF_EPI_COS || (ra && rw), "rf_gemm: norms required for EPI_COS");
   if (M == 0) return RF_OK;

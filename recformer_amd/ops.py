@@ -13,6 +13,7 @@ import torch
 
 from . import _lib
 from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_GELU_AUX, RF_EPI_BIAS_RESID, RF_EPI_COS,
+                   RF_EPI_DGELU,
                    RF_EPI_NONE, RF_F32, check)
 
 __all__ = [
@@ -21,6 +22,7 @@ __all__ = [
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_GELU_AUX", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
+    "RF_EPI_DGELU",
 ]
 
 

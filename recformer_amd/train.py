@@ -49,6 +49,9 @@ DW_SPLIT_K = True
 # neutral at C3 (25.8 vs 26.4 ms median, alternating A/B) — the GELU moves into the GEMM's
 # unhidden epilogue and the pre-activation is still written
 FUSED_GELU = False
+# 16-bit: the whole feed-forward block as one autograd node (_FFN): GELU in the FFN1 epilogue, its
+# backward in the epilogue of the dA GEMM of FFN2, both dA GEMMs on rf_gemm
+FFN_FUSED = True
 
 
 # ------------------------------------------------------------------------------------------
@@ -168,6 +171,37 @@ class _DecoderCE(torch.autograd.Function):
 def decoder_ce(x, w, b, labels, ignore_index: int = -100):
     """Mean cross entropy of x.W^T + b against labels (16-bit x; see _DecoderCE)."""
     return _DecoderCE.apply(x, w, b, labels.reshape(-1), ignore_index)
+
+
+class _FFN(torch.autograd.Function):
+    """The feed-forward block's two Linears around the exact GELU (TF:1107-1116, 1123-1126) for
+    16-bit compute, t2 = gelu(a.W1^T + b1).W2^T + b2: forward FFN1 with EPI_BIAS_GELU_AUX (GELU
+    output + the pre-activation z in one GEMM), FFN2 with EPI_BIAS; backward dz = (dt2.W2) *
+    gelu'(z) as ONE rf_gemm (EPI_DGELU, against a transposed copy of W2) — no du tensor and no
+    separate GELU-backward pass — and da = dz.W1 on rf_gemm too (transposed copy of W1); the
+    weight gradients (long token reductions) as for every Linear (_weight_grad, fp32)."""
+
+    @staticmethod
+    def forward(ctx, a, w1, w1_16, b1, w2, w2_16, b2):
+        a = a.contiguous()
+        z = torch.empty(a.shape[0], w1_16.shape[0], dtype=a.dtype, device=a.device)
+        u = ops.gemm(a, w1_16, b1, ops.RF_EPI_BIAS_GELU_AUX, resid=z)
+        t2 = ops.gemm(u, w2_16, b2, ops.RF_EPI_BIAS)
+        ctx.save_for_backward(a, u, z, w1_16, w2_16)
+        ctx.wdt = (w1.dtype, w2.dtype)
+        return t2
+
+    @staticmethod
+    def backward(ctx, dt2):
+        a, u, z, w1, w2 = ctx.saved_tensors
+        dt2 = dt2.to(a.dtype).contiguous()
+        dz = ops.gemm(dt2, w2.t().contiguous(), None, ops.RF_EPI_DGELU, resid=z)
+        dw2 = _weight_grad(dt2, u).to(ctx.wdt[1]) if ctx.needs_input_grad[4] else None
+        db2 = ops.colsum(dt2) if ctx.needs_input_grad[6] else None
+        da = ops.gemm(dz, w1.t().contiguous(), None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
+        dw1 = _weight_grad(dz, a).to(ctx.wdt[0]) if ctx.needs_input_grad[1] else None
+        db1 = ops.colsum(dz) if ctx.needs_input_grad[3] else None
+        return da, dw1, None, db1, dw2, None, db2
 
 
 def _ln_backward(dy, x, mean, rstd, w):
@@ -680,12 +714,15 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
             x1 = F.dropout(t.float(), p_hid, model.training) + h32
             a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
             a16 = a32.to(dt)
-        if dt == torch.bfloat16 and FUSED_GELU:
-            u = _GemmGelu.apply(a16, *lw["w_1"], lw["b_1"])
-        else:
-            u = F.gelu(_Gemm.apply(a16, *lw["w_1"], lw["b_1"], 0, 1.0))
         fo = lyr.output
-        t2 = _Gemm.apply(u, *lw["w_2"], lw["b_2"], 0, 1.0)
+        if fused and FFN_FUSED and D % 64 == 0 and lw["w_1"][1].shape[0] % 64 == 0:
+            t2 = _FFN.apply(a16, *lw["w_1"], lw["b_1"], *lw["w_2"], lw["b_2"])
+        else:
+            if dt == torch.bfloat16 and FUSED_GELU:
+                u = _GemmGelu.apply(a16, *lw["w_1"], lw["b_1"])
+            else:
+                u = F.gelu(_Gemm.apply(a16, *lw["w_1"], lw["b_1"], 0, 1.0))
+            t2 = _Gemm.apply(u, *lw["w_2"], lw["b_2"], 0, 1.0)
         if fused and li + 1 < nl:
             h32, h16 = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, True,
                                         seeds[2 * li + 1])

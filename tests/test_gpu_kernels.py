@@ -675,3 +675,17 @@ def test_rank_catalog_matches_full_ranker(dev, B, N, block):
     got = rank_catalog(q, items, labels, [10, 50], 0.05, block=block)
     assert got[:-1] == full[:-1]
     assert got[-1] == pytest.approx(full[-1], rel=1e-5, abs=1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (1000, 384, 192), (300, 256, 64)])
+def test_gemm_dgelu_epilogue(dev, dt, M, N, K):
+    """EPI_DGELU: C = (A.W^T) * gelu'(R) (the GELU backward fused into the next Linear's dA GEMM)
+    against torch's gelu_backward of the fp32 product on the same operands."""
+    a = _rand((M, K), dev, dt, 1.0, seed=61)
+    w = _rand((N, K), dev, dt, 0.1, seed=62)
+    z = _rand((M, N), dev, dt, 2.0, seed=63)
+    out = ops.gemm(a, w, None, ops.RF_EPI_DGELU, resid=z)
+    ref = torch.ops.aten.gelu_backward(a.float() @ w.float().t(), z.float())
+    err = float((out.float() - ref).abs().max())
+    assert err <= 1e-2 * max(float(ref.abs().max()), 1e-6), err
