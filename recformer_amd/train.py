@@ -52,6 +52,9 @@ FUSED_GELU = False
 # 16-bit: the whole feed-forward block as one autograd node (_FFN): GELU in the FFN1 epilogue, its
 # backward in the epilogue of the dA GEMM of FFN2, both dA GEMMs on rf_gemm
 FFN_FUSED = True
+# 16-bit: dA = dC.W of the other Linears (qkv, query_global, out-proj) on rf_gemm against a
+# transposed weight copy instead of hipBLASLt
+DA_RF_GEMM = True
 
 
 # ------------------------------------------------------------------------------------------
@@ -105,7 +108,12 @@ class _Gemm(torch.autograd.Function):
         if scaled and ctx.needs_input_grad[0]:
             wa = w.clone()
             wa[:sc] *= s
-        da = dc @ wa if ctx.needs_input_grad[0] else None
+        da = None
+        if ctx.needs_input_grad[0]:
+            if DA_RF_GEMM and dc.dtype != torch.float32 and dc.shape[1] % 64 == 0 and wa.shape[1] % 8 == 0:
+                da = ops.gemm(dc.contiguous(), wa.t().contiguous(), None, ops.RF_EPI_NONE)  # rf_gemm, W^T copy
+            else:
+                da = dc @ wa
         dw = _weight_grad(dc, a).to(ctx.wdt) if ctx.needs_input_grad[1] else None
         db = ops.colsum(dc) if ctx.needs_input_grad[3] else None  # deterministic HIP column sums
         if scaled:

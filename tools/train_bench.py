@@ -29,11 +29,19 @@ def main():
     ap.add_argument("--attn-dropout", type=float, default=0.1)
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16")
     ap.add_argument("--no-dw-split", action="store_true", help="A/B: weight gradients as one GEMM each")
+    ap.add_argument("--blas-da", action="store_true", help="A/B: dA of the non-FFN Linears on hipBLASLt")
+    ap.add_argument("--no-ffn-fused", action="store_true", help="A/B: FFN as two Linears + torch GELU")
     ap.add_argument("--no-fused-gelu", action="store_true", help="A/B: FFN1 GEMM then F.gelu")
     a = ap.parse_args()
     if a.no_fused_gelu:
         from recformer_amd import train
         train.FUSED_GELU = False
+    if a.blas_da:
+        from recformer_amd import train
+        train.DA_RF_GEMM = False
+    if a.no_ffn_fused:
+        from recformer_amd import train
+        train.FFN_FUSED = False
     if a.no_dw_split:
         from recformer_amd import train
         train.DW_SPLIT_K = False
