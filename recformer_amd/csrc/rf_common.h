@@ -107,8 +107,42 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + e
 
 // derivative of the exact-erf GELU, d/dz [z Phi(z)] = Phi(z) + z phi(z), as torch's gelu_backward
 // (approximate='none') computes it in fp32
+// (erf through erf_fast's form with its exp(-x^2) = exp(-z^2 / 2) shared with phi: one v_exp, one
+// v_rcp per value)
 __device__ __forceinline__ float dgelu_erf(float z) {
-  return 0.5f * (1.0f + erf_fast(z * 0.70710678118654752f)) + z * 0.3989422804014327f * __expf(-0.5f * z * z);
+  const float ax = fabsf(z) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float e = __expf(-ax * ax);
+  const float erf = copysignf(fmaf(-p * t, e, 1.0f), z);
+  return fmaf(0.5f, erf, 0.5f) + z * 0.3989422804014327f * e;
+}
+// the same on 8 values, one stage at a time across them (independent chains fill the
+// transcendental hazards; see gelu8_bf16out)
+__device__ __forceinline__ void dgelu8_erf(const float (&z)[8], float (&d)[8]) {
+  float ax[8], t[8], p[8], e[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ax[k] = fabsf(z[k]) * 0.70710678118654752f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[k] = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax[k], 1.0f));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e[k] = __expf(-ax[k] * ax[k]);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = fmaf(t[k], 1.061405429f, -1.453152027f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = fmaf(t[k], p[k], 1.421413741f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = fmaf(t[k], p[k], -0.284496736f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = fmaf(t[k], p[k], 0.254829592f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float erf = copysignf(fmaf(-p[k] * t[k], e[k], 1.0f), z[k]);
+    d[k] = fmaf(0.5f, erf, 0.5f) + z[k] * 0.3989422804014327f * e[k];
+  }
 }
 
 // GELU for 16-bit outputs: x * sigmoid(x (a + b x^2 + c x^4)) with (a, b, c) fitted minimax to

@@ -547,8 +547,12 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
     const E* z = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
     if (NV == 8) {
       const typename H16<E>::x8 x = *reinterpret_cast<const typename H16<E>::x8*>(z);
+      float zf[8], d[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] *= dgelu_erf((float)x[k]);
+      for (int k = 0; k < 8; ++k) zf[k] = (float)x[k];
+      dgelu8_erf(zf, d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= d[k];
     } else {
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[k] *= dgelu_erf(to_f32(z[k]));
