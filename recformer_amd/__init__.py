@@ -10,7 +10,7 @@ from .models import (RecformerEmbeddings, RecformerForPretraining, RecformerForS
                      RecformerPretrainingOutput, Similarity, create_position_ids_from_input_ids)
 
 _LAZY = {"RecformerTokenizer": "data", "FinetuneDataCollatorWithPadding": "data",
-         "EvalDataCollatorWithPadding": "data", "LitWrapper": "lit"}
+         "EvalDataCollatorWithPadding": "data", "LitWrapper": "lit", "GraphedForward": "graphs"}
 
 
 def __getattr__(name):  # host-side pieces load transformers / the host library on first use
@@ -24,5 +24,5 @@ __all__ = [
     "RecformerConfig", "RecformerModel", "RecformerForSeqRec", "RecformerForPretraining",
     "RecformerPretrainingOutput", "RecformerModelOutput", "RecformerEmbeddings", "RecformerPooler",
     "Similarity", "create_position_ids_from_input_ids", "Ranker", "rank_catalog", "CatalogShard", "retrieve", "RecformerTokenizer",
-    "FinetuneDataCollatorWithPadding", "EvalDataCollatorWithPadding", "LitWrapper",
+    "FinetuneDataCollatorWithPadding", "EvalDataCollatorWithPadding", "LitWrapper", "GraphedForward",
 ]

@@ -225,6 +225,8 @@ SHORT_SEQ = True
 FOLD_EARLY = True
 # training: RecformerForPretraining's four encoder passes share one autograd cast per weight
 SHARE_TRAIN_CASTS = True
+# set by graphs.GraphedForward during capture: the global-slot count of the captured shape
+_STATIC_GMAX = None
 # pretraining training: the LM-head decoder + masked-LM cross entropy on the HIP kernels
 # (train._DecoderCE) for 16-bit compute; False = torch ops (F.linear + F.cross_entropy)
 DECODER_CE_HIP = True
@@ -399,8 +401,11 @@ class RecformerModel(nn.Module):
         dt = _compute_dtype(self.dtype)
         pk = self._packed.get(self, dt)
 
-        # number of global slots (one host read per forward; the reference does ~265)
-        if global_attention_mask is not None:
+        # number of global slots (one host read per forward; the reference does ~265) — fixed by
+        # graphs.GraphedForward while it captures (no host read inside a HIP graph)
+        if _STATIC_GMAX is not None:
+            gmax = _STATIC_GMAX
+        elif global_attention_mask is not None:
             gm = global_attention_mask != 0
             if attention_mask is not None:
                 gm = gm & (attention_mask > 0)

@@ -224,3 +224,27 @@ def test_catalog_batch_vs_oracle(dev, catalog_case, monkeypatch, mode, short):
         assert e["max"] <= 1e-3 and ep["max"] <= 1e-3, (e, ep)
     else:
         _check_e2e(mode, e, out.pooler_output, p_ref)
+
+
+@pytest.mark.parametrize("B,L", [(1, 1024), (4, 300)])
+def test_graphed_forward_matches_eager(dev, B, L):
+    """graphs.GraphedForward: a HIP-graph replay of RecformerForSeqRec inference (bf16 weights) equals
+    the eager forward bit for bit on new inputs of the captured shape (ragged masks, fewer globals),
+    and rejects a batch with more global tokens than captured."""
+    from recformer_amd import GraphedForward
+    from recformer_amd.synth import synth_batch
+    model = hashed_model(BASE, seed=3, cls=RecformerForSeqRec, item_num=5000)
+    model.init_item_embedding(hash_tensor("catalog", (5000, 768), "weight", seed=4, std=1.0))
+    model = model.to(dev).to(torch.bfloat16).eval()
+    ex = {k: v.to(dev) for k, v in synth_batch(B, L, BASE["vocab_size"], seed=1).items()}
+    g = GraphedForward(model, ex)
+    for seed in (2, 3):
+        b = {k: v.to(dev) for k, v in synth_batch(B, L, BASE["vocab_size"], seed=seed).items()}
+        b["attention_mask"][0, L // 2:] = 0
+        with torch.no_grad():
+            ref = model(**b)
+        got = g(**b).clone()
+        assert torch.equal(got, ref)
+    b["global_attention_mask"][:, 1] = 1
+    with pytest.raises(ValueError):
+        g(**b)
