@@ -227,6 +227,23 @@ FOLD_EARLY = True
 SHARE_TRAIN_CASTS = True
 # set by graphs.GraphedForward during capture: the global-slot count of the captured shape
 _STATIC_GMAX = None
+# read the global-token count after the embedding is queued (False: before the prologue)
+ASYNC_GLOBAL_COUNT = True
+
+
+def _async_count(t: torch.Tensor):
+    """Start copying a device integer scalar to pinned host memory (no host wait yet)."""
+    buf = torch.empty((), dtype=t.dtype, pin_memory=True)
+    buf.copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return buf, ev
+
+
+def _read_count(p) -> int:
+    buf, ev = p
+    ev.synchronize()
+    return int(buf)
 # pretraining training: the LM-head decoder + masked-LM cross entropy on the HIP kernels
 # (train._DecoderCE) for 16-bit compute; False = torch ops (F.linear + F.cross_entropy)
 DECODER_CE_HIP = True
@@ -401,20 +418,39 @@ class RecformerModel(nn.Module):
         dt = _compute_dtype(self.dtype)
         pk = self._packed.get(self, dt)
 
-        # number of global slots (one host read per forward; the reference does ~265) — fixed by
-        # graphs.GraphedForward while it captures (no host read inside a HIP graph)
+        # number of global slots: one host read per forward (the reference does ~265) — fixed by
+        # graphs.GraphedForward while it captures (no host read inside a HIP graph). The count is
+        # reduced on the device and copied to pinned memory asynchronously; the host waits for it
+        # only after the token streams are prepared and the embedding + LayerNorm is queued, so the
+        # GPU has work while the host reads (the global index table is prepared afterwards).
+        pending = None
         if _STATIC_GMAX is not None:
             gmax = _STATIC_GMAX
-        elif global_attention_mask is not None:
+        elif global_attention_mask is not None and B > 0:
             gm = global_attention_mask != 0
             if attention_mask is not None:
                 gm = gm & (attention_mask > 0)
-            gmax = int(gm.sum(1).max().item()) if B > 0 else 0
+            if ASYNC_GLOBAL_COUNT:
+                pending = _async_count(gm.sum(1).max())
+                gmax = 0
+            else:
+                gmax = int(gm.sum(1).max().item())
         else:
             gmax = 0
         ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
             input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
             position_ids, Lp, cfg.pad_token_id, gmax)
+
+        def _globals():
+            # the global index table once the count is known (re-runs the prologue with gmax slots;
+            # the token streams it rewrites are identical)
+            nonlocal gmax, flags, gidx
+            if pending is not None:
+                gmax = _read_count(pending)
+                if gmax > 0:
+                    _, _, _, _, flags, gidx = ops.prepare_inputs(
+                        input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
+                        position_ids, Lp, cfg.pad_token_id, gmax)
         # bf16 path: GEMM operands in bf16, residual stream / LN outputs in fp32 (as the
         # reference's autocast run), the fp32 stream held split as (hi, lo) 16-bit planes whose
         # hi plane is the bf16 GEMM operand (ops.add_layernorm_split); fp32 path: everything fp32.
@@ -431,6 +467,7 @@ class RecformerModel(nn.Module):
                                   pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps, out_dtype=dt, want_f32=mixed)
             if not mixed:
                 h32 = h
+        _globals()
         hidden_all = [h32] if output_hidden_states else None
         scale = 1.0 / math.sqrt(hd)
         windows = cfg.window_per_layer()
