@@ -223,6 +223,18 @@ SPLIT_STREAM = True
 SHORT_SEQ = True
 # run the global fold's pass over h before the qkv GEMM (rf_global_attn_fold_h_stage)
 FOLD_EARLY = True
+# with FOLD_EARLY: queue the fold's first stage on a side stream that starts once the qkv GEMM is
+# done, so its launch-bound projection and its pass over h run beside the HBM-bound band attention
+# (the band kernel leaves LDS free on every CU); the main stream joins before the fold's last stage
+FOLD_OVERLAP = True
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _SIDE_STREAMS.get(dev.index)
+    if s is None:
+        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(dev)
+    return s
 # training: RecformerForPretraining's four encoder passes share one autograd cast per weight
 SHARE_TRAIN_CASTS = True
 # set by graphs.GraphedForward during capture: the global-slot count of the captured shape
@@ -482,16 +494,28 @@ class RecformerModel(nn.Module):
             gargs = (h, lw["w_qg"], lw["b_qg"], scale, lw["w_qkv"][3 * D:4 * D], lw["b_qkv"][3 * D:4 * D],
                      lw["w_qkv"][4 * D:5 * D], lw["b_qkv"][4 * D:5 * D], flags, gidx, B, Lp, H)
             early = gmax > 0 and fold and FOLD_EARLY
+            side = early and FOLD_OVERLAP and h.is_cuda
             if early:
-                # the fold's pass over h while h is still cache-resident from the LayerNorm
-                # that wrote it; its last stage runs after the local attention has written ctx
                 if gws is None:
                     gws = ops.global_fold_workspace(h, B, Lp, H, gmax)
-                ops.global_attention_fold_h_stage(1, gws, *gargs, tag="global_attn")
+                if not side:
+                    # the fold's pass over h while h is still cache-resident from the LayerNorm
+                    # that wrote it; its last stage runs after the local attention has written ctx
+                    ops.global_attention_fold_h_stage(1, gws, *gargs, tag="global_attn")
             qkv = ops.gemm(h, lw["w_qkv"][:nq], lw["b_qkv"][:nq], ops.RF_EPI_BIAS,
                            scale_cols=D, col_scale=scale, tag="gemm_qkv")
+            if side:
+                # stage 1 beside the band attention; h and gws stay alive and unwritten until the
+                # main stream has joined (the next writer of h is this layer's LayerNorm)
+                main_s = torch.cuda.current_stream(h.device)
+                side_s = _side_stream(h.device)
+                side_s.wait_stream(main_s)
+                with torch.cuda.stream(side_s):
+                    ops.global_attention_fold_h_stage(1, gws, *gargs, tag="global_attn")
             ctx = ops.band_attention(qkv[:, 0:D], qkv[:, D:2 * D], qkv[:, 2 * D:3 * D], flags,
                                      gidx, B, Lp, H, half_w, tag="band_attn")
+            if side:
+                main_s.wait_stream(side_s)
             if early:
                 ops.global_attention_fold_h_stage(2, gws, *gargs, out=ctx, tag="global_attn")
             elif gmax > 0:

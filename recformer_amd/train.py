@@ -43,6 +43,8 @@ __all__ = ["encode_train"]
 
 # the global rows' backward in closed form (_global_bwd); False: autograd over _global_torch
 GLOBAL_BWD_CLOSED_FORM = True
+# the closed form with its products over h merged into three batched GEMMs (False: six)
+GLOBAL_BWD_MERGED = True
 # weight gradients of the layer GEMMs as a split-K batched GEMM (_weight_grad)
 DW_SPLIT_K = True
 # bf16: FFN1 + GELU as one GEMM that also writes the pre-activation (_GemmGelu). Off: measured
@@ -409,29 +411,41 @@ def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout, z=None, b
     qH = qg.float().view(B * G, H, hd).transpose(0, 1)                       # (H, BG, hd)
     uH = torch.bmm(qH, wk)                                                   # (H, BG, D)
     u = uH.view(H, B, G, D).transpose(0, 1).reshape(B, HG, D)                # (B, HG, D)
-    s = torch.bmm(u, hf.transpose(1, 2))                                     # (B, HG, Lp)
-    s.masked_fill_((flags == 0).view(B, 1, Lp), float("-inf"))
+    doH = gout.float().view(B * G, H, hd).transpose(0, 1)                    # (H, BG, hd)
+    dwH = torch.bmm(doH, wv)                                                 # (H, BG, D)
+    dw = dwH.view(H, B, G, D).transpose(0, 1).reshape(B, HG, D)
+    if GLOBAL_BWD_MERGED:
+        # three passes over h instead of six: [u; dw].h^T gives the scores and d/dp' together,
+        # [p'; ds].h gives w and du, and dh = p'^T.dw + ds^T.u is one product with K = 2HG
+        sdp = torch.bmm(torch.cat((u, dw), 1), hf.transpose(1, 2))           # (B, 2HG, Lp)
+        s, dp = sdp[:, :HG], sdp[:, HG:]
+    else:
+        s = torch.bmm(u, hf.transpose(1, 2))                                 # (B, HG, Lp)
+        dp = torch.bmm(dw, hf.transpose(1, 2))                               # (B, HG, Lp): d/dp'
+    s = s.masked_fill((flags == 0).view(B, 1, Lp), float("-inf"))
     p = torch.softmax(s, -1)
     pd = p if z is None else p * z.reshape(B, HG, Lp)                        # dropped probabilities
-    w = torch.bmm(pd, hf)                                                    # (B, HG, D)
-    wH = w.view(B, H, G, D).transpose(0, 1).reshape(H, B * G, D)             # (H, BG, D)
-    doH = gout.float().view(B * G, H, hd).transpose(0, 1)                    # (H, BG, hd)
     if z is None:
         dbvg = doH.sum(1).reshape(D)
     else:  # out += bvg * S' with S' = sum_l p'_l per (b, h, g)
         sH = pd.sum(-1).view(B, H, G).permute(1, 0, 2).reshape(H, B * G, 1)
         dbvg = (doH * sH).sum(1).reshape(D)
-    dwvg = torch.bmm(doH.transpose(1, 2), wH).reshape(D, D)                  # (H, hd, D)
-    dwH = torch.bmm(doH, wv)                                                 # (H, BG, D)
-    dw = dwH.view(H, B, G, D).transpose(0, 1).reshape(B, HG, D)
-    dp = torch.bmm(dw, hf.transpose(1, 2))                                   # (B, HG, Lp): d/dp'
     if z is not None:
         dS = (doH * bvg.float().view(H, 1, hd)).sum(-1)                       # (H, BG): d/dS'
         dp = (dp + dS.view(H, B, G).permute(1, 0, 2).reshape(B, HG, 1)) * z.reshape(B, HG, Lp)
     ds = p * (dp - (p * dp).sum(-1, keepdim=True))
-    dh = torch.bmm(pd.transpose(1, 2), dw).add_(torch.bmm(ds.transpose(1, 2), u))  # (B, Lp, D)
-    du = torch.bmm(ds, hf)                                                   # (B, HG, D)
-    duH = du.view(B, H, G, D).transpose(0, 1).reshape(H, B * G, D)
+    if GLOBAL_BWD_MERGED:
+        pds = torch.cat((pd, ds), 1)                                         # (B, 2HG, Lp)
+        wdu = torch.bmm(pds, hf)                                             # (B, 2HG, D)
+        w, du = wdu[:, :HG], wdu[:, HG:]
+        dh = torch.bmm(pds.transpose(1, 2), torch.cat((dw, u), 1))           # (B, Lp, D)
+    else:
+        w = torch.bmm(pd, hf)                                                # (B, HG, D)
+        dh = torch.bmm(pd.transpose(1, 2), dw).add_(torch.bmm(ds.transpose(1, 2), u))  # (B, Lp, D)
+        du = torch.bmm(ds, hf)                                               # (B, HG, D)
+    wH = w.reshape(B, H, G, D).transpose(0, 1).reshape(H, B * G, D)          # (H, BG, D)
+    dwvg = torch.bmm(doH.transpose(1, 2), wH).reshape(D, D)                  # (H, hd, D)
+    duH = du.reshape(B, H, G, D).transpose(0, 1).reshape(H, B * G, D)
     dq = torch.bmm(duH, wk.transpose(1, 2)).transpose(0, 1).reshape(B * G, D)
     dwkg = torch.bmm(qH.transpose(1, 2), duH).reshape(D, D)
     dbkg = torch.zeros(D, dtype=torch.float32, device=h.device)

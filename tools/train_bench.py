@@ -32,7 +32,11 @@ def main():
     ap.add_argument("--blas-da", action="store_true", help="A/B: dA of the non-FFN Linears on hipBLASLt")
     ap.add_argument("--no-ffn-fused", action="store_true", help="A/B: FFN as two Linears + torch GELU")
     ap.add_argument("--no-fused-gelu", action="store_true", help="A/B: FFN1 GEMM then F.gelu")
+    ap.add_argument("--global-bwd-six", action="store_true", help="A/B: the global backward's six passes over h")
     a = ap.parse_args()
+    if a.global_bwd_six:
+        from recformer_amd import train
+        train.GLOBAL_BWD_MERGED = False
     if a.no_fused_gelu:
         from recformer_amd import train
         train.FUSED_GELU = False
