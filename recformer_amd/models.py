@@ -6,9 +6,9 @@ arguments, forward() keyword signatures and return types, and the same state-dic
 finetune.py / evaluate_seq.py / checkpoints load unchanged. The arithmetic runs in
 hand-written HIP kernels through ops.py; there is no PyTorch/CPU fallback.
 
-Compute dtype: bf16 when the parameters are bf16 or a CUDA autocast context with a
-16-bit dtype is active (fp16 autocast is computed in bf16: gfx950 kernels are bf16);
-fp32 otherwise (exact-fp32 MFMA GEMMs).
+Compute dtype: the autocast dtype under a CUDA autocast context (fp16 — torch.cuda.amp's
+default, the reference drivers' mode — or bf16), else the parameters' 16-bit type, else fp32
+(exact-fp32 MFMA GEMMs); see _compute_dtype.
 """
 from __future__ import annotations
 
@@ -225,8 +225,11 @@ SHORT_SEQ = True
 FOLD_EARLY = True
 # with FOLD_EARLY: queue the fold's first stage on a side stream that starts once the qkv GEMM is
 # done, so its launch-bound projection and its pass over h run beside the HBM-bound band attention
-# (the band kernel leaves LDS free on every CU); the main stream joins before the fold's last stage
-FOLD_OVERLAP = True
+# (the band kernel leaves LDS free on every CU); the main stream joins before the fold's last stage.
+# Off: measured slower at C2 (same-process A/B, tools/ab_step.py FOLD_OVERLAP: 13.44 vs 13.20 ms per
+# step) — the partial kernel's ~100 KiB-LDS blocks displace band-attention blocks instead of filling
+# idle CUs, and the fold's pass over h no longer hits the cache the LayerNorm left it in
+FOLD_OVERLAP = False
 _SIDE_STREAMS = {}
 
 

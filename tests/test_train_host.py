@@ -6,14 +6,17 @@ import torch
 from recformer_amd import train
 
 
+@pytest.mark.parametrize("merged", [True, False])
 @pytest.mark.parametrize("drop", [False, True])
 @pytest.mark.parametrize("B,Lp,H,G", [(2, 64, 2, 1), (3, 128, 3, 2), (1, 192, 12, 3)])
-def test_global_bwd_closed_form_matches_autograd(B, Lp, H, G, drop):
+def test_global_bwd_closed_form_matches_autograd(B, Lp, H, G, drop, merged, monkeypatch):
     """train._global_bwd (closed-form gradient of the global rows' fold algebra, TF:964-1057)
     against autograd through train._global_torch on the same inputs: ragged valid lengths,
     several global slots, one empty slot (zero query row and zero output gradient); with
     attention-probability dropout (TF:1036-1037: the dropped probabilities also scale the value
-    bias) through the kernels' hash mask."""
+    bias) through the kernels' hash mask. merged: the products over h as three batched GEMMs
+    (train.GLOBAL_BWD_MERGED) or six."""
+    monkeypatch.setattr(train, "GLOBAL_BWD_MERGED", merged)
     g = torch.Generator().manual_seed(B * 100 + Lp + H + G)
     D = 64 * H
     qg = torch.randn(B * G, D, generator=g, dtype=torch.float64)
