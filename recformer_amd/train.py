@@ -45,6 +45,8 @@ __all__ = ["encode_train"]
 GLOBAL_BWD_CLOSED_FORM = True
 # the closed form with its products over h merged into three batched GEMMs (False: six)
 GLOBAL_BWD_MERGED = True
+# bf16 training: the global branch's dh straight from a bf16-operand product (no fp32 (B*Lp, D) pass)
+GLOBAL_BWD_DH16 = True
 # weight gradients of the layer GEMMs as a split-K batched GEMM (_weight_grad)
 DW_SPLIT_K = True
 # bf16: FFN1 + GELU as one GEMM that also writes the pre-activation (_GemmGelu). Off: measured
@@ -395,12 +397,14 @@ def _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B: int, Lp: int, H: int, z=N
     return og.reshape(B * gmax, D)
 
 
-def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout, z=None, bvg=None):
+def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout, z=None, bvg=None, dh_dtype=None):
     """Closed-form gradient of _global_torch (the fold algebra, TF:964-1057) for the output
     gradient gout (B*gmax, D) — batched matmuls instead of autograd over einsums (a third of the
     ops, no nested graph). Returns fp32 (dqg, dh, dwkg, dbkg, dwvg, dbvg); dbkg is exactly zero:
     the key bias adds q.bkg to every score of a row, which the softmax cancels. z (B, H, gmax, Lp):
-    the forward's attention-dropout scale (then bvg, the value bias, is needed too)."""
+    the forward's attention-dropout scale (then bvg, the value bias, is needed too). dh_dtype =
+    torch.bfloat16: dh (the (B*Lp, D) output, rounded to bf16 by the caller anyway) is produced by a
+    bf16-operand product with fp32 accumulation instead of an fp32 product and a cast (merged form)."""
     D = h.shape[1]
     hd = D // H
     G = qg.shape[0] // B
@@ -438,7 +442,11 @@ def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout, z=None, b
         pds = torch.cat((pd, ds), 1)                                         # (B, 2HG, Lp)
         wdu = torch.bmm(pds, hf)                                             # (B, 2HG, D)
         w, du = wdu[:, :HG], wdu[:, HG:]
-        dh = torch.bmm(pds.transpose(1, 2), torch.cat((dw, u), 1))           # (B, Lp, D)
+        dwu = torch.cat((dw, u), 1)                                          # (B, 2HG, D)
+        if dh_dtype == torch.bfloat16:
+            dh = torch.bmm(pds.transpose(1, 2).to(dh_dtype), dwu.to(dh_dtype))  # (B, Lp, D) bf16
+        else:
+            dh = torch.bmm(pds.transpose(1, 2), dwu)                         # (B, Lp, D)
     else:
         w = torch.bmm(pd, hf)                                                # (B, HG, D)
         dh = torch.bmm(pd.transpose(1, 2), dw).add_(torch.bmm(ds.transpose(1, 2), u))  # (B, Lp, D)
@@ -573,7 +581,8 @@ class _Attention(torch.autograd.Function):
                 gout = dout[rows].float() * keep[:, None].to(torch.float32)
                 if GLOBAL_BWD_CLOSED_FORM:
                     with torch.autocast("cuda", enabled=False):
-                        grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, ctx.gz, bvg)
+                        grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, ctx.gz, bvg,
+                                            dh_dtype=h.dtype if GLOBAL_BWD_DH16 else None)
                 else:
                     gin = [t.detach().requires_grad_(True) for t in (qg, h, wkg, bkg, wvg, bvg)]
                     with torch.enable_grad(), torch.autocast("cuda", enabled=False):

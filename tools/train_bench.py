@@ -33,7 +33,13 @@ def main():
     ap.add_argument("--no-ffn-fused", action="store_true", help="A/B: FFN as two Linears + torch GELU")
     ap.add_argument("--no-fused-gelu", action="store_true", help="A/B: FFN1 GEMM then F.gelu")
     ap.add_argument("--global-bwd-six", action="store_true", help="A/B: the global backward's six passes over h")
+    ap.add_argument("--ab", default=None, help="A/B in one process: alternate blocks of steps with the "
+                    "train.py switch of this name True / False and print both medians")
+    ap.add_argument("--global-dh-f32", action="store_true", help="A/B: the global branch's dh as an fp32 product")
     a = ap.parse_args()
+    if a.global_dh_f32:
+        from recformer_amd import train
+        train.GLOBAL_BWD_DH16 = False
     if a.global_bwd_six:
         from recformer_amd import train
         train.GLOBAL_BWD_MERGED = False
@@ -79,6 +85,24 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    if a.ab:
+        # clocks differ across boxes and drift under load: alternate blocks in one process
+        from recformer_amd import train
+        res = {True: [], False: []}
+        for rep in range(6):
+            for val in (True, False):
+                setattr(train, a.ab, val)
+                step()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(a.steps):
+                    step()
+                torch.cuda.synchronize()
+                res[val].append((time.perf_counter() - t0) / a.steps * 1e3)
+        for val in (True, False):
+            v = sorted(res[val])
+            print(f"{a.ab}={val}: ms/step median {v[len(v) // 2]:.2f} min {v[0]:.2f} all {[round(x, 2) for x in res[val]]}")
+        return
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
