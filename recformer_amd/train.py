@@ -47,6 +47,8 @@ GLOBAL_BWD_CLOSED_FORM = True
 GLOBAL_BWD_MERGED = True
 # bf16 training: the global branch's dh straight from a bf16-operand product (no fp32 (B*Lp, D) pass)
 GLOBAL_BWD_DH16 = True
+# the global-key / -value row gradients as one block-diagonal batched product per sequence (no copy)
+GLOBAL_KV_BLOCKDIAG = True
 # weight gradients of the layer GEMMs as a split-K batched GEMM (_weight_grad)
 DW_SPLIT_K = True
 # bf16: FFN1 + GELU as one GEMM that also writes the pre-activation (_GemmGelu). Off: measured
@@ -460,6 +462,24 @@ def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout, z=None, b
     return dq, dh.view(B * Lp, D), dwkg, dbkg, dwvg, dbvg
 
 
+def _global_kv_grad(w, x, B: int, Lp: int, H: int):
+    """Gradient of the global-key (or -value) rows, sum_i w[b,h,i,g] * x[b,i,h,:] -> (B*G, D) in x's
+    dtype (bf16 operands, fp32 accumulation). w: (B, H, Lp, G) per-query score (or probability)
+    gradients of the global keys; x: (B*Lp, D) rows, e.g. the q column slice of the fused qkv.
+    With GLOBAL_KV_BLOCKDIAG: one batched product per sequence against x's rows in place (no
+    (b, h, i, d) copy of x; x may be a strided column slice): (H*G, Lp).(Lp, D) yields every head
+    pair, the diagonal head blocks are kept (12x the flops of the einsum, which are tiny, for no
+    pass over x besides the product's own read)."""
+    G = w.shape[-1]
+    D = x.shape[1]
+    if not GLOBAL_KV_BLOCKDIAG:
+        return torch.einsum("bhig,bihd->bghd", w.to(x.dtype), x.reshape(B, Lp, H, D // H)).reshape(B * G, D)
+    wt = w.permute(0, 1, 3, 2).reshape(B, H * G, Lp).to(x.dtype)
+    full = torch.bmm(wt, x.reshape(B, Lp, D))                                # (B, H*G, H*hd)
+    blk = full.view(B, H, G, H, D // H).diagonal(dim1=1, dim2=3)             # (B, G, hd, H)
+    return blk.permute(0, 1, 3, 2).reshape(B * G, D)
+
+
 def _global_rows(gidx, B: int, Lp: int):
     rows = (torch.arange(B, device=gidx.device)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
     return rows, (gidx >= 0).reshape(-1)
@@ -569,10 +589,8 @@ class _Attention(torch.autograd.Function):
                 rows32 = torch.where(keep, rows, -1).to(torch.int32)  # -1: empty slot, skipped
             # gradients of the global-key columns, reduced over every query of the sequence
             # bf16 operands, fp32 accumulation (no fp32 copies of the (B*Lp, D) q and dout)
-            qh = q.reshape(B, Lp, H, 64)
-            dh = d16.view(B, Lp, H, 64)
-            dkg = torch.einsum("bhig,bihd->bghd", gds[..., :gmax].to(q.dtype), qh).reshape(B * gmax, D)
-            dvg = torch.einsum("bhig,bihd->bghd", gpr[..., :gmax].to(q.dtype), dh).reshape(B * gmax, D)
+            dkg = _global_kv_grad(gds[..., :gmax], q, B, Lp, H)
+            dvg = _global_kv_grad(gpr[..., :gmax], d16, B, Lp, H)
             # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
             # added into dk / dv at the global positions (bf16, as dqkv) by one small kernel
             ops.scatter_add_rows(rows32, dkg.to(dk.dtype).contiguous(), dk, dvg.to(dv.dtype).contiguous(), dv)

@@ -124,3 +124,25 @@ def test_global_bwd_bf16_dh_close_to_fp32():
     assert err < 1e-2, float(err)  # measured 4.6e-3; bf16 rounding alone 2.2e-3
     for n in (0, 2, 4, 5):
         assert torch.equal(got[n], ref[n])
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_global_kv_grad_blockdiag_matches_einsum(G, monkeypatch):
+    """train._global_kv_grad: the block-diagonal batched product (no copy of the strided q slice)
+    equals the einsum form on the same bf16 operands (fp32 accumulation both ways)."""
+    g = torch.Generator().manual_seed(G)
+    B, Lp, H = 2, 96, 3
+    D = 64 * H
+    qkv = torch.randn(B * Lp, 3 * D, generator=g).to(torch.bfloat16)
+    q = qkv[:, :D]  # strided column slice, as in _Attention.backward
+    w = torch.randn(B, H, Lp, G, generator=g) * 0.1
+    monkeypatch.setattr(train, "GLOBAL_KV_BLOCKDIAG", False)
+    ref = train._global_kv_grad(w, q, B, Lp, H).float()
+    monkeypatch.setattr(train, "GLOBAL_KV_BLOCKDIAG", True)
+    got = train._global_kv_grad(w, q, B, Lp, H)
+    assert got.shape == (B * G, D) and got.dtype == torch.bfloat16
+    exact = (w.double().permute(0, 3, 1, 2).unsqueeze(-1) *
+             q.double().view(B, Lp, H, 64).permute(0, 2, 1, 3).unsqueeze(1)).sum(3).reshape(B * G, D)
+    scale = float(exact.abs().max())
+    assert float((got.double() - exact).abs().max()) <= 1e-2 * scale
+    assert float((got.float() - ref).abs().max()) <= 1e-2 * scale
