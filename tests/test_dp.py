@@ -16,6 +16,35 @@ import torch.multiprocessing as mp
 from recformer_amd import dp
 
 
+class _Arr:
+    """A tensor sent through a multiprocessing queue by value (numpy), not as a shared-memory
+    handle: torch's handle is only valid while the sending worker lives, and a worker that has
+    already exited makes the parent's unpickle fail with ConnectionResetError."""
+
+    def __init__(self, t):
+        self.a = t.detach().cpu().numpy()
+
+
+def _plain(x):
+    if torch.is_tensor(x):
+        return _Arr(x)
+    if isinstance(x, (list, tuple)):
+        return type(x)(_plain(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _plain(v) for k, v in x.items()}
+    return x
+
+
+def _unplain(x):
+    if isinstance(x, _Arr):
+        return torch.from_numpy(x.a)
+    if isinstance(x, (list, tuple)):
+        return type(x)(_unplain(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _unplain(v) for k, v in x.items()}
+    return x
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -64,7 +93,7 @@ def _worker(rank, ws, port, B, out_q):
         gathered = dp.gather_rows(local, B)
         t = dp.max_over_ranks(float(rank + 1))
         if rank == 0:
-            out_q.put((gathered, t))
+            out_q.put(_plain((gathered, t)))
     finally:
         dist.destroy_process_group()
 
@@ -78,7 +107,7 @@ def test_dp_gloo_world2_matches_single_process(B):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, B, q)) for r in range(2)]
     for p in procs:
         p.start()
-    gathered, tmax = q.get(timeout=300)
+    gathered, tmax = _unplain(q.get(timeout=300))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -102,7 +131,7 @@ def _grad_worker(rank, ws, port, out_q):
         loss.backward()
         n = dp.allreduce_grads(list(net.parameters()), bucket_bytes=1024)
         if rank == 0:
-            out_q.put(([p.grad.clone() for p in net.parameters()], n))
+            out_q.put(_plain(([p.grad.clone() for p in net.parameters()], n)))
     finally:
         dist.destroy_process_group()
 
@@ -115,7 +144,7 @@ def test_allreduce_grads_matches_full_batch():
     procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    grads, n = q.get(timeout=300)
+    grads, n = _unplain(q.get(timeout=300))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -137,9 +166,9 @@ def _pretrain_worker(rank, ws, port, out_q, bucketed):
     try:
         out = _pretrain_step(rank, ws, bucketed)
         if rank == 0:
-            out_q.put(out)
+            out_q.put(_plain(out))
         else:
-            out_q.put(None)
+            out_q.put(_plain(None))
     finally:
         dist.destroy_process_group()
 
@@ -179,7 +208,7 @@ def test_pretrain_contrastive_dp_world2_matches_single_process(bucketed):
     procs = [ctx.Process(target=_pretrain_worker, args=(r, 2, port, q, bucketed)) for r in range(2)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=300) for _ in range(2)]
+    got = [_unplain(q.get(timeout=300)) for _ in range(2)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -202,7 +231,7 @@ def _combine_worker(rank, ws, port, out_q):
         from recformer_amd.ranker import combine_shards
         parts = _shard_parts(rank, ws)
         out = combine_shards(parts, 5)
-        out_q.put((rank, {k: (v.clone() if torch.is_tensor(v) else v) for k, v in out.items()}))
+        out_q.put(_plain((rank, {k: (v.clone() if torch.is_tensor(v) else v) for k, v in out.items()})))
     finally:
         dist.destroy_process_group()
 
@@ -237,7 +266,7 @@ def test_retrieval_combine_world2_matches_one_shard():
     procs = [ctx.Process(target=_combine_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=300) for _ in range(2))
+    got = dict(_unplain(q.get(timeout=300)) for _ in range(2))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
