@@ -67,6 +67,15 @@ def gemm_flops_per_seq(L, d, ffn, layers, gmax=1, fold=True):
     return per_layer * layers
 
 
+def e2e_floor_us(L, d, ffn, layers, catalog, w=64, gmax=1):
+    """SURVEY §8d end-to-end MFMA bound per sequence: the GEMMs (folded global projections), the
+    exact band attention (4*d*sum|keys_i| + 4*G*L*d per layer, |keys_i| = w + 1 + G) and the
+    catalog scoring (2*N*d), at 2.5 PF dense bf16."""
+    attn = layers * (4 * d * L * (w + 1 + gmax) + 4 * gmax * L * d)
+    flops = gemm_flops_per_seq(L, d, ffn, layers, gmax) + attn + 2 * catalog * d
+    return flops / (BF16_PEAK_TFLOPS * 1e12) * 1e6
+
+
 def committed_profile(B, L, layers):
     """Per-kernel-tag rows of the newest committed rocprofv3 summary of this exact workload
     (profiles/r*/bench_pmc_summary.json, tools/profile_bench.sh: kernel-trace durations, HBM bytes
@@ -355,6 +364,12 @@ def main():
             "roofline": roofline,
             "attention_roofline": attn_roof,
             "model_tflops": round(value / world * flops_seq / 1e12, 1),
+            # end to end against the MFMA bound of the algorithm (GEMMs + exact band
+            # attention + scoring = 176.5 GFLOP/seq at C2 -> 70.6 us/seq at 2.5 PF dense bf16)
+            "e2e_roofline": {"bound": "mfma", "us_per_seq_floor": round(e2e_floor_us(L, d, ffn, args.layers,
+                                                                                      args.catalog), 2),
+                             "frac": round(value / world * e2e_floor_us(L, d, ffn, args.layers, args.catalog) * 1e-6, 4),
+                             "note": "per-GPU seq/s x the MFMA-bound us per sequence"},
             "kernels": kernels,
             "kernels_pass": ({"steps": inst_steps, "ms_per_step": round(1e3 * inst_s / inst_steps, 3),
                               "note": "separate HIP-event-instrumented steps after the timed ones"}

@@ -678,7 +678,6 @@ __device__ __forceinline__ void load_cols(const EpiArgs& e, int c0, float* bv, f
   }
 }
 
-constexpr int CV_OFF = 8 * PP_HALF + 1024;  // LDS: ring, stamp area, then 2 x 3 column vectors
 
 template <int EPI, int NV>
 __device__ __forceinline__ void lds_cols(const float* cb, int co, float* bv, float* gm, float* bt) {
@@ -698,6 +697,9 @@ __device__ __forceinline__ void lds_cols(const float* cb, int co, float* bv, flo
     }
   }
 }
+
+#if defined(RF_GEMM_EXPERIMENTS)  // retired main loop (tools/build_variant.sh builds only)
+constexpr int CV_OFF = 8 * PP_HALF + 1024;  // LDS: ring, stamp area, then 2 x 3 column vectors
 
 // s_waitcnt vmcnt(n) for a wave-uniform n from the small set the ping-pong kernel uses
 template <int S>
@@ -1005,6 +1007,8 @@ __global__ void __launch_bounds__(512, 1)
   }
 }
 
+#endif  // RF_GEMM_EXPERIMENTS
+
 static int num_cus() {
   static int n[16] = {0};
   int dev = 0;
@@ -1018,6 +1022,7 @@ static int num_cus() {
   return n[dev];
 }
 
+#if defined(RF_GEMM_EXPERIMENTS)  // retired main loop (tools/build_variant.sh builds only)
 template <typename E, int EPI, bool CF32, bool RF32>
 static void launch_pp(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
                       hipStream_t s) {
@@ -1032,6 +1037,8 @@ static void launch_pp(int M, int N, int K, const void* A, int lda, const void* W
   const int grid = min(nTm * nTn, num_cus());
   k_gemm_pp<E, EPI, CF32, RF32><<<grid, 512, lds, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
 }
+
+#endif  // RF_GEMM_EXPERIMENTS
 
 // ---- 4-wave 256x256 GEMM: one wave per SIMD, 128x128 accumulator block per wave ----------------
 // The alternative main loop to the ping-pong (knob gemm_variant 6): 4 waves (2 x 2), each owning a
@@ -1346,6 +1353,7 @@ static void launch_w4(int M, int N, int K, const void* A, int lda, const void* W
   k_gemm_w4<E, EPI, CF32, RF32, IL><<<grid, 256, W4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
 }
 
+#if defined(RF_GEMM_EXPERIMENTS)  // retired main loop (tools/build_variant.sh builds only)
 // ---- 4-wave 256x256 GEMM on a 4-deep BK = 32 ring (knob gemm_variant 7) ----------------------------
 // As k_gemm_w4 (one wave per SIMD, 128 x 128 accumulators per wave), but the K loop walks 32-wide
 // K-tiles through a 4-slot LDS ring: iteration g runs the 64 MFMAs of K-tile g from one register set
@@ -1585,6 +1593,8 @@ static void launch_w4r(int M, int N, int K, const void* A, int lda, const void* 
   k_gemm_w4r<E, EPI, CF32, RF32><<<grid, 256, R4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
 }
 
+#endif  // RF_GEMM_EXPERIMENTS
+
 template <typename E, int BM, int BN, int WM, int WN, int BK, int NSTAGE, int EPI, bool CF32, bool RF32>
 static void launch_bf16(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                         const EpiArgs& e, hipStream_t s) {
@@ -1613,7 +1623,9 @@ static unsigned long long* g_stamps = nullptr;  // set by rf_debug_gemm_stamps (
 // column groups of 6 tiles: qkv -2.7%, FFN1/FFN2 -1% vs 4 (tools/gemm_gn.py); full width loses on FFN1
 static int gemm_gn() { return g_knob[KNOB_GEMM_GN]; }
 
+#if defined(RF_GEMM_EXPERIMENTS)
 static int gemm_variant() { return g_knob[KNOB_GEMM_VARIANT]; }
+#endif
 
 
 // The ping-pong kernel DMAs its epilogue column vectors (and EPI_COS row norms) as 16-B
@@ -1629,42 +1641,24 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
                           const EpiArgs& e, hipStream_t s) {
   // 256x256 when the grid still covers the chip; 128x128 for skinny problems
   const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const bool w4_ok = pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
+                     (int64_t)N * ldw * 2 < 0x7FFFFFFF;
   if (tiles256 >= 128) {
+#if defined(RF_GEMM_EXPERIMENTS)
+    // retired main loops, compiled only into tools/build_variant.sh builds (A/B of the knob)
     switch (gemm_variant()) {
-      case 1: launch_bf16<E, 256, 256, 128, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
-      case 2: launch_bf16<E, 256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
-      case 3: launch_bf16<E, 128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
-      case 4: launch_bf16<E, 256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
-      case 8:
-        if (pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
-            (int64_t)N * ldw * 2 < 0x7FFFFFFF) {
-          launch_w4<E, EPI, CF32, RF32, true>(M, N, K, A, lda, W, ldw, e, s);
-          break;
-        }
-        [[fallthrough]];
-      case 7:
-        if (pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
-            (int64_t)N * ldw * 2 < 0x7FFFFFFF) {
-          launch_w4r<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
-          break;
-        }
-        [[fallthrough]];
-      case 6:
-        if (pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&
-            (int64_t)N * ldw * 2 < 0x7FFFFFFF) {
-          launch_w4<E, EPI, CF32, RF32, false>(M, N, K, A, lda, W, ldw, e, s);
-          break;
-        }
-        [[fallthrough]];
-      case 5:
-        if (pp_cols_ok(M, N, e)) {
-          launch_pp<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
-          break;
-        }
-        launch_bf16<E, 256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
-        break;
-      default: launch_bf16<E, 256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); break;
+      case 1: launch_bf16<E, 256, 256, 128, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); return;
+      case 2: launch_bf16<E, 256, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); return;
+      case 3: launch_bf16<E, 128, 128, 64, 64, 32, 3, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); return;
+      case 4: launch_bf16<E, 256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); return;
+      case 7: if (w4_ok) { launch_w4r<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); return; } break;
+      case 6: if (w4_ok) { launch_w4<E, EPI, CF32, RF32, false>(M, N, K, A, lda, W, ldw, e, s); return; } break;
+      case 5: if (pp_cols_ok(M, N, e)) { launch_pp<E, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s); return; } break;
+      default: break;
     }
+#endif
+    if (w4_ok) launch_w4<E, EPI, CF32, RF32, true>(M, N, K, A, lda, W, ldw, e, s);
+    else launch_bf16<E, 256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
   } else {
     launch_bf16<E, 128, 128, 64, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
   }

@@ -12,6 +12,7 @@ Works with any torch.distributed backend: `nccl` (RCCL over xGMI) on MI355X, `gl
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Dict, Tuple
 
 import torch
@@ -117,14 +118,29 @@ class GradBucketer:
 
     Parameters are grouped, in reverse registration order (the order backward produces their
     gradients), into buckets of <= bucket_bytes per (dtype, device). A post-accumulate-grad hook
-    counts each bucket's ready gradients; when the last one lands, the bucket is flattened and its
-    all-reduce is launched asynchronously, so communication of late layers overlaps the backward of
-    early ones. `finish()` waits for every bucket, divides by the world size (average: the mean of
-    the ranks' gradients, as DistributedDataParallel) and copies back into each .grad. Parameters
-    that received no gradient in a step are reduced as zeros, so every rank issues the same
-    collectives in the same order. With one rank it does nothing.
+    counts each bucket's ready gradients; once a bucket is complete AND every lower-numbered bucket
+    has been launched, it is flattened and its all-reduce launched asynchronously, so communication
+    of late layers overlaps the backward of early ones. Launches are strictly in bucket order on
+    every rank — a bucket whose parameters got no gradient on one rank (e.g. the global-attention
+    projections of a batch without global tokens) holds the later buckets back until `finish()`
+    instead of letting ranks pair different buckets in the collective. `finish()` launches what is
+    left, waits, divides by the world size (average: the mean of the ranks' gradients, as
+    DistributedDataParallel) and copies back into each .grad; parameters without a gradient are
+    reduced as zeros. With one rank it does nothing.
 
-        b = GradBucketer(model.parameters()); loss.backward(); b.finish(); opt.step()
+    Gradient accumulation (the reference accumulates 8 micro-batches per optimizer step under DDP,
+    finetune.py:112-126, lightning_pretrain.py:137): run the first k-1 backward passes inside
+    `no_sync()` (the hooks then do nothing and .grad accumulates locally), the last one outside, then
+    `finish()` — one collective per bucket per optimizer step, as DDP's no_sync:
+
+        b = GradBucketer(model.parameters())
+        for i, batch in enumerate(micro_batches):
+            with b.no_sync() if i < len(micro_batches) - 1 else contextlib.nullcontext():
+                model(**batch).backward()
+        b.finish(); opt.step()
+
+    A second backward outside `no_sync()` before `finish()` (its buckets may already be reduced)
+    raises instead of silently dropping that micro-batch.
     """
 
     def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, group=None):
@@ -134,6 +150,8 @@ class GradBucketer:
         self.params = [p for p in params if p.requires_grad]
         self.buckets = []
         self._handles = []
+        self._sync = True
+        self.collectives = 0  # collectives issued over the bucketer's lifetime (tests, logging)
         if self.ws == 1:
             return
         by = {}
@@ -155,31 +173,53 @@ class GradBucketer:
             for p in ps:
                 self._of[id(p)] = bi
                 p.register_post_accumulate_grad_hook(self._hook)
+        self._reset()
+
+    def _reset(self):
         self._ready = [0] * len(self.buckets)
         self._flat = [None] * len(self.buckets)
+        self._next = 0  # lowest bucket not yet launched
+        self._seen = set()  # parameters whose gradient arrived in this window's synced backward
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes inside accumulate into .grad with no collective (DDP.no_sync)."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
 
     def _hook(self, p):
+        if not self._sync:
+            return
         bi = self._of[id(p)]
+        if id(p) in self._seen:
+            raise RuntimeError("GradBucketer: a second backward reached an already reduced bucket before finish(); "
+                               "run all but the last micro-batch of an accumulation window under no_sync()")
+        self._seen.add(id(p))
         self._ready[bi] += 1
-        if self._ready[bi] == len(self.buckets[bi]):
-            self._launch(bi)
+        while self._next < len(self.buckets) and self._ready[self._next] >= len(self.buckets[self._next]):
+            self._launch(self._next)
+            self._next += 1
 
     def _launch(self, bi):
         ps = self.buckets[bi]
         flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps])
         self._flat[bi] = flat
         self._handles.append((bi, dist.all_reduce(flat, group=self.group, async_op=True)))
+        self.collectives += 1
 
     def finish(self) -> int:
-        """Wait for the step's buckets (launching any whose gradients never all arrived), average,
-        write back; returns the number of collectives issued this step."""
+        """Wait for the window's buckets (launching, in bucket order, any not launched during
+        backward), average, write back; returns the number of collectives issued this window."""
         if self.ws == 1:
             return 0
-        for bi in range(len(self.buckets)):
-            if self._flat[bi] is None:
-                self._launch(bi)
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+            self._next += 1
         n = len(self._handles)
-        for bi, h in sorted(self._handles, key=lambda t: t[0]):
+        for bi, h in self._handles:
             h.wait()
             flat = self._flat[bi]
             if self.average:
@@ -193,6 +233,5 @@ class GradBucketer:
                     p.grad.copy_(g)
                 off += p.numel()
         self._handles = []
-        self._ready = [0] * len(self.buckets)
-        self._flat = [None] * len(self.buckets)
+        self._reset()
         return n

@@ -204,6 +204,17 @@ def _needs_grad(module: nn.Module) -> bool:
     return torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters())
 
 
+def _train_path(model: "RecformerModel") -> bool:
+    """The training encoder (train.encode_train) when gradients are needed, or when the model is in
+    train mode with a nonzero dropout: nn.Dropout applies in train mode whatever the grad mode (the
+    reference's model.train() under torch.no_grad() still drops), so the no-grad inference path,
+    which has no dropout, is taken only in eval mode or with zero dropout probabilities."""
+    if _needs_grad(model):
+        return True
+    cfg = model.config
+    return model.training and (cfg.hidden_dropout_prob > 0 or cfg.attention_probs_dropout_prob > 0)
+
+
 def _cos_train(z: torch.Tensor, items: torch.Tensor, temp: float) -> torch.Tensor:
     """Differentiable Similarity (models.py:358-369): cos(z_b, items_n) / temp in fp32 (autocast
     computes cosine_similarity in fp32), as normalise + matmul instead of the (B,N,d) broadcast."""
@@ -400,7 +411,7 @@ class RecformerModel(nn.Module):
             raise NotImplementedError("recformer_amd: head_mask is not supported (callers pass None)")
         if output_attentions:
             raise NotImplementedError("recformer_amd: output_attentions is not supported on the HIP path")
-        if _needs_grad(self):
+        if _train_path(self):
             # autograd path (recformer_amd/train.py): same kernels, explicit backward
             from .train import encode_train
             last, hidden_all = encode_train(self, input_ids, attention_mask, global_attention_mask,
@@ -726,7 +737,9 @@ class RecformerForPretraining(nn.Module):
                                  item_position_ids_b) if mlm_input_ids_b is not None else None)
 
         z1, z2 = outputs_a.pooler_output, outputs_b.pooler_output
-        if _needs_grad(self):
+        if _needs_grad(self) or self.training:
+            # train mode (with or without gradients, like the reference's modules): the z all-gather
+            # across ranks and the differentiable heads
             return self._train_losses(z1, z2, outputs_a, mlm_outputs_a, mlm_labels_a, mlm_outputs_b,
                                       mlm_labels_b, batch_size)
         dt = _compute_dtype(self.longformer.dtype)

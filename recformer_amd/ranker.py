@@ -73,6 +73,17 @@ def _metrics(gt: torch.Tensor, valid: torch.Tensor, loss: float, metrics_ks: Seq
 # ---- C5 retrieval: catalog shards, fused score + rank + top-k (rf_retrieval.hip) -----------------
 TOPK_SAMPLE = 2048  # dense seed block that sets each row's first candidate threshold
 TOPK_CAP = 1024     # candidate list per row and chunk
+TOPK_MAX_K = 256    # rf_topk_* limits (rf_retrieval.hip TK_KMAX, TK_DENSE_MAX)
+TOPK_MAX_SAMPLE = 2048
+
+
+def _check_topk_args(k: int, sample: int, cap: int) -> None:
+    if not 0 <= k <= TOPK_MAX_K:
+        raise ValueError(f"top-k: k={k} must be in [0, {TOPK_MAX_K}]")
+    if k > 0 and not k <= sample <= TOPK_MAX_SAMPLE:
+        raise ValueError(f"top-k: sample={sample} must be in [k={k}, {TOPK_MAX_SAMPLE}]")
+    if k > 0 and cap < 1:
+        raise ValueError(f"top-k: cap={cap} must be positive")
 
 
 class CatalogShard:
@@ -166,6 +177,7 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     #{s > s_label}, #{s > -max_val} and sum exp(s - 1/temp) over the shard, and (k > 0) the shard's
     top-k (scores descending, ties by lower item id; global ids). The scores are produced tile by
     tile and consumed in the kernel's epilogue; only a (B, sample) seed block is ever written."""
+    _check_topk_args(k, sample, cap)
     q = _check_q(queries, shard)
     qn = ops.row_inv_norm(q) if q_rnorm is None else q_rnorm
     lib = _lib.load()
@@ -266,6 +278,7 @@ def retrieve(queries: torch.Tensor, shard: CatalogShard, labels: torch.Tensor, m
     (utils.py:76-108) without the (B, N) score matrix, plus the top-k items per query over the whole
     catalog. Returns (metrics list, top-k scores (B, k), top-k item ids (B, k))."""
     import torch.distributed as dist
+    _check_topk_args(k, TOPK_SAMPLE, TOPK_CAP)
     q = _check_q(queries, shard)
     qn = ops.row_inv_norm(q)
     sl = label_scores(q, shard, labels, temp, qn)
@@ -279,17 +292,61 @@ def retrieve(queries: torch.Tensor, shard: CatalogShard, labels: torch.Tensor, m
 def rank_catalog(queries: torch.Tensor, items: torch.Tensor, labels: torch.Tensor, metrics_ks: Sequence[int],
                  temp: float, block: int = 65536, items_rnorm: Optional[torch.Tensor] = None) -> List[float]:
     """Ranker(metrics_ks)(Similarity(queries, items) / temp, labels) without the (B, N) score matrix
-    (finetune.py:70-92 over a whole catalog): one fused score + rank kernel pass
-    (rf_score_rank, counts only) after the label scores (rf_label_scores, bit-identical to the
-    kernel's own value for that column, so the strict ranks match the full-matrix Ranker). `block`
-    is accepted for compatibility (the kernel tiles the catalog itself). Returns the Ranker's list
-    [NDCG@k, HR@k ..., MRR, AUC, loss]."""
+    (finetune.py:70-92 over a whole catalog). Returns the Ranker's list
+    [NDCG@k, HR@k ..., MRR, AUC, loss].
+
+    bf16 / fp16 queries and items of one dtype: one fused score + rank kernel pass (rf_score_rank,
+    counts only) after the label scores (rf_label_scores, bit-identical to the kernel's own value
+    for that column, so the strict ranks match the full-matrix Ranker); the kernel tiles the
+    catalog itself. fp32 (or mixed-dtype, computed in fp32) inputs: the exact-fp32 EPI_COS GEMM over
+    column blocks of `block` items, the label scores taken from the same blocks, the counts and the
+    exp-sum of the cross entropy accumulated per block by rf_rank_accum."""
     if not (queries.is_cuda and items.is_cuda):
         raise _lib.RecformerHipError("rank_catalog needs ROCm device tensors (no CPU fallback)")
-    shard = CatalogShard(items, 0, items_rnorm)
-    q = _check_q(queries, shard)
+    if queries.dtype == items.dtype and queries.dtype in (torch.bfloat16, torch.float16):
+        shard = CatalogShard(items, 0, items_rnorm)
+        q = _check_q(queries, shard)
+        qn = ops.row_inv_norm(q)
+        sl = label_scores(q, shard, labels, temp, qn)
+        parts = shard_rank(q, shard, sl, temp, 0, qn)
+        loss = float((torch.log(parts["sexp"]) + parts["shift"] - sl).mean())
+        return _metrics(parts["gt"], parts["valid"], loss, metrics_ks)
+    return _rank_catalog_blocks(queries.float().contiguous(), items.float().contiguous(), labels, metrics_ks, temp,
+                                max(int(block), 1), items_rnorm)
+
+
+def _rank_catalog_blocks(q: torch.Tensor, items: torch.Tensor, labels: torch.Tensor, metrics_ks: Sequence[int],
+                         temp: float, block: int, items_rnorm: Optional[torch.Tensor]) -> List[float]:
+    lib = _lib.load()
+    B, N = q.shape[0], items.shape[0]
+    dev = q.device
+    inv_t = 1.0 / temp
+    lab = labels.reshape(-1).to(torch.int64)
     qn = ops.row_inv_norm(q)
-    sl = label_scores(q, shard, labels, temp, qn)
-    parts = shard_rank(q, shard, sl, temp, 0, qn)
-    loss = float((torch.log(parts["sexp"]) + parts["shift"] - sl).mean())
-    return _metrics(parts["gt"], parts["valid"], loss, metrics_ks)
+    rn = ops.row_inv_norm(items) if items_rnorm is None else items_rnorm.float().contiguous()
+    blocks = [(c, min(block, N - c)) for c in range(0, N, block)]
+    rows = torch.arange(B, device=dev)
+
+    def scores(c, n):
+        return ops.cos_scores(q, items[c:c + n], inv_t, z_rnorm=qn, items_rnorm=rn[c:c + n])
+
+    # the label scores from the same blocks the counts see (strict ranks need the identical value)
+    sl = torch.zeros(B, dtype=torch.float32, device=dev)
+    cached = None
+    for c, n in blocks:
+        s = scores(c, n)
+        inb = (lab >= c) & (lab < c + n)
+        sl = torch.where(inb, s[rows, (lab - c).clamp(0, n - 1)], sl)
+        if len(blocks) == 1:
+            cached = s
+    gt = torch.zeros(B, dtype=torch.int32, device=dev)
+    valid = torch.zeros(B, dtype=torch.int32, device=dev)
+    sexp = torch.zeros(B, dtype=torch.float32, device=dev)
+    sl = sl.contiguous()
+    for c, n in blocks:
+        s = cached if cached is not None else scores(c, n)
+        _lib.check(lib.rf_rank_accum(B, n, s.data_ptr(), s.stride(0), sl.data_ptr(), float(MAX_VAL), float(inv_t),
+                                     gt.data_ptr(), valid.data_ptr(), sexp.data_ptr(), ops._stream(s)),
+                   "rf_rank_accum")
+    loss = float((torch.log(sexp) + inv_t - sl).mean())
+    return _metrics(gt, valid, loss, metrics_ks)

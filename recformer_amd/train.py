@@ -527,7 +527,9 @@ class _Attention(torch.autograd.Function):
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         G = gidx.shape[1]
         ctx.drop = (attn_p, seed) if attn_p > 0 else None
-        ctx.gz = None
+        # the global rows' dropout scale (B, H, G, Lp) fp32 is regenerated in the backward from the
+        # seed (ctx.gz_kind), not kept alive on ctx between forward and backward
+        ctx.gz_kind = None
         if ctx.drop is not None and q.dtype != torch.float32 and G > 32:
             # the band kernel's dropout form takes <= 32 global keys: recompute in fp32 (the
             # backward of this case is the fp32 recompute as well)
@@ -541,10 +543,10 @@ class _Attention(torch.autograd.Function):
                 # itself for the closed-form backward from one kernel (rf_attn_global_keep)
                 ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg,
                                           wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out, p_drop=attn_p, seed=seed)
-                ctx.gz = ops.attn_global_keep(gidx, B, Lp, H, attn_p, seed)
+                ctx.gz_kind = "hip"
             elif G > 0:
-                ctx.gz = _global_keep(gidx, B, Lp, H, attn_p, seed)
-                og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H, ctx.gz)
+                ctx.gz_kind = "torch"
+                og = _global_torch(qg, h, wkg, bkg, wvg, bvg, flags, B, Lp, H, _global_keep(gidx, B, Lp, H, attn_p, seed))
                 rows, keep = grows[:2] if grows is not None else _global_rows(gidx, B, Lp)
                 _put_global_rows(out, og, rows, keep, B, G)
         else:
@@ -597,14 +599,19 @@ class _Attention(torch.autograd.Function):
             # global branch: closed-form gradient of the fold algebra
             if any(ctx.needs_input_grad[1:7]):
                 gout = dout[rows].float() * keep[:, None].to(torch.float32)
+                gz = None
+                if ctx.gz_kind == "hip":  # the forward's mask, from the same kernel
+                    gz = ops.attn_global_keep(gidx, B, Lp, H, p_drop, seed)
+                elif ctx.gz_kind == "torch":
+                    gz = _global_keep(gidx, B, Lp, H, p_drop, seed)
                 if GLOBAL_BWD_CLOSED_FORM:
                     with torch.autocast("cuda", enabled=False):
-                        grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, ctx.gz, bvg,
+                        grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, gz, bvg,
                                             dh_dtype=h.dtype if GLOBAL_BWD_DH16 else None)
                 else:
                     gin = [t.detach().requires_grad_(True) for t in (qg, h, wkg, bkg, wvg, bvg)]
                     with torch.enable_grad(), torch.autocast("cuda", enabled=False):
-                        og = _global_torch(*gin, flags, B, Lp, H, ctx.gz)
+                        og = _global_torch(*gin, flags, B, Lp, H, gz)
                         grads = torch.autograd.grad(og, gin, gout, allow_unused=True)
                 for n, t in enumerate((qg, h, wkg, bkg, wvg, bvg)):
                     if ctx.needs_input_grad[1 + n]:

@@ -222,6 +222,85 @@ def test_pretrain_contrastive_dp_world2_matches_single_process(bucketed):
     assert n >= 2
 
 
+def _accum_net():
+    torch.manual_seed(0)
+    # a side branch used only by some micro-batches: its parameters get no gradient on a rank whose
+    # window never takes it (the data-dependent case of the global-attention projections)
+    return torch.nn.ModuleDict({"a": torch.nn.Linear(16, 32), "b": torch.nn.Linear(32, 4),
+                                "side": torch.nn.Linear(16, 32)})
+
+
+def _accum_loss(net, x, use_side):
+    h = torch.nn.functional.gelu(net["a"](x))
+    if use_side:
+        h = h + net["side"](x)
+    return net["b"](h).pow(2).mean()
+
+
+def _accum_data():
+    g = torch.Generator().manual_seed(5)
+    return torch.randn(3, 8, 16, generator=g)  # 3 micro-batches x 8 rows (4 per rank)
+
+
+def _accum_worker(rank, ws, port, out_q):
+    """Gradient accumulation over 3 micro-batches with GradBucketer.no_sync (finetune.py:112-126):
+    the side branch is taken only by rank 0's last micro-batch."""
+    import contextlib
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        net = _accum_net()
+        xs = _accum_data()
+        b = dp.GradBucketer(net.parameters(), bucket_bytes=2048)
+        nb = len(b.buckets)
+        for i in range(3):
+            x = xs[i, rank * 4:(rank + 1) * 4]
+            with b.no_sync() if i < 2 else contextlib.nullcontext():
+                (_accum_loss(net, x, use_side=(rank == 0 and i == 2)) / 3).backward()
+        n = b.finish()
+        during = b.collectives  # every collective of the window, the no_sync passes included
+        grads = [p.grad.clone() for p in net.parameters()]
+        # a second window that forgets no_sync must raise, not drop a micro-batch
+        raised = False
+        try:
+            for i in range(2):
+                _accum_loss(net, xs[i, rank * 4:(rank + 1) * 4], False).backward()
+        except RuntimeError:
+            raised = True
+        out_q.put(_plain((rank, grads if rank == 0 else None, n, nb, during, raised)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradbucketer_accumulation_world2():
+    """world-2 gloo, 3 micro-batches, one finish(): the averaged gradients equal one process
+    accumulating the whole 3 x 8 batch; exactly one collective per bucket per window (none during
+    the no_sync passes); a rank-dependent unused parameter does not reorder the collectives."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_accum_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (_unplain(q.get(timeout=300)) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    grads, n, nb, during, raised = got[0]
+    assert nb >= 3 and n == nb and got[1][1] == nb
+    assert during == nb and got[1][3] == nb
+    assert raised and got[1][4]
+    net = _accum_net()
+    xs = _accum_data()
+    for i in range(3):
+        # rank 0's rows take the side branch in the last micro-batch, rank 1's do not
+        l0 = _accum_loss(net, xs[i, :4], use_side=(i == 2))
+        l1 = _accum_loss(net, xs[i, 4:], use_side=False)
+        ((l0 + l1) / 2 / 3).backward()
+    for g, p in zip(grads, net.parameters()):
+        assert torch.allclose(g, p.grad, atol=1e-6, rtol=1e-5)
+
+
 def _combine_worker(rank, ws, port, out_q):
     """One rank's shard result for C5 retrieval (what rf_score_rank + rf_topk_* produce on the
     device): counts over its catalog shard and its top-k with global ids; combined over ranks."""

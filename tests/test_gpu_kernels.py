@@ -480,26 +480,49 @@ def test_ranker_matches_reference_fixture(dev, case):
     assert got[-1] == pytest.approx(ref[-1], rel=1e-5)
 
 
-@pytest.mark.parametrize("B,N,block", [(37, 1000, 1000), (37, 5003, 2048)])
-def test_rank_catalog_matches_restated_ranker(dev, B, N, block):
+@pytest.mark.parametrize("B,N,block,dts", [(37, 1000, 1000, "bf16"), (37, 5003, 2048, "bf16"),
+                                          (37, 5003, 2048, "fp32"), (37, 1000, 1000, "fp32"),
+                                          (37, 5003, 2048, "mixed")])
+def test_rank_catalog_matches_restated_ranker(dev, B, N, block, dts):
     """rank_catalog against utils.py:76-108 restated (oracle, pinned by tests/golden/ranker.npz)
     on the same fp32 cosine-score matrix: B not a multiple of 16, ragged column tails, every third
-    label in the last partial 16 columns of the catalog (or of a block), exact duplicate items."""
+    label in the last partial 16 columns of the catalog (or of a block), exact duplicate items.
+    fp32 (an fp32 model's pooler output and catalog) and mixed-dtype inputs take the exact-fp32
+    block path; its scores are the EPI_COS fp32 GEMM's, the same the reference matrix is made of."""
     from recformer_amd.ranker import rank_catalog
     g = torch.Generator(device=dev).manual_seed(B * N)
-    q = torch.randn(B, 768, device=dev, generator=g).to(torch.bfloat16)
-    items = torch.randn(N, 768, device=dev, generator=g).to(torch.bfloat16)
+    qdt = torch.bfloat16 if dts == "bf16" else torch.float32
+    idt = torch.float32 if dts == "fp32" else torch.bfloat16
+    q = torch.randn(B, 768, device=dev, generator=g).to(qdt)
+    items = torch.randn(N, 768, device=dev, generator=g).to(idt)
     labels = torch.randint(0, N, (B,), device=dev, generator=g)
     labels[::3] = N - 1 - torch.arange(len(labels[::3]), device=dev) % 8
     labels[1::3] = (block - 1 - torch.arange(len(labels[1::3]), device=dev) % 8) % N
     dup = labels[:8]
     items[(dup + N // 2) % N] = items[dup]
-    s = ops.cos_scores(q, items, 20.0).cpu()
+    if q.dtype != items.dtype:
+        s = ops.cos_scores(q.float(), items.float(), 20.0).cpu()
+    else:
+        s = ops.cos_scores(q, items, 20.0).cpu()
     ref = R.ranker_metrics(s, labels.cpu(), [1, 10, 50])
     got = rank_catalog(q, items, labels, [1, 10, 50], 0.05, block=block)
     for a, b in zip(got[:-1], ref[:-1]):
         assert a == pytest.approx(b, abs=1e-6), (got, ref)
     assert got[-1] == pytest.approx(ref[-1], rel=1e-4)
+
+
+def test_retrieval_topk_argument_checks(dev):
+    """k / sample outside the top-k kernels' limits fail with a clear ValueError (not a kernel error)."""
+    from recformer_amd.ranker import CatalogShard, retrieve, shard_rank
+    items = torch.randn(300, 64, device=dev).to(torch.float16)
+    q = torch.randn(4, 64, device=dev).to(torch.float16)
+    shard = CatalogShard(items)
+    sl = torch.zeros(4, device=dev)
+    for kw in (dict(k=257), dict(k=50, sample=4096), dict(k=50, sample=10)):
+        with pytest.raises(ValueError):
+            shard_rank(q, shard, sl, 0.05, **kw)
+    with pytest.raises(ValueError):
+        retrieve(q, shard, torch.zeros(4, dtype=torch.int64, device=dev), [10], 0.05, k=300)
 
 
 @pytest.mark.parametrize("M,D", [(333, 768), (64, 128), (1000, 1024)])

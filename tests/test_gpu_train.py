@@ -369,6 +369,28 @@ def test_seqrec_training_with_attention_dropout(dev, name):
         assert cos >= lim or float(r.abs().max()) < 1e-6, (k, cos)
 
 
+def test_train_mode_under_no_grad_applies_dropout(dev):
+    """nn.Dropout applies in train mode whatever the grad mode: model.train() under torch.no_grad()
+    draws the same masks (same torch seed) as the gradient-enabled forward — identical loss — and
+    differs from eval mode; eval mode under no_grad is the deterministic inference path."""
+    g = load_golden("c1_full")
+    batch = {k: v.to(dev) for k, v in batch_of(g).items()}
+    labels = torch.tensor([3, 17, 0, 39], device=dev)
+    m = _drop_model(dev, 0.1, 0.1)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        torch.manual_seed(5)
+        l_grad = float(m(**batch, labels=labels))
+        torch.manual_seed(5)
+        with torch.no_grad():
+            l_nograd = float(m(**batch, labels=labels))
+        m.eval()
+        with torch.no_grad():
+            l_eval = float(m(**batch, labels=labels))
+            l_eval2 = float(m(**batch, labels=labels))
+    assert l_nograd == pytest.approx(l_grad, rel=1e-5, abs=1e-5)
+    assert l_eval == l_eval2 and abs(l_eval - l_grad) > 1e-4
+
+
 @pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
 def test_c2_finetune_grads_match_reference(dev, mode):
     """C3 at full model size: RecformerForSeqRec fwd + bwd at 12L/768d, L=1024, B=2 (ragged

@@ -9,7 +9,9 @@ mkdir -p build/var ../../tools/var
 objs=""
 for f in rf_rowops rf_gemm rf_attn rf_attn_bwd rf_global rf_retrieval; do
   if [ "$f.hip" = "$src" ]; then
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function "$@" -c $src -o build/var/${f}_$name.o
+    # the retired GEMM main loops (knob gemm_variant 1-7) exist only in these A/B builds
+    extra=""; [ "$f" = rf_gemm ] && extra="-DRF_GEMM_EXPERIMENTS"
+    /opt/rocm/bin/hipcc $extra --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function "$@" -c $src -o build/var/${f}_$name.o
     objs="$objs build/var/${f}_$name.o"
   else
     objs="$objs build/$f.o"
