@@ -391,45 +391,21 @@ def test_train_mode_under_no_grad_applies_dropout(dev):
     assert l_eval == l_eval2 and abs(l_eval - l_grad) > 1e-4
 
 
-@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
-def test_c2_finetune_grads_match_reference(dev, mode):
-    """C3 at full model size: RecformerForSeqRec fwd + bwd at 12L/768d, L=1024, B=2 (ragged
-    lengths 1024 / 700) on the HIP training path against the REAL reference's gradients
-    (tests/golden/c2_grads.npz, oracle/gen_golden_grads.py: models.py full-softmax loss, dropout 0,
-    train mode). Per parameter: 256 gradient entries at fixed positions, the L2 norm and max-abs.
-    fp32: loss 1e-3 abs, dL/dz and every slice within 2e-3 x max|g| of the parameter, norms 1e-3
-    relative; autocast bf16 (the reference's finetune.py:106-110 setting): loss 1e-2 relative,
-    dL/dz cosine >= 0.99, slice cosine >= 0.99 (0.95 below 1e-3 of the largest gradient),
-    norms within 5%."""
-    import numpy as np
+def _c2_model(dev):
     from recformer_amd import RecformerConfig
     from recformer_amd.hashinit import hash_init_, hash_tensor
     from tests.common import BASE
-    gz = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2_grads.npz"))
-    g12 = load_golden("c2_12l")
     cfg = RecformerConfig(**dict(BASE, item_num=1000, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0))
     model = RecformerForSeqRec(cfg)
     hash_init_(model.longformer, seed=2)
     model.init_item_embedding(hash_tensor("catalog", (1000, 768), "weight", seed=3, std=1.0))
     model.config.finetune_negative_sample_size = 0
-    model = model.to(dev).train()
-    keep = {}
+    return model.to(dev).train()
 
-    def hook(_m, _i, out):
-        out.pooler_output.retain_grad()
-        keep["z"] = out.pooler_output
 
-    hdl = model.longformer.register_forward_hook(hook)
-    batch = {k: v.to(dev) for k, v in batch_of(g12).items()}
-    labels = torch.from_numpy(gz["labels"]).to(dev)
-    ctx = (torch.autocast("cuda", dtype=torch.bfloat16 if mode == "autocast" else torch.float16)
-           if mode != "fp32" else contextlib.nullcontext())
-    with ctx:
-        loss = model(**batch, labels=labels)
-    loss.backward()
-    hdl.remove()
+def _c2_check(model, loss, dz, mode, gz, dev, gscale=1.0):
+    """The C2 finetune gradients (times gscale) against tests/golden/c2_grads.npz."""
     ref_loss = float(gz["loss"])
-    dz = keep["z"].grad.float().cpu()
     dz_ref = torch.from_numpy(gz["dz"])
     if mode == "fp32":
         assert abs(float(loss) - ref_loss) <= 1e-3, (float(loss), ref_loss)
@@ -444,7 +420,8 @@ def test_c2_finetune_grads_match_reference(dev, mode):
         n = str(n)
         p = params[n]
         assert p.grad is not None, n
-        gr = p.grad.detach().double().flatten()
+        gr = p.grad.detach().double().flatten() * gscale
+        assert bool(torch.isfinite(gr).all()), n
         pos = torch.from_numpy(gz[f"g:{n}:pos"]).to(dev)
         got = gr[pos].float().cpu()
         ref = torch.from_numpy(gz[f"g:{n}:val"])
@@ -467,6 +444,79 @@ def test_c2_finetune_grads_match_reference(dev, mode):
                 assert cos >= lim, (n, cos)
         checked += 1
     assert checked + zero == len(gz["names"]) == 270 and zero == 29
+
+
+def _c2_fixtures():
+    import numpy as np
+    gz = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2_grads.npz"))
+    return gz, load_golden("c2_12l")
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
+def test_c2_finetune_grads_match_reference(dev, mode):
+    """C3 at full model size: RecformerForSeqRec fwd + bwd at 12L/768d, L=1024, B=2 (ragged
+    lengths 1024 / 700) on the HIP training path against the REAL reference's gradients
+    (tests/golden/c2_grads.npz, oracle/gen_golden_grads.py: models.py full-softmax loss, dropout 0,
+    train mode). Per parameter: 256 gradient entries at fixed positions, the L2 norm and max-abs.
+    fp32: loss 1e-3 abs, dL/dz and every slice within 2e-3 x max|g| of the parameter, norms 1e-3
+    relative; autocast bf16 (the reference's finetune.py:106-110 setting): loss 1e-2 relative,
+    dL/dz cosine >= 0.99, slice cosine >= 0.99 (0.95 below 1e-3 of the largest gradient),
+    norms within 5%."""
+    gz, g12 = _c2_fixtures()
+    model = _c2_model(dev)
+    keep = {}
+
+    def hook(_m, _i, out):
+        out.pooler_output.retain_grad()
+        keep["z"] = out.pooler_output
+
+    hdl = model.longformer.register_forward_hook(hook)
+    batch = {k: v.to(dev) for k, v in batch_of(g12).items()}
+    labels = torch.from_numpy(gz["labels"]).to(dev)
+    ctx = (torch.autocast("cuda", dtype=torch.bfloat16 if mode == "autocast" else torch.float16)
+           if mode != "fp32" else contextlib.nullcontext())
+    with ctx:
+        loss = model(**batch, labels=labels)
+    loss.backward()
+    hdl.remove()
+    _c2_check(model, loss, keep["z"].grad.float().cpu(), mode, gz, dev)
+
+
+def test_c2_finetune_fp16_gradscaler_step(dev):
+    """finetune.py:98-137 with --fp16 exactly: torch.cuda.amp.autocast() (fp16), loss divided by the
+    8 gradient-accumulation steps, GradScaler() at its initial scale 2^16, scaler.scale(loss).backward(),
+    then unscale_ + step + update. The scaled fp16 backward must not overflow where the reference's
+    does not: no inf/nan found, the optimizer step runs and the scale is unchanged after update(); the
+    unscaled gradients x 8 match the reference's (c2_grads.npz) at the autocast-fp16 tolerances."""
+    gz, g12 = _c2_fixtures()
+    model = _c2_model(dev)
+    keep = {}
+
+    def hook(_m, _i, out):
+        out.pooler_output.retain_grad()
+        keep["z"] = out.pooler_output
+
+    hdl = model.longformer.register_forward_hook(hook)
+    batch = {k: v.to(dev) for k, v in batch_of(g12).items()}
+    labels = torch.from_numpy(gz["labels"]).to(dev)
+    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=0.0)
+    scaler = torch.amp.GradScaler("cuda")
+    assert scaler.get_scale() == 2.0 ** 16
+    with torch.autocast("cuda", dtype=torch.float16):
+        loss = model(**batch, labels=labels)
+    loss8 = loss / 8
+    scaler.scale(loss8).backward()
+    hdl.remove()
+    scaler.unscale_(opt)
+    found = sum(float(v.item()) for v in scaler._found_inf_per_device(opt).values())
+    assert found == 0.0, "inf/nan in the scaled fp16 gradients"
+    before = scaler.get_scale()
+    scaler.step(opt)
+    scaler.update()
+    assert scaler.get_scale() == before == 2.0 ** 16  # optimizer_was_run (finetune.py:124-127)
+    # dL/dz of the retained (fp32) pooler output carries the scale: unscale it for the check
+    dz = keep["z"].grad.float().cpu() * 8 / before
+    _c2_check(model, loss, dz, "autocast16", gz, dev, gscale=8.0)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
