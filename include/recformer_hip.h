@@ -162,6 +162,14 @@ int rf_drop_add_ln_fwd_t(int dtype, int M, int D, const void* t, int ldt, const 
 int rf_drop_add_ln_bwd_t(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
                          const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
                          void* dt, float* dw, float* db, void* workspace, rf_stream_t stream);
+/* Weight gradient of an nn.Linear, C (=|+=) X^T Y: C[n][k] = sum_m X[m][n] Y[m][k] over the M token
+ * rows (X = dC (M x N), Y = A (M x K), 16-bit row-major; C fp32 N x K, the master weight's dtype) —
+ * the dW = dC^T A of autograd through TF:504-514, 1064-1130 and the LM head (models.py:499-510).
+ * MFMA with transposed LDS reads; the rows split over workgroups into fp32 slabs reduced in a fixed
+ * order (deterministic); accumulate != 0 adds into C. Workspace: rf_weight_grad_workspace bytes. */
+size_t rf_weight_grad_workspace(int M, int N, int K);
+int rf_weight_grad(int dtype, int M, int N, int K, const void* X, int ldx, const void* Y, int ldy, float* C, int ldc,
+                   int accumulate, void* workspace, size_t ws_bytes, rf_stream_t stream);
 /* Column sums out[n] = sum_m x[m][n] (fp32 out; x in dtype, row-major, leading dim ldx), two
  * deterministic stages through rf_colsum_workspace(M, N) bytes — the bias gradient of the
  * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias). */

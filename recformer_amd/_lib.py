@@ -52,6 +52,9 @@ SIGNATURES = {
     "rf_drop_add_ln_bwd_t": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
                                      P]),
     "rf_colsum_workspace": (ctypes.c_size_t, [c_int, c_int]),
+    "rf_weight_grad_workspace": (ctypes.c_size_t, [c_int, c_int, c_int]),
+    "rf_weight_grad": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_int, c_int, P, ctypes.c_size_t,
+                               P]),
     "rf_scatter_add_rows": (c_int, [c_int, c_int, c_int, P, P, P, c_int, P, P, c_int, P]),
     "rf_colsum": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, P, P]),
     "rf_layernorm_bwd": (c_int, [c_int, c_int, P, P, c_int, P, P, P, P, P, P, P, P]),

@@ -880,6 +880,290 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
 }
 
 // ------------------------------------------------------------------------------------
+// k_band_attn_pipe3: k_band_attn_pipe2 at three workgroups per CU. pipe2 holds 74 KB of LDS (the K/V
+// ring, a two-slot Q ring and the global keys' K/V image), so only two 256-thread workgroups fit a
+// CU: two waves per SIMD for a kernel that is issue- and latency-bound, not bandwidth-bound. Here
+// the Q fragments go straight to registers (two 16-B loads per lane per block, issued one block
+// ahead as inline asm so that hipcc's wait bookkeeping does not drain the K/V DMA queue, retired by
+// the kernel's counted vmcnt and fenced with "+v" before use), and the loop-invariant global-key K
+// and V^T fragments are loaded from global memory once per workgroup: 48.3 KB of LDS (the ring,
+// the chunk masks, the global positions) -> three workgroups per CU (VGPR budget <= 168).
+// (read-write operand: the load targets the registers the variable already lives in, so hipcc has
+// no reason to copy it between the load and the fence that follows the counted wait)
+template <typename V8>
+__device__ __forceinline__ void gload16(V8& dst, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(dst) : "v"(p) : "memory");
+}
+
+constexpr int AQ_KV = 0;          // 3 x (K 64 x 128 B, V 64 x 128 B)
+constexpr int AQ_GP = 49152;      // 32 x int global positions
+constexpr int AQ_MK = 49280;      // per chunk {local mask, valid mask} uint64
+
+template <typename E, bool DROP>
+__global__ void __launch_bounds__(256, 3) k_band_attn_pipe3(int Lp, int H, int qpb, const E* __restrict__ q,
+                                                             const E* __restrict__ k,
+                                                             const E* __restrict__ v, int ld,
+                                                             const uint8_t* __restrict__ flags,
+                                                             const int32_t* __restrict__ gidx, int gmax,
+                                                             E* __restrict__ out, int ldo, AttnDrop dr) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nqb = Lp >> 6;
+  const int nparts = (nqb + qpb - 1) / qpb;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int part = wg % nparts, bh = wg / nparts;
+  const int h = bh % H, b = bh / H;
+  const int x0 = part * qpb, x1 = min(nqb, x0 + qpb);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t rb = (int64_t)b * Lp;
+  const E* kb = k + rb * ld + h * 64;
+  const E* vb = v + rb * ld + h * 64;
+  const E* qb = q + rb * ld + h * 64;
+  E* ob = out + rb * ldo + h * 64;
+  int* gp = reinterpret_cast<int*>(smem + AQ_GP);
+  unsigned long long* mk = reinterpret_cast<unsigned long long*>(smem + AQ_MK);
+  const int gt = gmax > 16 ? 2 : (gmax > 0 ? 1 : 0);  // 16-key tiles of global keys
+
+  // ---- prologue: global positions, the global keys' K / V^T fragments (loop-invariant, ordinary
+  // loads issued before anything else, so their wait never drains the DMA queue), Q(x0) into
+  // registers, chunk masks, the first chunks ----
+  if (gmax > 0 && threadIdx.x < 32) gp[threadIdx.x] = (int)threadIdx.x < gmax ? gidx[(int64_t)b * gmax + threadIdx.x] : -1;
+  __syncthreads();  // gp (nothing in flight yet)
+  V8 kgf[2][2], vgf[4];
+  unsigned int gbits = 0;
+  if (gt > 0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int p = gp[16 * t + li];
+      const E* kr = kb + (int64_t)(p >= 0 ? p : 0) * ld;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) kgf[t][s2] = *reinterpret_cast<const V8*>(kr + 8 * (4 * s2 + g));
+    }
+    // V^T fragment dt: lane (li, g) holds V[gp[key]][16 dt + li] for keys 4g..4g+3, 16+4g..16+4g+3 (the
+    // MFMA K order of pipe2's transposed reads, matching the P fragment built from the S^T tiles)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int p = gp[(j < 4 ? 0 : 16) + 4 * g + (j & 3)];
+      const E* vr = vb + (int64_t)(p >= 0 ? p : 0) * ld + li;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) vgf[dt][j] = vr[16 * dt];
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gbits |= (gp[16 * t + 4 * g + r] >= 0 ? 1u : 0u) << (4 * t + r);
+  }
+  // this lane's Q fragment of block x: row 64 x + 16 wave + li, 16-B chunks 4 s2 + g
+  const E* qlane = qb + (int64_t)(16 * wave + li) * ld + 8 * g;
+  V8 qn[2];
+  gload16(qn[0], qlane + (int64_t)64 * x0 * ld);
+  gload16(qn[1], qlane + (int64_t)64 * x0 * ld + 32);
+  for (int c = x0 + wave; c <= x1; c += 4) {
+    const int row = 64 * c - 32 + lane;
+    const int f = (row >= 0 && row < Lp) ? flags[rb + row] : 0;
+    const unsigned long long ml = __ballot(f == 1), mv = __ballot(f != 0);
+    if (lane == 0) {
+      mk[2 * (c - x0)] = ml;
+      mk[2 * (c - x0) + 1] = mv;
+    }
+  }
+  const int prow = 16 * wave + (lane >> 3);  // DMA piece rows prow, prow + 8 (pieces 2w, 2w+1)
+  const int pch = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
+  auto dma_chunk = [&](int c) {
+    char* base = smem + AQ_KV + (c % 3) * 16384 + wave * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kp = min(max(64 * c - 32 + prow + 8 * j, 0), Lp - 1);
+      const uint32_t off = __umul24(kp, ld) + pch;
+      BAND_GLDS(kb + off, base + j * 1024);
+      BAND_GLDS(vb + off, base + 8192 + j * 1024);
+    }
+  };
+  dma_chunk(x0);
+  dma_chunk(x0 + 1);  // x0 + 1 <= x1 always
+  if (x0 + 2 <= x1) dma_chunk(x0 + 2);
+
+  // per-lane LDS offsets: fragment reads of 16-row tiles (row li, 16-B chunk 4 s2 + g) and the
+  // transposed V reads (rows rr, rr + 16 of a 32-row key step; columns 16 dt + 4 (li & 3))
+  const int rr = 4 * g + (li >> 2);
+  int koff[2], voff[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) koff[s2] = li * 128 + (((4 * s2 + g) ^ (li & 7)) << 4);
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) voff[dt] = swz_el(rr, 16 * dt + 4 * (li & 3));
+  const uint32_t lds0 = lds_addr(smem);
+  const int myw = 32 + 16 * wave + li;  // this lane's query row in the 128-row window
+  // band bits of the wave's 80-key span [16w, 16w + 80): relative rows [li, li + 64]
+  const unsigned int band0 = ~0u << li, band2 = (2u << li) - 1u;
+
+  for (int x = x0; x < x1; ++x) {
+    // retire chunks x, x+1 and Q(x); still in flight (issue order, newest last): chunk x+2 and the
+    // O stores of block x-1 (x > x0), or chunk x0+2 (x = x0)
+    if (x == x0) wait_vm_small(x0 + 2 <= x1 ? 4 : 0);
+    else wait_vm_small((x + 2 <= x1 ? 4 : 0) + 2);
+    asm volatile("" : "+v"(qn[0]), "+v"(qn[1]));  // Q(x) landed: no use of it above this point
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int i0 = 64 * x;
+    const int sb0 = AQ_KV + (x % 3) * 16384, sb1 = AQ_KV + ((x + 1) % 3) * 16384;
+    const unsigned long long ml0 = mk[2 * (x - x0)], ml1 = mk[2 * (x - x0) + 2];
+    const unsigned long long mv0 = mk[2 * (x - x0) + 1], mv1 = mk[2 * (x - x0) + 3];
+
+    // ---- scores: 5 local key tiles (window rows 16w + 16t) + gt global tiles ----
+    f32x4 st[5], sg[2];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int rt = 16 * wave + 16 * t;
+      const char* kt = smem + (rt >= 64 ? sb1 : sb0) + (rt & 63) * 128;
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        st[t] = mfma16(*reinterpret_cast<const V8*>(kt + koff[s2]), qn[s2], st[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sg[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < gt) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          sg[t] = mfma16(kgf[t][s2], qn[s2], sg[t]);
+      }
+    }
+    if (x + 1 < x1) {  // Q(x+1) into the same registers, once this block's scores have read them
+      gload16(qn[0], qlane + (int64_t)64 * (x + 1) * ld);
+      gload16(qn[1], qlane + (int64_t)64 * (x + 1) * ld + 32);
+    }
+    unsigned int aw[3];
+    {
+      const int ks = 16 * wave;
+      const unsigned long long lo = ks ? ((ml0 >> ks) | (ml1 << (64 - ks))) : ml0;
+      const unsigned long long hi = ml1 >> ks;
+      aw[0] = ((unsigned int)lo & band0) >> (4 * g);
+      aw[1] = (unsigned int)(lo >> 32) >> (4 * g);
+      aw[2] = ((unsigned int)hi & band2) >> (4 * g);
+    }
+    float mx = RF_NEG_INF;
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[t][r] = mask_score(aw[t >> 1], 16 * (t & 1) + r, st[t][r]);
+        mx = fmaxf(mx, st[t][r]);
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sg[t][r] = t < gt ? mask_score(gbits, 4 * t + r, sg[t][r]) : RF_NEG_INF;
+        mx = fmaxf(mx, sg[t][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float nmu = (mx == RF_NEG_INF) ? 0.f : -mx * LOG2E;
+    float lsum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[t][r] = __builtin_amdgcn_exp2f(fmaf(st[t][r], LOG2E, nmu));
+        lsum += st[t][r];
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sg[t][r] = __builtin_amdgcn_exp2f(fmaf(sg[t][r], LOG2E, nmu));
+        lsum += sg[t][r];
+      }
+
+    // ---- O = P V: 3 key steps of 32 (the last pairs tile 4 with p = 0) + the global step ----
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint64_t drow = DROP ? ((uint64_t)bh * Lp + i0 + 16 * wave + li) : 0;
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) {
+      V8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = 2 * s2 + (j >> 2);
+        float pv = t < 5 ? st[t < 5 ? t : 4][j & 3] : 0.f;
+        if (DROP && t < 5) pv *= attn_keep_scale(dr, drow, Lp, i0 - 32 + 16 * wave + 16 * t + 4 * g + (j & 3));
+        pf[j] = (E)pv;
+      }
+      const int ga = 16 * wave + 32 * s2, gb = s2 < 2 ? ga + 16 : ga;  // finite rows for p = 0
+      const uint32_t va = lds0 + (ga >= 64 ? sb1 : sb0) + 8192 + (ga & 63) * 128;
+      const uint32_t vb2 = lds0 + (gb >= 64 ? sb1 : sb0) + 8192 + (gb & 63) * 128;
+      uint32_t a[8];
+      V4 vv[8];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        a[2 * dt] = va + voff[dt];
+        a[2 * dt + 1] = vb2 + voff[dt];
+      }
+      tr_read8(a, vv);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const V8 vf = V8{vv[2 * dt][0], vv[2 * dt][1], vv[2 * dt][2], vv[2 * dt][3],
+                         vv[2 * dt + 1][0], vv[2 * dt + 1][1], vv[2 * dt + 1][2], vv[2 * dt + 1][3]};
+        o[dt] = mfma16(vf, pf, o[dt]);
+      }
+    }
+    if (gt > 0) {
+      V8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float pv = sg[j >> 2][j & 3];
+        if (DROP) {
+          const int gk = gp[16 * (j >> 2) + 4 * g + (j & 3)];
+          pv *= gk >= 0 ? attn_keep_scale(dr, drow, Lp, gk) : 0.f;
+        }
+        pf[j] = (E)pv;
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(vgf[dt], pf, o[dt]);
+    }
+
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    const unsigned long long qmw = (myw >> 6) ? mv1 : mv0;
+    const bool qvalid = (qmw >> (myw & 63)) & 1ull;
+    const float inv = (qvalid && lsum > 0.f) ? 1.0f / lsum : 0.f;
+
+    // every wave is done with chunk slot x%3: stage O in the slot's K rows 16w..16w+15 (what this
+    // wave's chunk DMA overwrites next), then refill three blocks ahead and store O as whole lines
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    char* ostg = smem + sb0 + wave * 2048;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      V4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (E)(o[dt][r] * inv);
+      *reinterpret_cast<V4*>(ostg + li * 128 + (((2 * dt + (g >> 1)) ^ (li & 7)) << 4) + (g & 1) * 8) = w;
+    }
+    V8 ov[2];
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2) {
+      const int orow = 8 * p2 + (lane >> 3);
+      ov[p2] = *reinterpret_cast<const V8*>(ostg + orow * 128 + (((lane & 7) ^ (orow & 7)) << 4));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (x + 3 <= x1) dma_chunk(x + 3);
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2) {
+      const int orow = 8 * p2 + (lane >> 3);
+      *reinterpret_cast<V8*>(ob + __umul24(i0 + 16 * wave + orow, ldo) + (lane & 7) * 8) = ov[p2];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ------------------------------------------------------------------------------------
 // Short sequences (Lp <= 64, a multiple of 16: catalog items of <s> + up to 63 tokens, padded to
 // a multiple of 16 instead of the 64-token window; finetune.py:38-63): every key of the sequence
 // is in one 64-row tile, so one workgroup per (sequence, head) scores all of them. Same contract
@@ -1192,14 +1476,29 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 80000);
           attr2 = true;
         }
-#define P2_(E, D) k_band_attn_pipe2<E, D><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const E*)q, (const E*)k, \
-                                                                       (const E*)v, ld_qkv, flags, gidx, gmax,   \
-                                                                       (E*)out, ld_out, dr)
+#define P2_(E, D)                                                                                        \
+  do {                                                                                                    \
+    if (band_pipe3) {                                                                                     \
+      k_band_attn_pipe3<E, D><<<nparts * H * B, 256, lds3, s>>>(Lp, H, qpb, (const E*)q, (const E*)k,       \
+                                                               (const E*)v, ld_qkv, flags, gidx, gmax,     \
+                                                               (E*)out, ld_out, dr);                       \
+    } else {                                                                                              \
+      k_band_attn_pipe2<E, D><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const E*)q, (const E*)k,        \
+                                                              (const E*)v, ld_qkv, flags, gidx, gmax,      \
+                                                              (E*)out, ld_out, dr);                        \
+    }                                                                                                     \
+  } while (0)
+        // pipe3 (three workgroups per CU) unless the knob asks for pipe2 (A/B tools: band_path 0)
+        const bool band_pipe3 = g_knob[KNOB_BAND_PATH] == 3;
+        const size_t lds3 = AQ_MK + (size_t)(qpb + 1) * 16;
+        // training (dropout) keeps pipe2: pipe3's dropout form would spill at the 3-wave register budget
         if (h16) {
-          if (dr.thresh) P2_(f16, true);
+          if (dr.thresh) k_band_attn_pipe2<f16, true><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const f16*)q,
+              (const f16*)k, (const f16*)v, ld_qkv, flags, gidx, gmax, (f16*)out, ld_out, dr);
           else P2_(f16, false);
         } else {
-          if (dr.thresh) P2_(bf16, true);
+          if (dr.thresh) k_band_attn_pipe2<bf16, true><<<nparts * H * B, 256, lds, s>>>(Lp, H, qpb, (const bf16*)q,
+              (const bf16*)k, (const bf16*)v, ld_qkv, flags, gidx, gmax, (bf16*)out, ld_out, dr);
           else P2_(bf16, false);
         }
 #undef P2_

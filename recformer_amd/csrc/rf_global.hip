@@ -80,6 +80,22 @@ template <typename E>
 __device__ __forceinline__ typename H16<E>::x4 tr_read_g(const char* p) {  // 16-bit bit patterns
   return __builtin_bit_cast(typename H16<E>::x4, __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_g*)p));
 }
+// The same read as inline asm, for reads that overlap an LDS-DMA in flight: hipcc puts an
+// s_waitcnt vmcnt(0) in front of every transposed-read builtin issued after an LDS-DMA (it cannot
+// rule out that the DMA writes the bytes read), which drained the partial kernel's refill of the
+// other image half before each P.H product. The asm read is invisible to hipcc's wait bookkeeping:
+// the caller retires it with tr_wait() (lgkmcnt(0) + a scheduling fence) before any use.
+template <typename E>
+__device__ __forceinline__ typename H16<E>::x4 tr_read_ga(const char* p) {
+  typename H16<E>::x4 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+__device__ __forceinline__ void tr_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 // 16-bit plane type of the u planes for an element type (fp32 mode writes none)
 template <typename T> struct Plane16 { typedef T type; };
 template <> struct Plane16<float> { typedef bf16 type; };
@@ -583,29 +599,51 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     float al[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) al[q] = alpha_s[4 * g + q];
+    // P.H over each image half: transposed reads as asm (no vmcnt(0) in front of them: the other
+    // half's refill stays in flight), in batches of PB column tiles, each retired by tr_wait()
     V8 pa[2];
+    {
+      V4 pv[4];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int rb = 32 * s2 + 8 * g + q4;
-      const V4 v0 = tr_read_g<E>(pimg + (rb * 16 + 4 * p4) * 2);
-      const V4 v1 = tr_read_g<E>(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
-      pa[s2] = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int rb = 32 * s2 + 8 * g + q4;
+        pv[2 * s2] = tr_read_ga<E>(pimg + (rb * 16 + 4 * p4) * 2);
+        pv[2 * s2 + 1] = tr_read_ga<E>(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
+      }
+      tr_wait();
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        pa[s2] = V8{pv[2 * s2][0], pv[2 * s2][1], pv[2 * s2][2], pv[2 * s2][3],
+                    pv[2 * s2 + 1][0], pv[2 * s2 + 1][1], pv[2 * s2 + 1][2], pv[2 * s2 + 1][3]};
     }
+    constexpr int PB = D >= 1024 ? 1 : (hmt % 3 == 0 ? 3 : (hmt % 2 == 0 ? 2 : 1));  // D = 1024: u fills the VGPRs
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
 #pragma unroll
-      for (int ii = 0; ii < hmt; ++ii) {
-        const int i = half * hmt + ii;
-        const int col = (half * (nmt * 2) + wave * hmt + ii) * 16 + 4 * p4;  // column tile of this half
+      for (int i0 = 0; i0 < hmt; i0 += PB) {
+        V4 hv[PB][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[i][q] *= al[q];
+        for (int ii = 0; ii < PB; ++ii) {
+          const int col = (half * (nmt * 2) + wave * hmt + i0 + ii) * 16 + 4 * p4;  // column tile of this half
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int rb = 32 * s2 + 8 * g + q4;
-          const V4 v0 = tr_read_g<E>(smem + gimg(rb, col));
-          const V4 v1 = tr_read_g<E>(smem + gimg(rb + 4, col));
-          const V8 hb8 = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          acc[i] = mfma16(pa[s2], hb8, acc[i]);
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int rb = 32 * s2 + 8 * g + q4;
+            hv[ii][2 * s2] = tr_read_ga<E>(smem + gimg(rb, col));
+            hv[ii][2 * s2 + 1] = tr_read_ga<E>(smem + gimg(rb + 4, col));
+          }
+        }
+        tr_wait();
+#pragma unroll
+        for (int ii = 0; ii < PB; ++ii) {
+          const int i = half * hmt + i0 + ii;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[i][q] *= al[q];
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const V4 v0 = hv[ii][2 * s2], v1 = hv[ii][2 * s2 + 1];
+            const V8 hb8 = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            acc[i] = mfma16(pa[s2], hb8, acc[i]);
+          }
         }
       }
       // every wave is done reading this half of the image: refill it with the next sub-chunk

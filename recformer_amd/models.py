@@ -273,6 +273,9 @@ def _read_count(p) -> int:
 # pretraining training: the LM-head decoder + masked-LM cross entropy on the HIP kernels
 # (train._DecoderCE) for 16-bit compute; False = torch ops (F.linear + F.cross_entropy)
 DECODER_CE_HIP = True
+# pretraining training: the LM head's dense + GELU + LayerNorm on the HIP kernels (16-bit compute,
+# train._LMHeadTransform); False = torch ops
+LM_HEAD_HIP = True
 # pretraining: the LM head runs on the masked (labelled) rows only (_mlm_rows)
 LM_HEAD_MASKED_ONLY = True
 
@@ -796,11 +799,18 @@ def _pretrain_train_losses(self, z1, z2, outputs_a, mlm_a, lab_a, mlm_b, lab_b, 
     for mo, ml in ((mlm_a, lab_a), (mlm_b, lab_b)):
         if mo is not None and ml is not None:
             hid, lab = _mlm_rows(mo.last_hidden_state, ml)
-            x = F.gelu(F.linear(hid, head.dense.weight, head.dense.bias))
-            x = F.layer_norm(x, (x.shape[-1],), head.layer_norm.weight, head.layer_norm.bias,
-                             self.config.layer_norm_eps)
             dt = _compute_dtype(self.longformer.dtype)
-            if x.is_cuda and dt != torch.float32 and DECODER_CE_HIP:
+            hip = hid.is_cuda and dt != torch.float32 and hid.shape[-1] % 64 == 0
+            if hip and LM_HEAD_HIP:
+                # dense + GELU + LayerNorm on the HIP kernels (train._LMHeadTransform)
+                from .train import lm_head_transform
+                x = lm_head_transform(hid.to(dt), head.dense.weight, head.dense.bias, head.layer_norm.weight,
+                                      head.layer_norm.bias, self.config.layer_norm_eps)
+            else:
+                x = F.gelu(F.linear(hid, head.dense.weight, head.dense.bias))
+                x = F.layer_norm(x, (x.shape[-1],), head.layer_norm.weight, head.layer_norm.bias,
+                                 self.config.layer_norm_eps)
+            if hip and DECODER_CE_HIP:
                 # decoder GEMM + CE + its backward on the HIP kernels (train._DecoderCE)
                 from .train import decoder_ce
                 mlm = decoder_ce(x.to(dt), head.decoder.weight, head.bias, lab)

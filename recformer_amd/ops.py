@@ -18,7 +18,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_GELU_AUX,
 
 __all__ = [
     "dtype_code", "prepare_inputs", "embed_ln", "embed_ln_split", "add_layernorm_split", "join_split",
-    "gemm", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
+    "gemm", "weight_grad", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_GELU_AUX", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -319,6 +319,30 @@ def colsum(x: torch.Tensor, tag: Optional[str] = None) -> torch.Tensor:
     with _region(tag):
         rc = lib.rf_colsum(dtype_code(x.dtype), M, N, _p(x), _rowmajor(x, "x"), _p(out), _p(ws), _stream(x))
     check(rc, "rf_colsum")
+    return out
+
+
+def weight_grad(dc: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False,
+                tag: Optional[str] = None) -> torch.Tensor:
+    """rf_weight_grad: dW = dc^T a in fp32 (N, K) for 16-bit dc (M, N) and a (M, K) row-major views (the
+    weight gradient of a Linear); `out` given with accumulate=True adds into it."""
+    lib = _lib.load()
+    _dev(dc, a)
+    M, N = dc.shape
+    K = a.shape[1]
+    if a.shape[0] != M or a.dtype != dc.dtype:
+        raise ValueError(f"weight_grad: dc {tuple(dc.shape)} {dc.dtype} vs a {tuple(a.shape)} {a.dtype}")
+    if out is None:
+        if accumulate:
+            raise ValueError("weight_grad: accumulate needs out")
+        out = torch.empty(N, K, dtype=torch.float32, device=dc.device)
+    if out.dtype != torch.float32 or tuple(out.shape) != (N, K):
+        raise ValueError("weight_grad: out must be an fp32 (N, K) tensor")
+    ws = torch.empty(max(lib.rf_weight_grad_workspace(M, N, K), 16), dtype=torch.uint8, device=dc.device)
+    with _region(tag):
+        rc = lib.rf_weight_grad(dtype_code(dc.dtype), M, N, K, _p(dc), _rowmajor(dc, "dc"), _p(a), _rowmajor(a, "a"),
+                                _p(out), _rowmajor(out, "out"), int(accumulate), _p(ws), ws.numel(), _stream(dc))
+    check(rc, "rf_weight_grad")
     return out
 
 

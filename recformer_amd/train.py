@@ -51,6 +51,9 @@ GLOBAL_BWD_DH16 = True
 GLOBAL_KV_BLOCKDIAG = True
 # weight gradients of the layer GEMMs as a split-K batched GEMM (_weight_grad)
 DW_SPLIT_K = True
+# weight gradients on the HIP kernel (rf_weight_grad: MFMA, transposed LDS reads, fixed-order split
+# reduction) instead of hipBLASLt
+DW_HIP = True
 # bf16: FFN1 + GELU as one GEMM that also writes the pre-activation (_GemmGelu). Off: measured
 # neutral at C3 (25.8 vs 26.4 ms median, alternating A/B) — the GELU moves into the GEMM's
 # unhidden epilogue and the pre-activation is still written
@@ -80,6 +83,11 @@ def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
     S chunks computed as one batched GEMM (S times the tiles) and the S fp32 partials summed."""
     M, N = dc.shape
     K = a.shape[1]
+    if (DW_HIP and dc.is_cuda and dc.dtype in (torch.bfloat16, torch.float16) and a.dtype == dc.dtype
+            and N % 16 == 0 and K % 16 == 0 and dc.stride(1) == 1 and a.stride(1) == 1
+            and dc.stride(0) % 8 == 0 and a.stride(0) % 8 == 0
+            and dc.data_ptr() % 16 == 0 and a.data_ptr() % 16 == 0):
+        return ops.weight_grad(dc, a)
     S = 1
     if DW_SPLIT_K and M >= 8192 and N * K <= 4 * 1024 * 1024:
         S = 8
@@ -180,6 +188,44 @@ class _DecoderCE(torch.autograd.Function):
         dw = _weight_grad(dlog, x.contiguous()).to(ctx.wdt) if ctx.needs_input_grad[1] else None
         db = ops.colsum(dlog) if ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None
+
+
+class _LMHeadTransform(torch.autograd.Function):
+    """LongformerLMHead's dense -> exact GELU -> LayerNorm (TF:1277-1282) for 16-bit compute, the
+    reference's autocast semantics: dense on rf_gemm with the bias + GELU epilogue writing both
+    gelu(z) and the pre-activation z in the compute dtype (EPI_BIAS_GELU_AUX), LayerNorm of that
+    16-bit tensor in fp32 on rf_layernorm_fwd, its output rounded to the compute dtype (the decoder's
+    operand — autocast's cast of the fp32 LayerNorm output). Backward: rf_layernorm_bwd in fp32, the
+    exact-erf GELU backward in the compute dtype (as autograd of F.gelu on a 16-bit tensor), dX on
+    rf_gemm (transposed weight copy), dW as every Linear's (_weight_grad, fp32), db / dgamma / dbeta
+    as deterministic column sums."""
+
+    @staticmethod
+    def forward(ctx, x, w, w16, b, ln_w, ln_b, eps: float):
+        x = x.contiguous()
+        z = torch.empty(x.shape[0], w16.shape[0], dtype=x.dtype, device=x.device)
+        u = ops.gemm(x, w16, b, ops.RF_EPI_BIAS_GELU_AUX, resid=z)
+        lw = ln_w.float().contiguous()
+        y, mean, rstd = ops.layernorm(u, lw, ln_b.float().contiguous(), eps, out_dtype=x.dtype, stats=True)
+        ctx.save_for_backward(x, w16, z, u, mean, rstd, lw)
+        ctx.wdt = w.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w16, z, u, mean, rstd, lw = ctx.saved_tensors
+        du, dlw, dlb = ops.layernorm_bwd(dy.float(), u.float(), mean, rstd, lw)
+        dz = torch.ops.aten.gelu_backward(du.to(z.dtype), z).contiguous()
+        dx = ops.gemm(dz, w16.t().contiguous(), None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
+        dw = _weight_grad(dz, x).to(ctx.wdt) if ctx.needs_input_grad[1] else None
+        db = ops.colsum(dz) if ctx.needs_input_grad[3] else None
+        return dx, dw, None, db, dlw, dlb, None
+
+
+def lm_head_transform(x, dense_w, dense_b, ln_w, ln_b, eps: float):
+    """gelu(x.W^T + b) -> LayerNorm, in x's 16-bit dtype (see _LMHeadTransform)."""
+    return _LMHeadTransform.apply(x, dense_w, dense_w.detach().to(x.dtype).contiguous(), dense_b.float(), ln_w,
+                                  ln_b, eps)
 
 
 def decoder_ce(x, w, b, labels, ignore_index: int = -100):

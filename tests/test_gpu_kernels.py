@@ -712,3 +712,60 @@ def test_gemm_dgelu_epilogue(dev, dt, M, N, K):
     ref = torch.ops.aten.gelu_backward(a.float() @ w.float().t(), z.float())
     err = float((out.float() - ref).abs().max())
     assert err <= 1e-2 * max(float(ref.abs().max()), 1e-6), err
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K,strided", [(16384, 2304, 768, False), (16384, 768, 3072, False),
+                                           (16384, 3072, 768, False), (1000, 768, 768, True), (333, 64, 128, False),
+                                           (70000, 768, 768, False), (64, 256, 272, False)])
+def test_weight_grad_matches_fp32_matmul(dev, dt, M, N, K, strided):
+    """rf_weight_grad (dW = dC^T A on MFMA with transposed LDS reads, rows split over workgroups and
+    reduced in a fixed order) against torch's fp32 product of the same 16-bit operands: products of
+    16-bit values are exact in fp32, only the summation order differs (<= 1e-4 x max|dW|); ragged M
+    (not a multiple of 64 or of the split), N / K not multiples of 256, a strided column-slice dC (the
+    fused q|k|v gradient's layout); bit-identical on a repeat (deterministic); accumulate adds."""
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    if strided:
+        big = torch.randn(M, 3 * N, device=dev, generator=g).to(dt)
+        dc = big[:, N:2 * N]
+    else:
+        dc = torch.randn(M, N, device=dev, generator=g).to(dt)
+    a = torch.randn(M, K, device=dev, generator=g).to(dt)
+    ref = dc.float().t() @ a.float()
+    got = ops.weight_grad(dc, a)
+    err = float((got - ref).abs().max())
+    assert err <= 1e-4 * float(ref.abs().max()) + 1e-5, err
+    assert torch.equal(got, ops.weight_grad(dc, a))
+    base = torch.randn(N, K, device=dev, generator=g)
+    acc = base.clone()
+    ops.weight_grad(dc, a, out=acc, accumulate=True)
+    assert float((acc - (base + ref)).abs().max()) <= 1e-4 * float(ref.abs().max()) + 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", [
+    dict(B=2, Lp=256, H=2, lens=[256, 100], globals_=((0, 0), (1, 0))),
+    dict(B=3, Lp=192, H=3, lens=[192, 150, 1], globals_=((0, 0), (0, 70), (0, 191), (1, 0), (1, 33), (1, 149), (2, 0))),
+    dict(B=1, Lp=128, H=1, lens=[128], globals_=()),
+    dict(B=2, Lp=1024, H=12, lens=[1024, 700], globals_=((0, 0), (1, 0), (1, 5))),
+    dict(B=1, Lp=640, H=2, lens=[600], globals_=tuple((0, 19 * i) for i in range(32))),
+])
+def test_band_pipe3_bit_identical_to_pipe2(dev, dt, case):
+    """The three-workgroups-per-CU band kernel (k_band_attn_pipe3: Q fragments and the global keys'
+    K / V^T fragments loaded straight into registers, 48 KB of LDS) computes exactly what
+    k_band_attn_pipe2 (pinned to the reference through test_band_and_global_attention) computes:
+    same MFMA chain, same softmax, same stores — outputs bit-identical, incl. ragged rows, padded
+    rows, up to 32 global keys, one run of 10 query blocks (Lp = 640) and two runs of 8 (Lp = 1024)."""
+    from recformer_amd import _lib
+    B, Lp, H = case["B"], case["Lp"], case["H"]
+    D = H * 64
+    qkv, merged, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, case["lens"], case["globals_"], 11)
+    q, k, v = (qkv[:, i * D:(i + 1) * D] for i in range(3))
+    old = _lib.set_knob("band_path", 0)
+    try:
+        ref = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, 32)
+        _lib.set_knob("band_path", 3)
+        got = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, 32)
+    finally:
+        _lib.set_knob("band_path", old)
+    assert torch.equal(got, ref)

@@ -543,9 +543,11 @@ def test_cross_entropy_bwd(dev, dt, N):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_pretrain_decoder_ce_hip_matches_torch(dev, monkeypatch, dt):
-    """Pretraining under autocast with the LM-head decoder + masked-LM CE on the HIP kernels
-    (models.DECODER_CE_HIP, train._DecoderCE) gives the loss and gradients of the torch ops
-    (F.linear under autocast + F.cross_entropy): loss within 1e-3, gradient cosine >= 0.999."""
+    """Pretraining under autocast with the whole LM head on the HIP kernels — dense + GELU +
+    LayerNorm (models.LM_HEAD_HIP, train._LMHeadTransform) and the decoder + masked-LM CE
+    (models.DECODER_CE_HIP, train._DecoderCE) — gives the loss and gradients of the torch ops
+    (F.linear / F.gelu / F.layer_norm under autocast + F.cross_entropy): loss within 1e-3, gradient
+    cosine >= 0.999 for every parameter, the LM head's included."""
     from recformer_amd import models
     from tests.common import hashed_pretrain, pretrain_inputs
     g = load_golden("c1_pretrain")
@@ -554,6 +556,7 @@ def test_pretrain_decoder_ce_hip_matches_torch(dev, monkeypatch, dt):
     res = {}
     for hip in (False, True):
         monkeypatch.setattr(models, "DECODER_CE_HIP", hip)
+        monkeypatch.setattr(models, "LM_HEAD_HIP", hip)
         m.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=dt):
             out = m(**kw)
