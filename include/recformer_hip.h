@@ -170,6 +170,23 @@ int rf_drop_add_ln_bwd_t(int dtype, int M, int D, const float* dy, const void* d
 size_t rf_weight_grad_workspace(int M, int N, int K);
 int rf_weight_grad(int dtype, int M, int N, int K, const void* X, int ldx, const void* Y, int ldy, float* C, int ldc,
                    int accumulate, void* workspace, size_t ws_bytes, rf_stream_t stream);
+/* Backward of the fused embedding + LayerNorm (RecformerEmbeddings, models.py:108-138): from dh (M x D
+ * fp32) the row gradient dx = dL/d(Ew[id] + Ep[pos] + Et[tt] + Ei[ip]) (M x D fp32; the pre-LN sum is
+ * regathered from the fp32 tables, not stored) and dgamma / dbeta (deterministic, fixed-order sums).
+ * Workspace: rf_embed_ln_bwd_workspace bytes. */
+size_t rf_embed_ln_bwd_workspace(int M, int D);
+int rf_embed_ln_bwd(int M, int D, const int32_t* ids, const int32_t* pos, const int32_t* tt, const int32_t* ip,
+                    const float* word_emb, const float* pos_emb, const float* type_emb, const float* ipos_emb,
+                    const float* ln_w, float eps, const float* dh, float* dx, float* dgamma, float* dbeta,
+                    void* workspace, rf_stream_t stream);
+/* An embedding table's gradient without atomics (nn.Embedding backward, models.py:82-138):
+ * dst[keys_sorted[j]] = sum of src[perm[j']] over the run of equal keys containing j, summed in the
+ * sorted order (perm / keys_sorted: a stable sort of the token indices); rows of key `pad`
+ * (padding_idx) and untouched rows are left as they are (the caller zero-fills dst).
+ * Workspace: rf_segment_rows_sum_workspace bytes. */
+size_t rf_segment_rows_sum_workspace(int M, int D);
+int rf_segment_rows_sum(int M, int D, const float* src, const int32_t* perm, const int32_t* keys_sorted, int pad,
+                        float* dst, int V, void* workspace, rf_stream_t stream);
 /* Column sums out[n] = sum_m x[m][n] (fp32 out; x in dtype, row-major, leading dim ldx), two
  * deterministic stages through rf_colsum_workspace(M, N) bytes — the bias gradient of the
  * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias). */
@@ -360,6 +377,29 @@ int rf_topk_dense(int B, int n, const float* vals, int64_t ldv, const int32_t* i
                   int k, float* out_v, int32_t* out_i, rf_stream_t stream);
 int rf_topk_merge(int B, int k0, const float* v0, const int32_t* i0, const float* cval, const int32_t* cidx,
                   const int32_t* rcnt, int capr, int k, float* out_v, int32_t* out_i, int32_t* overflow,
+                  rf_stream_t stream);
+
+/* AdamW over all of an optimizer's parameter tensors in one launch (torch.optim.AdamW as the
+ * reference's drivers use it: optimization.py:28-32, litmodels.py:42-56; host-side step counts and
+ * bias corrections as torch's non-capturable path). One descriptor per fp32 tensor (device memory);
+ * block_tensor[b] names the descriptor workgroup b updates — a tensor of n elements owns
+ * ceil(n / rf_adamw_chunk()) consecutive workgroups starting at its first_block.
+ *   p <- p decay;  m <- lerp(m, g, w1);  v <- beta2 v + w2 g^2;
+ *   p <- p - step_size m / (sqrt(v) / bias_correction2_sqrt + eps)
+ * with decay = 1 - lr weight_decay, w1 = 1 - beta1, w2 = 1 - beta2 (all rounded from double on the
+ * host, as torch passes them) and step_size = lr / (1 - beta1^step). */
+typedef struct rf_adamw_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+  int64_t first_block;
+  float decay, w1, beta2, w2, eps, step_size, bias_correction2_sqrt;
+  int32_t maximize;
+} rf_adamw_tensor; /* 80 bytes */
+int rf_adamw_chunk(void);
+int rf_adamw_step(const rf_adamw_tensor* tensors, int ntensors, const int32_t* block_tensor, int nblocks,
                   rf_stream_t stream);
 
 #ifdef __cplusplus

@@ -52,6 +52,12 @@ SIGNATURES = {
     "rf_drop_add_ln_bwd_t": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
                                      P]),
     "rf_colsum_workspace": (ctypes.c_size_t, [c_int, c_int]),
+    "rf_embed_ln_bwd_workspace": (ctypes.c_size_t, [c_int, c_int]),
+    "rf_embed_ln_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, c_float, P, P, P, P, P, P]),
+    "rf_segment_rows_sum_workspace": (ctypes.c_size_t, [c_int, c_int]),
+    "rf_segment_rows_sum": (c_int, [c_int, c_int, P, P, P, c_int, P, c_int, P, P]),
+    "rf_adamw_chunk": (c_int, []),
+    "rf_adamw_step": (c_int, [P, c_int, P, c_int, P]),
     "rf_weight_grad_workspace": (ctypes.c_size_t, [c_int, c_int, c_int]),
     "rf_weight_grad": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_int, c_int, P, ctypes.c_size_t,
                                P]),

@@ -6,7 +6,7 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
-from torch.optim import AdamW
+from .optim import AdamW
 
 try:  # Lightning is not in this image; the wrapper keeps its contract either way
     import pytorch_lightning as _pl
@@ -56,6 +56,7 @@ class LitWrapper(_Base):
             {"params": [p for n, p in named if not any(nd in n for nd in no_decay)], "weight_decay": self.weight_decay},
             {"params": [p for n, p in named if any(nd in n for nd in no_decay)], "weight_decay": 0.0},
         ]
+        # recformer_amd.optim.AdamW: torch's AdamW update, state_dict and GradScaler behaviour, one HIP launch
         optimizer = AdamW(groups, lr=self.learning_rate)
         total = (self.trainer.estimated_stepping_batches if _pl is not None and getattr(self, "_trainer", None)
                  else self.num_training_steps)

@@ -18,7 +18,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_GELU_AUX,
 
 __all__ = [
     "dtype_code", "prepare_inputs", "embed_ln", "embed_ln_split", "add_layernorm_split", "join_split",
-    "gemm", "weight_grad", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
+    "gemm", "weight_grad", "embed_ln_bwd", "embedding_grad", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_GELU_AUX", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -343,6 +343,47 @@ def weight_grad(dc: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] =
         rc = lib.rf_weight_grad(dtype_code(dc.dtype), M, N, K, _p(dc), _rowmajor(dc, "dc"), _p(a), _rowmajor(a, "a"),
                                 _p(out), _rowmajor(out, "out"), int(accumulate), _p(ws), ws.numel(), _stream(dc))
     check(rc, "rf_weight_grad")
+    return out
+
+
+def embed_ln_bwd(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, eps: float, dh: torch.Tensor):
+    """rf_embed_ln_bwd: (dx, dgamma, dbeta) of h = LN(Ew[ids] + Ep[pos] + Et[tt] + Ei[ip]) for the fp32
+    gradient dh (M, D); tables fp32 contiguous, index streams int32 (M,)."""
+    lib = _lib.load()
+    _dev(ids, word, dh)
+    M = ids.numel()
+    D = word.shape[1]
+    for t in (word, posemb, typeemb, iposemb):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.shape[1] != D:
+            raise ValueError("embed_ln_bwd: tables must be contiguous fp32 of one width")
+    dh = dh.float().contiguous()
+    if tuple(dh.shape) != (M, D):
+        raise ValueError(f"embed_ln_bwd: dh {tuple(dh.shape)} for {M} rows x {D}")
+    idx = [x.reshape(-1).to(torch.int32).contiguous() for x in (ids, pos, tt, ip)]
+    dx = torch.empty(M, D, dtype=torch.float32, device=dh.device)
+    dw = torch.empty(D, dtype=torch.float32, device=dh.device)
+    db = torch.empty_like(dw)
+    ws = torch.empty(max(lib.rf_embed_ln_bwd_workspace(M, D), 16), dtype=torch.uint8, device=dh.device)
+    check(lib.rf_embed_ln_bwd(M, D, *(_p(x) for x in idx), _p(word), _p(posemb), _p(typeemb), _p(iposemb),
+                              _p(ln_w.float().contiguous()), float(eps), _p(dh), _p(dx), _p(dw), _p(db), _p(ws),
+                              _stream(dh)), "rf_embed_ln_bwd")
+    return dx, dw, db
+
+
+def embedding_grad(src: torch.Tensor, index: torch.Tensor, num_rows: int, pad: Optional[int] = None) -> torch.Tensor:
+    """nn.Embedding's dense weight gradient (num_rows, D) fp32 from row gradients src (M, D) and the
+    token indices (M,), deterministically: a stable sort of the indices, then rf_segment_rows_sum adds
+    each index's rows in token order; the padding_idx row stays zero."""
+    lib = _lib.load()
+    _dev(src, index)
+    M, D = src.shape
+    src = src.float().contiguous()
+    keys, perm = torch.sort(index.reshape(-1).to(torch.int32), stable=True)
+    out = torch.zeros(num_rows, D, dtype=torch.float32, device=src.device)
+    ws = torch.empty(max(lib.rf_segment_rows_sum_workspace(M, D), 16), dtype=torch.uint8, device=src.device)
+    check(lib.rf_segment_rows_sum(M, D, _p(src), _p(perm.to(torch.int32).contiguous()), _p(keys.contiguous()),
+                                  -1 if pad is None else int(pad), _p(out), num_rows, _p(ws), _stream(src)),
+          "rf_segment_rows_sum")
     return out
 
 

@@ -4,14 +4,17 @@ Forward runs the same HIP kernels as inference; each is wrapped in a torch.autog
 whose backward is written out explicitly:
 
   _Gemm        C = A.W^T + b (optional q-scale on the first columns)      TF:504-514, 1064-1130
-               backward: dA = dC.W, dW = dC^T.A (hipBLASLt through torch.matmul: plain
-               library GEMMs), db = colsum(dC)
+               backward: dA = dC.W (rf_gemm against a transposed weight copy), dW = dC^T.A
+               (rf_weight_grad: MFMA, transposed LDS reads, deterministic split reduction),
+               db = colsum(dC)
   _LayerNorm   y = LN(x) from the HIP kernel (row stats saved)             TF:1071, 1130
                backward: the standard closed form in fp32, one HIP pass (rf_layernorm_bwd:
                dx per row, dgamma / dbeta as deterministic column sums)
   _EmbedLN     LN(Ew[id] + Ep[pos] + Et[tt] + Ei[ip])                       models.py:108-138
-               backward: LN backward, then index_add into the four tables (no gradient at
-               padding_idx rows of the word / position tables, as nn.Embedding)
+               backward: rf_embed_ln_bwd (LN backward, the pre-LN sum regathered) and, per table,
+               rf_segment_rows_sum over the stably sorted token indices — deterministic, no
+               atomics (no gradient at padding_idx rows of the word / position tables, as
+               nn.Embedding)
   _Attention   sliding-window local + global attention (band kernel + global fold)
                TF:482-1057; backward (bf16): the local branch on the HIP backward kernels
                (rf_attn_bwd.hip; global-key columns reduced per sequence here), the global
@@ -51,6 +54,8 @@ GLOBAL_BWD_DH16 = True
 GLOBAL_KV_BLOCKDIAG = True
 # weight gradients of the layer GEMMs as a split-K batched GEMM (_weight_grad)
 DW_SPLIT_K = True
+# embedding + LayerNorm backward on the HIP kernels (deterministic table gradients, no index_add_)
+EMBED_BWD_HIP = True
 # weight gradients on the HIP kernel (rf_weight_grad: MFMA, transposed LDS reads, fixed-order split
 # reduction) instead of hipBLASLt
 DW_HIP = True
@@ -330,6 +335,14 @@ class _EmbedLN(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh):
         ids, pos, tt, ip, word, pe, te, ie, ln_w = ctx.saved_tensors
+        if EMBED_BWD_HIP and dh.is_cuda and word.shape[1] % 4 == 0 and word.shape[1] <= 1024:
+            # rf_embed_ln_bwd (LN backward with the pre-LN sum regathered) + per-table deterministic row
+            # sums over the sorted token indices (rf_segment_rows_sum) — no atomics, no fp32 copy of x
+            dx, dw, db = ops.embed_ln_bwd(ids, pos, tt, ip, word.contiguous(), pe.contiguous(), te.contiguous(),
+                                          ie.contiguous(), ln_w, ctx.eps, dh.reshape(-1, word.shape[1]))
+            grads = [ops.embedding_grad(dx, idx, table.shape[0], pad)
+                     for table, idx, pad in ((word, ids, ctx.pad), (pe, pos, ctx.pad), (te, tt, None), (ie, ip, None))]
+            return (None, None, None, None, *grads, dw, db, None, None)
         i, p, t, q = (x.reshape(-1).long() for x in (ids, pos, tt, ip))
         x = word[i] + pe[p] + te[t] + ie[q]  # recompute the pre-LN sum (fp32)
         mean = x.mean(-1)

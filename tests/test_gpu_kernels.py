@@ -769,3 +769,83 @@ def test_band_pipe3_bit_identical_to_pipe2(dev, dt, case):
     finally:
         _lib.set_knob("band_path", old)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("M,D,V,kind", [
+    (1, 768, 50, "uniform"), (33, 768, 50, "uniform"), (5000, 768, 50265, "tokens"), (5000, 100, 300, "tokens"),
+    (4096, 1024, 1026, "positions"), (70000, 768, 4, "types"), (70000, 256, 51, "itempos"), (2100, 512, 3, "pad_only"),
+])
+def test_embedding_grad_matches_index_add(dev, M, D, V, kind):
+    """rf_segment_rows_sum (nn.Embedding's dense backward, models.py:82-138) against an fp64 index_add:
+    word-like ids with a frequent padding id (1, no gradient at that row) and repeated common tokens,
+    position ids, a 4-value type table whose segment spans more than 64 x 1024 sorted positions (two
+    ballot rounds of 1024-boundary chains), item positions, ragged D (100: not a multiple of 256),
+    a single row, and an all-padding input; deterministic (bit-identical on a repeat)."""
+    g = torch.Generator(device="cpu").manual_seed(M + D + V)
+    if kind == "tokens":
+        idx = torch.randint(0, V, (M,), generator=g)
+        idx[torch.rand(M, generator=g) < 0.3] = 1
+        idx[torch.rand(M, generator=g) < 0.1] = 2
+    elif kind == "positions":
+        idx = (torch.arange(M) % 1024) + 2
+    elif kind == "types":
+        idx = torch.zeros(M, dtype=torch.long)
+        idx[torch.rand(M, generator=g) < 0.02] = 3
+    elif kind == "pad_only":
+        idx = torch.ones(M, dtype=torch.long)
+    else:
+        idx = torch.randint(0, V, (M,), generator=g)
+    src = torch.randn(M, D, generator=g)
+    pad = None if kind in ("types", "itempos", "uniform") else 1
+    ref = torch.zeros(V, D, dtype=torch.float64).index_add_(0, idx, src.double())
+    if pad is not None:
+        ref[pad] = 0
+    got = ops.embedding_grad(src.to(dev), idx.to(dev), V, pad)
+    scale = float(ref.abs().max()) if ref.abs().max() > 0 else 1.0
+    err = float((got.double().cpu() - ref).abs().max())
+    assert err <= 2e-6 * scale * max(1.0, math.log2(M)) + 1e-6, (err, scale)
+    assert torch.equal(got, ops.embedding_grad(src.to(dev), idx.to(dev), V, pad))
+
+
+@pytest.mark.parametrize("M,D", [(1, 768), (3000, 768), (20000, 768), (777, 256), (500, 1024), (300, 100)])
+def test_embed_ln_bwd_matches_autograd(dev, M, D):
+    """rf_embed_ln_bwd (LayerNorm backward over the regathered 4-table sum, models.py:108-138) against
+    fp64 autograd of the same forward: dx and dgamma / dbeta (fixed-order block sums, bit-identical on
+    a repeat); then the full _EmbedLN backward (HIP kernels) against its torch path (index_add_)."""
+    from recformer_amd import train as T
+    g = torch.Generator(device="cpu").manual_seed(M + D)
+    Vw, P, Tt, I = 1000, 1026, 4, 51
+    word, pe, te, ie = (torch.randn(n, D, generator=g) * 0.5 for n in (Vw, P, Tt, I))
+    ids = torch.randint(0, Vw, (M,), generator=g)
+    ids[torch.rand(M, generator=g) < 0.2] = 1
+    pos = torch.randint(0, P, (M,), generator=g)
+    tt = torch.randint(0, Tt, (M,), generator=g)
+    ip = torch.randint(0, I, (M,), generator=g)
+    lw = 1 + 0.1 * torch.randn(D, generator=g)
+    lb = 0.1 * torch.randn(D, generator=g)
+    dh = torch.randn(M, D, generator=g)
+    x = (word[ids].double() + pe[pos].double() + te[tt].double() + ie[ip].double()).requires_grad_(True)
+    w64, b64 = lw.double().requires_grad_(True), lb.double().requires_grad_(True)
+    F.layer_norm(x, (D,), w64, b64, 1e-12).backward(dh.double())
+    args = [t.to(dev) for t in (ids, pos, tt, ip, word, pe, te, ie, lw)]
+    dx, dw, db = ops.embed_ln_bwd(*args, 1e-12, dh.to(dev))
+    for got, ref in ((dx, x.grad), (dw, w64.grad), (db, b64.grad)):
+        err = float((got.double().cpu() - ref).abs().max())
+        assert err <= 1e-5 * float(ref.abs().max()) + 1e-6, err
+    dx2, dw2, db2 = ops.embed_ln_bwd(*args, 1e-12, dh.to(dev))
+    assert torch.equal(dx, dx2) and torch.equal(dw, dw2) and torch.equal(db, db2)
+    if D % 64:
+        return  # the forward kernel (rf_embed_ln_fwd) takes widths in multiples of 64
+    grads = {}
+    for hip in (True, False):
+        old, T.EMBED_BWD_HIP = T.EMBED_BWD_HIP, hip
+        try:
+            tabs = [t.to(dev).requires_grad_(True) for t in (word, pe, te, ie, lw, lb)]
+            h = T._EmbedLN.apply(*args[:4], *tabs, 1e-12, 1)
+            h.backward(dh.to(dev))
+            grads[hip] = [t.grad for t in tabs]
+        finally:
+            T.EMBED_BWD_HIP = old
+    for a, b in zip(grads[True], grads[False]):
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-6
+    assert float(grads[True][0][1].abs().max()) == 0.0 and float(grads[True][1][1].abs().max()) == 0.0

@@ -8,7 +8,8 @@
    finetune check (loss 1e-3, slices 2e-3 x max|g|, norms 1e-3). 16-bit autocast: loss 1e-2
    relative, dL/dz cosine >= 0.99, per-parameter slice cosine >= min(0.99, c_ref - 0.02) and norm
    within max(5%, |r_ref - 1| + 2%), where c_ref / r_ref are the cosine / norm ratio of the
-   REFERENCE's own bf16-autocast gradients to its fp32 ones (stored in the fixture): its
+   REFERENCE's own bf16-autocast gradients to its fp32 ones (stored in the fixture; fp16 runs with
+   the loss scaled by 2^16 as GradScaler does in the reference's drivers): its
    value_global.bias gradients, for one, are only 0.97-0.99 cosine-close to fp32 in its own
    mixed-precision run, so a flat 0.99 would demand more than the reference achieves.
 2. test_c4_pretrain_dp_world2 — the data-parallel step of lightning_pretrain.py (one process per
@@ -92,8 +93,17 @@ def test_c4_pretrain_grads_match_reference(dev, mode):
     batch = {k: v.to(dev) for k, v in fixture_inputs(gz).items()}
     with _ctx(mode):
         out = m(**batch)
-    out.loss.backward()
+    # fp16 runs as the reference's drivers run it: the loss scaled by GradScaler's initial 2^16
+    # (finetune.py:106-126), the gradients unscaled before the comparison
+    scale = 65536.0 if mode == "autocast16" else 1.0
+    (out.loss * scale).backward()
     hdl.remove()
+    if scale != 1.0:
+        for p in m.parameters():
+            if p.grad is not None:
+                p.grad.div_(scale)
+        for z in zs:
+            z.grad.div_(scale)
     ref_loss = float(gz["loss"])
     assert int(out.cl_correct_num) == int(gz["cl_correct_num"])
     dz = [z.grad.float().cpu() for z in zs]
@@ -119,9 +129,8 @@ def test_c4_pretrain_grads_match_reference(dev, mode):
         mref, nref = float(gz[f"g:{n}:maxabs"]), float(gz[f"g:{n}:norm"])
         if _zero_grad_param(n):
             # mathematically zero (a softmax-row shift): rounding noise on both sides. The reference's
-            # own bf16 run leaves ~2e-5 x gmax of it (norm, fixture gb:); fp16 without a loss
-            # scaler (this test; finetune.py scales by 2^16) takes key gradients of ~1e-6 into fp16
-            # subnormals, so its column-sum noise is larger
+            # own bf16 run leaves ~2e-5 x gmax of it (norm, fixture gb:); fp16's column sums of the
+            # key gradients carry somewhat more
             assert mref < 1e-6 * gmax, (n, mref)
             lim = {"fp32": 1e-5, "autocast": 2e-4, "autocast16": 5e-4}[mode]
             assert float(gr.abs().max()) <= lim * gmax, n

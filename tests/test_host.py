@@ -137,3 +137,23 @@ def test_litwrapper_contract():
     assert decay["weight_decay"] == 0.1 and no_decay["weight_decay"] == 0.0
     assert len(decay["params"]) == 1 and len(no_decay["params"]) == 3  # dense.weight | biases, LN.weight
     assert sch["interval"] == "step" and opt.param_groups[0]["lr"] == 0.0  # warmup starts at 0
+
+
+def test_adamw_host_checks():
+    """recformer_amd.optim.AdamW: torch's argument checks, amsgrad refused, and no CPU fallback (a
+    CPU parameter raises before any launch)."""
+    import pytest
+    import torch
+    from recformer_amd.optim import AdamW
+    p = torch.zeros(3, requires_grad=True)
+    with pytest.raises(ValueError):
+        AdamW([p], lr=-1.0)
+    with pytest.raises(ValueError):
+        AdamW([p], betas=(1.0, 0.9))
+    with pytest.raises(NotImplementedError):
+        AdamW([p], amsgrad=True)
+    opt = AdamW([p])
+    opt.step()  # no gradient: nothing to do
+    p.grad = torch.ones(3)
+    with pytest.raises(ValueError):
+        opt.step()

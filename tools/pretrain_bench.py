@@ -18,6 +18,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from recformer_amd import RecformerConfig, RecformerForPretraining, dp  # noqa: E402
+from recformer_amd.optim import AdamW  # noqa: E402
 from recformer_amd.synth import BASE, synth_batch  # noqa: E402
 
 
@@ -40,6 +41,7 @@ def main():
     ap.add_argument("--len-b", type=int, default=128)
     ap.add_argument("--no-share-casts", action="store_true", help="A/B: per-pass weight casts")
     ap.add_argument("--autograd-global-bwd", action="store_true", help="A/B: global rows' backward by autograd")
+    ap.add_argument("--torch-adamw", action="store_true", help="A/B: torch.optim.AdamW instead of the HIP AdamW")
     ap.add_argument("--full-lm-head", action="store_true", help="A/B: LM head over every token")
     a = ap.parse_args()
     if a.full_lm_head:
@@ -61,7 +63,7 @@ def main():
     cfg = RecformerConfig(**dict(BASE, attention_probs_dropout_prob=0.0))
     torch.manual_seed(0)
     model = RecformerForPretraining(cfg).to(dev).train()
-    opt = torch.optim.AdamW(model.parameters(), lr=5e-5)
+    opt = (torch.optim.AdamW if a.torch_adamw else AdamW)(model.parameters(), lr=5e-5)
     g = torch.Generator().manual_seed(100 + rank)
     va, mlm_a, lab_a = view(a.batch, a.len_a, cfg.vocab_size, 10 + rank, 21, cfg.vocab_size - 1, g)
     vb, mlm_b, lab_b = view(a.batch, a.len_b, cfg.vocab_size, 20 + rank, 96, cfg.vocab_size - 1, g)

@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from recformer_amd import RecformerConfig, RecformerForSeqRec  # noqa: E402
+from recformer_amd.optim import AdamW  # noqa: E402
 from recformer_amd.synth import BASE, synth_batch  # noqa: E402
 
 
@@ -35,6 +36,8 @@ def main():
     ap.add_argument("--global-bwd-six", action="store_true", help="A/B: the global backward's six passes over h")
     ap.add_argument("--ab", default=None, help="A/B in one process: alternate blocks of steps with the "
                     "train.py switch of this name True / False and print both medians")
+    ap.add_argument("--torch-adamw", action="store_true", help="A/B: torch.optim.AdamW (multi-tensor) instead of "
+                    "recformer_amd.optim.AdamW (one HIP launch)")
     ap.add_argument("--global-dh-f32", action="store_true", help="A/B: the global branch's dh as an fp32 product")
     a = ap.parse_args()
     if a.global_dh_f32:
@@ -62,7 +65,7 @@ def main():
     model = RecformerForSeqRec(cfg)
     model.init_item_embedding(torch.randn(a.catalog, cfg.hidden_size) * 0.5)
     model = model.to(dev).train()
-    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=5e-5)
+    opt = (torch.optim.AdamW if a.torch_adamw else AdamW)([p for p in model.parameters() if p.requires_grad], lr=5e-5)
     batch = {k: v.to(dev) for k, v in synth_batch(a.batch, 1024, cfg.vocab_size, seed=7, item_len=21).items()}
     labels = torch.randint(0, a.catalog, (a.batch,), device=dev)
 
@@ -112,7 +115,7 @@ def main():
                                   f"attention dropout {a.attn_dropout}",
                       "batch": a.batch, "negatives": a.negatives, "catalog": a.catalog,
                       "ms_per_step": round(1e3 * el / a.steps, 2), "seq_per_s": round(a.batch * a.steps / el, 2),
-                      "loss": float(loss.detach()),
+                      "loss": float(loss.detach()), "optimizer": type(opt).__module__ + ".AdamW",
                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}))
 
 

@@ -25,7 +25,8 @@ def main():
     model = RecformerForSeqRec(cfg)
     model.init_item_embedding(torch.randn(10000, cfg.hidden_size) * 0.5)
     model = model.to(dev).train()
-    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=5e-5)
+    from recformer_amd.optim import AdamW
+    opt = AdamW([p for p in model.parameters() if p.requires_grad], lr=5e-5)
     batch = {k: v.to(dev) for k, v in synth_batch(a.batch, 1024, cfg.vocab_size, seed=7, item_len=21).items()}
     labels = torch.randint(0, 10000, (a.batch,), device=dev)
 
