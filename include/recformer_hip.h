@@ -47,6 +47,12 @@ enum {
 };
 
 const char* rf_last_error(void);
+/* Device-side dropout seeds for captured (hipGraph) training steps: registers a device uint64 step
+ * counter (NULL: none, the default). Every dropout launch made while one is registered uses
+ * seed + counter * 0x9E3779B97F4A7C15 (read on the device at kernel start), so a captured step whose
+ * graph advances the counter draws new masks on each replay while its backward regenerates the
+ * forward's. Returns the previous counter. Process-wide; not thread-safe. */
+const uint64_t* rf_set_seed_source(const uint64_t* step_counter);
 int rf_abi_version(void);
 /* Diagnostics (A/B tools only, not used by the product path): set a launch-path tuning knob
  * ("gemm_gn", "gemm_variant", "band_qpb", "band_path", "gfold_path", "gfold_qsplit") for the
@@ -380,24 +386,26 @@ int rf_topk_merge(int B, int k0, const float* v0, const int32_t* i0, const float
                   rf_stream_t stream);
 
 /* AdamW over all of an optimizer's parameter tensors in one launch (torch.optim.AdamW as the
- * reference's drivers use it: optimization.py:28-32, litmodels.py:42-56; host-side step counts and
- * bias corrections as torch's non-capturable path). One descriptor per fp32 tensor (device memory);
- * block_tensor[b] names the descriptor workgroup b updates — a tensor of n elements owns
- * ceil(n / rf_adamw_chunk()) consecutive workgroups starting at its first_block.
+ * reference's drivers use it: optimization.py:28-32, litmodels.py:42-56). One descriptor per fp32
+ * tensor (device memory); block_tensor[b] names the descriptor workgroup b updates — a tensor of n
+ * elements owns ceil(n / rf_adamw_chunk()) consecutive workgroups starting at its first_block.
  *   p <- p decay;  m <- lerp(m, g, w1);  v <- beta2 v + w2 g^2;
  *   p <- p - step_size m / (sqrt(v) / bias_correction2_sqrt + eps)
- * with decay = 1 - lr weight_decay, w1 = 1 - beta1, w2 = 1 - beta2 (all rounded from double on the
- * host, as torch passes them) and step_size = lr / (1 - beta1^step). */
+ * with decay = 1 - lr weight_decay, w1 = 1 - beta1, w2 = 1 - beta2 (rounded from double on the host,
+ * as torch passes them). step == NULL: step_size = lr / (1 - beta1^t) and bias_correction2_sqrt
+ * are the host's (torch's non-capturable AdamW); otherwise both are computed on the device from the
+ * step count *step (already advanced), so a captured optimizer step needs no host values. */
 typedef struct rf_adamw_tensor {
   float* param;
   const float* grad;
   float* exp_avg;
   float* exp_avg_sq;
+  const float* step;
   int64_t numel;
   int64_t first_block;
-  float decay, w1, beta2, w2, eps, step_size, bias_correction2_sqrt;
+  float decay, beta1, w1, beta2, w2, eps, lr, step_size, bias_correction2_sqrt;
   int32_t maximize;
-} rf_adamw_tensor; /* 80 bytes */
+} rf_adamw_tensor; /* 96 bytes */
 int rf_adamw_chunk(void);
 int rf_adamw_step(const rf_adamw_tensor* tensors, int ntensors, const int32_t* block_tensor, int nblocks,
                   rf_stream_t stream);

@@ -57,6 +57,7 @@ SIGNATURES = {
     "rf_segment_rows_sum_workspace": (ctypes.c_size_t, [c_int, c_int]),
     "rf_segment_rows_sum": (c_int, [c_int, c_int, P, P, P, c_int, P, c_int, P, P]),
     "rf_adamw_chunk": (c_int, []),
+    "rf_set_seed_source": (P, [P]),
     "rf_adamw_step": (c_int, [P, c_int, P, c_int, P]),
     "rf_weight_grad_workspace": (ctypes.c_size_t, [c_int, c_int, c_int]),
     "rf_weight_grad": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_int, c_int, P, ctypes.c_size_t,

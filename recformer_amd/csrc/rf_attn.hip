@@ -610,6 +610,7 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
                                                           const uint8_t* __restrict__ flags,
                                                           const int32_t* __restrict__ gidx, int gmax,
                                                           E* __restrict__ out, int ldo, AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
   typedef typename H16<E>::x8 V8;
   typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -906,6 +907,7 @@ __global__ void __launch_bounds__(256, 3) k_band_attn_pipe3(int Lp, int H, int q
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx, int gmax,
                                                              E* __restrict__ out, int ldo, AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
   typedef typename H16<E>::x8 V8;
   typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1275,6 +1277,7 @@ __global__ void __launch_bounds__(256) k_band_attn_valu(int Lp, int half_w, cons
                                                          const uint8_t* __restrict__ flags,
                                                          const int32_t* __restrict__ gidx,
                                                          int gmax, T* __restrict__ out, int ldo, AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int h = blockIdx.y, b = blockIdx.z;
@@ -1423,7 +1426,7 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
                                      const uint8_t* flags, const int32_t* gidx, int gmax, void* out,
                                      int ld_out, float p_drop, uint64_t seed, rf_stream_t stream) {
   RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_band_attn_fwd: dropout p=%g outside [0, 1)", p_drop);
-  const AttnDrop dr{seed, drop_thresh(p_drop), 1.0f / (1.0f - p_drop)};
+  const AttnDrop dr{seed, drop_thresh(p_drop), 1.0f / (1.0f - p_drop), g_seed_dev};
   RF_REQUIRE(hd == 64, "rf_band_attn_fwd: head_dim must be 64 (got %d)", hd);
   RF_REQUIRE(B >= 0 && H > 0 && Lp >= 0 && gmax >= 0, "rf_band_attn_fwd: bad shape");
   RF_REQUIRE(ld_qkv >= H * hd && ld_out >= H * hd, "rf_band_attn_fwd: bad leading dims");

@@ -83,6 +83,7 @@ __global__ void __launch_bounds__(256) k_band_bwd_q(int Lp, int H, const E* __re
                                                      GT* __restrict__ dq, int lddq, float* __restrict__ lse2,
                                                      float* __restrict__ delta, float* __restrict__ gds,
                                                      float* __restrict__ gpr, AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
   typedef typename H16<E>::x8 V8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
@@ -325,6 +326,7 @@ __global__ void __launch_bounds__(256) k_band_bwd_kv(int Lp, int H, const E* __r
                                                       const float* __restrict__ lse2,
                                                       const float* __restrict__ delta, GT* __restrict__ dk,
                                                       GT* __restrict__ dv, int lddkv, AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
   typedef typename H16<E>::x8 V8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = Lp >> 6;
@@ -473,7 +475,7 @@ extern "C" int rf_band_attn_bwd_drop(int dtype, int grad_dtype, int B, int Lp, i
   RF_REQUIRE(grad_dtype == RF_F32 || grad_dtype == dtype,
              "rf_band_attn_bwd: gradients fp32 or the operand type (got %d for %d)", grad_dtype, dtype);
   RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_band_attn_bwd: dropout p=%g outside [0, 1)", p_drop);
-  const AttnDrop dr{seed, drop_thresh(p_drop), 1.0f / (1.0f - p_drop)};
+  const AttnDrop dr{seed, drop_thresh(p_drop), 1.0f / (1.0f - p_drop), g_seed_dev};
   RF_REQUIRE(hd == 64 && half_w == 32, "rf_band_attn_bwd: head_dim 64 and window 64 only (got %d, %d)", hd,
              2 * half_w);
   RF_REQUIRE(B >= 0 && H > 0 && Lp >= 0 && gmax >= 0 && gmax <= 32, "rf_band_attn_bwd: bad shape");

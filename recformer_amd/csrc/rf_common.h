@@ -231,9 +231,24 @@ inline uint32_t drop_thresh(float p) {
 // per (sequence b, head h, query position i, key position j), index ((b H + h) Lp + i) Lp + j.
 struct AttnDrop {
   uint64_t seed;
-  uint32_t thresh;  // 0: off
-  float scale;      // 1 / (1 - p)
+  uint32_t thresh;                   // 0: off
+  float scale;                       // 1 / (1 - p)
+  const uint64_t* seed_dev = nullptr;  // step counter in device memory (g_seed_dev), mixed in at kernel start
 };
+// Device-side dropout seeds for captured (hipGraph) training steps: rf_set_seed_source() registers a
+// device uint64 step counter; every dropout launch made while it is set passes the pointer, and the
+// kernel uses seed + counter * SEED_STEP_MIX, so one captured graph draws fresh masks on each replay
+// (the caller advances the counter inside the graph) while the forward and the backward of one step
+// agree. Unset (the default) the seeds are exactly the host values.
+extern const uint64_t* g_seed_dev;
+constexpr uint64_t SEED_STEP_MIX = 0x9E3779B97F4A7C15ull;
+__device__ __forceinline__ uint64_t seed_resolve(uint64_t seed, const uint64_t* dev) {
+  return dev ? seed + *dev * SEED_STEP_MIX : seed;
+}
+__device__ __forceinline__ void drop_resolve(AttnDrop& d) {
+  if (d.thresh && d.seed_dev) d.seed = seed_resolve(d.seed, d.seed_dev);
+  d.seed_dev = nullptr;
+}
 __device__ __forceinline__ float attn_keep_scale(const AttnDrop& d, uint64_t row, int Lp, int key) {
   return drop_keep(d.seed, row * (uint64_t)Lp + (uint64_t)key, d.thresh) ? d.scale : 0.f;
 }

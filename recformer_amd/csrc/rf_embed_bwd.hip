@@ -27,7 +27,7 @@ namespace rf {
 
 constexpr int EB_SLICE = 32;     // sorted positions per k_seg_partial wave
 constexpr int EB_SUPER = 1024;   // positions per k_seg_chain wave (32 slices)
-constexpr int EB_BLOCKS = 2048;  // k_embed_ln_bwd blocks (4 waves each, grid-stride over the rows)
+constexpr int EB_BLOCKS = 512;   // k_embed_ln_bwd blocks (4 waves each, grid-stride over the rows)
 
 template <int NV>
 __device__ __forceinline__ void row_load(float4 (&r)[NV / 4], const float* p, int lane, int D) {
@@ -146,23 +146,28 @@ __global__ void __launch_bounds__(256) k_embed_ln_bwd(int M, int D, const int32_
   }
 }
 
-// gamma / beta: block partials summed in block order — 64 columns per block, the 4 waves take a
-// contiguous quarter of the partials each, combined in wave order
-__global__ void __launch_bounds__(256) k_embed_affine_fin(int D, int nb, const float* __restrict__ part,
-                                                          float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ float red[4][64];
+// gamma / beta: block partials summed in block order — 64 columns per workgroup of 16 waves, wave w
+// summing a contiguous sixteenth of the partials, the 16 combined in wave order
+__global__ void __launch_bounds__(1024) k_embed_affine_fin(int D, int nb, const float* __restrict__ part,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;  // over 2 D: gamma columns then beta columns
   const int which = c >= D ? 1 : 0, col = c - which * D;
-  const int q = (nb + 3) / 4, b0 = w * q, b1 = min(nb, b0 + q);
+  const int q = (nb + 15) / 16, b0 = w * q, b1 = min(nb, b0 + q);
   float s = 0.f;
   if (c < 2 * D) {
-#pragma unroll 16
+#pragma unroll 8
     for (int b = b0; b < b1; ++b) s += part[((int64_t)b * 2 + which) * D + col];
   }
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && c < 2 * D) (which ? dbeta : dgamma)[col] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (w == 0 && c < 2 * D) {
+    float t = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) t += red[i][lane];
+    (which ? dbeta : dgamma)[col] = t;
+  }
 }
 
 // level 1: runs of equal keys inside each 32-position slice -> part[run start]
@@ -334,7 +339,7 @@ extern "C" int rf_embed_ln_bwd(int M, int D, const int32_t* ids, const int32_t* 
   else
     ELB_(16);
 #undef ELB_
-  k_embed_affine_fin<<<(2 * D + 63) / 64, 256, 0, s>>>(D, nb, part, dgamma, dbeta);
+  k_embed_affine_fin<<<(2 * D + 63) / 64, 1024, 0, s>>>(D, nb, part, dgamma, dbeta);
   RF_LAUNCH_CHECK("rf_embed_ln_bwd");
 }
 

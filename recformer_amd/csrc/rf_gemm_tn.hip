@@ -258,11 +258,13 @@ static int tn_cus() {
   return n;
 }
 
-// split count and row chunk: about one workgroup per CU, each split at least 512 rows
+// split count and row chunk: at most one workgroup per CU (the kernel holds a CU: 128 KiB LDS,
+// 512 registers a lane), so all of them run in ONE round — ceil(CUs / tiles) splits put 4-32 of them
+// into a second round that doubled the kernel's time; each split at least 512 rows
 static void tn_plan(int M, int N, int K, int& S, int& mchunk) {
   const int T = ((N + 255) / 256) * ((K + 255) / 256);
   const int cus = tn_cus();
-  int s = (cus + T - 1) / T;
+  int s = cus / T;
   const int max_s = max(1, M / 512);
   s = max(1, min(s, max_s));
   mchunk = ((M + s - 1) / s + 63) / 64 * 64;

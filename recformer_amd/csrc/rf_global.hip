@@ -460,6 +460,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
                                                              GfoldWs ws, int H, AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
   typedef typename H16<E>::x8 V8;
   typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -678,6 +679,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
                                                              GfoldWs ws, int H, AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
   typedef typename H16<E>::x8 V8;
   typedef typename H16<E>::x4 V4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1070,7 +1072,7 @@ extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int
   (void)bkg;  // softmax-invariant (see header comment)
   RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_global_attn_fold_fwd: p_drop %f not in [0, 1)", p_drop);
   RF_REQUIRE(p_drop == 0.f || dtype != RF_F32, "rf_global_attn_fold_fwd: attention dropout needs 16-bit operands");
-  const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f};
+  const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f, g_seed_dev};
   RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0, "rf_global_attn_fold_fwd: bad shape");
   RF_REQUIRE(D == H * 64, "rf_global_attn_fold_fwd: D=%d must be H*64", D);
   RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_fwd: at most %d heads", GF_HP);
@@ -1111,6 +1113,7 @@ extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, c
 // slot (gidx < 0) uses position 0 (its gradient is zero). recformer_amd/train.py _global_keep.
 __global__ void k_attn_global_keep(int B, int H, int Lp, int gmax, const int32_t* __restrict__ gidx, AttnDrop dr,
                                    float* __restrict__ z) {
+  drop_resolve(dr);  // device step counter (captured training steps)
   const int bhg = blockIdx.y;  // (b H + h) gmax + g
   const int g = bhg % gmax, bh = bhg / gmax, b = bh / H;
   const uint64_t row = (uint64_t)bh * Lp + (uint64_t)max(gidx[b * gmax + g], 0);
@@ -1124,7 +1127,7 @@ extern "C" int rf_attn_global_keep(int B, int H, int Lp, const int32_t* gidx, in
   RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_attn_global_keep: p_drop %f not in [0, 1)", p_drop);
   if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
   RF_REQUIRE(gidx && z, "rf_attn_global_keep: null pointer");
-  const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f};
+  const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f, g_seed_dev};
   k_attn_global_keep<<<dim3((Lp + 255) / 256, B * H * gmax), 256, 0, as_stream(stream)>>>(B, H, Lp, gmax, gidx, dr, z);
   RF_LAUNCH_CHECK("rf_attn_global_keep");
 }

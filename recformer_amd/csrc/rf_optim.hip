@@ -7,7 +7,8 @@
 //   v  <- v beta2 + (1 - beta2) g g
 //   p  <- p - step_size m / (sqrt(v) / sqrt(bc2) + eps),  step_size = lr / bc1
 // The optimizer (recformer_amd/optim.py) keeps the step counts and bias corrections on the host,
-// as torch's non-capturable AdamW, and hands one descriptor per tensor plus a block -> tensor table.
+// as torch's non-capturable AdamW (or, capturable, the step counts on the device and the bias
+// corrections computed here), and hands one descriptor per tensor plus a block -> tensor table.
 // 28 B of HBM traffic per fp32 element (read p g m v, write p m v): an HBM-bound stream.
 #include "rf_common.h"
 
@@ -15,19 +16,26 @@ namespace rf {
 
 constexpr int ADAM_CHUNK = 8192;  // elements per workgroup (256 threads x 8 float4)
 
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const rf_adamw_tensor& d) {
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const rf_adamw_tensor& d,
+                                          float step_size, float bc2_sqrt) {
   if (d.maximize) g = -g;
   p = p * d.decay;
   const float w = d.w1;
   m = w < 0.5f ? m + w * (g - m) : g - (g - m) * (1.0f - w);
   v = v * d.beta2 + d.w2 * g * g;
-  const float denom = sqrtf(v) / d.bias_correction2_sqrt + d.eps;
-  p = p + (-d.step_size) * (m / denom);
+  const float denom = sqrtf(v) / bc2_sqrt + d.eps;
+  p = p + (-step_size) * (m / denom);
 }
 
 __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict__ descs,
                                                const int32_t* __restrict__ block_tensor) {
   const rf_adamw_tensor d = descs[block_tensor[blockIdx.x]];
+  float step_size = d.step_size, bc2_sqrt = d.bias_correction2_sqrt;
+  if (d.step) {  // capturable: bias corrections from the device step count
+    const float t = *d.step;
+    step_size = d.lr / (1.0f - powf(d.beta1, t));
+    bc2_sqrt = sqrtf(1.0f - powf(d.beta2, t));
+  }
   const int64_t e0 = ((int64_t)blockIdx.x - d.first_block) * ADAM_CHUNK;
   const int64_t n = min((int64_t)ADAM_CHUNK, d.numel - e0);
   float* __restrict__ P = d.param + e0;
@@ -49,10 +57,10 @@ __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      adam_elem(p[i].x, g[i].x, m[i].x, v[i].x, d);
-      adam_elem(p[i].y, g[i].y, m[i].y, v[i].y, d);
-      adam_elem(p[i].z, g[i].z, m[i].z, v[i].z, d);
-      adam_elem(p[i].w, g[i].w, m[i].w, v[i].w, d);
+      adam_elem(p[i].x, g[i].x, m[i].x, v[i].x, d, step_size, bc2_sqrt);
+      adam_elem(p[i].y, g[i].y, m[i].y, v[i].y, d, step_size, bc2_sqrt);
+      adam_elem(p[i].z, g[i].z, m[i].z, v[i].z, d, step_size, bc2_sqrt);
+      adam_elem(p[i].w, g[i].w, m[i].w, v[i].w, d, step_size, bc2_sqrt);
       const int o = 4 * (threadIdx.x + 256 * i);
       *reinterpret_cast<float4*>(P + o) = p[i];
       *reinterpret_cast<float4*>(Mm + o) = m[i];
@@ -61,7 +69,7 @@ __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict
   } else {
     for (int64_t i = threadIdx.x; i < n; i += 256) {
       float p = P[i], m = Mm[i], v = Vv[i];
-      adam_elem(p, G[i], m, v, d);
+      adam_elem(p, G[i], m, v, d, step_size, bc2_sqrt);
       P[i] = p;
       Mm[i] = m;
       Vv[i] = v;

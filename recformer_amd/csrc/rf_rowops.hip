@@ -13,6 +13,7 @@ namespace rf {
 
 static thread_local char g_err[512];
 int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8};
+const uint64_t* g_seed_dev = nullptr;
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -425,12 +426,13 @@ __global__ void __launch_bounds__(256) k_add_ln_split(int M, const bf16* __restr
 template <typename E, int VEC, int NCH>
 __global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const E* __restrict__ t, int ldt,
                                                           const float* __restrict__ res, uint32_t thresh,
-                                                          float keep_scale, uint64_t seed,
+                                                          float keep_scale, uint64_t seed, const uint64_t* seed_dev,
                                                           const float* __restrict__ lw, const float* __restrict__ lb,
                                                           float eps, float* __restrict__ xo, float* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                           E* __restrict__ y16) {
   constexpr int D = 64 * VEC * NCH;
+  if (thresh) seed = seed_resolve(seed, seed_dev);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -495,8 +497,9 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
                                                         const float* __restrict__ w, float* __restrict__ dx,
                                                         float* __restrict__ part, E* __restrict__ dt,
                                                         uint32_t thresh, float keep_scale, uint64_t seed,
-                                                        const E* __restrict__ dy2) {
+                                                        const uint64_t* seed_dev, const E* __restrict__ dy2) {
   constexpr int D = 64 * VEC * NCH;
+  if (thresh) seed = seed_resolve(seed, seed_dev);
   __shared__ float red[4][2][D];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float pw[NCH][VEC], pb[NCH][VEC], wr[NCH][VEC];
@@ -1063,6 +1066,12 @@ static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, c
 }
 
 
+const uint64_t* rf_set_seed_source(const uint64_t* step_counter) {
+  const uint64_t* old = g_seed_dev;
+  g_seed_dev = step_counter;
+  return old;
+}
+
 int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
                        const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,
                        rf_stream_t stream) {
@@ -1087,7 +1096,7 @@ int rf_drop_add_ln_fwd_t(int dtype, int M, int D, const void* t, int ldt, const 
   const float ks = 1.0f / (1.0f - p);
   dim3 grid((M + 3) / 4);
 #define L_(V, N)                                                                                   \
-  k_drop_add_ln_fwd<E, V, N><<<grid, 256, 0, s>>>(M, (const E*)t, ldt, res, th, ks, seed, w, b, eps, x, y, \
+  k_drop_add_ln_fwd<E, V, N><<<grid, 256, 0, s>>>(M, (const E*)t, ldt, res, th, ks, seed, g_seed_dev, w, b, eps, x, y, \
                                                   mean, rstd, (E*)y16)
   if (dtype == RF_F16) {
     typedef f16 E;
@@ -1145,7 +1154,7 @@ static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, c
   hipStream_t s = as_stream(stream);
   const int nb = (M + LNB_ROWS - 1) / LNB_ROWS;
   float* part = reinterpret_cast<float*>(workspace);
-#define L_(V, N) k_layernorm_bwd<E, V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, dy2)
+#define L_(V, N) k_layernorm_bwd<E, V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, g_seed_dev, dy2)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
   colsum<float>(nb, 2 * D, part, 2 * D, part + (size_t)nb * 2 * D, dw, db, D, s);  // [dw | db] columns

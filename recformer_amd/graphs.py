@@ -1,79 +1,120 @@
-"""HIP-graph replay of inference forwards (small serving batches).
+"""A whole training step — forward, backward and the optimizer — captured once as a HIP graph and
+replayed per batch (the reference runs every step eagerly through autograd: finetune.py:98-137,
+lightning_pretrain.py). A C3/C4 step issues ~1500 launches through Python autograd; replaying the
+captured graph removes that host work, so the step costs its GPU time.
 
-An inference forward of `RecformerModel` / `RecformerForSeqRec` is ~150 kernel launches, each
-preceded by Python argument checks and a ctypes call; at a few sequences per batch the host side,
-not the GPU, sets the latency. `GraphedForward` captures one forward for a fixed batch shape into
-a HIP graph (torch.cuda.CUDAGraph, i.e. hipGraph on ROCm) and replays it: new inputs are copied
-into the captured input buffers, one graph launch runs every kernel, and the outputs are the
-captured output tensors (overwritten by each replay).
-
-The library itself never allocates, synchronises or reads back inside a forward except for one
-host read of the number of global tokens per sequence (models.RecformerModel._encode); during
-capture that count is fixed to the example batch's (models._STATIC_GMAX). A replay batch with
-more global tokens per sequence than the example is rejected (check=True reads the count back:
-one host read instead of ~150 launches), and attention_mask / global_attention_mask keep their
-meaning otherwise (ragged lengths and fewer globals are fine: the masks are inputs of the graph).
+What capture needs from the step, and how the build provides it:
+  * no host reads of device values: the global-slot count (train.encode_train's gmax) is fixed at
+    capture to the maximum over the example batch's global_attention_mask(s) (train._STATIC_GMAX);
+    a later batch may have fewer global tokens (empty slots are inert) but not more — __call__
+    checks that unless check=False;
+  * fresh dropout masks on every replay: a device step counter registered with rf_set_seed_source
+    is advanced inside the graph; every dropout kernel mixes it into its (capture-time) seed, and the
+    backward regenerates the forward's masks from the same counter value (torch's own dropout, e.g.
+    after the embeddings, uses its graph-safe philox offsets);
+  * an optimizer without host state: recformer_amd.optim.AdamW(capturable=True) (device step
+    counts, bias corrections in the kernel);
+  * static inputs: the batch is copied into the graph's input buffers before each replay.
+Gradients are written (not accumulated) by each replay; the graph owns them.
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Callable, Dict, Optional
 
 import torch
 
-from . import models
+from . import _lib, train
+
+__all__ = ["CapturedTrainStep", "static_gmax"]
 
 
-class GraphedForward:
-    """Capture `module(**example)` (inference, no grad) once; `__call__(**batch)` replays it.
+def static_gmax(batch: Dict[str, torch.Tensor]) -> int:
+    """Largest number of global tokens in any sequence of any view of the batch (host read)."""
+    g = 0
+    for k, v in batch.items():
+        if k.startswith("global_attention_mask") and torch.is_tensor(v):
+            am = batch.get("attention_mask" + k[len("global_attention_mask"):])
+            gm = v != 0
+            if am is not None:
+                gm = gm & (am > 0)
+            if gm.numel():
+                g = max(g, int(gm.sum(1).max()))
+    return g
 
-        g = GraphedForward(model, example_batch)   # example tensors on the GPU, fixed shapes
-        scores = g(**batch)                        # same keys / shapes / dtypes as the example
-    """
 
-    def __init__(self, module: torch.nn.Module, example: Dict[str, torch.Tensor], warmup: int = 2,
-                 check: bool = True):
-        if not all(isinstance(v, torch.Tensor) and v.is_cuda for v in example.values()):
-            raise ValueError("GraphedForward: example inputs must be tensors on the GPU")
-        self.module = module
-        self.check = check
-        self.static = {k: v.clone() for k, v in example.items()}
-        self.gmax = self._global_count(self.static)
-        stream = torch.cuda.Stream()
-        stream.wait_stream(torch.cuda.current_stream())
-        old = models._STATIC_GMAX
+def _default_loss(model, batch):
+    out = model(**batch)
+    return out if torch.is_tensor(out) else out.loss
+
+
+class CapturedTrainStep:
+    """step = CapturedTrainStep(model, optimizer, example_batch); loss = step(batch)
+
+    optimizer: recformer_amd.optim.AdamW(..., capturable=True). loss_fn(model, batch) -> scalar
+    loss (default: model(**batch), or its .loss). autocast_dtype: the autocast dtype of the step
+    (None: fp32). warmup eager steps run on a side stream first (they are real training steps)."""
+
+    def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer, example: Dict[str, torch.Tensor],
+                 loss_fn: Optional[Callable] = None, autocast_dtype: Optional[torch.dtype] = torch.bfloat16,
+                 warmup: int = 3):
+        if not all(g.get("capturable", False) for g in optimizer.param_groups):
+            raise ValueError("CapturedTrainStep needs an optimizer constructed with capturable=True")
+        self.model, self.opt = model, optimizer
+        self.loss_fn = loss_fn or _default_loss
+        self.dtype = autocast_dtype
+        dev = next(model.parameters()).device
+        self.static = {k: (v.to(dev).clone() if torch.is_tensor(v) else v) for k, v in example.items()}
+        self.gmax = static_gmax(self.static)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        lib = _lib.load()
+
+        def body():
+            if self.dtype is None:
+                loss = self.loss_fn(self.model, self.static)
+            else:
+                with torch.autocast("cuda", dtype=self.dtype, cache_enabled=False):
+                    loss = self.loss_fn(self.model, self.static)
+            loss.backward()
+            self.opt.step()
+            return loss
+
+        old_g = train._STATIC_GMAX
+        train._STATIC_GMAX = self.gmax
         try:
-            models._STATIC_GMAX = self.gmax
-            with torch.no_grad():
-                with torch.cuda.stream(stream):  # warm-up: caches, packed weights, kernel attributes
-                    for _ in range(max(1, warmup)):
-                        module(**self.static)
-                torch.cuda.current_stream().wait_stream(stream)
-                self.graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    self.opt.zero_grad(set_to_none=True)
+                    body()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.opt.zero_grad(set_to_none=True)
+            self.graph = torch.cuda.CUDAGraph()
+            old_src = lib.rf_set_seed_source(self.counter.data_ptr())
+            try:
                 with torch.cuda.graph(self.graph):
-                    self.out = module(**self.static)
+                    self.counter.add_(1)
+                    self.loss = body().detach()
+            finally:
+                lib.rf_set_seed_source(old_src)
         finally:
-            models._STATIC_GMAX = old
+            train._STATIC_GMAX = old_g
+        self.replays = 0
 
-    @staticmethod
-    def _global_count(b: Dict[str, torch.Tensor]) -> int:
-        gam = b.get("global_attention_mask")
-        if gam is None:
-            return 0
-        gm = gam != 0
-        am = b.get("attention_mask")
-        if am is not None:
-            gm = gm & (am > 0)
-        return int(gm.sum(1).max().item()) if gm.shape[0] > 0 else 0
-
-    def __call__(self, **batch):
-        if batch.keys() != self.static.keys():
-            raise ValueError(f"GraphedForward: inputs {sorted(batch)} != captured {sorted(self.static)}")
-        for k, v in batch.items():
-            if v.shape != self.static[k].shape or v.dtype != self.static[k].dtype:
-                raise ValueError(f"GraphedForward: {k} {tuple(v.shape)} {v.dtype} != captured "
-                                 f"{tuple(self.static[k].shape)} {self.static[k].dtype}")
-            self.static[k].copy_(v, non_blocking=True)
-        if self.check and self._global_count(self.static) > self.gmax:
-            raise ValueError(f"GraphedForward: more global tokens per sequence than captured ({self.gmax})")
+    def __call__(self, batch: Optional[Dict[str, torch.Tensor]] = None, check: bool = True) -> torch.Tensor:
+        """Copy batch (same shapes as the example) into the graph's inputs and replay one step;
+        returns the step's loss (a tensor the next replay overwrites)."""
+        if batch is not None:
+            if check:
+                g = static_gmax(batch)
+                if g > self.gmax:
+                    raise ValueError(f"batch has {g} global tokens in a sequence; the step was captured for {self.gmax}")
+            for k, v in batch.items():
+                if torch.is_tensor(v):
+                    dst = self.static[k]
+                    if dst.shape != v.shape:
+                        raise ValueError(f"{k}: shape {tuple(v.shape)} != captured {tuple(dst.shape)}")
+                    dst.copy_(v, non_blocking=True)
         self.graph.replay()
-        return self.out
+        self.replays += 1
+        return self.loss

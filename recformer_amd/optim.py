@@ -9,6 +9,12 @@ litmodels.py:42-56 for pretraining, stepped through GradScaler in fp16 runs, fin
 torch's multi-tensor sequence of ~8 passes. Step counts and bias corrections stay on the host as
 in torch, so GradScaler uses its ordinary unscale-and-skip path (an inf step is never taken).
 
+capturable=True (as torch's flag): the step counts live on the device, are advanced by a
+foreach add and the bias corrections are computed in the kernel, so a whole training step including
+the optimizer can be captured in a HIP graph (recformer_amd.graphs). The hyperparameters (lr, betas,
+eps, weight_decay) are read when the descriptors are built: a captured graph keeps the values of its
+capture (re-capture after changing them).
+
 Parameters must be fp32 CUDA tensors with dense, contiguous gradients; anything else raises
 (there is no CPU fallback).
 """
@@ -25,12 +31,12 @@ from .ops import check
 
 __all__ = ["AdamW"]
 
-# rf_adamw_tensor (include/recformer_hip.h): 4 pointers, numel, first_block, 7 floats, 1 int
-_DESC = np.dtype([("param", "<u8"), ("grad", "<u8"), ("exp_avg", "<u8"), ("exp_avg_sq", "<u8"),
-                  ("numel", "<i8"), ("first_block", "<i8"), ("decay", "<f4"), ("w1", "<f4"),
-                  ("beta2", "<f4"), ("w2", "<f4"), ("eps", "<f4"), ("step_size", "<f4"), ("bc2_sqrt", "<f4"),
-                  ("maximize", "<i4")])
-assert _DESC.itemsize == 80
+# rf_adamw_tensor (include/recformer_hip.h): 5 pointers, numel, first_block, 9 floats, 1 int
+_DESC = np.dtype([("param", "<u8"), ("grad", "<u8"), ("exp_avg", "<u8"), ("exp_avg_sq", "<u8"), ("step", "<u8"),
+                  ("numel", "<i8"), ("first_block", "<i8"), ("decay", "<f4"), ("beta1", "<f4"), ("w1", "<f4"),
+                  ("beta2", "<f4"), ("w2", "<f4"), ("eps", "<f4"), ("lr", "<f4"), ("step_size", "<f4"),
+                  ("bc2_sqrt", "<f4"), ("maximize", "<i4")])
+assert _DESC.itemsize == 96
 
 
 class AdamW(torch.optim.Optimizer):
@@ -38,7 +44,8 @@ class AdamW(torch.optim.Optimizer):
     one rf_adamw_step launch per step()."""
 
     def __init__(self, params: Iterable, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 1e-2, amsgrad: bool = False, *, maximize: bool = False):
+                 weight_decay: float = 1e-2, amsgrad: bool = False, *, maximize: bool = False,
+                 capturable: bool = False):
         if not 0.0 <= lr:
             raise ValueError(f"Invalid learning rate: {lr}")
         if not 0.0 <= eps:
@@ -52,16 +59,19 @@ class AdamW(torch.optim.Optimizer):
         if amsgrad:
             raise NotImplementedError("recformer_amd.optim.AdamW: amsgrad is not supported")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
-                                      amsgrad=False, maximize=maximize))
+                                      amsgrad=False, maximize=maximize, capturable=capturable))
         self._chunk: Optional[int] = None
         self._table_key = None
         self._table: Optional[np.ndarray] = None
+        self._blob_key = None
+        self._blob = None  # (pinned host copy, device copy) of the last descriptors
+        self._spare = None  # pinned buffer reserved for a captured step's descriptors
         self._launches = 0
 
-    def _state(self, p: torch.Tensor) -> dict:
+    def _state(self, p: torch.Tensor, capturable: bool) -> dict:
         st = self.state[p]
         if not st:
-            st["step"] = torch.tensor(0.0)
+            st["step"] = torch.zeros((), dtype=torch.float32, device=p.device) if capturable else torch.tensor(0.0)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         return st
@@ -76,9 +86,10 @@ class AdamW(torch.optim.Optimizer):
         if self._chunk is None:
             self._chunk = int(lib.rf_adamw_chunk())
         chunk = self._chunk
-        rows, device = [], None
+        rows, device, dev_steps = [], None, []
         for group in self.param_groups:
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+            cap = group.get("capturable", False)
             if isinstance(lr, torch.Tensor):
                 lr = float(lr)
             for p in group["params"]:
@@ -96,33 +107,63 @@ class AdamW(torch.optim.Optimizer):
                     device = p.device
                 elif p.device != device:
                     raise ValueError("recformer_amd.optim.AdamW: all parameters must be on one device")
-                st = self._state(p)
-                st["step"] += 1
-                step = float(st["step"])
-                bc1 = 1 - b1 ** step
-                bc2 = 1 - b2 ** step
+                st = self._state(p, cap)
+                if cap:
+                    if not st["step"].is_cuda:
+                        st["step"] = st["step"].to(p.device)
+                    dev_steps.append(st["step"])
+                    step_ptr, step_size, bc2s = st["step"].data_ptr(), 0.0, 1.0
+                else:
+                    st["step"] += 1
+                    step = float(st["step"])
+                    step_ptr, step_size, bc2s = 0, lr / (1 - b1 ** step), math.sqrt(1 - b2 ** step)
                 rows.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                             p.numel(), 1 - lr * wd, 1 - b1, b2, 1 - b2, eps, lr / bc1, math.sqrt(bc2),
+                             step_ptr, p.numel(), 1 - lr * wd, b1, 1 - b1, b2, 1 - b2, eps, lr, step_size, bc2s,
                              1 if group["maximize"] else 0))
         if not rows:
             return loss
-        numels = tuple(r[4] for r in rows)
+        if dev_steps:
+            torch._foreach_add_(dev_steps, 1.0)
+        numels = tuple(r[5] for r in rows)
         if numels != self._table_key:
             nblk = np.array([(n + chunk - 1) // chunk for n in numels], dtype=np.int64)
             self._first = np.concatenate([[0], np.cumsum(nblk)[:-1]]).astype(np.int64)
             self._table = np.repeat(np.arange(len(numels), dtype=np.int32), nblk)
             self._table_key = numels
-        d = np.zeros(len(rows), dtype=_DESC)
-        cols = list(zip(*rows))
-        for name, col in zip(("param", "grad", "exp_avg", "exp_avg_sq", "numel", "decay", "w1", "beta2", "w2",
-                              "eps", "step_size", "bc2_sqrt", "maximize"), cols):
-            d[name] = col
-        d["first_block"] = self._first
-        # one host->device copy per step: descriptors then the block -> tensor table
-        blob = np.concatenate([d.view(np.uint8), self._table.view(np.uint8)])
-        dev_blob = torch.from_numpy(blob).pin_memory().to(device, non_blocking=True)
-        base = dev_blob.data_ptr()
         stream = torch.cuda.current_stream(device).cuda_stream
-        check(lib.rf_adamw_step(base, len(rows), base + d.nbytes, int(self._table.size), stream), "rf_adamw_step")
+        key = tuple(rows) if dev_steps else None
+        if key is not None and key == self._blob_key:
+            # capturable and nothing changed: the device descriptors of the last step stand (no copy,
+            # so nothing host-side enters a captured graph)
+            base, nd = self._blob[1].data_ptr(), len(rows)
+        else:
+            d = np.zeros(len(rows), dtype=_DESC)
+            cols = list(zip(*rows))
+            names = ("param", "grad", "exp_avg", "exp_avg_sq", "step", "numel", "decay", "beta1", "w1", "beta2",
+                     "w2", "eps", "lr", "step_size", "bc2_sqrt", "maximize")
+            for name, col in zip(names, cols):
+                d[name] = col
+            d["first_block"] = self._first
+            # one host->device copy: descriptors then the block -> tensor table, from pinned memory kept
+            # with the device copy (a captured graph replays the copy from it). Pinned memory cannot be
+            # allocated while a stream captures: uncaptured steps stage through a fresh pinned tensor
+            # (torch's host allocator guards its reuse) and keep one spare, unused buffer for a capture.
+            blob = np.concatenate([d.view(np.uint8), self._table.view(np.uint8)])
+            if torch.cuda.is_current_stream_capturing():
+                host = self._spare
+                if host is None or host.numel() < blob.size:
+                    raise RuntimeError("recformer_amd.optim.AdamW: run one uncaptured step before capturing")
+                self._spare = None
+                host = host[: blob.size]
+                host.numpy()[:] = blob
+            else:
+                host = torch.from_numpy(blob).pin_memory()
+                if self._spare is None or self._spare.numel() < blob.size:
+                    self._spare = torch.empty(blob.size, dtype=torch.uint8, pin_memory=True)
+            dev_blob = torch.empty(blob.size, dtype=torch.uint8, device=device)
+            dev_blob.copy_(host, non_blocking=True)
+            self._blob, self._blob_key = (host, dev_blob), key
+            base, nd = dev_blob.data_ptr(), len(rows)
+        check(lib.rf_adamw_step(base, nd, base + nd * _DESC.itemsize, int(self._table.size), stream), "rf_adamw_step")
         self._launches += 1
         return loss

@@ -710,6 +710,12 @@ class _Attention(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------------
+# Global-slot count of a captured training step (set by recformer_amd.graphs while capturing and
+# replaying): encode_train then takes it instead of reading max(#global tokens) back from the device.
+_STATIC_GMAX: Optional[int] = None
+
+
+# ------------------------------------------------------------------------------------------
 # Per-forward cache of the autograd-tracked weight casts (bf16 copies, the fused q|k|v weight):
 # RecformerForPretraining runs four encoder passes over the same parameters, and one cast node
 # per parameter shared by all four (gradients accumulate through it) replaces four.
@@ -782,7 +788,9 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         gm = global_attention_mask != 0
         if attention_mask is not None:
             gm = gm & (attention_mask > 0)
-        gmax = int(gm.sum(1).max().item()) if B > 0 else 0
+        # a captured step (recformer_amd.graphs) fixes the global-slot count: no host sync, empty slots
+        # (gidx < 0) are inert
+        gmax = _STATIC_GMAX if _STATIC_GMAX is not None else (int(gm.sum(1).max().item()) if B > 0 else 0)
     else:
         gmax = 0
     ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(

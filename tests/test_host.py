@@ -45,7 +45,7 @@ def test_reference_checkpoint_loads_strict():
 def _header_functions():
     with open(os.path.join(ROOT, "include", "recformer_hip.h")) as f:
         txt = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(rf_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*|const uint64_t\*)\s+(rf_\w+)\s*\(", txt, re.M)))
 
 
 def test_library_exports_every_header_symbol():

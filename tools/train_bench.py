@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--global-bwd-six", action="store_true", help="A/B: the global backward's six passes over h")
     ap.add_argument("--ab", default=None, help="A/B in one process: alternate blocks of steps with the "
                     "train.py switch of this name True / False and print both medians")
+    ap.add_argument("--graph", action="store_true", help="replay the step as one captured HIP graph "
+                    "(recformer_amd.graphs.CapturedTrainStep)")
     ap.add_argument("--torch-adamw", action="store_true", help="A/B: torch.optim.AdamW (multi-tensor) instead of "
                     "recformer_amd.optim.AdamW (one HIP launch)")
     ap.add_argument("--global-dh-f32", action="store_true", help="A/B: the global branch's dh as an fp32 product")
@@ -65,7 +67,8 @@ def main():
     model = RecformerForSeqRec(cfg)
     model.init_item_embedding(torch.randn(a.catalog, cfg.hidden_size) * 0.5)
     model = model.to(dev).train()
-    opt = (torch.optim.AdamW if a.torch_adamw else AdamW)([p for p in model.parameters() if p.requires_grad], lr=5e-5)
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = torch.optim.AdamW(params, lr=5e-5) if a.torch_adamw else AdamW(params, lr=5e-5, capturable=a.graph)
     batch = {k: v.to(dev) for k, v in synth_batch(a.batch, 1024, cfg.vocab_size, seed=7, item_len=21).items()}
     labels = torch.randint(0, a.catalog, (a.batch,), device=dev)
 
@@ -85,6 +88,14 @@ def main():
         opt.zero_grad(set_to_none=True)
         return loss
 
+    if a.graph:
+        if scaler is not None:
+            raise SystemExit("--graph: the bf16 step only (GradScaler's host-side inf check is not capturable)")
+        from recformer_amd.graphs import CapturedTrainStep
+        captured = CapturedTrainStep(model, opt, dict(batch, labels=labels), autocast_dtype=dt, warmup=a.warmup)
+
+        def step():  # noqa: F811 - the captured replay replaces the eager step
+            return captured()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -115,7 +126,7 @@ def main():
                                   f"attention dropout {a.attn_dropout}",
                       "batch": a.batch, "negatives": a.negatives, "catalog": a.catalog,
                       "ms_per_step": round(1e3 * el / a.steps, 2), "seq_per_s": round(a.batch * a.steps / el, 2),
-                      "loss": float(loss.detach()), "optimizer": type(opt).__module__ + ".AdamW",
+                      "loss": float(loss.detach()), "optimizer": type(opt).__module__ + ".AdamW", "graph": a.graph,
                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}))
 
 

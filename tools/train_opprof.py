@@ -44,7 +44,7 @@ def main():
         for _ in range(2):
             step()
         torch.cuda.synchronize()
-    print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=60,
+    print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=110,
                                                              max_name_column_width=40, max_shapes_column_width=70))
 
 
