@@ -8,6 +8,9 @@ What capture needs from the step, and how the build provides it:
     capture to the maximum over the example batch's global_attention_mask(s) (train._STATIC_GMAX);
     a later batch may have fewer global tokens (empty slots are inert) but not more — __call__
     checks that unless check=False;
+  * the masked-LM head over a fixed number of rows (models._STATIC_MLM_ROWS): the labelled rows
+    first, padded with ignored rows up to a capacity of 1.25x the example's count (mlm_slack), so
+    batches with up to that many labelled tokens per view replay the same graph;
   * fresh dropout masks on every replay: a device step counter registered with rf_set_seed_source
     is advanced inside the graph; every dropout kernel mixes it into its (capture-time) seed, and the
     backward regenerates the forward's masks from the same counter value (torch's own dropout, e.g.
@@ -23,7 +26,7 @@ from typing import Callable, Dict, Optional
 
 import torch
 
-from . import _lib, train
+from . import _lib, models, train
 
 __all__ = ["CapturedTrainStep", "static_gmax"]
 
@@ -42,6 +45,15 @@ def static_gmax(batch: Dict[str, torch.Tensor]) -> int:
     return g
 
 
+def mlm_rows(batch: Dict[str, torch.Tensor]) -> int:
+    """Largest number of labelled masked-LM tokens in any view of the batch (host read)."""
+    n = 0
+    for k, v in batch.items():
+        if k.startswith("mlm_labels") and torch.is_tensor(v):
+            n = max(n, int((v != -100).sum()))
+    return n
+
+
 def _default_loss(model, batch):
     out = model(**batch)
     return out if torch.is_tensor(out) else out.loss
@@ -56,7 +68,7 @@ class CapturedTrainStep:
 
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer, example: Dict[str, torch.Tensor],
                  loss_fn: Optional[Callable] = None, autocast_dtype: Optional[torch.dtype] = torch.bfloat16,
-                 warmup: int = 3):
+                 warmup: int = 3, mlm_slack: float = 1.25):
         if not all(g.get("capturable", False) for g in optimizer.param_groups):
             raise ValueError("CapturedTrainStep needs an optimizer constructed with capturable=True")
         self.model, self.opt = model, optimizer
@@ -65,6 +77,8 @@ class CapturedTrainStep:
         dev = next(model.parameters()).device
         self.static = {k: (v.to(dev).clone() if torch.is_tensor(v) else v) for k, v in example.items()}
         self.gmax = static_gmax(self.static)
+        n = mlm_rows(self.static)
+        self.mlm_cap = ((int(n * mlm_slack) + 63) // 64) * 64 if n else None
         self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
         lib = _lib.load()
 
@@ -78,8 +92,8 @@ class CapturedTrainStep:
             self.opt.step()
             return loss
 
-        old_g = train._STATIC_GMAX
-        train._STATIC_GMAX = self.gmax
+        old_g, old_m = train._STATIC_GMAX, models._STATIC_MLM_ROWS
+        train._STATIC_GMAX, models._STATIC_MLM_ROWS = self.gmax, self.mlm_cap
         try:
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -98,7 +112,7 @@ class CapturedTrainStep:
             finally:
                 lib.rf_set_seed_source(old_src)
         finally:
-            train._STATIC_GMAX = old_g
+            train._STATIC_GMAX, models._STATIC_MLM_ROWS = old_g, old_m
         self.replays = 0
 
     def __call__(self, batch: Optional[Dict[str, torch.Tensor]] = None, check: bool = True) -> torch.Tensor:
@@ -109,6 +123,9 @@ class CapturedTrainStep:
                 g = static_gmax(batch)
                 if g > self.gmax:
                     raise ValueError(f"batch has {g} global tokens in a sequence; the step was captured for {self.gmax}")
+                n = mlm_rows(batch)
+                if n and (self.mlm_cap is None or n > self.mlm_cap):
+                    raise ValueError(f"batch has {n} masked-LM labels in a view; the step was captured for {self.mlm_cap}")
             for k, v in batch.items():
                 if torch.is_tensor(v):
                     dst = self.static[k]

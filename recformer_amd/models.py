@@ -762,6 +762,10 @@ class RecformerForPretraining(nn.Module):
                                           global_attentions=outputs_a.global_attentions)
 
 
+# Row capacity of the masked-LM head in a captured training step (set by recformer_amd.graphs)
+_STATIC_MLM_ROWS: Optional[int] = None
+
+
 def _mlm_rows(hidden: torch.Tensor, labels: torch.Tensor):
     """The rows the masked-LM loss reads: CrossEntropyLoss ignores label -100
     (models.py:499-510), so the LM head over only the labelled rows gives the same loss as over
@@ -771,6 +775,13 @@ def _mlm_rows(hidden: torch.Tensor, labels: torch.Tensor):
     lab = labels.reshape(-1)
     if not LM_HEAD_MASKED_ONLY:
         return h, lab
+    if _STATIC_MLM_ROWS is not None:
+        # captured step (recformer_amd.graphs): a fixed row count without a host read — the labelled
+        # rows first, in order (a stable sort of the ignore flag), then unlabelled rows (label -100,
+        # ignored by the CE) up to the capacity
+        cap = min(_STATIC_MLM_ROWS, lab.numel())
+        sel = torch.argsort((lab == -100).to(torch.uint8), stable=True)[:cap]
+        return h.index_select(0, sel), lab.index_select(0, sel)
     sel = (lab != -100).nonzero().squeeze(1)
     if sel.numel() == 0:
         return h, lab

@@ -114,3 +114,33 @@ def test_captured_step_refuses_more_global_tokens(dev):
         step(more)
     with pytest.raises(ValueError):
         graphs.CapturedTrainStep(m, torch.optim.SGD(m.parameters(), lr=0.1), batch)
+
+
+def test_captured_pretrain_step_matches_eager(dev):
+    """RecformerForPretraining (two views, MLM on both, contrastive; models.py:382-520) captured:
+    the masked-LM head over the fixed-capacity row set (labelled rows first, ignored rows after)
+    gives the eager step's loss and parameters."""
+    from tests.common import hashed_pretrain, pretrain_inputs
+    from tests.test_gpu_train import CFG
+    g = load_golden("c1_pretrain")
+    kw = {k: v.to(dev) for k, v in pretrain_inputs(g).items()}
+    a, b = hashed_pretrain(CFG).to(dev).train(), hashed_pretrain(CFG).to(dev).train()
+    oa = AdamW(a.parameters(), lr=1e-3, capturable=True)
+    ob = AdamW(b.parameters(), lr=1e-3, capturable=True)
+    step = graphs.CapturedTrainStep(a, oa, kw, warmup=1)
+    assert step.mlm_cap is not None
+
+    def eager():
+        ob.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = b(**kw)
+        out.loss.backward()
+        ob.step()
+        return float(out.loss)
+
+    eager()
+    for _ in range(2):
+        la, lb = float(step()), eager()
+        assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-6), n

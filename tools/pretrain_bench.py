@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--len-b", type=int, default=128)
     ap.add_argument("--no-share-casts", action="store_true", help="A/B: per-pass weight casts")
     ap.add_argument("--autograd-global-bwd", action="store_true", help="A/B: global rows' backward by autograd")
+    ap.add_argument("--graph", action="store_true", help="replay the step as one captured HIP graph (world 1)")
     ap.add_argument("--torch-adamw", action="store_true", help="A/B: torch.optim.AdamW instead of the HIP AdamW")
     ap.add_argument("--full-lm-head", action="store_true", help="A/B: LM head over every token")
     a = ap.parse_args()
@@ -63,7 +64,8 @@ def main():
     cfg = RecformerConfig(**dict(BASE, attention_probs_dropout_prob=0.0))
     torch.manual_seed(0)
     model = RecformerForPretraining(cfg).to(dev).train()
-    opt = (torch.optim.AdamW if a.torch_adamw else AdamW)(model.parameters(), lr=5e-5)
+    opt = torch.optim.AdamW(model.parameters(), lr=5e-5) if a.torch_adamw else AdamW(model.parameters(), lr=5e-5,
+                                                                                        capturable=a.graph)
     g = torch.Generator().manual_seed(100 + rank)
     va, mlm_a, lab_a = view(a.batch, a.len_a, cfg.vocab_size, 10 + rank, 21, cfg.vocab_size - 1, g)
     vb, mlm_b, lab_b = view(a.batch, a.len_b, cfg.vocab_size, 20 + rank, 96, cfg.vocab_size - 1, g)
@@ -84,6 +86,19 @@ def main():
         opt.zero_grad(set_to_none=True)
         return out
 
+    if a.graph:
+        if world > 1:
+            raise SystemExit("--graph: world 1 only (the bucketed all-reduce is not captured)")
+        from recformer_amd.graphs import CapturedTrainStep
+        captured = CapturedTrainStep(model, opt, batch, warmup=a.warmup)
+
+        class _Out:
+            cl_correct_num = -1
+
+        def step():  # noqa: F811 - the captured replay replaces the eager step
+            o = _Out()
+            o.loss = captured()
+            return o
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -102,7 +117,7 @@ def main():
                           "n_gpus": world, "batch_per_rank": a.batch, "len_a": a.len_a, "len_b": a.len_b,
                           "ms_per_step": round(1e3 * dt / a.steps, 2),
                           "seq_per_s": round(world * a.batch * a.steps / dt, 2),
-                          "loss": float(out.loss.detach()), "cl_correct": int(out.cl_correct_num),
+                          "loss": float(out.loss.detach()), "cl_correct": int(out.cl_correct_num), "graph": a.graph,
                           "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
