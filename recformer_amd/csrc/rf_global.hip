@@ -902,6 +902,122 @@ __global__ void __launch_bounds__(256) k_gfold_partial_f32(int Lp, int D, int H,
   }
 }
 
+// ---- bf16 merge + out on MFMA, 16 global rows per block (few global rows) ---------------------
+// grid (H, ceil(R/16)). For the C2 shape (R = 64: one CLS row per sequence) the 64-row kernel
+// launches only H blocks and the per-row GEMV kernel re-reads the head's Wvg slice once per row
+// (768 blocks x 96 KiB of L2 reads, phases serialised by barriers); here 4 x H blocks each DMA the
+// head's slice once, merge the chunk partials of 16 rows with all loads of a chunk in flight
+// (thread = row t/16, 4-column groups 4(t%16) + 64j), keep w as hi + lo 16-bit planes in LDS (rows
+// padded by 16 B: conflict-free B-operand reads) and wave w computes output columns 16w..16w+15 of
+// the 16 rows with v_mfma_f32_16x16x32 (A: the Wvg image, B: the w planes).
+template <typename E, int D>
+__global__ void __launch_bounds__(256) k_gfold_out16(int Lp, int R, int gmax, int nch,
+                                                      const E* __restrict__ wvg, const float* __restrict__ bvg,
+                                                      const int32_t* __restrict__ gidx, GfoldWs ws,
+                                                      E* __restrict__ out, int ldo, bool drop) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NK = D / 32;
+  constexpr int nseg = D >> 6;
+  constexpr int WLD = D + 8;  // w plane row stride (elements)
+  E* whi = reinterpret_cast<E*>(smem + D * 128);
+  E* wlo = whi + 16 * WLD;
+  float* bws = reinterpret_cast<float*>(wlo + 16 * WLD);
+  const int h = blockIdx.x, r0 = blockIdx.y * 16;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  for (int p = wave; p < nseg * 8; p += 4) {
+    const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
+    const int chk = (lane & 7) ^ (row & 7);
+    glds16(wvg + (int64_t)(h * 64 + row) * D + seg * 64 + chk * 8, smem + (seg * 64 + (p & 7) * 8) * 128);
+  }
+  // ---- merge: w[i] = sum_c exp(m_c - M) w_c / sum_c exp(m_c - M) l_c for row i = t / 16 ----
+  const int i = t >> 4, cb = 4 * (t & 15);
+  const int r = r0 + i;
+  const int pos = r < R ? gidx[r] : -1;
+  float4 acc[D / 64];
+#pragma unroll
+  for (int j = 0; j < D / 64; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the row's 16 threads hold chunk q = t % 16's max / sum (nch <= 16: one round of loads, lane
+  // shuffles instead of a load per chunk), then all of a chunk pair's w loads are in flight at once
+  float inv = 0.f, bw = 1.f;
+  if (pos >= 0) {
+    const int q = t & 15;
+    const int64_t mo = ((int64_t)r * nch + q) * GF_HP + h;
+    const float mq = q < nch ? ws.m[mo] : GF_NEG_INF;
+    const float lq = q < nch ? ws.l[mo] : 0.f;
+    const float dq = (drop && q < nch) ? ws.ld[mo] : 0.f;
+    float mx = mq;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
+    const float scq = mq == GF_NEG_INF ? 0.f : __expf(mq - mx);
+    float lsum = scq * lq, dsum = scq * dq;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      lsum += __shfl_xor(lsum, o, 16);
+      dsum += __shfl_xor(dsum, o, 16);
+    }
+    inv = lsum > 0.f ? 1.0f / lsum : 0.f;
+    bw = drop ? dsum * inv : 1.f;
+    const float scn = scq * inv;
+    const float* wrow = ws.w + ((int64_t)r * nch * GF_HP + h) * D + cb;
+    for (int c = 0; c < nch; c += 2) {
+      float4 x0[D / 64], x1[D / 64];
+      const bool two = c + 1 < nch;
+#pragma unroll
+      for (int j = 0; j < D / 64; ++j) {
+        x0[j] = *reinterpret_cast<const float4*>(wrow + (int64_t)c * GF_HP * D + 64 * j);
+        x1[j] = two ? *reinterpret_cast<const float4*>(wrow + (int64_t)(c + 1) * GF_HP * D + 64 * j)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const float s0 = __shfl(scn, c, 16), s1 = two ? __shfl(scn, c + 1, 16) : 0.f;
+#pragma unroll
+      for (int j = 0; j < D / 64; ++j) {
+        acc[j].x = fmaf(s1, x1[j].x, fmaf(s0, x0[j].x, acc[j].x));
+        acc[j].y = fmaf(s1, x1[j].y, fmaf(s0, x0[j].y, acc[j].y));
+        acc[j].z = fmaf(s1, x1[j].z, fmaf(s0, x0[j].z, acc[j].z));
+        acc[j].w = fmaf(s1, x1[j].w, fmaf(s0, x0[j].w, acc[j].w));
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < D / 64; ++j) {
+    const float v[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
+    V4 vh, vl;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      vh[k] = (E)v[k];
+      vl[k] = (E)(v[k] - (float)vh[k]);
+    }
+    *reinterpret_cast<V4*>(whi + i * WLD + cb + 64 * j) = vh;
+    *reinterpret_cast<V4*>(wlo + i * WLD + cb + 64 * j) = vl;
+  }
+  if ((t & 15) == 0) bws[i] = bw;
+  wait_vmcnt0();
+  __syncthreads();
+  // ---- out[row li][16 wave + 4g + k] = Wvg_h[16 wave + 4g + k] . w[li] + bvg ----
+  f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int s = 0; s < NK; ++s) {
+    const V8 wa = *reinterpret_cast<const V8*>(smem + gimg(16 * wave + li, 32 * s + 8 * g));
+    const V8 bh = *reinterpret_cast<const V8*>(whi + li * WLD + 32 * s + 8 * g);
+    const V8 bl = *reinterpret_cast<const V8*>(wlo + li * WLD + 32 * s + 8 * g);
+    o = mfma16(wa, bh, o);
+    o = mfma16(wa, bl, o);
+  }
+  const int ro = r0 + li;
+  const int po = ro < R ? gidx[ro] : -1;
+  if (po >= 0) {
+    const float bwr = bws[li];
+    const int d0 = h * 64 + 16 * wave + 4 * g;
+    V4 v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (E)(o[k] + (drop ? bvg[d0 + k] * bwr : bvg[d0 + k]));
+    *reinterpret_cast<V4*>(out + ((int64_t)(ro / gmax) * Lp + po) * ldo + d0) = v;
+  }
+}
+
 // ---- merge chunks + out = Wvg_h w_h + bvg_h -------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256) k_gfold_out(int Lp, int D, int gmax, int nch,
@@ -1016,7 +1132,20 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
         RF_REQUIRE(false, "rf_global_attn_fold(16-bit): unsupported hidden size %d", D);
     }
 #undef GP_
+    const size_t lds_16 = (size_t)D * 128 + (size_t)2 * 16 * (D + 8) * 2 + 16 * 4;
     if (!do_out) {
+    } else if (ld_out % 4 == 0 && !gfold_use_mfma(R, false) && g_knob[KNOB_GFOLD_PATH] != 1 && nch <= 16 &&
+               (D == 64 || D == 128 || D == 192 || D == 256 || D == 384 || D == 512 || D == 768) &&
+               lds_16 <= 160 * 1024) {
+#define G16_(DD)                                                                                \
+  case DD:                                                                                      \
+    (void)hipFuncSetAttribute((const void*)k_gfold_out16<E, DD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              (int)lds_16);                                                     \
+    k_gfold_out16<E, DD><<<dim3(H, (R + 15) / 16), 256, lds_16, s>>>(Lp, R, gmax, nch, (const E*)wvg, bvg, gidx, \
+                                                                  ws, (E*)out, ld_out, dr.thresh != 0); \
+    break;
+      switch (D) { G16_(64) G16_(128) G16_(192) G16_(256) G16_(384) G16_(512) G16_(768) default: break; }
+#undef G16_
     } else if (ld_out % 4 == 0 && gfold_use_mfma(R, false)) {
       const size_t lds_w = (size_t)D * 128;
 #define GO_(DD)                                                                                 \

@@ -16,6 +16,10 @@ from tools.kbench import timeit  # noqa: E402
 if os.environ.get("RF_GFOLD_GEMV"):  # tools/gpu/gf.sh: force the GEMV fold kernels
     from recformer_amd._lib import set_knob
     set_knob("gfold_path", 1)
+for kv in filter(None, os.environ.get("RF_KNOBS", "").split(",")):  # e.g. RF_KNOBS=gfold_qsplit=4
+    from recformer_amd._lib import set_knob
+    k, v = kv.split("=")
+    set_knob(k, int(v))
 
 
 def main():
