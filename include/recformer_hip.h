@@ -410,6 +410,25 @@ int rf_adamw_chunk(void);
 int rf_adamw_step(const rf_adamw_tensor* tensors, int ntensors, const int32_t* block_tensor, int nblocks,
                   rf_stream_t stream);
 
+/* Training-step weight packing (autocast's per-op weight casts, finetune.py:106-110): every
+ * descriptor's fp32 source (rows x cols, row-major, lda) rounded to the compute dtype (RF_BF16 /
+ * RF_F16) at row row_off of dst (ld_dst elements, may be NULL) and, if dstT is not NULL, transposed
+ * at column row_off of dstT (ld_T), the first scale_n source rows of the transposed copy multiplied
+ * by t_scale after rounding. One launch: workgroup b packs 64 x 64 tile b - first_tile of
+ * descriptor block_entry[b] (a descriptor owns ceil(rows/64) * ceil(cols/64) consecutive blocks). */
+typedef struct rf_pack_entry {
+  const float* src;
+  void* dst;
+  void* dstT;
+  int64_t lda, ld_dst, ld_T;
+  int64_t first_tile;
+  int32_t rows, cols, row_off, scale_n;
+  float t_scale;
+  int32_t pad_;
+} rf_pack_entry; /* 80 bytes */
+int rf_pack_weights(int dtype, const rf_pack_entry* entries, int nentries, const int32_t* block_entry, int nblocks,
+                    rf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

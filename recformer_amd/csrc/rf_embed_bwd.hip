@@ -11,22 +11,22 @@
 //   partials in block order.
 // Table gradients: the caller sorts a table's token indices (stable), giving keys (sorted) and perm;
 //   the rows src[perm[j]] are then summed per run of equal keys in three fixed-order levels:
-//   k_seg_partial  one wave per slice of 32 sorted positions: the sum of each run of equal keys inside
+//   k_seg_partial  one wave per slice of 16 sorted positions: the sum of each run of equal keys inside
 //                  the slice, stored at the run's first position (part, indexed by position);
-//   k_seg_chain    one wave per 1024 positions: the slice-start pieces that continue a segment
-//                  (keys[b] == keys[b-1], b a multiple of 32) summed per chain of consecutive slices,
+//   k_seg_chain    one wave per 256 positions: the slice-start pieces that continue a segment
+//                  (keys[b] == keys[b-1], b a multiple of 16) summed per chain of consecutive slices,
 //                  stored at the chain's first slice (part2, indexed by slice);
 //   k_seg_final    one wave per segment head h: part[h] + the chain starting at the first slice after h
-//                  + one chain per 1024-boundary inside the segment, written to dst[key].
+//                  + one chain per 256-boundary inside the segment, written to dst[key].
 //   Loads are issued in batches (indices broadcast from lanes, rows loaded 8 at a time) so a wave pays a
 //   few memory latencies per slice, not one per row; long segments (type / item-position tables) cost
-//   segment_length / 1024 chain reads at the head.
+//   segment_length / 256 chain reads at the head (64 per ballot round).
 #include "rf_common.h"
 
 namespace rf {
 
-constexpr int EB_SLICE = 32;     // sorted positions per k_seg_partial wave
-constexpr int EB_SUPER = 1024;   // positions per k_seg_chain wave (32 slices)
+constexpr int EB_SLICE = 16;     // sorted positions per k_seg_partial wave
+constexpr int EB_SUPER = 256;    // positions per k_seg_chain wave (16 slices)
 constexpr int EB_BLOCKS = 512;   // k_embed_ln_bwd blocks (4 waves each, grid-stride over the rows)
 
 template <int NV>
@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(1024) k_embed_affine_fin(int D, int nb, const 
   }
 }
 
-// level 1: runs of equal keys inside each 32-position slice -> part[run start]
+// level 1: runs of equal keys inside each 16-position slice -> part[run start]
 template <int NV>
 __global__ void __launch_bounds__(256) k_seg_partial(int M, int D, const float* __restrict__ src,
                                                      const int32_t* __restrict__ perm, const int32_t* __restrict__ keys,
@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(256) k_seg_partial(int M, int D, const float* 
   row_store<NV>(part + (int64_t)start * D, acc, lane, D);
 }
 
-// level 2: per 1024 positions, the continuation pieces at slice starts summed per chain -> part2[slice]
+// level 2: per 256 positions, the continuation pieces at slice starts summed per chain -> part2[slice]
 template <int NV>
 __global__ void __launch_bounds__(256) k_seg_chain(int M, int D, const int32_t* __restrict__ keys, int pad,
                                                    const float* __restrict__ part, float* __restrict__ part2) {
@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(256) k_seg_final(int M, int D, const int32_t* 
       row_load<NV>(r, part2 + (int64_t)(b1 / EB_SLICE) * D, lane, D);
       row_add<NV>(acc, r);
     }
-    // chains starting at the 1024-boundaries inside the segment, 64 boundaries per round
+    // chains starting at the 256-boundaries inside the segment, 64 boundaries per round
     for (int B0 = (b1 / EB_SUPER + 1) * EB_SUPER; B0 < M; B0 += 64 * EB_SUPER) {
       const int64_t Bl = (int64_t)B0 + (int64_t)lane * EB_SUPER;
       const bool in = Bl < M && keys[Bl] == key;

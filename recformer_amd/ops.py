@@ -18,7 +18,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_GELU_AUX,
 
 __all__ = [
     "dtype_code", "prepare_inputs", "embed_ln", "embed_ln_split", "add_layernorm_split", "join_split",
-    "gemm", "weight_grad", "embed_ln_bwd", "embedding_grad", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
+    "gemm", "weight_grad", "WeightPack", "embed_ln_bwd", "embedding_grad", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_GELU_AUX", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
@@ -344,6 +344,83 @@ def weight_grad(dc: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] =
                                 _p(out), _rowmajor(out, "out"), int(accumulate), _p(ws), ws.numel(), _stream(dc))
     check(rc, "rf_weight_grad")
     return out
+
+
+class WeightPack:
+    """Persistent compute-dtype copies of a fixed set of fp32 weights, refreshed by ONE rf_pack_weights
+    launch (the training step's weight casts and transposes). specs: dicts with src (fp32, 2-D,
+    row-major), dst / dstT ((tensor, row_off) or None: the row-major copy and the transposed copy),
+    scale_n / t_scale (the first scale_n source rows of the transposed copy scaled by t_scale). The
+    descriptors are copied to the device once, at construction (outside any graph capture); refresh()
+    only launches — it refuses sources that moved (rebuild the pack then)."""
+
+    _DESC = None
+
+    def __init__(self, specs, dtype: torch.dtype):
+        import numpy as np
+        if WeightPack._DESC is None:
+            WeightPack._DESC = np.dtype([("src", "<u8"), ("dst", "<u8"), ("dstT", "<u8"), ("lda", "<i8"),
+                                         ("ld_dst", "<i8"), ("ld_T", "<i8"), ("first_tile", "<i8"), ("rows", "<i4"),
+                                         ("cols", "<i4"), ("row_off", "<i4"), ("scale_n", "<i4"),
+                                         ("t_scale", "<f4"), ("pad", "<i4")])
+            assert WeightPack._DESC.itemsize == 80
+        if dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError("WeightPack: bf16 or fp16")
+        self.code = dtype_code(dtype)
+        self.specs = list(specs)
+        d = np.zeros(len(self.specs), dtype=WeightPack._DESC)
+        ntile, first = 0, []
+        for i, sp in enumerate(self.specs):
+            src = sp["src"]
+            if src.dtype != torch.float32 or src.dim() != 2 or src.stride(1) != 1 or not src.is_cuda:
+                raise ValueError("WeightPack: sources must be 2-D row-major fp32 CUDA tensors")
+            rows, cols = src.shape
+            dst, dstT = sp.get("dst"), sp.get("dstT")
+            for t, off, width in ((dst, 0, cols), (dstT, 1, rows)):
+                if t is not None:
+                    buf, ro = t
+                    if buf.dtype != dtype or buf.stride(1) != 1:
+                        raise ValueError("WeightPack: destinations must be row-major in the compute dtype")
+            d[i]["src"] = src.data_ptr()
+            d[i]["lda"] = src.stride(0)
+            d[i]["rows"], d[i]["cols"] = rows, cols
+            ro = None
+            if dst is not None:
+                buf, ro = dst
+                if ro + rows > buf.shape[0] or cols > buf.shape[1]:
+                    raise ValueError("WeightPack: dst too small")
+                d[i]["dst"], d[i]["ld_dst"] = buf.data_ptr(), buf.stride(0)
+            if dstT is not None:
+                buf, roT = dstT
+                if ro is not None and roT != ro:
+                    raise ValueError("WeightPack: dst and dstT take the same row offset")
+                ro = roT
+                if cols > buf.shape[0] or ro + rows > buf.shape[1]:
+                    raise ValueError("WeightPack: dstT too small")
+                d[i]["dstT"], d[i]["ld_T"] = buf.data_ptr(), buf.stride(0)
+            d[i]["row_off"] = ro or 0
+            d[i]["scale_n"] = int(sp.get("scale_n", 0))
+            d[i]["t_scale"] = float(sp.get("t_scale", 1.0))
+            d[i]["first_tile"] = ntile
+            first.append(ntile)
+            ntile += ((rows + 63) // 64) * ((cols + 63) // 64)
+        table = np.repeat(np.arange(len(self.specs), dtype=np.int32),
+                          [((sp["src"].shape[0] + 63) // 64) * ((sp["src"].shape[1] + 63) // 64) for sp in self.specs])
+        blob = np.concatenate([d.view(np.uint8), table.view(np.uint8)])
+        dev = self.specs[0]["src"].device
+        self.blob = torch.from_numpy(blob).to(dev)
+        self.nent, self.nblk = len(self.specs), int(table.size)
+        self.ptrs = tuple(sp["src"].data_ptr() for sp in self.specs)
+
+    def valid(self) -> bool:
+        return tuple(sp["src"].data_ptr() for sp in self.specs) == self.ptrs
+
+    def refresh(self):
+        if not self.valid():
+            raise RuntimeError("WeightPack: a source weight moved; build a new pack")
+        base = self.blob.data_ptr()
+        check(_lib.load().rf_pack_weights(self.code, base, self.nent, base + self.nent * 80, self.nblk,
+                                          _stream(self.blob)), "rf_pack_weights")
 
 
 def embed_ln_bwd(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, eps: float, dh: torch.Tensor):

@@ -35,6 +35,7 @@ equal torch's RNG draws, so dropout-on runs match the reference in distribution,
 from __future__ import annotations
 
 import math
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -143,6 +144,44 @@ class _Gemm(torch.autograd.Function):
         return da, dw, None, db, None, None
 
 
+class _GemmP(torch.autograd.Function):
+    """_Gemm over packed weights (ops.WeightPack, one rf_pack_weights launch per forward): the forward
+    reads the compute-dtype copy w16, the backward's dA = dC.W the packed transposed copy w16t (its
+    first scale_cols rows already multiplied by col_scale), and dW = dC^T.A is split by rows over the
+    masters — the fused q|k|v weight's three nn.Linear weights get their gradients as row blocks of
+    one rf_weight_grad result, with no concatenation in the forward and no split copy."""
+
+    @staticmethod
+    def forward(ctx, a, b, w16, w16t, scale_cols: int, col_scale: float, *masters):
+        ctx.save_for_backward(a, w16t)
+        ctx.sc = (scale_cols, col_scale)
+        ctx.rows = [m.shape[0] for m in masters]
+        ctx.wdt = masters[0].dtype
+        return ops.gemm(a.contiguous(), w16, b, ops.RF_EPI_BIAS, scale_cols=scale_cols, col_scale=col_scale)
+
+    @staticmethod
+    def backward(ctx, dc):
+        a, wt = ctx.saved_tensors
+        sc, s = ctx.sc
+        dc = dc.to(a.dtype).contiguous()
+        scaled = sc > 0 and s != 1.0
+        da = ops.gemm(dc, wt, None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
+        dw = _weight_grad(dc, a).to(ctx.wdt) if any(ctx.needs_input_grad[6:]) else None
+        db = ops.colsum(dc) if ctx.needs_input_grad[1] else None
+        if scaled:
+            if dw is not None:
+                dw[:sc] *= s
+            if db is not None:
+                db[:sc] *= s
+        dws = [None] * len(ctx.rows)
+        if dw is not None:
+            r0 = 0
+            for i, n in enumerate(ctx.rows):
+                dws[i] = dw[r0:r0 + n] if ctx.needs_input_grad[6 + i] else None
+                r0 += n
+        return (da, db, None, None, None, None, *dws)
+
+
 class _GemmGelu(torch.autograd.Function):
     """u = gelu(A.W^T + b) (TF:1107-1116) in one rf_gemm (EPI_BIAS_GELU_AUX), which also writes
     the bf16 pre-activation z the GELU backward needs (no separate GELU pass over z)."""
@@ -247,26 +286,30 @@ class _FFN(torch.autograd.Function):
     weight gradients (long token reductions) as for every Linear (_weight_grad, fp32)."""
 
     @staticmethod
-    def forward(ctx, a, w1, w1_16, b1, w2, w2_16, b2):
+    def forward(ctx, a, w1, w1_16, b1, w2, w2_16, b2, w1t=None, w2t=None):
         a = a.contiguous()
         z = torch.empty(a.shape[0], w1_16.shape[0], dtype=a.dtype, device=a.device)
         u = ops.gemm(a, w1_16, b1, ops.RF_EPI_BIAS_GELU_AUX, resid=z)
         t2 = ops.gemm(u, w2_16, b2, ops.RF_EPI_BIAS)
-        ctx.save_for_backward(a, u, z, w1_16, w2_16)
+        # the transposed copies dA needs: packed ones (ops.WeightPack) when given, else made here
+        ctx.save_for_backward(a, u, z, w1_16 if w1t is None else w1t, w2_16 if w2t is None else w2t)
+        ctx.packed = (w1t is not None, w2t is not None)
         ctx.wdt = (w1.dtype, w2.dtype)
         return t2
 
     @staticmethod
     def backward(ctx, dt2):
         a, u, z, w1, w2 = ctx.saved_tensors
+        w1t = w1 if ctx.packed[0] else w1.t().contiguous()
+        w2t = w2 if ctx.packed[1] else w2.t().contiguous()
         dt2 = dt2.to(a.dtype).contiguous()
-        dz = ops.gemm(dt2, w2.t().contiguous(), None, ops.RF_EPI_DGELU, resid=z)
+        dz = ops.gemm(dt2, w2t, None, ops.RF_EPI_DGELU, resid=z)
         dw2 = _weight_grad(dt2, u).to(ctx.wdt[1]) if ctx.needs_input_grad[4] else None
         db2 = ops.colsum(dt2) if ctx.needs_input_grad[6] else None
-        da = ops.gemm(dz, w1.t().contiguous(), None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
+        da = ops.gemm(dz, w1t, None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
         dw1 = _weight_grad(dz, a).to(ctx.wdt[0]) if ctx.needs_input_grad[1] else None
         db1 = ops.colsum(dz) if ctx.needs_input_grad[3] else None
-        return da, dw1, None, db1, dw2, None, db2
+        return da, dw1, None, db1, dw2, None, db2, None, None
 
 
 def _ln_backward(dy, x, mean, rstd, w):
@@ -769,6 +812,83 @@ def _layer_weights(li: int, lyr, dt: torch.dtype) -> dict:
     return _cast((id(lyr), li, dt), make)
 
 
+# One rf_pack_weights launch per forward writes every encoder GEMM weight's compute-dtype copy and
+# its transposed copy (ops.WeightPack, persistent buffers per model and dtype) — instead of a cast,
+# a q|k|v concatenation and, in the backward, a transpose (+ scaled clone) per weight per step.
+PACK_WEIGHTS = True
+_PACKS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _pack_sources(model):
+    out = []
+    for lyr in model.encoder.layer:
+        sa = lyr.attention.self
+        out += [sa.query.weight, sa.key.weight, sa.value.weight, sa.query_global.weight,
+                lyr.attention.output.dense.weight, lyr.intermediate.dense.weight, lyr.output.dense.weight]
+    return out
+
+
+def _encoder_pack(model, dt: torch.dtype, scale: float):
+    """(pack, per-layer buffers) for the model's current weights, (re)built when they moved."""
+    srcs = _pack_sources(model)
+    per = _PACKS.setdefault(model, {})
+    ent = per.get(dt)
+    if ent is not None and ent[2] == scale and ent[0].ptrs == tuple(w.data_ptr() for w in srcs):
+        return ent
+    layers, specs = [], []
+    for li, lyr in enumerate(model.encoder.layer):
+        q, k, v, qg, o, f1, f2 = (w.detach() for w in srcs[7 * li:7 * li + 7])
+        D, Fd = q.shape[1], f1.shape[0]
+
+        def e(*shape):
+            return torch.empty(*shape, dtype=dt, device=q.device)
+        bufs = {"qkv": (e(3 * D, D), e(D, 3 * D)), "qg": (e(D, D), e(D, D)), "o": (e(D, D), e(D, D)),
+                "f1": (e(Fd, D), e(D, Fd)), "f2": (e(D, Fd), e(Fd, D))}
+        qb, qt = bufs["qkv"]
+        specs += [dict(src=q, dst=(qb, 0), dstT=(qt, 0), scale_n=D, t_scale=scale),
+                  dict(src=k, dst=(qb, D), dstT=(qt, D)), dict(src=v, dst=(qb, 2 * D), dstT=(qt, 2 * D)),
+                  dict(src=qg, dst=(bufs["qg"][0], 0), dstT=(bufs["qg"][1], 0), scale_n=D, t_scale=scale),
+                  dict(src=o, dst=(bufs["o"][0], 0), dstT=(bufs["o"][1], 0)),
+                  dict(src=f1, dst=(bufs["f1"][0], 0), dstT=(bufs["f1"][1], 0)),
+                  dict(src=f2, dst=(bufs["f2"][0], 0), dstT=(bufs["f2"][1], 0))]
+        layers.append(bufs)
+    ent = (ops.WeightPack(specs, dt), layers, scale)
+    per[dt] = ent
+    return ent
+
+
+def _packed_layer_weights(model, dt: torch.dtype, scale: float):
+    """Per-layer weights for the packed path, the pack refreshed once per forward (once per step
+    under shared_casts, the four pretraining passes)."""
+    def make():
+        pack, layers, _ = _encoder_pack(model, dt, scale)
+        pack.refresh()
+        out = []
+        for lyr, bufs in zip(model.encoder.layer, layers):
+            sa, ao, fo = lyr.attention.self, lyr.attention.output, lyr.output
+            out.append({
+                "packed": True,
+                "w_qkv": ((sa.query.weight, sa.key.weight, sa.value.weight),) + bufs["qkv"],
+                "b_qkv": torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0).float(),
+                "w_qg": ((sa.query_global.weight,),) + bufs["qg"], "b_qg": sa.query_global.bias.float(),
+                "w_kg": sa.key_global.weight.to(dt), "b_kg": sa.key_global.bias.float(),
+                "w_vg": sa.value_global.weight.to(dt), "b_vg": sa.value_global.bias.float(),
+                "w_o": ((ao.dense.weight,),) + bufs["o"], "b_o": ao.dense.bias.float(),
+                "w_1": ((lyr.intermediate.dense.weight,),) + bufs["f1"], "b_1": lyr.intermediate.dense.bias.float(),
+                "w_2": ((fo.dense.weight,),) + bufs["f2"], "b_2": fo.dense.bias.float(),
+            })
+        return out
+    return _cast(("pack", id(model), dt, scale), make)
+
+
+def _lin(a, lw, wkey: str, bkey: str, scale_cols: int, col_scale: float):
+    """One of the layer's Linears: _GemmP over the packed weights, or _Gemm (master, w16)."""
+    if lw.get("packed"):
+        masters, w16, w16t = lw[wkey]
+        return _GemmP.apply(a, lw[bkey], w16, w16t, scale_cols, col_scale, *masters)
+    return _Gemm.apply(a, *lw[wkey], lw[bkey], scale_cols, col_scale)
+
+
 def encode_train(model, input_ids, attention_mask, global_attention_mask, token_type_ids,
                  position_ids, item_position_ids, output_hidden_states: bool
                  ) -> Tuple[torch.Tensor, Optional[tuple]]:
@@ -818,18 +938,21 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     # the pass's dropout seeds (two LayerNorms per layer) in one draw from torch's CPU generator
     seeds = torch.randint(0, 2 ** 62, (2 * nl,)).tolist() if p_hid > 0 else [0] * (2 * nl)
     att_seeds = torch.randint(0, 2 ** 62, (nl,)).tolist() if p_att > 0 else [0] * nl
+    packed = None
+    if PACK_WEIGHTS and fused and FFN_FUSED and D % 64 == 0 and cfg.intermediate_size % 64 == 0 and input_ids.is_cuda:
+        packed = _packed_layer_weights(model, dt, scale)
     for li, lyr in enumerate(model.encoder.layer):
-        lw = _layer_weights(li, lyr, dt)
+        lw = packed[li] if packed is not None else _layer_weights(li, lyr, dt)
         h = h16 if h16 is not None else h32.to(dt)
-        qkv = _Gemm.apply(h, *lw["w_qkv"], lw["b_qkv"], D, scale)
+        qkv = _lin(h, lw, "w_qkv", "b_qkv", D, scale)
         qg = None
         if gmax > 0:
             hg = h[rows] * gvalid.to(h.dtype)
-            qg = _Gemm.apply(hg, *lw["w_qg"], lw["b_qg"], D, scale)
+            qg = _lin(hg, lw, "w_qg", "b_qg", D, scale)
         ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
                                flags, gidx, B, Lp, H, windows[li] // 2, fold, grows, p_att, att_seeds[li])
         ao = lyr.attention.output
-        t = _Gemm.apply(ctx, *lw["w_o"], lw["b_o"], 0, 1.0)
+        t = _lin(ctx, lw, "w_o", "b_o", 0, 1.0)
         if fused:
             a32, a16 = _DropAddLN.apply(t, h32, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid, True,
                                         seeds[2 * li])
@@ -838,7 +961,11 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
             a32 = _LayerNorm.apply(x1, ao.LayerNorm.weight.float(), ao.LayerNorm.bias.float(), eps, torch.float32)
             a16 = a32.to(dt)
         fo = lyr.output
-        if fused and FFN_FUSED and D % 64 == 0 and lw["w_1"][1].shape[0] % 64 == 0:
+        if lw.get("packed"):
+            (w1,), w1_16, w1t = lw["w_1"]
+            (w2,), w2_16, w2t = lw["w_2"]
+            t2 = _FFN.apply(a16, w1, w1_16, lw["b_1"], w2, w2_16, lw["b_2"], w1t, w2t)
+        elif fused and FFN_FUSED and D % 64 == 0 and lw["w_1"][1].shape[0] % 64 == 0:
             t2 = _FFN.apply(a16, *lw["w_1"], lw["b_1"], *lw["w_2"], lw["b_2"])
         else:
             if dt == torch.bfloat16 and FUSED_GELU:

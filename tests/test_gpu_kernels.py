@@ -780,7 +780,7 @@ def test_band_pipe3_bit_identical_to_pipe2(dev, dt, case):
 def test_embedding_grad_matches_index_add(dev, M, D, V, kind):
     """rf_segment_rows_sum (nn.Embedding's dense backward, models.py:82-138) against an fp64 index_add:
     word-like ids with a frequent padding id (1, no gradient at that row) and repeated common tokens,
-    position ids, a 4-value type table whose segment spans more than 64 x 1024 sorted positions (two
+    position ids, a 4-value type table whose segment spans more than 64 x 256 sorted positions (several
     ballot rounds of 1024-boundary chains), item positions, ragged D (100: not a multiple of 256),
     a single row, and an all-padding input; deterministic (bit-identical on a repeat)."""
     g = torch.Generator(device="cpu").manual_seed(M + D + V)
@@ -851,3 +851,46 @@ def test_embed_ln_bwd_matches_autograd(dev, M, D):
     for a, b in zip(grads[True], grads[False]):
         assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-6
     assert float(grads[True][0][1].abs().max()) == 0.0 and float(grads[True][1][1].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_weight_pack_matches_torch_casts(dev, dt):
+    """rf_pack_weights (ops.WeightPack): row-major compute-dtype copies and transposed copies of fp32
+    sources, three sources stacked into one destination (the fused q|k|v weight), the first rows of
+    the transposed copy scaled after rounding (round(round(w) * s), the q-column scale), ragged shapes
+    (not multiples of 64), a source view with a row stride, a transposed-only and a plain-only entry:
+    bit-identical to torch's .to(dt) / .t() / the scaled clone; refresh() re-reads updated sources."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    q, k, v = (torch.randn(200, 136, generator=g).to(dev) for _ in range(3))
+    big = torch.randn(70, 300, generator=g).to(dev)
+    view = big[:, 20:220]                       # lda 300
+    w5 = torch.randn(64, 64, generator=g).to(dev)
+    w6 = torch.randn(33, 100, generator=g).to(dev)
+    qb, qt = torch.empty(600, 136, dtype=dt, device=dev), torch.empty(136, 600, dtype=dt, device=dev)
+    vb, vt = torch.empty(70, 200, dtype=dt, device=dev), torch.empty(200, 70, dtype=dt, device=dev)
+    t5 = torch.empty(64, 64, dtype=dt, device=dev)
+    b6 = torch.empty(33, 100, dtype=dt, device=dev)
+    s = 0.125
+    pack = ops.WeightPack([dict(src=q, dst=(qb, 0), dstT=(qt, 0), scale_n=200, t_scale=s),
+                           dict(src=k, dst=(qb, 200), dstT=(qt, 200)), dict(src=v, dst=(qb, 400), dstT=(qt, 400)),
+                           dict(src=view, dst=(vb, 0), dstT=(vt, 0), scale_n=17, t_scale=0.3),
+                           dict(src=w5, dstT=(t5, 0)), dict(src=w6, dst=(b6, 0))], dt)
+    for rnd in range(2):
+        pack.refresh()
+        cat = torch.cat([q, k, v]).to(dt)
+        assert torch.equal(qb, cat)
+        ref_t = cat.clone()
+        ref_t[:200] *= s
+        assert torch.equal(qt, ref_t.t())
+        vr = view.to(dt)
+        assert torch.equal(vb, vr)
+        vrt = vr.clone()
+        vrt[:17] = (vrt[:17].float() * 0.3).to(dt)
+        assert torch.equal(vt, vrt.t())
+        assert torch.equal(t5, w5.to(dt).t())
+        assert torch.equal(b6, w6.to(dt))
+        with torch.no_grad():
+            for w in (q, k, v, big, w5, w6):
+                w.mul_(1.5)
+    with pytest.raises(ValueError):
+        ops.WeightPack([dict(src=q.t(), dst=(qb, 0))], dt)
