@@ -10,3 +10,5 @@ timeout -k 10 300 python tools/train_bench.py --steps 8 --warmup 2 --graph > gpu
 tail -1 gpurun_out/r03_pack_graph.log
 timeout -k 10 300 python tools/pretrain_bench.py --batch 4 --steps 6 --warmup 2 --graph > gpurun_out/r03_pack_c4.log 2>&1 || { tail -20 gpurun_out/r03_pack_c4.log; exit 1; }
 tail -1 gpurun_out/r03_pack_c4.log
+timeout -k 10 300 python tools/train_opprof.py > gpurun_out/r03_opprof2.txt 2>&1 || { tail -5 gpurun_out/r03_opprof2.txt; exit 1; }
+tail -1 gpurun_out/r03_pack_c4.log
