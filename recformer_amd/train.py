@@ -70,6 +70,9 @@ FFN_FUSED = True
 # 16-bit: dA = dC.W of the other Linears (qkv, query_global, out-proj) on rf_gemm against a
 # transposed weight copy instead of hipBLASLt
 DA_RF_GEMM = True
+# below this many rows (the global query rows' Linear: B*G rows) the backward's dA / dW are single
+# library GEMMs: the 256 x 256-tile kernels would run one mostly empty K-step per tile
+SMALL_M = 512
 
 
 # ------------------------------------------------------------------------------------------
@@ -89,6 +92,10 @@ def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
     S chunks computed as one batched GEMM (S times the tiles) and the S fp32 partials summed."""
     M, N = dc.shape
     K = a.shape[1]
+    if M < SMALL_M and dc.is_cuda and dc.dtype != torch.float32:
+        # a few rows (the global query rows): one library GEMM with fp32 output (the big-tile
+        # kernels would run one mostly empty K-step per tile)
+        return _mm_f32(dc.t(), a)
     if (DW_HIP and dc.is_cuda and dc.dtype in (torch.bfloat16, torch.float16) and a.dtype == dc.dtype
             and N % 16 == 0 and K % 16 == 0 and dc.stride(1) == 1 and a.stride(1) == 1
             and dc.stride(0) % 8 == 0 and a.stride(0) % 8 == 0
@@ -165,7 +172,9 @@ class _GemmP(torch.autograd.Function):
         sc, s = ctx.sc
         dc = dc.to(a.dtype).contiguous()
         scaled = sc > 0 and s != 1.0
-        da = ops.gemm(dc, wt, None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
+        da = None
+        if ctx.needs_input_grad[0]:
+            da = dc @ wt.t() if dc.shape[0] < SMALL_M else ops.gemm(dc, wt, None, ops.RF_EPI_NONE)
         dw = _weight_grad(dc, a).to(ctx.wdt) if any(ctx.needs_input_grad[6:]) else None
         db = ops.colsum(dc) if ctx.needs_input_grad[1] else None
         if scaled:
@@ -624,7 +633,10 @@ class _Attention(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold, grows=None,
-                attn_p: float = 0.0, seed: int = 0):
+                attn_p: float = 0.0, seed: int = 0, wkg_master=None, wvg_master=None):
+        # wkg / wvg: the global key / value weights in the compute dtype; with the masters given
+        # (packed copies, not tracked) their gradients go to the fp32 masters directly
+        ctx.masters = wkg_master is not None
         D = qkv.shape[1] // 3
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         G = gidx.shape[1]
@@ -699,7 +711,7 @@ class _Attention(torch.autograd.Function):
             # added into dk / dv at the global positions (bf16, as dqkv) by one small kernel
             ops.scatter_add_rows(rows32, dkg.to(dk.dtype).contiguous(), dk, dvg.to(dv.dtype).contiguous(), dv)
             # global branch: closed-form gradient of the fold algebra
-            if any(ctx.needs_input_grad[1:7]):
+            if any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]):
                 gout = dout[rows].float() * keep[:, None].to(torch.float32)
                 gz = None
                 if ctx.gz_kind == "hip":  # the forward's mask, from the same kernel
@@ -719,16 +731,25 @@ class _Attention(torch.autograd.Function):
                     if ctx.needs_input_grad[1 + n]:
                         g = grads[n]
                         res[1 + n] = None if g is None else g.to(t.dtype)
+                if ctx.masters:  # fp32 gradients straight to the masters (no bf16 round trip)
+                    extra = [grads[2].float() if ctx.needs_input_grad[17] and grads[2] is not None else None,
+                             grads[4].float() if ctx.needs_input_grad[18] and grads[4] is not None else None]
         if ctx.needs_input_grad[0]:
             res[0] = dqkv.to(qkv.dtype)
-        return (*res, None, None, None, None, None, None, None, None, None, None)
+        tail = [None] * 12  # the forward's non-tensor inputs, then the two masters
+        if ctx.masters and gmax > 0 and (any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19])):
+            tail[10:] = extra
+        return (*res, *tail)
 
     @staticmethod
     def _backward_torch(ctx, dout):
         qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, _ = ctx.saved_tensors
         B, Lp, H, half_w = ctx.dims
         D = qkv.shape[1] // 3
-        need = ctx.needs_input_grad
+        need = list(ctx.needs_input_grad)
+        if ctx.masters:  # gradients of the packed copies go to the masters
+            need[3] = need[3] or need[17]
+            need[5] = need[5] or need[18]
         inputs = [t.detach().requires_grad_(nd) for t, nd in
                   zip((qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], qg, h, wkg, bkg, wvg, bvg),
                       (need[0],) * 3 + tuple(need[1:7]))]
@@ -749,7 +770,12 @@ class _Attention(torch.autograd.Function):
             res = [torch.cat(z, 1)] + res[3:]
         else:
             res = [None] + res[3:]
-        return (*res, None, None, None, None, None, None, None, None, None, None)
+        tail = [None] * 12  # the forward's non-tensor inputs, then the two masters
+        if ctx.masters:
+            g_k, g_v = res[3], res[5]
+            res[3] = res[5] = None
+            tail[10:] = [None if g_k is None else g_k.float(), None if g_v is None else g_v.float()]
+        return (*res, *tail)
 
 
 # ------------------------------------------------------------------------------------------
@@ -824,7 +850,8 @@ def _pack_sources(model):
     for lyr in model.encoder.layer:
         sa = lyr.attention.self
         out += [sa.query.weight, sa.key.weight, sa.value.weight, sa.query_global.weight,
-                lyr.attention.output.dense.weight, lyr.intermediate.dense.weight, lyr.output.dense.weight]
+                lyr.attention.output.dense.weight, lyr.intermediate.dense.weight, lyr.output.dense.weight,
+                sa.key_global.weight, sa.value_global.weight]
     return out
 
 
@@ -837,20 +864,21 @@ def _encoder_pack(model, dt: torch.dtype, scale: float):
         return ent
     layers, specs = [], []
     for li, lyr in enumerate(model.encoder.layer):
-        q, k, v, qg, o, f1, f2 = (w.detach() for w in srcs[7 * li:7 * li + 7])
+        q, k, v, qg, o, f1, f2, kg, vg = (w.detach() for w in srcs[9 * li:9 * li + 9])
         D, Fd = q.shape[1], f1.shape[0]
 
         def e(*shape):
             return torch.empty(*shape, dtype=dt, device=q.device)
         bufs = {"qkv": (e(3 * D, D), e(D, 3 * D)), "qg": (e(D, D), e(D, D)), "o": (e(D, D), e(D, D)),
-                "f1": (e(Fd, D), e(D, Fd)), "f2": (e(D, Fd), e(Fd, D))}
+                "f1": (e(Fd, D), e(D, Fd)), "f2": (e(D, Fd), e(Fd, D)), "kg": e(D, D), "vg": e(D, D)}
         qb, qt = bufs["qkv"]
         specs += [dict(src=q, dst=(qb, 0), dstT=(qt, 0), scale_n=D, t_scale=scale),
                   dict(src=k, dst=(qb, D), dstT=(qt, D)), dict(src=v, dst=(qb, 2 * D), dstT=(qt, 2 * D)),
                   dict(src=qg, dst=(bufs["qg"][0], 0), dstT=(bufs["qg"][1], 0), scale_n=D, t_scale=scale),
                   dict(src=o, dst=(bufs["o"][0], 0), dstT=(bufs["o"][1], 0)),
                   dict(src=f1, dst=(bufs["f1"][0], 0), dstT=(bufs["f1"][1], 0)),
-                  dict(src=f2, dst=(bufs["f2"][0], 0), dstT=(bufs["f2"][1], 0))]
+                  dict(src=f2, dst=(bufs["f2"][0], 0), dstT=(bufs["f2"][1], 0)),
+                  dict(src=kg, dst=(bufs["kg"], 0)), dict(src=vg, dst=(bufs["vg"], 0))]
         layers.append(bufs)
     ent = (ops.WeightPack(specs, dt), layers, scale)
     per[dt] = ent
@@ -871,8 +899,8 @@ def _packed_layer_weights(model, dt: torch.dtype, scale: float):
                 "w_qkv": ((sa.query.weight, sa.key.weight, sa.value.weight),) + bufs["qkv"],
                 "b_qkv": torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0).float(),
                 "w_qg": ((sa.query_global.weight,),) + bufs["qg"], "b_qg": sa.query_global.bias.float(),
-                "w_kg": sa.key_global.weight.to(dt), "b_kg": sa.key_global.bias.float(),
-                "w_vg": sa.value_global.weight.to(dt), "b_vg": sa.value_global.bias.float(),
+                "w_kg": bufs["kg"], "b_kg": sa.key_global.bias.float(), "wkg_master": sa.key_global.weight,
+                "w_vg": bufs["vg"], "b_vg": sa.value_global.bias.float(), "wvg_master": sa.value_global.weight,
                 "w_o": ((ao.dense.weight,),) + bufs["o"], "b_o": ao.dense.bias.float(),
                 "w_1": ((lyr.intermediate.dense.weight,),) + bufs["f1"], "b_1": lyr.intermediate.dense.bias.float(),
                 "w_2": ((fo.dense.weight,),) + bufs["f2"], "b_2": fo.dense.bias.float(),
@@ -950,7 +978,8 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
             hg = h[rows] * gvalid.to(h.dtype)
             qg = _lin(hg, lw, "w_qg", "b_qg", D, scale)
         ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
-                               flags, gidx, B, Lp, H, windows[li] // 2, fold, grows, p_att, att_seeds[li])
+                               flags, gidx, B, Lp, H, windows[li] // 2, fold, grows, p_att, att_seeds[li],
+                               lw.get("wkg_master"), lw.get("wvg_master"))
         ao = lyr.attention.output
         t = _lin(ctx, lw, "w_o", "b_o", 0, 1.0)
         if fused:
