@@ -429,6 +429,20 @@ typedef struct rf_pack_entry {
 int rf_pack_weights(int dtype, const rf_pack_entry* entries, int nentries, const int32_t* block_entry, int nblocks,
                     rf_stream_t stream);
 
+/* Training backward of the global rows through the fold (autograd of TF:964-1057; closed form of
+ * train._global_bwd) in one pass over h, from the forward's fold workspace (rf_global_attn_fold_fwd_drop
+ * with the same arguments; kept between forward and backward). dw: (B*gmax, 16, D) fp32 = Wvg_h^T do_h
+ * per head (heads >= H zero); cb: (B*gmax, 16) fp32 = do_h . bvg_h (attention dropout only, else NULL).
+ * Outputs: dh (B*Lp rows, lddh, 16-bit) = the global branch's gradient of h; du (B*gmax, 16, D) fp32
+ * (dq = Wkg du, dWkg = q du^T per head); w (B*gmax, 16, D) fp32 = sum_j p'_j h_j (dWvg = do w^T);
+ * stats (B*gmax, 16, 4) fp32 = (M, 1/L, Delta, S'), S' = sum_j p'_j (dbvg = do S'). 16-bit, D a multiple
+ * of 128 up to 768, gmax <= 4. Workspace: rf_global_fold_bwd_workspace bytes. */
+size_t rf_global_fold_bwd_workspace(int B, int Lp, int D, int gmax);
+int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const uint8_t* flags,
+                       const int32_t* gidx, int gmax, const void* fwd_workspace, const float* dw, const float* cb,
+                       float p_drop, uint64_t seed, void* dh, int lddh, float* du, float* w, float* stats,
+                       void* workspace, rf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1332,3 +1332,340 @@ extern "C" int rf_global_attn_fold_h_fwd(int dtype, int B, int Lp, int D, int H,
   return rf_global_attn_fold_h_stage(3, dtype, B, Lp, D, H, h, ldh, wqg, bqg, q_scale, wkg, bkg, wvg, bvg, flags,
                                      gidx, gmax, workspace, out, ld_out, stream);
 }
+
+
+// =====================================================================================================
+// Backward of the global rows through the fold algebra (TF:964-1057 under autograd; the closed form of
+// recformer_amd/train.py _global_bwd) in ONE pass over h, from the forward's fold workspace (u planes,
+// per-chunk softmax statistics and w partials, which the caller keeps between forward and backward).
+// Per global row r and head h, with dw_h = Wvg_h^T do_h (given, fp32) and c_h = do_h . bvg_h (dropout):
+//   M, L       the merged softmax statistics;  w_h = sum_j p'_j h_j (merged partials);  S'_h = sum_j p'_j
+//   Delta_h    = dw_h . w_h + c_h S'_h  (= sum_j p_j dp_j: no pass over h needed for it)
+//   s_j = u_h . h_j,  p_j = exp(s_j - M) / L,  p'_j = p_j z_j,  dp_j = (dw_h . h_j + c_h) z_j,
+//   ds_j = p_j (dp_j - Delta_h),  du_h = sum_j ds_j h_j,  dh_j = sum_{g, h} (p'_j dw_h + ds_j u_h)
+// k_gbwd_prep (R, 16): merges w, S' and the statistics, writes dw as hi + lo 16-bit planes and the
+//   dh product's operand [dw_hi ; u_hi] transposed (per column, 32 values: 16 B per MFMA fragment);
+// k_gbwd_main (Lp/64, B): one 64-row chunk of one sequence for all of its global rows: the chunk DMA'd
+//   once; the s and dp products on MFMA with the reduction over D split by k range across the 4 waves
+//   and summed in LDS (the u / dw fragments of a quarter of D fit the registers); the softmax backward
+//   per (row, head); du partial = dS^T.H (transposed LDS reads, as the forward's P.H); dh = [p' | ds] .
+//   [dw ; u] on MFMA (K = 32 per global row), staged through LDS and stored as whole lines;
+// k_gbwd_reduce: du = sum of the chunk partials in chunk order (deterministic).
+namespace rf {
+
+constexpr int GB_ROWS = 64;  // rows per k_gbwd_main block
+constexpr int GB_GMAX = 4;   // global rows per sequence the kernel takes (more: the torch path)
+
+template <typename E>
+__global__ void __launch_bounds__(256) k_gbwd_prep(int D, int H, int nch, const int32_t* __restrict__ gidx,
+                                                   GfoldWs ws, const float* __restrict__ dw,
+                                                   const float* __restrict__ cb, int drop, float* __restrict__ wout,
+                                                   float* __restrict__ st, E* __restrict__ dwp, E* __restrict__ bt) {
+  __shared__ float red[4];
+  const int r = blockIdx.x, h = blockIdx.y, t = threadIdx.x;
+  const bool live = h < H && gidx[r] >= 0;
+  float M = GF_NEG_INF, L = 0.f, LD = 0.f;
+  if (live) {
+    for (int c = 0; c < nch; ++c) M = fmaxf(M, ws.m[((int64_t)r * nch + c) * GF_HP + h]);
+    for (int c = 0; c < nch; ++c) {
+      const float mc = ws.m[((int64_t)r * nch + c) * GF_HP + h];
+      const float sc = mc == GF_NEG_INF ? 0.f : __expf(mc - M);
+      L += sc * ws.l[((int64_t)r * nch + c) * GF_HP + h];
+      if (drop) LD += sc * ws.ld[((int64_t)r * nch + c) * GF_HP + h];
+    }
+  }
+  const float inv = L > 0.f ? 1.0f / L : 0.f;
+  const float Sp = live ? (drop ? LD * inv : 1.f) : 0.f;
+  const float c = (live && cb) ? cb[r * GF_HP + h] : 0.f;
+  const E* u16 = reinterpret_cast<const E*>(ws.u16);
+  float dsum = 0.f;
+  for (int k = t; k < D; k += 256) {
+    float wv = 0.f, dv = 0.f;
+    E uh = (E)0.f;
+    if (live) {
+      for (int cc = 0; cc < nch; ++cc) {
+        const float mc = ws.m[((int64_t)r * nch + cc) * GF_HP + h];
+        const float sc = (mc == GF_NEG_INF ? 0.f : __expf(mc - M)) * inv;
+        wv += sc * ws.w[(((int64_t)r * nch + cc) * GF_HP + h) * D + k];
+      }
+      dv = dw[((int64_t)r * GF_HP + h) * D + k];
+      uh = u16[((int64_t)r * 2 * GF_HP + h) * D + k];
+    }
+    wout[((int64_t)r * GF_HP + h) * D + k] = wv;
+    dsum += dv * wv;
+    const E hi = (E)dv, lo = (E)(dv - (float)hi);
+    dwp[((int64_t)r * 2 * GF_HP + h) * D + k] = hi;
+    dwp[((int64_t)r * 2 * GF_HP + GF_HP + h) * D + k] = lo;
+    bt[((int64_t)r * D + k) * 32 + h] = hi;
+    bt[((int64_t)r * D + k) * 32 + 16 + h] = uh;
+  }
+  dsum = wave_sum(dsum);
+  if ((t & 63) == 0) red[t >> 6] = dsum;
+  __syncthreads();
+  if (t == 0) {
+    float* o = st + ((int64_t)r * GF_HP + h) * 4;
+    o[0] = live ? M : 0.f;
+    o[1] = inv;
+    o[2] = ((red[0] + red[1]) + red[2]) + red[3] + c * Sp;
+    o[3] = Sp;
+  }
+}
+
+template <typename E, int D>
+__global__ void __launch_bounds__(256) k_gbwd_main(int Lp, int gmax, int H, const E* __restrict__ hs, int ldh,
+                                                   const uint8_t* __restrict__ flags, const int32_t* __restrict__ gidx,
+                                                   GfoldWs ws, const E* __restrict__ dwp, const E* __restrict__ bt,
+                                                   const float* __restrict__ st, const float* __restrict__ cb,
+                                                   float* __restrict__ dupart, E* __restrict__ dh, int lddh,
+                                                   AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NK = D / 32;
+  constexpr int nseg = D >> 6;
+  constexpr int KW = NK / 4;   // k-steps of the s / dp products per wave
+  constexpr int nmt = D >> 6;  // du column tiles per wave
+  char* himg = smem;
+  float* red = reinterpret_cast<float*>(smem + D * 128);                  // [2][4][64][16]
+  E* pds = reinterpret_cast<E*>(smem + D * 128 + 2 * 4 * 64 * 16 * 4);    // [GB_GMAX][64][32]
+  const int ch = blockIdx.x, b = blockIdx.y, nch2 = gridDim.x;
+  const int j0 = ch * GB_ROWS;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int q4 = li >> 2, p4 = li & 3;
+  const E* hb = hs + (int64_t)b * Lp * ldh;
+  for (int p = wave; p < nseg * 8; p += 4) {
+    const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
+    const int chk = (lane & 7) ^ (row & 7);
+    const int jr = min(j0 + row, Lp - 1);
+    glds16(hb + (int64_t)jr * ldh + seg * 64 + chk * 8, himg + (seg * 64 + (p & 7) * 8) * 128);
+  }
+  const int jv = j0 + lane;
+  const bool okv = jv < Lp && flags[(int64_t)b * Lp + min(jv, Lp - 1)] != 0;
+  const unsigned long long vm = __ballot(okv);
+  wait_vmcnt0();
+  __syncthreads();
+  const E* u16 = reinterpret_cast<const E*>(ws.u16);
+  int ng = 0;
+  for (int gq = 0; gq < gmax; ++gq) {
+    const int r = b * gmax + gq;
+    const int pos = gidx[r];
+    if (pos < 0) continue;
+    // ---- s and dp over this wave's k range: S^T[row][head] = h_row . u_head ----
+    {
+      V8 uhf[KW], ulf[KW], dhf[KW], dlf[KW];
+      const E* up = u16 + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
+      const E* dq = dwp + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
+#pragma unroll
+      for (int kk = 0; kk < KW; ++kk) {
+        const int s2 = wave * KW + kk;
+        uhf[kk] = *reinterpret_cast<const V8*>(up + 32 * s2);
+        ulf[kk] = *reinterpret_cast<const V8*>(up + GF_HP * D + 32 * s2);
+        dhf[kk] = *reinterpret_cast<const V8*>(dq + 32 * s2);
+        dlf[kk] = *reinterpret_cast<const V8*>(dq + GF_HP * D + 32 * s2);
+      }
+      f32x4 sa[4], da[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) sa[t] = da[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KW; ++kk) {
+        const int s2 = wave * KW + kk;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const V8 a = *reinterpret_cast<const V8*>(himg + gimg(16 * t + li, 32 * s2 + 8 * g));
+          sa[t] = mfma16(a, uhf[kk], sa[t]);
+          sa[t] = mfma16(a, ulf[kk], sa[t]);
+          da[t] = mfma16(a, dhf[kk], da[t]);
+          da[t] = mfma16(a, dlf[kk], da[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 16 * t + 4 * g + i;
+          red[((0 * 4 + wave) * 64 + row) * 16 + li] = sa[t][i];
+          red[((1 * 4 + wave) * 64 + row) * 16 + li] = da[t][i];
+        }
+    }
+    __syncthreads();
+    // ---- softmax backward per (row, head): thread -> row t/4, heads 4 (t%4) .. +3 ----
+    {
+      const int jr = threadIdx.x >> 2, h0 = (threadIdx.x & 3) * 4;
+      const int j = j0 + jr;
+      const bool ok = (vm >> jr) & 1ull;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int hh = h0 + k;
+        float s = 0.f, dpv = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          s += red[((0 * 4 + w) * 64 + jr) * 16 + hh];
+          dpv += red[((1 * 4 + w) * 64 + jr) * 16 + hh];
+        }
+        const float* sp = st + ((int64_t)r * GF_HP + hh) * 4;
+        const bool live = ok && hh < H;
+        const float p = live ? __expf(s - sp[0]) * sp[1] : 0.f;
+        const float z = (live && dr.thresh) ? attn_keep_scale(dr, ((uint64_t)b * H + hh) * Lp + pos, Lp, j) : 1.f;
+        const float c = cb ? cb[r * GF_HP + hh] : 0.f;
+        const float ds = p * ((dpv + c) * z - sp[2]);
+        pds[(ng * 64 + jr) * 32 + hh] = (E)(p * z);
+        pds[(ng * 64 + jr) * 32 + 16 + hh] = (E)ds;
+      }
+    }
+    __syncthreads();
+    // ---- du partial: du[head][col] = sum_j ds[j][head] h_j[col] (the forward's P.H with ds) ----
+    {
+      const char* pbase = reinterpret_cast<const char*>(pds + ng * 64 * 32);
+      V8 pa[2];
+      {
+        V4 pv[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int rb = 32 * s2 + 8 * g + q4;
+          pv[2 * s2] = tr_read_ga<E>(pbase + (rb * 32 + 16 + 4 * p4) * 2);
+          pv[2 * s2 + 1] = tr_read_ga<E>(pbase + ((rb + 4) * 32 + 16 + 4 * p4) * 2);
+        }
+        tr_wait();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          pa[s2] = V8{pv[2 * s2][0], pv[2 * s2][1], pv[2 * s2][2], pv[2 * s2][3],
+                      pv[2 * s2 + 1][0], pv[2 * s2 + 1][1], pv[2 * s2 + 1][2], pv[2 * s2 + 1][3]};
+      }
+      float* dout = dupart + ((int64_t)r * nch2 + ch) * GF_HP * D;
+#pragma unroll
+      for (int i = 0; i < nmt; ++i) {
+        const int c0 = (wave * nmt + i) * 16;
+        V4 hv[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int rb = 32 * s2 + 8 * g + q4;
+          hv[2 * s2] = tr_read_ga<E>(himg + gimg(rb, c0 + 4 * p4));
+          hv[2 * s2 + 1] = tr_read_ga<E>(himg + gimg(rb + 4, c0 + 4 * p4));
+        }
+        tr_wait();
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const V4 v0 = hv[2 * s2], v1 = hv[2 * s2 + 1];
+          acc = mfma16(pa[s2], V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]}, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dout[(int64_t)(4 * g + q) * D + c0 + li] = acc[q];
+      }
+    }
+    ++ng;
+    __syncthreads();  // red is rewritten by the next global row
+  }
+  // ---- dh[j][col] = sum over the global rows of [p' | ds][j] . [dw ; u][col]; staged in the image ----
+  E* stg = reinterpret_cast<E*>(himg);
+  constexpr int NT = D / 16;  // column tiles
+  for (int cb0 = 0; cb0 < NT; cb0 += 12) {
+    f32x4 acc[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int slot = 0;
+    for (int gq = 0; gq < gmax; ++gq) {
+      const int r = b * gmax + gq;
+      if (gidx[r] < 0) continue;
+      const V8 a = *reinterpret_cast<const V8*>(pds + (slot * 64 + 16 * wave + li) * 32 + 8 * g);
+      const E* bp = bt + ((int64_t)r * D + 16 * cb0 + li) * 32 + 8 * g;
+#pragma unroll
+      for (int i = 0; i < 12; ++i)
+        if (cb0 + i < NT) acc[i] = mfma16(a, *reinterpret_cast<const V8*>(bp + (int64_t)16 * i * 32), acc[i]);
+      ++slot;
+    }
+#pragma unroll
+    for (int i = 0; i < 12; ++i)
+      if (cb0 + i < NT) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) stg[(16 * wave + 4 * g + q) * D + 16 * (cb0 + i) + li] = (E)acc[i][q];
+      }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x * 8; e < GB_ROWS * D; e += 256 * 8) {
+    const int row = e / D, col = e - row * D;
+    if (j0 + row < Lp)
+      *reinterpret_cast<V8*>(dh + ((int64_t)b * Lp + j0 + row) * lddh + col) = *reinterpret_cast<const V8*>(stg + e);
+  }
+}
+
+// du[r][h][col] = sum over the chunks, in chunk order (empty global slots: 0, their partials unwritten)
+__global__ void __launch_bounds__(256) k_gbwd_reduce(int R, int D, int nch2, const int32_t* __restrict__ gidx,
+                                                     const float* __restrict__ dupart, float* __restrict__ du) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)R * GF_HP * D) return;
+  const int64_t r = idx / ((int64_t)GF_HP * D), rem = idx - r * GF_HP * D;
+  float s = 0.f;
+  if (gidx[r] >= 0)
+    for (int c = 0; c < nch2; ++c) s += dupart[(r * nch2 + c) * GF_HP * D + rem];
+  du[idx] = s;
+}
+
+struct GbwdWs {
+  char* dwp;
+  char* bt;
+  float* dupart;
+};
+
+inline size_t gbwd_bytes(int R, int Lp, int D) {
+  const int nch2 = (Lp + GB_ROWS - 1) / GB_ROWS;
+  return align256((size_t)R * 2 * GF_HP * D * 2) + align256((size_t)R * D * 32 * 2) +
+         (size_t)R * nch2 * GF_HP * D * 4;
+}
+
+}  // namespace rf
+
+extern "C" size_t rf_global_fold_bwd_workspace(int B, int Lp, int D, int gmax) {
+  if (B <= 0 || gmax <= 0 || Lp <= 0) return 0;
+  return gbwd_bytes(B * gmax, Lp, D);
+}
+
+extern "C" int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
+                                  const uint8_t* flags, const int32_t* gidx, int gmax, const void* fwd_workspace,
+                                  const float* dw, const float* cb, float p_drop, uint64_t seed, void* dh, int lddh,
+                                  float* du, float* w, float* stats, void* workspace, rf_stream_t stream) {
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_global_fold_bwd: 16-bit operands only");
+  RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0 && H <= GF_HP && D == 64 * H,
+             "rf_global_fold_bwd: bad shape B=%d Lp=%d D=%d H=%d", B, Lp, D, H);
+  RF_REQUIRE(D % 128 == 0 && D <= 768, "rf_global_fold_bwd: D=%d (multiples of 128 up to 768)", D);
+  RF_REQUIRE(gmax <= GB_GMAX, "rf_global_fold_bwd: at most %d global rows per sequence", GB_GMAX);
+  RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_global_fold_bwd: p_drop %f", p_drop);
+  if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
+  RF_REQUIRE(h && flags && gidx && fwd_workspace && dw && dh && du && w && stats && workspace,
+             "rf_global_fold_bwd: null pointer");
+  RF_REQUIRE(ldh % 8 == 0 && lddh % 8 == 0 && ldh >= D && lddh >= D, "rf_global_fold_bwd: leading dims");
+  const int R = B * gmax;
+  const int nch = (Lp + GF_CH - 1) / GF_CH;
+  const int nch2 = (Lp + GB_ROWS - 1) / GB_ROWS;
+  GfoldWs fws = gfold_carve(const_cast<void*>(fwd_workspace), R, nch, H, D);
+  char* p = reinterpret_cast<char*>(workspace);
+  GbwdWs bw;
+  bw.dwp = p; p += align256((size_t)R * 2 * GF_HP * D * 2);
+  bw.bt = p; p += align256((size_t)R * D * 32 * 2);
+  bw.dupart = reinterpret_cast<float*>(p);
+  const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f, g_seed_dev};
+  hipStream_t s = as_stream(stream);
+  const size_t lds = (size_t)D * 128 + 2 * 4 * 64 * 16 * 4 + (size_t)GB_GMAX * 64 * 32 * 2;
+#define GB_(EE, DD)                                                                                          \
+  case DD:                                                                                                   \
+    k_gbwd_prep<EE><<<dim3(R, GF_HP), 256, 0, s>>>(D, H, nch, gidx, fws, dw, cb, p_drop > 0.f ? 1 : 0, w,      \
+                                                   stats, (EE*)bw.dwp, (EE*)bw.bt);                            \
+    (void)hipFuncSetAttribute((const void*)k_gbwd_main<EE, DD>, hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                              (int)lds);                                                                       \
+    k_gbwd_main<EE, DD><<<dim3(nch2, B), 256, lds, s>>>(Lp, gmax, H, (const EE*)h, ldh, flags, gidx, fws,      \
+                                                        (const EE*)bw.dwp, (const EE*)bw.bt, stats, cb,        \
+                                                        bw.dupart, (EE*)dh, lddh, dr);                         \
+    break;
+  if (dtype == RF_F16) {
+    switch (D) { GB_(f16, 128) GB_(f16, 256) GB_(f16, 384) GB_(f16, 512) GB_(f16, 640) GB_(f16, 768) default: break; }
+  } else {
+    switch (D) { GB_(bf16, 128) GB_(bf16, 256) GB_(bf16, 384) GB_(bf16, 512) GB_(bf16, 640) GB_(bf16, 768) default: break; }
+  }
+#undef GB_
+  const int64_t n = (int64_t)R * GF_HP * D;
+  k_gbwd_reduce<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(R, D, nch2, gidx, bw.dupart, du);
+  RF_LAUNCH_CHECK("rf_global_fold_bwd");
+}

@@ -632,10 +632,12 @@ def global_attention(qg, kg, vg, flags, gidx, B: int, Lp: int, H: int, out: torc
 
 
 def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int,
-                          out: torch.Tensor, tag: Optional[str] = None, p_drop: float = 0.0, seed: int = 0):
+                          out: torch.Tensor, tag: Optional[str] = None, p_drop: float = 0.0, seed: int = 0,
+                          ws: Optional[torch.Tensor] = None):
     """Global query rows through the key/value-projection fold (rf_global_attn_fold_fwd_drop):
     overwrites ctx rows at the global positions; p_drop > 0: attention-probability dropout with
-    the counter-hash mask of `seed` (16-bit dtypes)."""
+    the counter-hash mask of `seed` (16-bit dtypes). ws: the fold workspace to use (a training
+    forward keeps it for global_fold_bwd), else a fresh one."""
     lib = _lib.load()
     gmax = gidx.shape[1]
     if gmax == 0:
@@ -643,7 +645,10 @@ def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: in
     _dev(qg, h, wkg, wvg, flags)
     D = h.shape[1]
     ws_bytes = lib.rf_global_fold_workspace(B, Lp, D, H, gmax)
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=h.device)
+    if ws is None:
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=h.device)
+    elif ws.numel() < ws_bytes:
+        raise ValueError("global_attention_fold: workspace too small")
     for t in (wkg, wvg):
         if not t.is_contiguous() or t.dtype != h.dtype:
             raise ValueError("global_attention_fold: weights must be contiguous in the compute dtype")
@@ -655,6 +660,31 @@ def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: in
                                               _stream(out))
     check(rc, "rf_global_attn_fold_fwd_drop")
     return out
+
+
+def global_fold_bwd(h, flags, gidx, B: int, Lp: int, H: int, fwd_ws: torch.Tensor, dw: torch.Tensor,
+                    cb: Optional[torch.Tensor], p_drop: float, seed: int, dh: torch.Tensor):
+    """rf_global_fold_bwd: the global rows' backward in one pass over h from the forward's fold
+    workspace. dw (R, 16, D) fp32, cb (R, 16) fp32 or None; writes dh (B*Lp, D) in h's dtype and
+    returns (du, w, stats): (R, 16, D), (R, 16, D) fp32 and (R, 16, 4) fp32 (M, 1/L, Delta, S')."""
+    lib = _lib.load()
+    gmax = gidx.shape[1]
+    D = h.shape[1]
+    R = B * gmax
+    dev = h.device
+    if tuple(dw.shape) != (R, 16, D) or dw.dtype != torch.float32 or not dw.is_contiguous():
+        raise ValueError("global_fold_bwd: dw must be contiguous fp32 (R, 16, D)")
+    if cb is not None and (tuple(cb.shape) != (R, 16) or cb.dtype != torch.float32 or not cb.is_contiguous()):
+        raise ValueError("global_fold_bwd: cb must be contiguous fp32 (R, 16)")
+    du = torch.empty(R, 16, D, dtype=torch.float32, device=dev)
+    w = torch.empty_like(du)
+    stats = torch.empty(R, 16, 4, dtype=torch.float32, device=dev)
+    ws = torch.empty(max(lib.rf_global_fold_bwd_workspace(B, Lp, D, gmax), 16), dtype=torch.uint8, device=dev)
+    check(lib.rf_global_fold_bwd(dtype_code(h.dtype), B, Lp, D, H, _p(h), _rowmajor(h, "h"), _p(flags),
+                                 _p(gidx.to(torch.int32).contiguous()), gmax, _p(fwd_ws), _p(dw), _p(cb),
+                                 float(p_drop), int(seed) & (2**64 - 1), _p(dh), _rowmajor(dh, "dh"), _p(du), _p(w),
+                                 _p(stats), _p(ws), _stream(h)), "rf_global_fold_bwd")
+    return du, w, stats
 
 
 def attn_global_keep(gidx, B: int, Lp: int, H: int, p_drop: float, seed: int) -> torch.Tensor:

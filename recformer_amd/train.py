@@ -57,6 +57,8 @@ GLOBAL_KV_BLOCKDIAG = True
 DW_SPLIT_K = True
 # embedding + LayerNorm backward on the HIP kernels (deterministic table gradients, no index_add_)
 EMBED_BWD_HIP = True
+# global rows' backward on rf_global_fold_bwd (one pass over h from the forward's fold workspace)
+GLOBAL_BWD_HIP = True
 # weight gradients on the HIP kernel (rf_weight_grad: MFMA, transposed LDS reads, fixed-order split
 # reduction) instead of hipBLASLt
 DW_HIP = True
@@ -573,6 +575,46 @@ def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout, z=None, b
     return dq, dh.view(B * Lp, D), dwkg, dbkg, dwvg, dbvg
 
 
+def _fold_ws(h, B: int, Lp: int, H: int, G: int):
+    """A fold workspace the training forward keeps for the HIP global backward (16-bit, D a multiple
+    of 128 up to 768, at most 4 global rows per sequence), else None (a fresh one per call)."""
+    D = h.shape[1]
+    if GLOBAL_BWD_HIP and h.is_cuda and h.dtype != torch.float32 and D % 128 == 0 and D <= 768 and G <= 4 \
+            and H <= 16 and D == 64 * H:
+        return ops.global_fold_workspace(h, B, Lp, H, G)
+    return None
+
+
+def _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, gout, ws, p_drop: float, seed: int):
+    """_global_bwd on rf_global_fold_bwd (one pass over h, from the forward's fold workspace): the
+    per-head GEMVs of do / du with the (d x d) weights stay torch (a few hundred KB); returns fp32
+    (dqg, dh (h's dtype), dwkg, dbkg, dwvg, dbvg) like _global_bwd."""
+    D = h.shape[1]
+    hd = D // H
+    G = gidx.shape[1]
+    R = B * G
+    dev = h.device
+    wk = wkg.float().view(H, hd, D)
+    wv = wvg.float().view(H, hd, D)
+    qH = qg.float().view(R, H, hd).transpose(0, 1)                           # (H, R, hd)
+    doH = gout.float().view(R, H, hd).transpose(0, 1)                        # (H, R, hd)
+    dw = torch.zeros(R, 16, D, dtype=torch.float32, device=dev)
+    dw[:, :H] = torch.bmm(doH, wv).transpose(0, 1)
+    cb = None
+    if p_drop > 0:
+        cb = torch.zeros(R, 16, dtype=torch.float32, device=dev)
+        cb[:, :H] = (doH * bvg.float().view(H, 1, hd)).sum(-1).t()
+    dh = torch.empty(B * Lp, D, dtype=h.dtype, device=dev)
+    du, w, stats = ops.global_fold_bwd(h.contiguous(), flags, gidx, B, Lp, H, ws, dw, cb, p_drop, seed, dh)
+    duH = du[:, :H].transpose(0, 1)                                          # (H, R, D)
+    dq = torch.bmm(duH, wk.transpose(1, 2)).transpose(0, 1).reshape(R, D)
+    dwkg = torch.bmm(qH.transpose(1, 2), duH).reshape(D, D)
+    dwvg = torch.bmm(doH.transpose(1, 2), w[:, :H].transpose(0, 1)).reshape(D, D)
+    dbvg = (doH * stats[:, :H, 3].t().unsqueeze(-1)).sum(1).reshape(D)
+    dbkg = torch.zeros(D, dtype=torch.float32, device=dev)
+    return dq, dh, dwkg, dbkg, dwvg, dbvg
+
+
 def _global_kv_grad(w, x, B: int, Lp: int, H: int):
     """Gradient of the global-key (or -value) rows, sum_i w[b,h,i,g] * x[b,i,h,:] -> (B*G, D) in x's
     dtype (bf16 operands, fp32 accumulation). w: (B, H, Lp, G) per-query score (or probability)
@@ -637,6 +679,7 @@ class _Attention(torch.autograd.Function):
         # wkg / wvg: the global key / value weights in the compute dtype; with the masters given
         # (packed copies, not tracked) their gradients go to the fp32 masters directly
         ctx.masters = wkg_master is not None
+        ctx.fold_ws = None  # the forward fold's workspace when the HIP global backward can use it
         D = qkv.shape[1] // 3
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         G = gidx.shape[1]
@@ -655,8 +698,11 @@ class _Attention(torch.autograd.Function):
             if G > 0 and fold and q.dtype != torch.float32:
                 # the fold kernels with the same mask (rf_global_attn_fold_fwd_drop); the mask
                 # itself for the closed-form backward from one kernel (rf_attn_global_keep)
+                ws = _fold_ws(h, B, Lp, H, G)
                 ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg,
-                                          wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out, p_drop=attn_p, seed=seed)
+                                          wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out, p_drop=attn_p, seed=seed,
+                                          ws=ws)
+                ctx.fold_ws = ws
                 ctx.gz_kind = "hip"
             elif G > 0:
                 ctx.gz_kind = "torch"
@@ -667,8 +713,10 @@ class _Attention(torch.autograd.Function):
             out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w)
         if ctx.drop is None and G > 0:
             if fold:
+                ws = _fold_ws(h, B, Lp, H, G) if q.dtype != torch.float32 else None
                 ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg,
-                                          wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out)
+                                          wvg.contiguous(), bvg, flags, gidx, B, Lp, H, out, ws=ws)
+                ctx.fold_ws = ws
             else:
                 kg = ops.gemm(h.contiguous(), wkg.contiguous(), bkg, ops.RF_EPI_BIAS)
                 vg = ops.gemm(h.contiguous(), wvg.contiguous(), bvg, ops.RF_EPI_BIAS)
@@ -714,11 +762,16 @@ class _Attention(torch.autograd.Function):
             if any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]):
                 gout = dout[rows].float() * keep[:, None].to(torch.float32)
                 gz = None
-                if ctx.gz_kind == "hip":  # the forward's mask, from the same kernel
+                hip_bwd = GLOBAL_BWD_HIP and ctx.fold_ws is not None
+                if ctx.gz_kind == "hip" and not hip_bwd:  # the forward's mask, from the same kernel
                     gz = ops.attn_global_keep(gidx, B, Lp, H, p_drop, seed)
                 elif ctx.gz_kind == "torch":
                     gz = _global_keep(gidx, B, Lp, H, p_drop, seed)
-                if GLOBAL_BWD_CLOSED_FORM:
+                if GLOBAL_BWD_HIP and ctx.fold_ws is not None:
+                    with torch.autocast("cuda", enabled=False):
+                        grads = _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B, Lp, H, gout, ctx.fold_ws,
+                                                p_drop, seed)
+                elif GLOBAL_BWD_CLOSED_FORM:
                     with torch.autocast("cuda", enabled=False):
                         grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, gz, bvg,
                                             dh_dtype=h.dtype if GLOBAL_BWD_DH16 else None)

@@ -572,3 +572,54 @@ def test_pretrain_decoder_ce_hip_matches_torch(dev, monkeypatch, dt):
             continue
         cos = F.cosine_similarity(ga.reshape(1, -1), gb.reshape(1, -1)).item()
         assert cos >= 0.999, (k, cos)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", [
+    dict(B=3, Lp=1024, H=12, lens=[1024, 700, 129], gpos=[[0], [0], [5]], p=0.0),
+    dict(B=2, Lp=256, H=2, lens=[256, 100], gpos=[[0, 77], [3, -1]], p=0.0),
+    dict(B=2, Lp=512, H=12, lens=[512, 300], gpos=[[0], [0]], p=0.1),
+    dict(B=4, Lp=192, H=6, lens=[192, 64, 190, 1], gpos=[[0, 1, 100, -1], [0, 2, -1, -1], [5, -1, -1, -1], [0, -1, -1, -1]], p=0.1),
+])
+def test_global_fold_bwd_matches_closed_form(dev, dt, case):
+    """rf_global_fold_bwd (the global rows' backward in one pass over h from the forward's fold
+    workspace, train._global_bwd_hip) against the closed-form torch backward (train._global_bwd,
+    fp32, pinned to autograd by tests/test_train_host.py): dq, dh, dWkg, dWvg, dbvg, with ragged
+    lengths, several / empty global slots per sequence and attention dropout (the forward's mask)."""
+    from recformer_amd import train as T
+    B, Lp, H, p = case["B"], case["Lp"], case["H"], case["p"]
+    D = 64 * H
+    G = len(case["gpos"][0])
+    g = torch.Generator(device="cpu").manual_seed(B * Lp + H)
+    flags = torch.zeros(B, Lp, dtype=torch.uint8)
+    gidx = torch.full((B, G), -1, dtype=torch.int32)
+    for b in range(B):
+        flags[b, :case["lens"][b]] = 1
+        for k, q in enumerate(case["gpos"][b]):
+            if q >= 0:
+                flags[b, q] = 2
+                gidx[b, k] = q
+    flags, gidx = flags.to(dev), gidx.to(dev)
+    h = (torch.randn(B * Lp, D, generator=g)).to(dev).to(dt)
+    qg = (torch.randn(B * G, D, generator=g) * 0.125).to(dev).to(dt)
+    wkg, wvg = ((torch.randn(D, D, generator=g) * 0.05).to(dev).to(dt) for _ in range(2))
+    bkg, bvg = ((torch.randn(D, generator=g) * 0.1).to(dev) for _ in range(2))
+    out = torch.zeros(B * Lp, D, dtype=dt, device=dev)
+    ws = ops.global_fold_workspace(h, B, Lp, H, G)
+    seed = 1234
+    ops.global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, out, p_drop=p, seed=seed, ws=ws)
+    keep = (gidx >= 0).reshape(-1, 1).float()
+    gout = torch.randn(B * G, D, generator=g).to(dev) * keep
+    gz = ops.attn_global_keep(gidx, B, Lp, H, p, seed) if p > 0 else None
+    ref = T._global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, gz, bvg)
+    got = T._global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B, Lp, H, gout, ws, p, seed)
+    for name, a, r in zip(("dq", "dh", "dwkg", "dbkg", "dwvg", "dbvg"), got, ref):
+        a, r = a.float(), r.float()
+        scale = float(r.abs().max())
+        if scale == 0.0:
+            assert float(a.abs().max()) == 0.0, name
+            continue
+        err = float((a - r).abs().max())
+        assert err <= 2e-2 * scale, (name, err, scale)
+        cos = F.cosine_similarity(a.reshape(1, -1), r.reshape(1, -1)).item()
+        assert cos >= 0.9995, (name, cos)
