@@ -672,6 +672,231 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     }
 }
 
+// ---- partial pass on a 3-slot ring of 32-row sub-chunks (round 3; D a multiple of 128, <= 768) ------
+// The two-half image above keeps one 64-row sub-chunk in flight and waits one memory latency per
+// sub-chunk. Here the chunk walks 32-row sub-chunks through three LDS slots with two of them in flight
+// while the third is computed. The score product S^T = H.U^T splits its D-reduction over the four waves
+// (each wave holds only its quarter of u: 12 fragments instead of 48, so the loop has registers to
+// spare) and sums the partial scores in LDS; the online softmax runs with one head per 16 lanes (max
+// and sum by lane shuffles, the running statistics in registers); P.H as the old kernel (transposed LDS
+// reads, accumulators rescaled by alpha). LDS stores that follow an LDS-DMA in flight are inline asm:
+// hipcc would otherwise wait for every DMA outstanding before each of them.
+template <int D>
+__device__ __forceinline__ int gimg32(int row, int col) {
+  return (((col >> 6) * 32 + row) << 7) + ((((col >> 3) & 7) ^ (row & 7)) << 4) + ((col & 7) << 1);
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ void lds_st32(const void* p, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st16(const void* p, uint32_t v) {
+  asm volatile("ds_write_b16 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_fence_barrier() {  // the asm stores above are complete, then barrier
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <typename E, int D>
+__global__ void __launch_bounds__(256) k_gfold_partial_ring(int Lp, int gmax, const E* __restrict__ hs, int ldh,
+                                                            const uint8_t* __restrict__ flags,
+                                                            const int32_t* __restrict__ gidx, GfoldWs ws, int H,
+                                                            AttnDrop dr) {
+  drop_resolve(dr);  // device step counter (captured training steps)
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NK = D / 32;
+  constexpr int KW = NK / 4 > 0 ? NK / 4 : 1;  // score k-steps per wave
+  constexpr int nseg = D >> 6;
+  constexpr int SLOT = 32 * D * 2;    // bytes per 32-row sub-chunk image
+  constexpr int PPW = nseg * 4 / 4;   // DMA pieces (8 rows x 128 B) per wave per sub-chunk
+  constexpr int nmt = D >> 6;         // P.H column tiles per wave
+  if constexpr (NK % 4 != 0 || D > 768) return;  // D a multiple of 128 up to 768 (host dispatch)
+  float* red = reinterpret_cast<float*>(smem + 3 * SLOT);            // [4 waves][32 rows][16 heads]
+  char* pimg = smem + 3 * SLOT + 4 * 32 * 16 * 4;                     // P [32 rows][16 heads] 16-bit
+  float* alpha_s = reinterpret_cast<float*>(pimg + 32 * 16 * 2);      // [16]
+  const int ch = blockIdx.x, r = blockIdx.y, nch = gridDim.x;
+  if (gidx[r] < 0) return;
+  const int pos = gidx[r];
+  const int b = r / gmax;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int q4 = li >> 2, p4 = li & 3;
+  const E* hb = hs + (int64_t)b * Lp * ldh;
+  const int row_begin = ch * GF_CH;
+  const int row_end = min(row_begin + GF_CH, Lp);
+  const int nsub = (row_end - row_begin + 31) >> 5;
+  // validity flags of the chunk's rows (up to 256), loaded with u (one memory round trip in all)
+  uint32_t fl[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) fl[q] = flags[(int64_t)b * Lp + min(row_begin + 64 * q + lane, Lp - 1)];
+  // u fragments of this wave's k range (hi and lo planes); heads >= H score 0
+  V8 uh[KW], ul[KW];
+  {
+    const E* uhi = reinterpret_cast<const E*>(ws.u16) + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
+    const E* ulo = uhi + (int64_t)GF_HP * D;
+#pragma unroll
+    for (int kk = 0; kk < KW; ++kk) {
+      const int s2 = wave * KW + kk;
+      uh[kk] = li < H ? *reinterpret_cast<const V8*>(uhi + 32 * s2) : V8{};
+      ul[kk] = li < H ? *reinterpret_cast<const V8*>(ulo + 32 * s2) : V8{};
+    }
+  }
+  unsigned long long vm[4];  // row validity, ballots of 64 rows
+#pragma unroll
+  for (int q = 0; q < 4; ++q) vm[q] = __ballot(row_begin + 64 * q + lane < row_end && fl[q] != 0);
+  // u and the flags are in registers before the DMA stream starts: the fence makes hipcc wait for them
+  // here, not (with vmcnt(0), draining the ring) at their first use inside the loop
+#pragma unroll
+  for (int kk = 0; kk < KW; ++kk) asm volatile("" : "+v"(uh[kk]), "+v"(ul[kk]));
+  // sub-chunk k (rows row_begin + 32 k ..) into slot k % 3; rows past the chunk read clamped rows
+  auto dma = [&](int k) {
+    char* slot = smem + (k % 3) * SLOT;
+    const int j0 = row_begin + 32 * k;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave * PPW + i;                  // piece: segment pc / 4, rows 8 (pc % 4) ..
+      const int seg = pc >> 2, row = (pc & 3) * 8 + (lane >> 3);
+      const int chk = (lane & 7) ^ (row & 7);
+      const int jr = min(j0 + row, Lp - 1);
+      glds16(hb + (int64_t)jr * ldh + seg * 64 + chk * 8, slot + (seg * 32 + (pc & 3) * 8) * 128);
+    }
+  };
+  dma(0);
+  dma(1);
+  // running statistics of head hh = lane-group of 16 (thread -> head t / 16, rows 2 (t % 16) + {0, 1})
+  const int hh = threadIdx.x >> 4, tr = threadIdx.x & 15;
+  float m_run = GF_NEG_INF, l_run = 0.f, ld_run = 0.f;
+  const uint64_t drow = ((uint64_t)b * H + min(hh, H - 1)) * Lp + (uint64_t)pos;
+  f32x4 acc[nmt];
+#pragma unroll
+  for (int i = 0; i < nmt; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int sub = 0; sub < nsub; ++sub) {
+    dma(sub + 2);  // into the slot sub - 1 used (released by the barrier ending the last iteration)
+    wait_vm_n<2 * PPW>();  // sub-chunk sub landed (sub + 1, sub + 2 may fly)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* slot = smem + (sub % 3) * SLOT;
+    // ---- partial scores over this wave's k range, two 16-row tiles ----
+    f32x4 st0 = f32x4{0.f, 0.f, 0.f, 0.f}, st1 = st0;
+#pragma unroll
+    for (int kk = 0; kk < KW; ++kk) {
+      const int s2 = wave * KW + kk;
+      const V8 a0 = *reinterpret_cast<const V8*>(slot + gimg32<D>(li, 32 * s2 + 8 * g));
+      const V8 a1 = *reinterpret_cast<const V8*>(slot + gimg32<D>(16 + li, 32 * s2 + 8 * g));
+      st0 = mfma16(a0, uh[kk], st0);
+      st0 = mfma16(a0, ul[kk], st0);
+      st1 = mfma16(a1, uh[kk], st1);
+      st1 = mfma16(a1, ul[kk], st1);
+    }
+    // C[row 4g + i (+16)][head li] -> red[wave][row][head]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lds_st32(red + (wave * 32 + 4 * g + i) * 16 + li, st0[i]);
+      lds_st32(red + (wave * 32 + 16 + 4 * g + i) * 16 + li, st1[i]);
+    }
+    lds_fence_barrier();
+    // ---- online softmax: head hh, rows 2 tr, 2 tr + 1 ----
+    {
+      const int j0 = row_begin + 32 * sub;
+      float sv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int jr = 2 * tr + u;
+        float sc = ((red[(0 * 32 + jr) * 16 + hh] + red[(1 * 32 + jr) * 16 + hh]) + red[(2 * 32 + jr) * 16 + hh]) +
+                   red[(3 * 32 + jr) * 16 + hh];
+        const int jl = 32 * sub + jr;  // row within the chunk
+        const bool ok = ((vm[jl >> 6] >> (jl & 63)) & 1ull) && hh < H;
+        sv[u] = ok ? sc : GF_NEG_INF;
+      }
+      float mx = fmaxf(sv[0], sv[1]);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
+      const float m_new = fmaxf(m_run, mx);
+      const float mu = m_new == GF_NEG_INF ? 0.f : m_new;
+      float ls = 0.f, lsd = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int jr = 2 * tr + u;
+        float pv = __expf(sv[u] - mu);
+        ls += pv;
+        if (dr.thresh) {
+          pv *= attn_keep_scale(dr, drow, Lp, j0 + jr);
+          lsd += pv;
+        }
+        lds_st16(pimg + (jr * 16 + hh) * 2, (uint32_t)__builtin_bit_cast(uint16_t, (E)pv));
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {
+        ls += __shfl_xor(ls, o, 16);
+        lsd += __shfl_xor(lsd, o, 16);
+      }
+      const float a = __expf(m_run - mu);  // 0 when m_run = -inf
+      l_run = l_run * a + ls;
+      ld_run = ld_run * a + lsd;
+      m_run = m_new;
+      if (tr == 0) lds_st32(alpha_s + hh, a);
+    }
+    lds_fence_barrier();
+    // ---- W[head][c] = alpha W + sum_j p[j][head] h[j][c] (K = 32 rows) ----
+    float al[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) al[q] = alpha_s[4 * g + q];
+    V8 pa;
+    {
+      const int rb = 8 * g + q4;
+      const V4 v0 = tr_read_ga<E>(pimg + (rb * 16 + 4 * p4) * 2);
+      const V4 v1 = tr_read_ga<E>(pimg + ((rb + 4) * 16 + 4 * p4) * 2);
+      tr_wait();
+      pa = V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+    constexpr int PB = nmt % 3 == 0 ? 3 : (nmt % 2 == 0 ? 2 : 1);
+#pragma unroll
+    for (int i0 = 0; i0 < nmt; i0 += PB) {
+      V4 hv[PB][2];
+#pragma unroll
+      for (int ii = 0; ii < PB; ++ii) {
+        const int col = (wave * nmt + i0 + ii) * 16 + 4 * p4;
+        const int rb = 8 * g + q4;
+        hv[ii][0] = tr_read_ga<E>(slot + gimg32<D>(rb, col));
+        hv[ii][1] = tr_read_ga<E>(slot + gimg32<D>(rb + 4, col));
+      }
+      tr_wait();
+#pragma unroll
+      for (int ii = 0; ii < PB; ++ii) {
+        const int i = i0 + ii;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][q] *= al[q];
+        const V4 v0 = hv[ii][0], v1 = hv[ii][1];
+        acc[i] = mfma16(pa, V8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]}, acc[i]);
+      }
+    }
+    // every wave is done with this slot, pimg and alpha before the next iteration's DMA / stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the (unused) tail DMAs land before the stores / exit
+  if (tr == 0 && hh < GF_HP) {
+    ws.m[((int64_t)r * nch + ch) * GF_HP + hh] = m_run;
+    ws.l[((int64_t)r * nch + ch) * GF_HP + hh] = l_run;
+    if (dr.thresh) ws.ld[((int64_t)r * nch + ch) * GF_HP + hh] = ld_run;
+  }
+  float* wout = ws.w + ((int64_t)r * nch + ch) * GF_HP * D;
+#pragma unroll
+  for (int i = 0; i < nmt; ++i) {
+    const int c0 = (wave * nmt + i) * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * g + q < H) wout[(int64_t)(4 * g + q) * D + c0 + li] = acc[i][q];
+  }
+}
+
 // Single-buffered form for D not a multiple of 128 (one 64-row DMA, then compute).
 template <typename E, int D>
 __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
@@ -1111,10 +1336,16 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
   const int R = B * gmax;
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
     const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + GF_RED_FLOATS * sizeof(float);
+    const size_t lds_r = (size_t)3 * 32 * D * 2 + 4 * 32 * 16 * 4 + 32 * 16 * 2 + 16 * 4;
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
 #define GP_(DD)                                                                                 \
   case DD:                                                                                      \
-    if (DD % 128 == 0) {                                                                        \
+    if (DD % 128 == 0 && DD <= 768 && g_knob[KNOB_GFOLD_PATH] != 3) {                            \
+      (void)hipFuncSetAttribute((const void*)k_gfold_partial_ring<E, DD>,                          \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_r);        \
+      k_gfold_partial_ring<E, DD><<<dim3(nch, R), 256, lds_r, s>>>(Lp, gmax, (const E*)h, ldh,  \
+                                                                flags, gidx, ws, H, dr);        \
+    } else if (DD % 128 == 0) {                                                                 \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<E, DD>,                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
       k_gfold_partial_bf16<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const E*)h, ldh,  \

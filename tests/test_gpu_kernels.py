@@ -412,8 +412,9 @@ def test_global_fold_h_stages_match_one_call(dev, dt, B, Lp, H):
 @pytest.mark.parametrize("B,Lp,H", [(300, 64, 12), (70, 192, 3), (5, 1024, 12)])
 def test_global_fold_mfma_matches_gemv(dev, monkeypatch, B, Lp, H, dt):
     """The 64-row MFMA qg/u and out kernels (chosen for >= 256 global rows, e.g. a catalog of
-    short item sequences) and the default choice (below 256 rows: the 16-row MFMA out kernel
-    k_gfold_out16) against the per-row GEMV kernels (pinned to the torch reference by
+    short item sequences), the default choice (below 256 rows: the 16-row MFMA out kernel
+    k_gfold_out16) and the two-half partial kernel the 32-row ring replaced (knob 3) against the
+    per-row GEMV kernels (pinned to the torch reference by
     test_band_and_global_attention) on the same inputs: ragged lengths, sequences without a
     global token (gidx -1), several globals per sequence and partial last 64- / 16-row tiles."""
     D = H * 64
@@ -426,15 +427,15 @@ def test_global_fold_mfma_matches_gemv(dev, monkeypatch, B, Lp, H, dt):
     w = [_rand((D, D), dev, dt, 0.05, seed=61 + i) for i in range(3)]
     bias = [_rand((D,), dev, torch.float32, 0.1, seed=64 + i) for i in range(3)]
     outs = {}
-    for path in ("gemv", "mfma", "auto"):
-        old = _lib.set_knob("gfold_path", {"gemv": 1, "mfma": 2, "auto": 0}[path])
+    for path in ("gemv", "mfma", "auto", "two_half"):
+        old = _lib.set_knob("gfold_path", {"gemv": 1, "mfma": 2, "auto": 0, "two_half": 3}[path])
         ctx = torch.zeros(B * Lp, D, dtype=dt, device=dev)
         ops.global_attention_fold_h(h, w[0], bias[0], 0.125, w[1], bias[1], w[2], bias[2], flags, gidx, B, Lp, H,
                                     ctx)
         torch.cuda.synchronize()
         _lib.set_knob("gfold_path", old)
         outs[path] = ctx.float()
-    for other in ("mfma", "auto"):
+    for other in ("mfma", "auto", "two_half"):
         err = (outs["gemv"] - outs[other]).abs().max().item()
         assert err <= 2e-2, (other, err)
     written = outs["auto"].abs().sum(1) > 0
