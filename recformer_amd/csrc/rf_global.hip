@@ -1340,7 +1340,7 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
 #define GP_(DD)                                                                                 \
   case DD:                                                                                      \
-    if (DD % 128 == 0 && DD <= 768 && g_knob[KNOB_GFOLD_PATH] != 3) {                            \
+    if (DD % 128 == 0 && DD <= 768 && Lp <= 128 && g_knob[KNOB_GFOLD_PATH] != 3) {                \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_ring<E, DD>,                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_r);        \
       k_gfold_partial_ring<E, DD><<<dim3(nch, R), 256, lds_r, s>>>(Lp, gmax, (const E*)h, ldh,  \

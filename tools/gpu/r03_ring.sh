@@ -22,3 +22,8 @@ PY
 done
 timeout -k 10 300 python tools/ab_knob.py gfold_path 0 3 > gpurun_out/r03_ring_ab.log 2>&1 || { tail -20 gpurun_out/r03_ring_ab.log; exit 1; }
 tail -3 gpurun_out/r03_ring_ab.log | cut -c1-400
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_train.py -k "colsum or layernorm or c2_ or seqrec or lm_head" -q --timeout 200 --timeout-method thread > gpurun_out/r03_colsum.log 2>&1
+rc=$?; tail -2 gpurun_out/r03_colsum.log
+[ $rc -eq 0 ] || { grep -E "^E  |FAILED" gpurun_out/r03_colsum.log | cut -c1-300 | head -20; exit 1; }
+timeout -k 10 300 python tools/train_bench.py --steps 8 --warmup 2 --graph > gpurun_out/r03_c3_g5.log 2>&1 || { tail -20 gpurun_out/r03_c3_g5.log; exit 1; }
+tail -1 gpurun_out/r03_c3_g5.log

@@ -40,6 +40,8 @@ def main():
                     "(recformer_amd.graphs.CapturedTrainStep)")
     ap.add_argument("--torch-adamw", action="store_true", help="A/B: torch.optim.AdamW (multi-tensor) instead of "
                     "recformer_amd.optim.AdamW (one HIP launch)")
+    ap.add_argument("--ab-knob", default=None, help="A/B in one process: a library knob "
+                    "(recformer_amd._lib.set_knob) at 1 / 0")
     ap.add_argument("--global-dh-f32", action="store_true", help="A/B: the global branch's dh as an fp32 product")
     a = ap.parse_args()
     if a.global_dh_f32:
@@ -99,13 +101,16 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    if a.ab:
+    if a.ab or a.ab_knob:
         # clocks differ across boxes and drift under load: alternate blocks in one process
-        from recformer_amd import train
+        from recformer_amd import _lib, train
         res = {True: [], False: []}
         for rep in range(6):
             for val in (True, False):
-                setattr(train, a.ab, val)
+                if a.ab:
+                    setattr(train, a.ab, val)
+                else:
+                    _lib.set_knob(a.ab_knob, 1 if val else 0)
                 step()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -115,7 +120,7 @@ def main():
                 res[val].append((time.perf_counter() - t0) / a.steps * 1e3)
         for val in (True, False):
             v = sorted(res[val])
-            print(f"{a.ab}={val}: ms/step median {v[len(v) // 2]:.2f} min {v[0]:.2f} all {[round(x, 2) for x in res[val]]}")
+            print(f"{a.ab or a.ab_knob}={val}: ms/step median {v[len(v) // 2]:.2f} min {v[0]:.2f} all {[round(x, 2) for x in res[val]]}")
         return
     t0 = time.perf_counter()
     for _ in range(a.steps):
