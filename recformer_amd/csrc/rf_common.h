@@ -53,6 +53,7 @@ enum Knob {
   KNOB_BAND_PATH,       // band attention kernel: 0 pipe2, 1 pipe (v1), 2 one-shot
   KNOB_GFOLD_PATH,      // global fold: 0 auto, 1 GEMV, 2 MFMA, 3 auto without the ring partial kernel
   KNOB_GFOLD_QSPLIT,    // global fold query/key kernel: max column splits (8)
+  KNOB_GEMM_PF,         // four-wave GEMM L2 prefetch: -1 auto (2 for K >= 2048), else distance in K-tiles (0 = off), + 256: W rows too
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];

@@ -44,6 +44,7 @@ struct EpiArgs {
   const float* lbeta;
   unsigned long long* stamps;  // diagnostic s_memtime stamps (tools only), nullptr = off
   int gn;                      // ping-pong kernel: column tiles per raster group (0 = all)
+  int pf;                      // four-wave kernel: L2 prefetch distance in K-tiles (0 = off); bit 8: W rows too
 };
 
 // scalar epilogue (fp32 kernel and ragged tails)
@@ -1053,7 +1054,8 @@ static void launch_pp(int M, int N, int K, const void* A, int lda, const void* W
 // next tile's first two K-tiles are fetched across the tile boundary (virtual K-tiles nk, nk+1).
 constexpr int W4_BUF = 4 * PP_HALF;          // one K-tile: A rows 0-127, 128-255, W rows 0-127, 128-255
 constexpr int W4_CV = 2 * W4_BUF;            // column vectors [parity][3][1 KiB]
-constexpr int W4_LDS = W4_CV + 6 * 1024;
+constexpr int W4_PF = W4_CV + 6 * 1024;     // L2-prefetch landing area, 256 B per wave (never read)
+constexpr int W4_LDS = W4_PF + 1024;
 
 template <typename E, int EPI, bool CF32, bool RF32, bool IL>
 __global__ void __launch_bounds__(256, 1)
@@ -1163,6 +1165,23 @@ __global__ void __launch_bounds__(256, 1)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
+  // L2 prefetch (e.pf): at the end of phase B(t), one dword per operand row (lane = row) of virtual
+  // K-tile t + 2 + pfd, as a 4-B LDS-DMA into a landing area nothing reads (no register is written
+  // asynchronously). It is the youngest memory operation at the next mid-sync, which waits for all
+  // but it (vmcnt(npf)): a prefetch has two phases to land before a wait covers it, and the DMA of
+  // its K-tile later hits L2 instead of waiting one HBM latency. Not issued in a tile's last phase B
+  // (the relaxed wait of the next tile's first mid-sync counts only the epilogue stores).
+  const int pfd = e.pf & 0xff;
+  const int npf = pfd ? 1 + ((e.pf >> 8) & 1) : 0;
+  auto prefetch = [&](int kv) {
+    const bool nxt = kv >= nk;
+    const int kt = min(nxt ? kv - nk : kv, nk - 1);
+    const int prow = wave * 64 + lane;
+    auto* dst = (__attribute__((address_space(3))) void*)(smem + W4_PF + wave * 256);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 4, ((nxt ? nm0 : m0) + prow) * lda * 2, kt * 128, 0, 0);
+    if (npf == 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, dst, 4, ((nxt ? nn0 : n0) + prow) * ldw * 2, kt * 128, 0, 0);
+  };
 
   // prologue: K-tiles 0, 1 of the first tile, its column vectors
   dma_cols(m0, n0, 0);
@@ -1207,6 +1226,8 @@ __global__ void __launch_bounds__(256, 1)
     auto midsync = [&](int t) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (t == 0 && relax) wait_vmcnt<(S < 63 ? S : 63)>();  // the previous tile's stores may stay in flight
+      else if (t > 0 && npf == 1) wait_vmcnt<1>();          // the prefetch of phase B(t-1) may stay in flight
+      else if (t > 0 && npf == 2) wait_vmcnt<2>();
       else wait_vmcnt<0>();
 #if !(defined(RF_W4_DIAG) && (RF_W4_DIAG & 1))  // timing diagnostic: no barrier (wrong results)
       bar();
@@ -1261,6 +1282,7 @@ __global__ void __launch_bounds__(256, 1)
         }
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
+      if (npf && t + 1 < nk && t + 2 + pfd < 2 * nk) prefetch(t + 2 + pfd);
       kb ^= 1;
     };
     if (IL) {  // the first phase A initialises the accumulators (MFMA with a zero C operand)
@@ -1622,6 +1644,10 @@ static unsigned long long* g_stamps = nullptr;  // set by rf_debug_gemm_stamps (
 
 // column groups of 6 tiles: qkv -2.7%, FFN1/FFN2 -1% vs 4 (tools/gemm_gn.py); full width loses on FFN1
 static int gemm_gn() { return g_knob[KNOB_GEMM_GN]; }
+// L2 prefetch 2 K-tiles ahead for long K only: FFN2 (K = 3072) waits on its A-panel DMA from HBM,
+// 241.8 -> 230.2 us in a same-process C2 step A/B; at K = 768 (qkv, out-proj, FFN1) the A panel is
+// re-read from L2 by the tiles of its row and the extra loads cost 1-4 % (tools/gemm_gn.py gemm_pf)
+static int gemm_pf(int K) { return g_knob[KNOB_GEMM_PF] >= 0 ? g_knob[KNOB_GEMM_PF] : (K >= 2048 ? 2 : 0); }
 
 #if defined(RF_GEMM_EXPERIMENTS)
 static int gemm_variant() { return g_knob[KNOB_GEMM_VARIANT]; }
@@ -1721,7 +1747,7 @@ extern "C" int rf_gemm(int dtype, int M, int N, int K, const void* A, int lda, c
   RF_REQUIRE(epilogue != RF_EPI_COS || (ra && rw), "rf_gemm: norms required for EPI_COS");
   if (M == 0) return RF_OK;
   EpiArgs e{M, N, bias, resid, ldr, C, ldc, scale_cols, col_scale, ra, rw,
-            nullptr, nullptr, nullptr, nullptr, g_stamps, gemm_gn()};
+            nullptr, nullptr, nullptr, nullptr, g_stamps, gemm_gn(), gemm_pf(K)};
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16 || dtype == RF_F16) {
     RF_REQUIRE(K % 64 == 0, "rf_gemm(16-bit): K=%d must be a multiple of 64", K);
@@ -1758,7 +1784,7 @@ extern "C" int rf_gemm_resid_ln(int dtype, int M, int N, int K, const void* A, i
              "rf_gemm_resid_ln: null pointer");
   if (M == 0) return RF_OK;
   EpiArgs e{M, N, bias, resid_pre, ldr, C, ldc, 0, 1.0f, nullptr, nullptr,
-            r_mean, r_rstd, r_gamma, r_beta, g_stamps, gemm_gn()};
+            r_mean, r_rstd, r_gamma, r_beta, g_stamps, gemm_gn(), gemm_pf(K)};
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16) {
     RF_REQUIRE(K % 64 == 0, "rf_gemm_resid_ln(bf16): K=%d must be a multiple of 64", K);

@@ -28,7 +28,13 @@ constexpr float GF_NEG_INF = -__builtin_inff();
 #define RF_GF_CH 256
 #endif
 constexpr int GF_CH = RF_GF_CH;  // rows per chunk (bf16 kernel walks it in 64-row sub-chunks)
-constexpr int GF_CHF = 64;    // rows per chunk of the fp32 VALU kernel
+constexpr int GF_CHF = 64;
+#if defined(RF_GF_DIAG)  // timing diagnostics of k_gfold_partial_bf16 (tools/build_variant.sh only)
+constexpr bool RF_GF_DIAG_SC = (RF_GF_DIAG & 1) != 0;  // no score MFMAs
+constexpr bool RF_GF_DIAG_PH = (RF_GF_DIAG & 4) != 0;  // no P.H products
+#else
+constexpr bool RF_GF_DIAG_SC = false, RF_GF_DIAG_PH = false;
+#endif    // rows per chunk of the fp32 VALU kernel
 constexpr int GF_HP = 16;     // heads padded to one MFMA column tile (H <= 16)
 constexpr int GF_RED_LD = 176;  // partial kernels' LDS reduction area: dropped sums at red + 176
 constexpr int GF_RED_FLOATS = GF_RED_LD + 64;
@@ -41,6 +47,21 @@ struct GfoldWs {
   float* ld;     // [R][nch][16]  sum of the dropped probabilities (attention dropout only)
   float* w;      // [R][nch][16][D]
 };
+
+// Rows per chunk of the training forward's 16-bit partial pass (rf_global_attn_fold_fwd_drop; one
+// block per (chunk, global row)): GF_CH = 256 when the grid fills the chip, halved down to 64 while it
+// has fewer blocks than the chip has CUs and at most 16 chunks (C3, B = 16: 64 -> 256 blocks; C4 at 4
+// per rank: 16 -> 64) — every block streams its chunk once, so a short grid leaves CUs idle. The
+// backward reads the forward's chunk partials with the same count. The inference entry points keep
+// GF_CH: the chunking sets the rounding of the softmax merge, and a sequence's scores there must
+// not depend on the batch it is encoded in (test_c2_full_size_properties).
+constexpr int GF_FILL = 256;  // MI355X CUs
+inline int gfold_chunk(int dtype, int R, int Lp) {
+  if (dtype == RF_F32) return GF_CHF;
+  int ch = GF_CH;
+  while (ch > 64 && (int64_t)R * ((Lp + ch - 1) / ch) < GF_FILL && (Lp + ch / 2 - 1) / (ch / 2) <= 16) ch /= 2;
+  return ch;
+}
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -455,7 +476,7 @@ __global__ void __launch_bounds__(256) k_gfold_out_mfma(int Lp, int R, int gmax,
 // with it. Row validity comes from per-sub-chunk ballots taken in the prologue (no global
 // load inside the loop, whose hipcc wait would drain the DMA queue).
 template <typename E, int D>
-__global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
+__global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, int chr,
                                                              const E* __restrict__ hs, int ldh,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
@@ -484,8 +505,8 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
   float* alpha_s = red + 144;
   unsigned long long* vmask = reinterpret_cast<unsigned long long*>(red + 160);  // per sub-chunk
   const E* hb = hs + (int64_t)b * Lp * ldh;
-  const int row_begin = ch * GF_CH;
-  const int row_end = min(row_begin + GF_CH, Lp);
+  const int row_begin = ch * chr;
+  const int row_end = min(row_begin + chr, Lp);
   const int nsub = (row_end - row_begin + 63) >> 6;
 
   auto dma_half = [&](int j0, int half) {
@@ -535,7 +556,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int s2 = 0; s2 < NK / 2; ++s2) {
+    for (int s2 = 0; s2 < (RF_GF_DIAG_SC ? 0 : NK / 2); ++s2) {
       const V8 a = *reinterpret_cast<const V8*>(smem + gimg(arow, 32 * s2 + 8 * g));
       st = mfma16(a, uh[s2], st);
       st = mfma16(a, ul[s2], st);
@@ -544,7 +565,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int s2 = NK / 2; s2 < NK; ++s2) {
+    for (int s2 = NK / 2; s2 < (RF_GF_DIAG_SC ? NK / 2 : NK); ++s2) {
       const V8 a = *reinterpret_cast<const V8*>(smem + gimg(arow, 32 * s2 + 8 * g));
       st = mfma16(a, uh[s2], st);
       st = mfma16(a, ul[s2], st);
@@ -621,7 +642,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
 #pragma unroll
-      for (int i0 = 0; i0 < hmt; i0 += PB) {
+      for (int i0 = 0; i0 < (RF_GF_DIAG_PH ? 0 : hmt); i0 += PB) {
         V4 hv[PB][4];
 #pragma unroll
         for (int ii = 0; ii < PB; ++ii) {
@@ -651,7 +672,9 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax,
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+#if !(defined(RF_GF_DIAG) && (RF_GF_DIAG & 2))  // diagnostic: no refill DMA (stale image)
       if (more) dma_half(j0 + 64, half);
+#endif
     }
   }
   if (wave == 0 && g == 0) {
@@ -701,7 +724,7 @@ __device__ __forceinline__ void lds_fence_barrier() {  // the asm stores above a
 }
 
 template <typename E, int D>
-__global__ void __launch_bounds__(256) k_gfold_partial_ring(int Lp, int gmax, const E* __restrict__ hs, int ldh,
+__global__ void __launch_bounds__(256) k_gfold_partial_ring(int Lp, int gmax, int chr, const E* __restrict__ hs, int ldh,
                                                             const uint8_t* __restrict__ flags,
                                                             const int32_t* __restrict__ gidx, GfoldWs ws, int H,
                                                             AttnDrop dr) {
@@ -728,8 +751,8 @@ __global__ void __launch_bounds__(256) k_gfold_partial_ring(int Lp, int gmax, co
   const int g = lane >> 4, li = lane & 15;
   const int q4 = li >> 2, p4 = li & 3;
   const E* hb = hs + (int64_t)b * Lp * ldh;
-  const int row_begin = ch * GF_CH;
-  const int row_end = min(row_begin + GF_CH, Lp);
+  const int row_begin = ch * chr;
+  const int row_end = min(row_begin + chr, Lp);
   const int nsub = (row_end - row_begin + 31) >> 5;
   // validity flags of the chunk's rows (up to 256), loaded with u (one memory round trip in all)
   uint32_t fl[4];
@@ -899,7 +922,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_ring(int Lp, int gmax, co
 
 // Single-buffered form for D not a multiple of 128 (one 64-row DMA, then compute).
 template <typename E, int D>
-__global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
+__global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax, int chr,
                                                              const E* __restrict__ hs, int ldh,
                                                              const uint8_t* __restrict__ flags,
                                                              const int32_t* __restrict__ gidx,
@@ -940,8 +963,8 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax,
 #pragma unroll
   for (int i = 0; i < nmt; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int row_begin = ch * GF_CH;
-  const int row_end = min(row_begin + GF_CH, Lp);
+  const int row_begin = ch * chr;
+  const int row_end = min(row_begin + chr, Lp);
   for (int j0 = row_begin; j0 < row_end; j0 += 64) {
     __syncthreads();  // previous sub-chunk's LDS reads are done
     for (int p = wave; p < nseg * 8; p += 4) {
@@ -1331,8 +1354,8 @@ static bool gfold_use_mfma(int R, bool qu) {
 template <typename E>
 static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
                               const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax, GfoldWs ws,
-                              int nch, void* out, int ld_out, hipStream_t s, bool do_partial, bool do_out,
-                              AttnDrop dr) {
+                              int nch, int chr, void* out, int ld_out, hipStream_t s, bool do_partial,
+                              bool do_out, AttnDrop dr) {
   const int R = B * gmax;
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
     const size_t lds_p = (size_t)(D / 64) * 64 * 128 + 64 * 16 * 2 + GF_RED_FLOATS * sizeof(float);
@@ -1343,17 +1366,17 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
     if (DD % 128 == 0 && DD <= 768 && Lp <= 128 && g_knob[KNOB_GFOLD_PATH] != 3) {                \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_ring<E, DD>,                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_r);        \
-      k_gfold_partial_ring<E, DD><<<dim3(nch, R), 256, lds_r, s>>>(Lp, gmax, (const E*)h, ldh,  \
+      k_gfold_partial_ring<E, DD><<<dim3(nch, R), 256, lds_r, s>>>(Lp, gmax, chr, (const E*)h, ldh,  \
                                                                 flags, gidx, ws, H, dr);        \
     } else if (DD % 128 == 0) {                                                                 \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<E, DD>,                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
-      k_gfold_partial_bf16<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const E*)h, ldh,  \
+      k_gfold_partial_bf16<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, chr, (const E*)h, ldh,  \
                                                                 flags, gidx, ws, H, dr);        \
     } else {                                                                                    \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16_1<E, DD>,                        \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
-      k_gfold_partial_bf16_1<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, (const E*)h, ldh, \
+      k_gfold_partial_bf16_1<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, chr, (const E*)h, ldh, \
                                                                   flags, gidx, ws, H, dr);      \
     }                                                                                           \
     break;
@@ -1399,15 +1422,15 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
 // partial + out stages shared by both entry points (u already in the workspace)
 static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const void* wvg,
                             const float* bvg, const uint8_t* flags, const int32_t* gidx, int gmax,
-                            GfoldWs ws, int nch, void* out, int ld_out, hipStream_t s, bool do_partial = true,
+                            GfoldWs ws, int nch, int chr, void* out, int ld_out, hipStream_t s, bool do_partial = true,
                             bool do_out = true, AttnDrop dr = AttnDrop{0, 0, 1.f}) {
   const int R = B * gmax;
   const size_t lds_o = (size_t)(D + nch) * sizeof(float);
   if (dtype == RF_BF16 || dtype == RF_F16) {
     return dtype == RF_F16
-               ? fold_partial_out16<f16>(B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s,
+               ? fold_partial_out16<f16>(B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, chr, out, ld_out, s,
                                          do_partial, do_out, dr)
-               : fold_partial_out16<bf16>(B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s,
+               : fold_partial_out16<bf16>(B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, chr, out, ld_out, s,
                                           do_partial, do_out, dr);
   } else {
     const size_t lds_p = (size_t)(H * (D + 4) + H * GF_CHF) * sizeof(float);
@@ -1443,7 +1466,8 @@ extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int
   RF_REQUIRE(dtype == RF_F32 || ldh % 8 == 0, "rf_global_attn_fold_fwd(16-bit): ldh must be a multiple of 8");
   RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_fwd(f32): ldh must be a multiple of 4");
   const int R = B * gmax;
-  const int nch = (Lp + (dtype != RF_F32 ? GF_CH : GF_CHF) - 1) / (dtype != RF_F32 ? GF_CH : GF_CHF);
+  const int chr = gfold_chunk(dtype, R, Lp);
+  const int nch = (Lp + chr - 1) / chr;
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16)
@@ -1455,7 +1479,8 @@ extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int
     k_gfold_u<float><<<dim3(H, R), 192, 0, s>>>(D, H, R, (const float*)qg, ld_qg, (const float*)wkg, gidx,
                                                  ws, false);
   const int rc =
-      fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s, true, true, dr);
+      fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, chr, out, ld_out, s, true,
+                       true, dr);
   if (rc != RF_OK) return rc;
   RF_LAUNCH_CHECK("rf_global_attn_fold_fwd");
 }
@@ -1509,7 +1534,9 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
   RF_REQUIRE(dtype == RF_F32 || ldh % 8 == 0, "rf_global_attn_fold_h(16-bit): ldh must be a multiple of 8");
   RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_h(f32): ldh must be a multiple of 4");
   const int R = B * gmax;
-  const int nch = (Lp + (dtype != RF_F32 ? GF_CH : GF_CHF) - 1) / (dtype != RF_F32 ? GF_CH : GF_CHF);
+  // fixed chunks here (inference): a sequence's result does not depend on the batch it is in
+  const int chr = dtype != RF_F32 ? GF_CH : GF_CHF;
+  const int nch = (Lp + chr - 1) / chr;
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
   if (!(stage & 1)) {
@@ -1549,8 +1576,8 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
   else
     k_gfold_qu<float><<<dim3(H, R), 256, 0, s>>>(Lp, D, H, gmax, (const float*)h, ldh, (const float*)wqg, bqg,
                                                   q_scale, (const float*)wkg, gidx, ws, false);
-  const int rc = fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, out, ld_out, s,
-                                  (stage & 1) != 0, (stage & 2) != 0);
+  const int rc = fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, chr, out, ld_out,
+                                  s, (stage & 1) != 0, (stage & 2) != 0);
   if (rc != RF_OK) return rc;
   RF_LAUNCH_CHECK("rf_global_attn_fold_h_stage");
 }
@@ -1869,7 +1896,7 @@ extern "C" int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const 
              "rf_global_fold_bwd: null pointer");
   RF_REQUIRE(ldh % 8 == 0 && lddh % 8 == 0 && ldh >= D && lddh >= D, "rf_global_fold_bwd: leading dims");
   const int R = B * gmax;
-  const int nch = (Lp + GF_CH - 1) / GF_CH;
+  const int nch = (Lp + gfold_chunk(dtype, R, Lp) - 1) / gfold_chunk(dtype, R, Lp);  // the forward's chunks
   const int nch2 = (Lp + GB_ROWS - 1) / GB_ROWS;
   GfoldWs fws = gfold_carve(const_cast<void*>(fwd_workspace), R, nch, H, D);
   char* p = reinterpret_cast<char*>(workspace);

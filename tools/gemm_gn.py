@@ -18,7 +18,7 @@ from tools.gemm_ab import timeit  # noqa: E402
 def main():
     gns = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "2,3,4,6,12").split(",")]
     knob = sys.argv[2] if len(sys.argv) > 2 else "gemm_gn"
-    default = {"gemm_gn": 6, "gemm_variant": 5}[knob]
+    default = {"gemm_gn": 6, "gemm_variant": 8, "gemm_pf": -1}[knob]
     dev = torch.device("cuda")
     torch.manual_seed(0)
     M = 65536

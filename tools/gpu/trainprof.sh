@@ -10,7 +10,7 @@ f = glob.glob('gpurun_out/' + __import__('os').environ.get('TRAIN_OUT', 'trainpr
 rows = list(csv.DictReader(open(f)))
 tot = sum(float(r['TotalDurationNs']) for r in rows)
 print("kernel ms per step", round(tot / 1e6 / 4, 2))
-for r in rows[:25]:
+for r in rows[:int(__import__('os').environ.get('TOPN', '25'))]:
     print(f"{float(r['TotalDurationNs'])/tot*100:5.1f}% {int(r['Calls']):5d} {float(r['AverageNs'])/1e3:8.1f}us  {r['Name'][:100]}")
 PY
 tail -1 gpurun_out/$OUT.log

@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--torch-adamw", action="store_true", help="A/B: torch.optim.AdamW (multi-tensor) instead of "
                     "recformer_amd.optim.AdamW (one HIP launch)")
     ap.add_argument("--ab-knob", default=None, help="A/B in one process: a library knob "
-                    "(recformer_amd._lib.set_knob) at 1 / 0")
+                    "(recformer_amd._lib.set_knob) at 1 / 0, or name=a,b for values a / b")
     ap.add_argument("--global-dh-f32", action="store_true", help="A/B: the global branch's dh as an fp32 product")
     a = ap.parse_args()
     if a.global_dh_f32:
@@ -105,12 +105,16 @@ def main():
         # clocks differ across boxes and drift under load: alternate blocks in one process
         from recformer_amd import _lib, train
         res = {True: [], False: []}
+        kname, kvals = a.ab_knob, (1, 0)
+        if a.ab_knob and "=" in a.ab_knob:
+            kname, v = a.ab_knob.split("=")
+            kvals = tuple(int(x) for x in v.split(","))
         for rep in range(6):
             for val in (True, False):
                 if a.ab:
                     setattr(train, a.ab, val)
                 else:
-                    _lib.set_knob(a.ab_knob, 1 if val else 0)
+                    _lib.set_knob(kname, kvals[0] if val else kvals[1])
                 step()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
