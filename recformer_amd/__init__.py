@@ -10,7 +10,8 @@ from .models import (RecformerEmbeddings, RecformerForPretraining, RecformerForS
                      RecformerPretrainingOutput, Similarity, create_position_ids_from_input_ids)
 
 _LAZY = {"RecformerTokenizer": "data", "FinetuneDataCollatorWithPadding": "data",
-         "EvalDataCollatorWithPadding": "data", "LitWrapper": "lit", "GraphedForward": "graphs"}
+         "EvalDataCollatorWithPadding": "data", "LitWrapper": "lit", "GraphedForward": "graphs",
+         "CapturedTrainStep": "graphs", "AdamW": "optim"}
 
 
 def __getattr__(name):  # host-side pieces load transformers / the host library on first use
@@ -25,4 +26,5 @@ __all__ = [
     "RecformerPretrainingOutput", "RecformerModelOutput", "RecformerEmbeddings", "RecformerPooler",
     "Similarity", "create_position_ids_from_input_ids", "Ranker", "rank_catalog", "CatalogShard", "retrieve", "RecformerTokenizer",
     "FinetuneDataCollatorWithPadding", "EvalDataCollatorWithPadding", "LitWrapper", "GraphedForward",
+    "CapturedTrainStep", "AdamW",
 ]

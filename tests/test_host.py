@@ -157,3 +157,10 @@ def test_adamw_host_checks():
     p.grad = torch.ones(3)
     with pytest.raises(ValueError):
         opt.step()
+
+
+def test_package_exports_resolve():
+    """Every name in recformer_amd.__all__ resolves (lazy host-side pieces included)."""
+    import recformer_amd
+    for name in recformer_amd.__all__:
+        assert getattr(recformer_amd, name) is not None, name
