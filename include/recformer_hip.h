@@ -443,6 +443,34 @@ int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const void* h, in
                        float p_drop, uint64_t seed, void* dh, int lddh, float* du, float* w, float* stats,
                        void* workspace, rf_stream_t stream);
 
+/* The whole global-branch backward of one attention layer (the autograd of TF:964-1057 for the global
+ * query rows and the key_global / value_global weights), from the attention output gradient: do_h is
+ * read at the global rows of dout (B*Lp rows, lddout, 16-bit; empty slots contribute 0), dw_h = Wvg_h^T
+ * do_h and c_h = do_h . bvg_h are formed inside, then rf_global_fold_bwd's pass over h (dh written),
+ * then dqg (B*gmax, D) fp32 = per head Wkg_h du_h, dWkg = sum_r qg_r du_r^T and dWvg = sum_r do_r w_r^T
+ * (D x D fp32, written, not accumulated), dbvg = sum_r do_r S'_r (D fp32) and dbkg = 0 (D fp32, may be
+ * NULL; softmax-invariant). qg: the forward's scaled query_global rows (B*gmax, ldqg, 16-bit); wkg / wvg:
+ * the (D x D) key_global / value_global weights in the compute dtype. Same shapes and limits as
+ * rf_global_fold_bwd, B*gmax <= 1024. Workspace: rf_global_fold_bwd_full_workspace bytes. */
+size_t rf_global_fold_bwd_full_workspace(int B, int Lp, int D, int gmax);
+int rf_global_fold_bwd_full(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const uint8_t* flags,
+                            const int32_t* gidx, int gmax, const void* fwd_workspace, const void* dout, int lddout,
+                            const void* qg, int ldqg, const void* wkg, const void* wvg, const float* bvg, float p_drop,
+                            uint64_t seed, void* dh, int lddh, float* dqg, float* dwkg, float* dwvg, float* dbvg,
+                            float* dbkg, void* workspace, rf_stream_t stream);
+
+/* Gradient of the global-key / global-value rows of the local branch (the key / value projections at
+ * the global positions, TF:562-575 under autograd): with gds / gpr the band backward's (B, H, Lp, gmax)
+ * fp32 dS / P columns of the global keys (rf_band_attn_bwd_drop),
+ *   dk[b*Lp + gidx[b][g]][h*64+d] += sum_i gds[b][h][i][g] q[b*Lp+i][h*64+d]
+ *   dv[b*Lp + gidx[b][g]][h*64+d] += sum_i gpr[b][h][i][g] dout[b*Lp+i][h*64+d]
+ * in place (16-bit dk / dv, e.g. column views of the fused dqkv), fp32 accumulation in a fixed order;
+ * empty slots (gidx < 0) skipped. Replaces the reference's gather of the global key / value rows'
+ * gradients through autograd (and a batched product plus a scatter). */
+int rf_global_kv_grad(int dtype, int B, int Lp, int H, int gmax, const float* gds, const float* gpr, const void* q,
+                      int ldq, const void* dout, int lddout, const int32_t* gidx, void* dk, int ldk, void* dv,
+                      int ldv, rf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,11 @@ SIGNATURES = {
     "rf_global_fold_bwd_workspace": (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),
     "rf_global_fold_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P, P, c_float,
                                    ctypes.c_uint64, P, c_int, P, P, P, P, P]),
+    "rf_global_fold_bwd_full_workspace": (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),
+    "rf_global_fold_bwd_full": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P, c_int, P,
+                                        c_int, P, P, P, c_float, ctypes.c_uint64, P, c_int, P, P, P, P, P, P, P]),
+    "rf_global_kv_grad": (c_int, [c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, c_int, P, P, c_int, P, c_int,
+                                  P]),
     "rf_adamw_chunk": (c_int, []),
     "rf_set_seed_source": (P, [P]),
     "rf_adamw_step": (c_int, [P, c_int, P, c_int, P]),

@@ -1614,39 +1614,77 @@ namespace rf {
 constexpr int GB_ROWS = 64;  // rows per k_gbwd_main block
 constexpr int GB_GMAX = 4;   // global rows per sequence the kernel takes (more: the torch path)
 
-template <typename E>
-__global__ void __launch_bounds__(256) k_gbwd_prep(int D, int H, int nch, const int32_t* __restrict__ gidx,
-                                                   GfoldWs ws, const float* __restrict__ dw,
-                                                   const float* __restrict__ cb, int drop, float* __restrict__ wout,
-                                                   float* __restrict__ st, E* __restrict__ dwp, E* __restrict__ bt) {
+// Per (global row r, head h). FROM_DOUT (rf_global_fold_bwd_full): dw_h = Wvg_h^T do_h and
+// c_h = do_h . bvg_h from the attention output gradient's global row and the weights, else given.
+// The chunk statistics are merged by one lane per chunk (nch <= 64) and the per-chunk scales kept in
+// LDS, so the w merge issues its chunk loads together instead of one dependent load per chunk.
+template <typename E, bool FROM_DOUT>
+__global__ void __launch_bounds__(256) k_gbwd_prep(int D, int H, int nch, int Lp, int gmax,
+                                                   const int32_t* __restrict__ gidx, GfoldWs ws,
+                                                   const float* __restrict__ dw, const float* __restrict__ cb,
+                                                   const E* __restrict__ dout, int ldd, const E* __restrict__ wvg,
+                                                   const float* __restrict__ bvg, float* __restrict__ cbw, int drop,
+                                                   float* __restrict__ wout, float* __restrict__ st,
+                                                   E* __restrict__ dwp, E* __restrict__ bt) {
   __shared__ float red[4];
+  __shared__ float scs[64];    // per-chunk scale exp(m_c - M) / L
+  __shared__ float dos[64];    // do_h (FROM_DOUT)
+  __shared__ float stat[4];    // M, 1/L, S', c
   const int r = blockIdx.x, h = blockIdx.y, t = threadIdx.x;
-  const bool live = h < H && gidx[r] >= 0;
-  float M = GF_NEG_INF, L = 0.f, LD = 0.f;
-  if (live) {
-    for (int c = 0; c < nch; ++c) M = fmaxf(M, ws.m[((int64_t)r * nch + c) * GF_HP + h]);
-    for (int c = 0; c < nch; ++c) {
-      const float mc = ws.m[((int64_t)r * nch + c) * GF_HP + h];
-      const float sc = mc == GF_NEG_INF ? 0.f : __expf(mc - M);
-      L += sc * ws.l[((int64_t)r * nch + c) * GF_HP + h];
-      if (drop) LD += sc * ws.ld[((int64_t)r * nch + c) * GF_HP + h];
+  const int pos = gidx[r];
+  const bool live = h < H && pos >= 0;
+  if (t < 64) {
+    float mc = GF_NEG_INF, lc = 0.f, ldc = 0.f;
+    if (live && t < nch) {
+      const int64_t o = ((int64_t)r * nch + t) * GF_HP + h;
+      mc = ws.m[o];
+      lc = ws.l[o];
+      if (drop) ldc = ws.ld[o];
+    }
+    const float M = wave_max(mc);
+    const float sc = mc == GF_NEG_INF ? 0.f : __expf(mc - M);
+    const float L = wave_sum(sc * lc);
+    const float LD = drop ? wave_sum(sc * ldc) : 0.f;
+    const float inv = L > 0.f ? 1.0f / L : 0.f;
+    if (t < nch) scs[t] = sc * inv;
+    if (t == 0) {
+      stat[0] = live ? M : 0.f;
+      stat[1] = inv;
+      stat[2] = live ? (drop ? LD * inv : 1.f) : 0.f;
+    }
+  } else if (t < 128) {
+    float c = 0.f;
+    if (FROM_DOUT) {
+      const int d = t - 64;
+      const float v = live ? to_f32(dout[((int64_t)(r / gmax) * Lp + pos) * ldd + h * 64 + d]) : 0.f;
+      dos[d] = v;
+      if (drop) c = wave_sum(v * bvg[h * 64 + d]);
+    } else if (live && cb) {
+      c = cb[r * GF_HP + h];
+    }
+    if (t == 64) {
+      stat[3] = c;
+      if (FROM_DOUT && cbw) cbw[r * GF_HP + h] = c;
     }
   }
-  const float inv = L > 0.f ? 1.0f / L : 0.f;
-  const float Sp = live ? (drop ? LD * inv : 1.f) : 0.f;
-  const float c = (live && cb) ? cb[r * GF_HP + h] : 0.f;
+  __syncthreads();
+  const float inv = stat[1], Sp = stat[2], c = stat[3];
   const E* u16 = reinterpret_cast<const E*>(ws.u16);
   float dsum = 0.f;
   for (int k = t; k < D; k += 256) {
     float wv = 0.f, dv = 0.f;
     E uh = (E)0.f;
     if (live) {
-      for (int cc = 0; cc < nch; ++cc) {
-        const float mc = ws.m[((int64_t)r * nch + cc) * GF_HP + h];
-        const float sc = (mc == GF_NEG_INF ? 0.f : __expf(mc - M)) * inv;
-        wv += sc * ws.w[(((int64_t)r * nch + cc) * GF_HP + h) * D + k];
+      const float* wp = ws.w + ((int64_t)r * nch * GF_HP + h) * D + k;
+#pragma unroll 4
+      for (int cc = 0; cc < nch; ++cc) wv += scs[cc] * wp[(int64_t)cc * GF_HP * D];
+      if (FROM_DOUT) {
+        const E* vp = wvg + (int64_t)(h * 64) * D + k;
+#pragma unroll 16
+        for (int d = 0; d < 64; ++d) dv = fmaf(dos[d], to_f32(vp[(int64_t)d * D]), dv);
+      } else {
+        dv = dw[((int64_t)r * GF_HP + h) * D + k];
       }
-      dv = dw[((int64_t)r * GF_HP + h) * D + k];
       uh = u16[((int64_t)r * 2 * GF_HP + h) * D + k];
     }
     wout[((int64_t)r * GF_HP + h) * D + k] = wv;
@@ -1662,7 +1700,7 @@ __global__ void __launch_bounds__(256) k_gbwd_prep(int D, int H, int nch, const 
   __syncthreads();
   if (t == 0) {
     float* o = st + ((int64_t)r * GF_HP + h) * 4;
-    o[0] = live ? M : 0.f;
+    o[0] = stat[0];
     o[1] = inv;
     o[2] = ((red[0] + red[1]) + red[2]) + red[3] + c * Sp;
     o[3] = Sp;
@@ -1862,6 +1900,138 @@ __global__ void __launch_bounds__(256) k_gbwd_reduce(int R, int D, int nch2, con
   du[idx] = s;
 }
 
+// dqg / dWkg / dWvg / dbvg / dbkg of the global branch from du, w and S' (rf_global_fold_bwd_full);
+// grid R*H + 2*D blocks. Block (r, h) < R*H: dqg[r][h*64+i] = sum_c du[r][h][c] Wkg[h*64+i][c] (four
+// threads per output over the row of Wkg). Then one block per output row o of dWkg (which = 0) or
+// dWvg (which = 1), h = o / 64, over the global rows (K = R, a few):
+//   dWkg[o][c] = sum_r qg[r][o] du[r][h][c],  dWvg[o][c] = sum_r do[r][o] w[r][h][c],
+//   dbvg[o] = sum_r do[r][o] S'[r][h],  dbkg[o] = 0 (softmax-invariant); empty slots contribute 0.
+template <typename E>
+__global__ void __launch_bounds__(256) k_gbwd_post(int D, int H, int Lp, int gmax, int R,
+                                                   const int32_t* __restrict__ gidx, const E* __restrict__ dout,
+                                                   int ldd, const E* __restrict__ qg, int ldq,
+                                                   const E* __restrict__ wkg, const float* __restrict__ du,
+                                                   const float* __restrict__ w, const float* __restrict__ st,
+                                                   float* __restrict__ dqg, float* __restrict__ dwkg,
+                                                   float* __restrict__ dwvg, float* __restrict__ dbvg,
+                                                   float* __restrict__ dbkg) {
+  __shared__ float sh[1024];
+  const int bid = blockIdx.x, t = threadIdx.x;
+  if (bid < R * H) {
+    const int r = bid / H, h = bid - (bid / H) * H;
+    const bool live = gidx[r] >= 0;
+    for (int k = t; k < D; k += 256) sh[k] = live ? du[((int64_t)r * GF_HP + h) * D + k] : 0.f;
+    __syncthreads();
+    const int i = t >> 2, part = t & 3;
+    const E* wr = wkg + (int64_t)(h * 64 + i) * D;
+    float a = 0.f;
+    for (int k = 8 * part; k < D; k += 32) {
+      float x[8];
+      load4(wr + k, x);
+      load4(wr + k + 4, x + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a = fmaf(x[j], sh[k + j], a);
+    }
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (part == 0) dqg[(int64_t)r * D + h * 64 + i] = a;
+    return;
+  }
+  const int o2 = bid - R * H, which = o2 >= D ? 1 : 0, o = o2 - which * D, h = o >> 6;
+  for (int rr = t; rr < R; rr += 256) {
+    const int pos = gidx[rr];
+    float c = 0.f;
+    if (pos >= 0)
+      c = which == 0 ? to_f32(qg[(int64_t)rr * ldq + o]) : to_f32(dout[((int64_t)(rr / gmax) * Lp + pos) * ldd + o]);
+    sh[rr] = c;
+  }
+  __syncthreads();
+  const float* src = (which == 0 ? du : w) + (int64_t)h * D;
+  float* dst = (which == 0 ? dwkg : dwvg) + (int64_t)o * D;
+  for (int c = t; c < D; c += 256) {
+    float a = 0.f;
+#pragma unroll 4
+    for (int rr = 0; rr < R; ++rr) a = fmaf(sh[rr], src[(int64_t)rr * GF_HP * D + c], a);
+    dst[c] = a;
+  }
+  if (t == 0) {
+    if (which == 1) {
+      float a = 0.f;
+      for (int rr = 0; rr < R; ++rr) a = fmaf(sh[rr], st[((int64_t)rr * GF_HP + h) * 4 + 3], a);
+      dbvg[o] = a;
+    } else if (dbkg) {
+      dbkg[o] = 0.f;
+    }
+  }
+}
+
+// Gradient of the global-key (value) rows of the local branch: the band backward's dS (P) columns of
+// the global keys, reduced over every query of the sequence and added at the global positions:
+//   dk[b*Lp + gidx[b][g]][h*64+d] += sum_i gds[b][h][i][g] q[b*Lp+i][h*64+d]   (blockIdx.y = 0)
+//   dv[b*Lp + gidx[b][g]][h*64+d] += sum_i gpr[b][h][i][g] dout[b*Lp+i][h*64+d] (blockIdx.y = 1)
+// Block (b*H + h, k|v): thread (32 row groups x 8 column octets, 16-B loads, 8 rows in flight), 4
+// global slots per pass, fp32 accumulation in a fixed order (row group, then the 32 groups summed in
+// order), one rounding into dk.
+template <typename E>
+__global__ void __launch_bounds__(256) k_global_kv_grad(int Lp, int H, int gmax, const float* __restrict__ gds,
+                                                        const float* __restrict__ gpr, const E* __restrict__ q,
+                                                        int ldq, const E* __restrict__ dout, int ldd,
+                                                        const int32_t* __restrict__ gidx, E* __restrict__ dk,
+                                                        int ldk, E* __restrict__ dv, int ldv) {
+  typedef typename H16<E>::x8 V8;
+  __shared__ float red[32][4][64];
+  const int bh = blockIdx.x, b = bh / H, h = bh - (bh / H) * H, kv = blockIdx.y;
+  const float* wsrc = (kv ? gpr : gds) + (int64_t)bh * Lp * gmax;
+  const E* x = (kv ? dout : q) + (int64_t)b * Lp * (kv ? ldd : ldq) + h * 64;
+  const int ldx = kv ? ldd : ldq;
+  E* dst = kv ? dv : dk;
+  const int ldo = kv ? ldv : ldk;
+  const int t = threadIdx.x, c8 = (t & 7) * 8, rg = t >> 3;
+  for (int g0 = 0; g0 < gmax; g0 += 4) {
+    const int gn = min(4, gmax - g0);
+    float acc[4][8];
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[gg][j] = 0.f;
+    // rows rg, rg + 32, ...: 8 rows per batch, their loads issued together
+    for (int i0 = rg; i0 < Lp; i0 += 32 * 8) {
+      V8 xv[8];
+      float wv[8][4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 32 * u;
+        xv[u] = i < Lp ? *reinterpret_cast<const V8*>(x + (int64_t)i * ldx + c8) : V8{};
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) wv[u][gg] = (i < Lp && gg < gn) ? wsrc[(int64_t)i * gmax + g0 + gg] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[gg][j] = fmaf(wv[u][gg], to_f32(xv[u][j]), acc[gg][j]);
+    }
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[rg][gg][c8 + j] = acc[gg][j];
+    __syncthreads();
+    const int gg = t >> 6, col = t & 63;
+    if (gg < gn) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) sum += red[k][gg][col];
+      const int pos = gidx[b * gmax + g0 + gg];
+      if (pos >= 0) {
+        E* o = dst + ((int64_t)b * Lp + pos) * ldo + h * 64 + col;
+        *o = (E)(to_f32(*o) + sum);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 struct GbwdWs {
   char* dwp;
   char* bt;
@@ -1881,20 +2051,14 @@ extern "C" size_t rf_global_fold_bwd_workspace(int B, int Lp, int D, int gmax) {
   return gbwd_bytes(B * gmax, Lp, D);
 }
 
-extern "C" int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
-                                  const uint8_t* flags, const int32_t* gidx, int gmax, const void* fwd_workspace,
-                                  const float* dw, const float* cb, float p_drop, uint64_t seed, void* dh, int lddh,
-                                  float* du, float* w, float* stats, void* workspace, rf_stream_t stream) {
-  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_global_fold_bwd: 16-bit operands only");
-  RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0 && H <= GF_HP && D == 64 * H,
-             "rf_global_fold_bwd: bad shape B=%d Lp=%d D=%d H=%d", B, Lp, D, H);
-  RF_REQUIRE(D % 128 == 0 && D <= 768, "rf_global_fold_bwd: D=%d (multiples of 128 up to 768)", D);
-  RF_REQUIRE(gmax <= GB_GMAX, "rf_global_fold_bwd: at most %d global rows per sequence", GB_GMAX);
-  RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_global_fold_bwd: p_drop %f", p_drop);
-  if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
-  RF_REQUIRE(h && flags && gidx && fwd_workspace && dw && dh && du && w && stats && workspace,
-             "rf_global_fold_bwd: null pointer");
-  RF_REQUIRE(ldh % 8 == 0 && lddh % 8 == 0 && ldh >= D && lddh >= D, "rf_global_fold_bwd: leading dims");
+// shared by rf_global_fold_bwd (dw / cb given) and rf_global_fold_bwd_full (FROM_DOUT: dw / c from
+// the output gradient's global rows and Wvg / bvg inside the prep kernel; cbw receives c)
+static void gbwd_run(int dtype, int B, int Lp, int D, int H, const void* h, int ldh, const uint8_t* flags,
+                     const int32_t* gidx, int gmax, const void* fwd_workspace, const float* dw, const float* cb,
+                     const void* dout, int ldd, const void* wvg, const float* bvg, float* cbw, float p_drop,
+                     uint64_t seed, void* dh, int lddh, float* du, float* w, float* stats, void* workspace,
+                     hipStream_t s) {
+  const bool from_dout = dout != nullptr;
   const int R = B * gmax;
   const int nch = (Lp + gfold_chunk(dtype, R, Lp) - 1) / gfold_chunk(dtype, R, Lp);  // the forward's chunks
   const int nch2 = (Lp + GB_ROWS - 1) / GB_ROWS;
@@ -1905,16 +2069,23 @@ extern "C" int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const 
   bw.bt = p; p += align256((size_t)R * D * 32 * 2);
   bw.dupart = reinterpret_cast<float*>(p);
   const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f, g_seed_dev};
-  hipStream_t s = as_stream(stream);
+  const int drop = p_drop > 0.f ? 1 : 0;
+  const float* cbm = from_dout ? (drop ? cbw : nullptr) : cb;  // the main kernel's c terms
   const size_t lds = (size_t)D * 128 + 2 * 4 * 64 * 16 * 4 + (size_t)GB_GMAX * 64 * 32 * 2;
 #define GB_(EE, DD)                                                                                          \
   case DD:                                                                                                   \
-    k_gbwd_prep<EE><<<dim3(R, GF_HP), 256, 0, s>>>(D, H, nch, gidx, fws, dw, cb, p_drop > 0.f ? 1 : 0, w,      \
-                                                   stats, (EE*)bw.dwp, (EE*)bw.bt);                            \
+    if (from_dout)                                                                                           \
+      k_gbwd_prep<EE, true><<<dim3(R, GF_HP), 256, 0, s>>>(D, H, nch, Lp, gmax, gidx, fws, nullptr, nullptr,  \
+                                                           (const EE*)dout, ldd, (const EE*)wvg, bvg, cbw,    \
+                                                           drop, w, stats, (EE*)bw.dwp, (EE*)bw.bt);          \
+    else                                                                                                     \
+      k_gbwd_prep<EE, false><<<dim3(R, GF_HP), 256, 0, s>>>(D, H, nch, Lp, gmax, gidx, fws, dw, cb, nullptr,  \
+                                                            0, nullptr, nullptr, nullptr, drop, w, stats,     \
+                                                            (EE*)bw.dwp, (EE*)bw.bt);                         \
     (void)hipFuncSetAttribute((const void*)k_gbwd_main<EE, DD>, hipFuncAttributeMaxDynamicSharedMemorySize,    \
                               (int)lds);                                                                       \
     k_gbwd_main<EE, DD><<<dim3(nch2, B), 256, lds, s>>>(Lp, gmax, H, (const EE*)h, ldh, flags, gidx, fws,      \
-                                                        (const EE*)bw.dwp, (const EE*)bw.bt, stats, cb,        \
+                                                        (const EE*)bw.dwp, (const EE*)bw.bt, stats, cbm,       \
                                                         bw.dupart, (EE*)dh, lddh, dr);                         \
     break;
   if (dtype == RF_F16) {
@@ -1925,5 +2096,93 @@ extern "C" int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const 
 #undef GB_
   const int64_t n = (int64_t)R * GF_HP * D;
   k_gbwd_reduce<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(R, D, nch2, gidx, bw.dupart, du);
+}
+
+static int gbwd_check(int dtype, int B, int Lp, int D, int H, int gmax, float p_drop, const char* name) {
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "%s: 16-bit operands only", name);
+  RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0 && H <= GF_HP && D == 64 * H,
+             "%s: bad shape B=%d Lp=%d D=%d H=%d", name, B, Lp, D, H);
+  RF_REQUIRE(D % 128 == 0 && D <= 768, "%s: D=%d (multiples of 128 up to 768)", name, D);
+  RF_REQUIRE(gmax <= GB_GMAX, "%s: at most %d global rows per sequence", name, GB_GMAX);
+  RF_REQUIRE(Lp <= 64 * 64, "%s: Lp=%d (at most 64 chunks of the forward pass)", name, Lp);
+  RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "%s: p_drop %f", name, p_drop);
+  return RF_OK;
+}
+
+extern "C" int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
+                                  const uint8_t* flags, const int32_t* gidx, int gmax, const void* fwd_workspace,
+                                  const float* dw, const float* cb, float p_drop, uint64_t seed, void* dh, int lddh,
+                                  float* du, float* w, float* stats, void* workspace, rf_stream_t stream) {
+  const int rc = gbwd_check(dtype, B, Lp, D, H, gmax, p_drop, "rf_global_fold_bwd");
+  if (rc != RF_OK) return rc;
+  if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
+  RF_REQUIRE(h && flags && gidx && fwd_workspace && dw && dh && du && w && stats && workspace,
+             "rf_global_fold_bwd: null pointer");
+  RF_REQUIRE(ldh % 8 == 0 && lddh % 8 == 0 && ldh >= D && lddh >= D, "rf_global_fold_bwd: leading dims");
+  gbwd_run(dtype, B, Lp, D, H, h, ldh, flags, gidx, gmax, fwd_workspace, dw, cb, nullptr, 0, nullptr, nullptr,
+           nullptr, p_drop, seed, dh, lddh, du, w, stats, workspace, as_stream(stream));
   RF_LAUNCH_CHECK("rf_global_fold_bwd");
+}
+
+extern "C" size_t rf_global_fold_bwd_full_workspace(int B, int Lp, int D, int gmax) {
+  if (B <= 0 || gmax <= 0 || Lp <= 0) return 0;
+  const size_t R = (size_t)B * gmax;
+  return gbwd_bytes(B * gmax, Lp, D) + 2 * align256(R * GF_HP * D * 4) + align256(R * GF_HP * 4 * 4) +
+         align256(R * GF_HP * 4) + 256;
+}
+
+extern "C" int rf_global_fold_bwd_full(int dtype, int B, int Lp, int D, int H, const void* h, int ldh,
+                                       const uint8_t* flags, const int32_t* gidx, int gmax,
+                                       const void* fwd_workspace, const void* dout, int lddout, const void* qg,
+                                       int ldqg, const void* wkg, const void* wvg, const float* bvg, float p_drop,
+                                       uint64_t seed, void* dh, int lddh, float* dqg, float* dwkg, float* dwvg,
+                                       float* dbvg, float* dbkg, void* workspace, rf_stream_t stream) {
+  const int rc = gbwd_check(dtype, B, Lp, D, H, gmax, p_drop, "rf_global_fold_bwd_full");
+  if (rc != RF_OK) return rc;
+  if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
+  RF_REQUIRE(h && flags && gidx && fwd_workspace && dout && qg && wkg && wvg && bvg && dh && dqg && dwkg && dwvg &&
+                 dbvg && workspace,
+             "rf_global_fold_bwd_full: null pointer");
+  RF_REQUIRE(ldh % 8 == 0 && lddh % 8 == 0 && ldh >= D && lddh >= D && lddout >= D && ldqg >= D,
+             "rf_global_fold_bwd_full: leading dims");
+  RF_REQUIRE(B * gmax <= 1024, "rf_global_fold_bwd_full: at most 1024 global rows");
+  const int R = B * gmax;
+  char* p = reinterpret_cast<char*>(workspace) + gbwd_bytes(R, Lp, D);
+  p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255);
+  float* du = reinterpret_cast<float*>(p); p += align256((size_t)R * GF_HP * D * 4);
+  float* w = reinterpret_cast<float*>(p); p += align256((size_t)R * GF_HP * D * 4);
+  float* st = reinterpret_cast<float*>(p); p += align256((size_t)R * GF_HP * 4 * 4);
+  float* cbw = reinterpret_cast<float*>(p);
+  hipStream_t s = as_stream(stream);
+  gbwd_run(dtype, B, Lp, D, H, h, ldh, flags, gidx, gmax, fwd_workspace, nullptr, nullptr, dout, lddout, wvg, bvg,
+           cbw, p_drop, seed, dh, lddh, du, w, st, workspace, s);
+  if (dtype == RF_F16)
+    k_gbwd_post<f16><<<R * H + 2 * D, 256, 0, s>>>(D, H, Lp, gmax, R, gidx, (const f16*)dout, lddout, (const f16*)qg,
+                                                   ldqg, (const f16*)wkg, du, w, st, dqg, dwkg, dwvg, dbvg, dbkg);
+  else
+    k_gbwd_post<bf16><<<R * H + 2 * D, 256, 0, s>>>(D, H, Lp, gmax, R, gidx, (const bf16*)dout, lddout,
+                                                    (const bf16*)qg, ldqg, (const bf16*)wkg, du, w, st, dqg, dwkg,
+                                                    dwvg, dbvg, dbkg);
+  RF_LAUNCH_CHECK("rf_global_fold_bwd_full");
+}
+
+extern "C" int rf_global_kv_grad(int dtype, int B, int Lp, int H, int gmax, const float* gds, const float* gpr,
+                                 const void* q, int ldq, const void* dout, int lddout, const int32_t* gidx, void* dk,
+                                 int ldk, void* dv, int ldv, rf_stream_t stream) {
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_global_kv_grad: 16-bit operands only");
+  RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && H > 0, "rf_global_kv_grad: bad shape");
+  if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
+  RF_REQUIRE(gds && gpr && q && dout && gidx && dk && dv, "rf_global_kv_grad: null pointer");
+  RF_REQUIRE(ldq % 8 == 0 && lddout % 8 == 0 && ldq >= 64 * H && lddout >= 64 * H && ldk >= 64 * H && ldv >= 64 * H,
+             "rf_global_kv_grad: leading dims");
+  RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)dout & 15) == 0, "rf_global_kv_grad: q / dout 16-B aligned");
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_F16)
+    k_global_kv_grad<f16><<<dim3(B * H, 2), 256, 0, s>>>(Lp, H, gmax, gds, gpr, (const f16*)q, ldq, (const f16*)dout,
+                                                         lddout, gidx, (f16*)dk, ldk, (f16*)dv, ldv);
+  else
+    k_global_kv_grad<bf16><<<dim3(B * H, 2), 256, 0, s>>>(Lp, H, gmax, gds, gpr, (const bf16*)q, ldq,
+                                                          (const bf16*)dout, lddout, gidx, (bf16*)dk, ldk, (bf16*)dv,
+                                                          ldv);
+  RF_LAUNCH_CHECK("rf_global_kv_grad");
 }

@@ -687,6 +687,55 @@ def global_fold_bwd(h, flags, gidx, B: int, Lp: int, H: int, fwd_ws: torch.Tenso
     return du, w, stats
 
 
+def global_fold_bwd_full(h, flags, gidx, B: int, Lp: int, H: int, fwd_ws: torch.Tensor, dout, qg, wkg, wvg, bvg,
+                         p_drop: float, seed: int, dh: torch.Tensor, want_dbkg: bool = True):
+    """rf_global_fold_bwd_full: the global branch's whole backward from the attention output gradient
+    dout (B*Lp, >= D) 16-bit: writes dh (B*Lp, D) in h's dtype and returns fp32 (dqg (R, D), dwkg
+    (D, D), dbkg (D) of zeros or None, dwvg (D, D), dbvg (D)). qg (R, D) the forward's scaled
+    query_global rows; wkg / wvg (D, D) and bvg (D,) the weights the forward used."""
+    lib = _lib.load()
+    gmax = gidx.shape[1]
+    D = h.shape[1]
+    R = B * gmax
+    dev = h.device
+    for name, t in (("qg", qg), ("wkg", wkg), ("wvg", wvg)):
+        if t.dtype != h.dtype or t.stride(-1) != 1:
+            raise ValueError(f"global_fold_bwd_full: {name} must be row-major in h's dtype")
+    if tuple(wkg.shape) != (D, D) or tuple(wvg.shape) != (D, D) or not wkg.is_contiguous() or not wvg.is_contiguous():
+        raise ValueError("global_fold_bwd_full: wkg / wvg must be contiguous (D, D)")
+    bvg = bvg.float().contiguous()
+    dqg = torch.empty(R, D, dtype=torch.float32, device=dev)
+    dwkg = torch.empty(D, D, dtype=torch.float32, device=dev)
+    dwvg = torch.empty_like(dwkg)
+    dbvg = torch.empty(D, dtype=torch.float32, device=dev)
+    dbkg = torch.empty(D, dtype=torch.float32, device=dev) if want_dbkg else None
+    ws = torch.empty(max(lib.rf_global_fold_bwd_full_workspace(B, Lp, D, gmax), 16), dtype=torch.uint8, device=dev)
+    check(lib.rf_global_fold_bwd_full(dtype_code(h.dtype), B, Lp, D, H, _p(h), _rowmajor(h, "h"), _p(flags),
+                                      _p(gidx.to(torch.int32).contiguous()), gmax, _p(fwd_ws), _p(dout),
+                                      _rowmajor(dout, "dout"), _p(qg), _rowmajor(qg, "qg"), _p(wkg), _p(wvg), _p(bvg),
+                                      float(p_drop), int(seed) & (2**64 - 1), _p(dh), _rowmajor(dh, "dh"), _p(dqg),
+                                      _p(dwkg), _p(dwvg), _p(dbvg), _p(dbkg), _p(ws), _stream(h)),
+          "rf_global_fold_bwd_full")
+    return dqg, dwkg, dbkg, dwvg, dbvg
+
+
+def global_kv_grad(gds, gpr, q, dout, gidx, B: int, Lp: int, H: int, dk, dv):
+    """rf_global_kv_grad: dk / dv (16-bit row-major views, e.g. column slices of the fused dqkv) +=
+    the global-key / global-value rows' gradients reduced from the band backward's (B, H, Lp, gmax)
+    fp32 gds / gpr against q / dout (16-bit), at the global positions gidx (in place)."""
+    gmax = gidx.shape[1]
+    for name, t in (("gds", gds), ("gpr", gpr)):
+        if tuple(t.shape) != (B, H, Lp, gmax) or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"global_kv_grad: {name} must be contiguous fp32 (B, H, Lp, gmax)")
+    for name, t in (("dout", dout), ("dk", dk), ("dv", dv)):
+        if t.dtype != q.dtype:
+            raise ValueError(f"global_kv_grad: {name} must have q's dtype")
+    check(_lib.load().rf_global_kv_grad(dtype_code(q.dtype), B, Lp, H, gmax, _p(gds), _p(gpr), _p(q),
+                                        _rowmajor(q, "q"), _p(dout), _rowmajor(dout, "dout"),
+                                        _p(gidx.to(torch.int32).contiguous()), _p(dk), _rowmajor(dk, "dk"), _p(dv),
+                                        _rowmajor(dv, "dv"), _stream(q)), "rf_global_kv_grad")
+
+
 def attn_global_keep(gidx, B: int, Lp: int, H: int, p_drop: float, seed: int) -> torch.Tensor:
     """(B, H, gmax, Lp) fp32 attention-dropout scale of the global query rows (rf_attn_global_keep;
     the mask rf_global_attn_fold_fwd_drop applies)."""

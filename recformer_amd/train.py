@@ -57,8 +57,12 @@ GLOBAL_KV_BLOCKDIAG = True
 DW_SPLIT_K = True
 # embedding + LayerNorm backward on the HIP kernels (deterministic table gradients, no index_add_)
 EMBED_BWD_HIP = True
-# global rows' backward on rf_global_fold_bwd (one pass over h from the forward's fold workspace)
+# global rows' backward on rf_global_fold_bwd_full (one pass over h from the forward's fold workspace,
+# the per-head products with the key/value weights and the weight gradients inside)
 GLOBAL_BWD_HIP = True
+# the global-key / -value rows' gradients of the local branch on rf_global_kv_grad (one launch,
+# added in place into dk / dv) instead of two batched products, their copies and a scatter
+GLOBAL_KV_HIP = True
 # weight gradients on the HIP kernel (rf_weight_grad: MFMA, transposed LDS reads, fixed-order split
 # reduction) instead of hipBLASLt
 DW_HIP = True
@@ -585,34 +589,17 @@ def _fold_ws(h, B: int, Lp: int, H: int, G: int):
     return None
 
 
-def _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, gout, ws, p_drop: float, seed: int):
-    """_global_bwd on rf_global_fold_bwd (one pass over h, from the forward's fold workspace): the
-    per-head GEMVs of do / du with the (d x d) weights stay torch (a few hundred KB); returns fp32
-    (dqg, dh (h's dtype), dwkg, dbkg, dwvg, dbvg) like _global_bwd."""
+def _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, d16, ws, p_drop: float, seed: int):
+    """_global_bwd on rf_global_fold_bwd_full: the global rows' whole backward from the attention output
+    gradient d16 (16-bit, the global rows read at gidx) and the forward's fold workspace (one pass over
+    h; the per-head products with the (d x d) weights inside); returns fp32 (dqg, dh (h's dtype), dwkg,
+    dbkg, dwvg, dbvg) like _global_bwd."""
     D = h.shape[1]
-    hd = D // H
-    G = gidx.shape[1]
-    R = B * G
-    dev = h.device
-    wk = wkg.float().view(H, hd, D)
-    wv = wvg.float().view(H, hd, D)
-    qH = qg.float().view(R, H, hd).transpose(0, 1)                           # (H, R, hd)
-    doH = gout.float().view(R, H, hd).transpose(0, 1)                        # (H, R, hd)
-    dw = torch.zeros(R, 16, D, dtype=torch.float32, device=dev)
-    dw[:, :H] = torch.bmm(doH, wv).transpose(0, 1)
-    cb = None
-    if p_drop > 0:
-        cb = torch.zeros(R, 16, dtype=torch.float32, device=dev)
-        cb[:, :H] = (doH * bvg.float().view(H, 1, hd)).sum(-1).t()
-    dh = torch.empty(B * Lp, D, dtype=h.dtype, device=dev)
-    du, w, stats = ops.global_fold_bwd(h.contiguous(), flags, gidx, B, Lp, H, ws, dw, cb, p_drop, seed, dh)
-    duH = du[:, :H].transpose(0, 1)                                          # (H, R, D)
-    dq = torch.bmm(duH, wk.transpose(1, 2)).transpose(0, 1).reshape(R, D)
-    dwkg = torch.bmm(qH.transpose(1, 2), duH).reshape(D, D)
-    dwvg = torch.bmm(doH.transpose(1, 2), w[:, :H].transpose(0, 1)).reshape(D, D)
-    dbvg = (doH * stats[:, :H, 3].t().unsqueeze(-1)).sum(1).reshape(D)
-    dbkg = torch.zeros(D, dtype=torch.float32, device=dev)
-    return dq, dh, dwkg, dbkg, dwvg, dbvg
+    dh = torch.empty(B * Lp, D, dtype=h.dtype, device=h.device)
+    dqg, dwkg, dbkg, dwvg, dbvg = ops.global_fold_bwd_full(
+        h.contiguous(), flags, gidx, B, Lp, H, ws, d16, qg.contiguous(), wkg.contiguous(), wvg.contiguous(), bvg,
+        p_drop, seed, dh)
+    return dqg, dh, dwkg, dbkg, dwvg, dbvg
 
 
 def _global_kv_grad(w, x, B: int, Lp: int, H: int):
@@ -751,25 +738,29 @@ class _Attention(torch.autograd.Function):
             else:
                 rows, keep = _global_rows(gidx, B, Lp)
                 rows32 = torch.where(keep, rows, -1).to(torch.int32)  # -1: empty slot, skipped
-            # gradients of the global-key columns, reduced over every query of the sequence
-            # bf16 operands, fp32 accumulation (no fp32 copies of the (B*Lp, D) q and dout)
-            dkg = _global_kv_grad(gds[..., :gmax], q, B, Lp, H)
-            dvg = _global_kv_grad(gpr[..., :gmax], d16, B, Lp, H)
-            # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
-            # added into dk / dv at the global positions (bf16, as dqkv) by one small kernel
-            ops.scatter_add_rows(rows32, dkg.to(dk.dtype).contiguous(), dk, dvg.to(dv.dtype).contiguous(), dv)
+            # gradients of the global-key columns, reduced over every query of the sequence and added
+            # into dk / dv at the global positions (bf16, as dqkv)
+            if GLOBAL_KV_HIP and gds.shape[-1] == gmax:
+                ops.global_kv_grad(gds, gpr, q, d16, gidx, B, Lp, H, dk, dv)
+            else:
+                # bf16 operands, fp32 accumulation (no fp32 copies of the (B*Lp, D) q and dout)
+                dkg = _global_kv_grad(gds[..., :gmax], q, B, Lp, H)
+                dvg = _global_kv_grad(gpr[..., :gmax], d16, B, Lp, H)
+                # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
+                ops.scatter_add_rows(rows32, dkg.to(dk.dtype).contiguous(), dk, dvg.to(dv.dtype).contiguous(), dv)
             # global branch: closed-form gradient of the fold algebra
             if any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]):
-                gout = dout[rows].float() * keep[:, None].to(torch.float32)
-                gz = None
                 hip_bwd = GLOBAL_BWD_HIP and ctx.fold_ws is not None
+                gout = gz = None
+                if not hip_bwd:
+                    gout = dout[rows].float() * keep[:, None].to(torch.float32)
                 if ctx.gz_kind == "hip" and not hip_bwd:  # the forward's mask, from the same kernel
                     gz = ops.attn_global_keep(gidx, B, Lp, H, p_drop, seed)
                 elif ctx.gz_kind == "torch":
                     gz = _global_keep(gidx, B, Lp, H, p_drop, seed)
-                if GLOBAL_BWD_HIP and ctx.fold_ws is not None:
+                if hip_bwd:
                     with torch.autocast("cuda", enabled=False):
-                        grads = _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B, Lp, H, gout, ctx.fold_ws,
+                        grads = _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B, Lp, H, d16, ctx.fold_ws,
                                                 p_drop, seed)
                 elif GLOBAL_BWD_CLOSED_FORM:
                     with torch.autocast("cuda", enabled=False):
