@@ -471,6 +471,15 @@ int rf_global_kv_grad(int dtype, int B, int Lp, int H, int gmax, const float* gd
                       int ldq, const void* dout, int lddout, const int32_t* gidx, void* dk, int ldk, void* dv,
                       int ldv, rf_stream_t stream);
 
+/* Backward of the query_global projection of the global rows, qg = (h_g Wqg^T + bqg) * q_scale
+ * (TF:966-967 under autograd), from dqg (B*gmax, D) fp32 (rf_global_fold_bwd_full; rows of empty slots
+ * ignored): dWqg (D x D) and dbqg (D) fp32 written, and dh (B*Lp rows, lddh, 16-bit) += dqg . Wqg * q_scale
+ * at the global rows, in place. wqgT: the (D x D) transposed weight Wqg^T * q_scale in the compute dtype
+ * (the training path's packed copy); h: the layer input (B*Lp rows, ldh). B*gmax <= 1024. */
+int rf_global_query_bwd(int dtype, int B, int Lp, int D, int gmax, const int32_t* gidx, const float* dqg,
+                        float q_scale, const void* h, int ldh, const void* wqgT, float* dwqg, float* dbqg, void* dh,
+                        int lddh, rf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

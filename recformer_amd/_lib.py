@@ -65,6 +65,8 @@ SIGNATURES = {
                                         c_int, P, P, P, c_float, ctypes.c_uint64, P, c_int, P, P, P, P, P, P, P]),
     "rf_global_kv_grad": (c_int, [c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, c_int, P, P, c_int, P, c_int,
                                   P]),
+    "rf_global_query_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, P, c_float, P, c_int, P, P, P, P, c_int,
+                                    P]),
     "rf_adamw_chunk": (c_int, []),
     "rf_set_seed_source": (P, [P]),
     "rf_adamw_step": (c_int, [P, c_int, P, c_int, P]),

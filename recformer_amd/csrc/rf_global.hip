@@ -2032,6 +2032,65 @@ __global__ void __launch_bounds__(256) k_global_kv_grad(int Lp, int H, int gmax,
   }
 }
 
+// Backward of the query_global projection of the global rows, qg = (h_g Wqg^T + bqg) * q_scale
+// (TF:966-967), from dqg (R x D fp32; 0 for empty slots) — rf_global_query_bwd, grid D + R * (D / 64):
+//   block o < D:  dWqg[o][c] = q_scale sum_r dqg[r][o] h[row r][c],  dbqg[o] = q_scale sum_r dqg[r][o]
+//   then (r, 64 columns c): dh[row r][c] += sum_o dqg[r][o] WqgT[c][o]   (WqgT: the transposed weight
+//   with q_scale folded in, the packed training copy; four threads per output over its row).
+template <typename E>
+__global__ void __launch_bounds__(256) k_gq_bwd(int D, int Lp, int gmax, int R, const int32_t* __restrict__ gidx,
+                                                const float* __restrict__ dqg, float q_scale,
+                                                const E* __restrict__ hs, int ldh, const E* __restrict__ wqgT,
+                                                float* __restrict__ dwqg, float* __restrict__ dbqg,
+                                                E* __restrict__ dh, int lddh) {
+  __shared__ float sh[1024];
+  __shared__ int64_t rowof[1024];
+  const int bid = blockIdx.x, t = threadIdx.x;
+  if (bid < D) {
+    const int o = bid;
+    for (int r = t; r < R; r += 256) {
+      const int pos = gidx[r];
+      sh[r] = pos >= 0 ? q_scale * dqg[(int64_t)r * D + o] : 0.f;
+      rowof[r] = pos >= 0 ? (int64_t)(r / gmax) * Lp + pos : -1;
+    }
+    __syncthreads();
+    for (int c = t; c < D; c += 256) {
+      float a = 0.f;
+#pragma unroll 4
+      for (int r = 0; r < R; ++r)
+        if (rowof[r] >= 0) a = fmaf(sh[r], to_f32(hs[rowof[r] * ldh + c]), a);
+      dwqg[(int64_t)o * D + c] = a;
+    }
+    if (t == 0) {
+      float a = 0.f;
+      for (int r = 0; r < R; ++r) a += sh[r];
+      dbqg[o] = a;
+    }
+    return;
+  }
+  const int nct = D / 64, b2 = bid - D, r = b2 / nct, ct = b2 - (b2 / nct) * nct;
+  const int pos = gidx[r];
+  if (pos < 0) return;
+  for (int k = t; k < D; k += 256) sh[k] = dqg[(int64_t)r * D + k];
+  __syncthreads();
+  const int c = ct * 64 + (t >> 2), part = t & 3;
+  const E* wr = wqgT + (int64_t)c * D;
+  float a = 0.f;
+  for (int k = 8 * part; k < D; k += 32) {
+    float x[8];
+    load4(wr + k, x);
+    load4(wr + k + 4, x + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a = fmaf(x[j], sh[k + j], a);
+  }
+  a += __shfl_xor(a, 1, 64);
+  a += __shfl_xor(a, 2, 64);
+  if (part == 0) {
+    E* o = dh + ((int64_t)(r / gmax) * Lp + pos) * lddh + c;
+    *o = (E)(to_f32(*o) + a);
+  }
+}
+
 struct GbwdWs {
   char* dwp;
   char* bt;
@@ -2185,4 +2244,24 @@ extern "C" int rf_global_kv_grad(int dtype, int B, int Lp, int H, int gmax, cons
                                                           (const bf16*)dout, lddout, gidx, (bf16*)dk, ldk, (bf16*)dv,
                                                           ldv);
   RF_LAUNCH_CHECK("rf_global_kv_grad");
+}
+
+extern "C" int rf_global_query_bwd(int dtype, int B, int Lp, int D, int gmax, const int32_t* gidx, const float* dqg,
+                                   float q_scale, const void* h, int ldh, const void* wqgT, float* dwqg, float* dbqg,
+                                   void* dh, int lddh, rf_stream_t stream) {
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_global_query_bwd: 16-bit operands only");
+  RF_REQUIRE(B >= 0 && Lp >= 0 && gmax >= 0 && D > 0 && D % 64 == 0, "rf_global_query_bwd: bad shape");
+  if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
+  RF_REQUIRE(B * gmax <= 1024, "rf_global_query_bwd: at most 1024 global rows");
+  RF_REQUIRE(gidx && dqg && h && wqgT && dwqg && dbqg && dh, "rf_global_query_bwd: null pointer");
+  RF_REQUIRE(ldh >= D && lddh >= D && ((uintptr_t)wqgT & 7) == 0, "rf_global_query_bwd: leading dims / alignment");
+  const int R = B * gmax;
+  hipStream_t s = as_stream(stream);
+  if (dtype == RF_F16)
+    k_gq_bwd<f16><<<D + R * (D / 64), 256, 0, s>>>(D, Lp, gmax, R, gidx, dqg, q_scale, (const f16*)h, ldh,
+                                                    (const f16*)wqgT, dwqg, dbqg, (f16*)dh, lddh);
+  else
+    k_gq_bwd<bf16><<<D + R * (D / 64), 256, 0, s>>>(D, Lp, gmax, R, gidx, dqg, q_scale, (const bf16*)h, ldh,
+                                                     (const bf16*)wqgT, dwqg, dbqg, (bf16*)dh, lddh);
+  RF_LAUNCH_CHECK("rf_global_query_bwd");
 }

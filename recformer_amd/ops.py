@@ -736,6 +736,24 @@ def global_kv_grad(gds, gpr, q, dout, gidx, B: int, Lp: int, H: int, dk, dv):
                                         _rowmajor(dv, "dv"), _stream(q)), "rf_global_kv_grad")
 
 
+def global_query_bwd(gidx, dqg, q_scale: float, h, wqgT, dh, B: int, Lp: int):
+    """rf_global_query_bwd: backward of qg = (h[global rows] Wqg^T + bqg) * q_scale from dqg (R, D)
+    fp32: returns fp32 (dWqg (D, D), dbqg (D,)) and adds the global rows' input gradient into dh (in
+    place). wqgT (D, D): Wqg^T * q_scale in h's dtype."""
+    gmax = gidx.shape[1]
+    D = h.shape[1]
+    if tuple(dqg.shape) != (B * gmax, D) or dqg.dtype != torch.float32 or not dqg.is_contiguous():
+        raise ValueError("global_query_bwd: dqg must be contiguous fp32 (B*gmax, D)")
+    if tuple(wqgT.shape) != (D, D) or wqgT.dtype != h.dtype or not wqgT.is_contiguous() or dh.dtype != h.dtype:
+        raise ValueError("global_query_bwd: wqgT (D, D) contiguous and dh in h's dtype")
+    dwqg = torch.empty(D, D, dtype=torch.float32, device=h.device)
+    dbqg = torch.empty(D, dtype=torch.float32, device=h.device)
+    check(_lib.load().rf_global_query_bwd(dtype_code(h.dtype), B, Lp, D, gmax, _p(gidx.to(torch.int32).contiguous()),
+                                          _p(dqg), float(q_scale), _p(h), _rowmajor(h, "h"), _p(wqgT), _p(dwqg),
+                                          _p(dbqg), _p(dh), _rowmajor(dh, "dh"), _stream(h)), "rf_global_query_bwd")
+    return dwqg, dbqg
+
+
 def attn_global_keep(gidx, B: int, Lp: int, H: int, p_drop: float, seed: int) -> torch.Tensor:
     """(B, H, gmax, Lp) fp32 attention-dropout scale of the global query rows (rf_attn_global_keep;
     the mask rf_global_attn_fold_fwd_drop applies)."""

@@ -60,6 +60,10 @@ EMBED_BWD_HIP = True
 # global rows' backward on rf_global_fold_bwd_full (one pass over h from the forward's fold workspace,
 # the per-head products with the key/value weights and the weight gradients inside)
 GLOBAL_BWD_HIP = True
+# packed bf16 / fp16 training with the HIP global backward: the query_global projection of the global
+# rows runs inside _Attention, its backward on rf_global_query_bwd (dWqg, dbqg, and the rows' input
+# gradient added into the branch's dh in place: no gather backward, zero fill or extra dh sum)
+GLOBAL_QG_INSIDE = True
 # the global-key / -value rows' gradients of the local branch on rf_global_kv_grad (one launch,
 # added in place into dk / dv) instead of two batched products, their copies and a scatter
 GLOBAL_KV_HIP = True
@@ -662,10 +666,20 @@ class _Attention(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold, grows=None,
-                attn_p: float = 0.0, seed: int = 0, wkg_master=None, wvg_master=None):
+                attn_p: float = 0.0, seed: int = 0, wkg_master=None, wvg_master=None, wqg16=None, wqgT16=None,
+                bqg=None, wqg_master=None, q_scale: float = 1.0):
         # wkg / wvg: the global key / value weights in the compute dtype; with the masters given
-        # (packed copies, not tracked) their gradients go to the fp32 masters directly
+        # (packed copies, not tracked) their gradients go to the fp32 masters directly.
+        # wqg16 given (GLOBAL_QG_INSIDE): qg = (h[global rows] Wqg^T + bqg) * q_scale is computed here
+        # and its backward runs here too (gradients to bqg and the fp32 master wqg_master)
         ctx.masters = wkg_master is not None
+        ctx.qin = wqg16 is not None
+        ctx.q_scale = q_scale
+        if ctx.qin:
+            D0 = qkv.shape[1] // 3
+            qg = ops.gemm(h.index_select(0, grows[0]), wqg16, bqg, ops.RF_EPI_BIAS, scale_cols=D0,
+                          col_scale=q_scale)
+            ctx.qw = (wqg16, wqgT16)
         ctx.fold_ws = None  # the forward fold's workspace when the HIP global backward can use it
         D = qkv.shape[1] // 3
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
@@ -749,7 +763,7 @@ class _Attention(torch.autograd.Function):
                 # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
                 ops.scatter_add_rows(rows32, dkg.to(dk.dtype).contiguous(), dk, dvg.to(dv.dtype).contiguous(), dv)
             # global branch: closed-form gradient of the fold algebra
-            if any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]):
+            if any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]) or ctx.qin:
                 hip_bwd = GLOBAL_BWD_HIP and ctx.fold_ws is not None
                 gout = gz = None
                 if not hip_bwd:
@@ -772,18 +786,44 @@ class _Attention(torch.autograd.Function):
                         og = _global_torch(*gin, flags, B, Lp, H, gz)
                         grads = torch.autograd.grad(og, gin, gout, allow_unused=True)
                 for n, t in enumerate((qg, h, wkg, bkg, wvg, bvg)):
-                    if ctx.needs_input_grad[1 + n]:
+                    if ctx.needs_input_grad[1 + n] or (n == 1 and ctx.qin):
                         g = grads[n]
                         res[1 + n] = None if g is None else g.to(t.dtype)
                 if ctx.masters:  # fp32 gradients straight to the masters (no bf16 round trip)
                     extra = [grads[2].float() if ctx.needs_input_grad[17] and grads[2] is not None else None,
                              grads[4].float() if ctx.needs_input_grad[18] and grads[4] is not None else None]
+                if ctx.qin:
+                    res[2], qtail = _Attention._qg_backward(ctx, grads[0], res[2], h, gidx, B, Lp, hip_bwd)
         if ctx.needs_input_grad[0]:
             res[0] = dqkv.to(qkv.dtype)
-        tail = [None] * 12  # the forward's non-tensor inputs, then the two masters
-        if ctx.masters and gmax > 0 and (any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19])):
-            tail[10:] = extra
+        tail = [None] * 17  # the forward's non-tensor inputs, the two masters, the query weights
+        if ctx.masters and gmax > 0 and (any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]) or
+                                         ctx.qin):
+            tail[10:12] = extra
+        if ctx.qin and gmax > 0:
+            tail[12:17] = qtail
         return (*res, *tail)
+
+    @staticmethod
+    def _qg_backward(ctx, dqg, dh, h, gidx, B: int, Lp: int, hip: bool):
+        """Backward of the query_global projection computed in the forward (GLOBAL_QG_INSIDE): returns
+        (h's gradient with the global rows' part added, the tail for (wqg16, wqgT16, bqg, wqg_master,
+        q_scale)). HIP: rf_global_query_bwd in place into dh; else torch."""
+        wqg16, wqgT16 = ctx.qw
+        s = ctx.q_scale
+        if dh is None:
+            dh = torch.zeros_like(h)
+        if hip and dh.dtype == h.dtype and dh.is_contiguous() and wqgT16.is_contiguous():
+            dwqg, dbqg = ops.global_query_bwd(gidx, dqg.float().contiguous(), s, h, wqgT16, dh, B, Lp)
+        else:
+            rows, keep = _global_rows(gidx, B, Lp)
+            dqs = dqg.float() * s * keep[:, None].to(torch.float32)
+            hg = h.index_select(0, rows).float()
+            dwqg = dqs.t() @ hg
+            dbqg = dqs.sum(0)
+            dh = dh.index_add(0, rows, (dqs @ wqg16.float()).to(dh.dtype))
+        return dh, [None, None, dbqg if ctx.needs_input_grad[21] else None,
+                    dwqg if ctx.needs_input_grad[22] else None, None]
 
     @staticmethod
     def _backward_torch(ctx, dout):
@@ -794,6 +834,8 @@ class _Attention(torch.autograd.Function):
         if ctx.masters:  # gradients of the packed copies go to the masters
             need[3] = need[3] or need[17]
             need[5] = need[5] or need[18]
+        if ctx.qin:  # qg was computed in the forward: its gradient feeds the projection's backward
+            need[1] = need[2] = True
         inputs = [t.detach().requires_grad_(nd) for t, nd in
                   zip((qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], qg, h, wkg, bkg, wvg, bvg),
                       (need[0],) * 3 + tuple(need[1:7]))]
@@ -814,11 +856,16 @@ class _Attention(torch.autograd.Function):
             res = [torch.cat(z, 1)] + res[3:]
         else:
             res = [None] + res[3:]
-        tail = [None] * 12  # the forward's non-tensor inputs, then the two masters
+        tail = [None] * 17  # the forward's non-tensor inputs, the two masters, the query weights
         if ctx.masters:
             g_k, g_v = res[3], res[5]
             res[3] = res[5] = None
-            tail[10:] = [None if g_k is None else g_k.float(), None if g_v is None else g_v.float()]
+            tail[10:12] = [None if g_k is None else g_k.float(), None if g_v is None else g_v.float()]
+        if ctx.qin and gidx.shape[1] > 0:
+            dqg = res[1] if res[1] is not None else torch.zeros_like(qg, dtype=torch.float32)
+            res[1] = None
+            B, Lp = ctx.dims[0], ctx.dims[1]
+            res[2], tail[12:17] = _Attention._qg_backward(ctx, dqg, res[2], h, gidx, B, Lp, False)
         return (*res, *tail)
 
 
@@ -1013,17 +1060,26 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     packed = None
     if PACK_WEIGHTS and fused and FFN_FUSED and D % 64 == 0 and cfg.intermediate_size % 64 == 0 and input_ids.is_cuda:
         packed = _packed_layer_weights(model, dt, scale)
+    # query_global projection inside _Attention when its backward takes the HIP global path (the fold
+    # workspace's limits, the HIP local backward's window)
+    qg_inside = (GLOBAL_QG_INSIDE and GLOBAL_BWD_HIP and packed is not None and gmax <= 4 and fold and
+                 D % 128 == 0 and D <= 768 and D == 64 * H and B * gmax <= 1024 and
+                 all(w == 64 for w in windows))
     for li, lyr in enumerate(model.encoder.layer):
         lw = packed[li] if packed is not None else _layer_weights(li, lyr, dt)
         h = h16 if h16 is not None else h32.to(dt)
         qkv = _lin(h, lw, "w_qkv", "b_qkv", D, scale)
         qg = None
-        if gmax > 0:
+        qin = ()
+        if gmax > 0 and qg_inside:
+            (wqg_m,), wqg16, wqgT16 = lw["w_qg"]
+            qin = (wqg16, wqgT16, lw["b_qg"], wqg_m, scale)
+        elif gmax > 0:
             hg = h[rows] * gvalid.to(h.dtype)
             qg = _lin(hg, lw, "w_qg", "b_qg", D, scale)
         ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
                                flags, gidx, B, Lp, H, windows[li] // 2, fold, grows, p_att, att_seeds[li],
-                               lw.get("wkg_master"), lw.get("wvg_master"))
+                               lw.get("wkg_master"), lw.get("wvg_master"), *qin)
         ao = lyr.attention.output
         t = _lin(ctx, lw, "w_o", "b_o", 0, 1.0)
         if fused:

@@ -694,3 +694,34 @@ def test_global_kv_grad_matches_torch(dev, dt, B, Lp, H, gpos):
             if gpos[b][k] >= 0:
                 untouched[b * Lp + gpos[b][k]] = False
     assert torch.equal(dqkv[untouched], before[untouched])
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_global_query_bwd_matches_torch(dev, dt):
+    """rf_global_query_bwd (backward of qg = (h[global rows] Wqg^T + b) * s) against torch in fp32:
+    dWqg, dbqg, and the global rows' input gradient added in place into dh (other rows untouched;
+    an empty slot contributes nothing)."""
+    B, Lp, D, G = 3, 128, 256, 2
+    s = 0.125
+    g = torch.Generator(device="cpu").manual_seed(5)
+    gidx = torch.tensor([[0, 37], [5, -1], [-1, -1]], dtype=torch.int32, device=dev)
+    h = torch.randn(B * Lp, D, generator=g).to(dev).to(dt)
+    w = (torch.randn(D, D, generator=g) * 0.05).to(dev).to(dt)
+    wT = (w.float() * s).to(dt).t().contiguous()
+    dqg = torch.randn(B * G, D, generator=g).to(dev)
+    dqg[gidx.reshape(-1) < 0] = 0
+    dh = torch.randn(B * Lp, D, generator=g).to(dev).to(dt)
+    before = dh.clone()
+    dwqg, dbqg = ops.global_query_bwd(gidx, dqg, s, h, wT, dh, B, Lp)
+    rows = (torch.arange(B, device=dev)[:, None] * Lp + gidx.clamp(min=0).long()).reshape(-1)
+    keep = (gidx.reshape(-1) >= 0).float()[:, None]
+    dqs = dqg * s * keep
+    ref_w = dqs.t() @ h.index_select(0, rows).float()
+    assert torch.allclose(dwqg, ref_w, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(dbqg, dqs.sum(0), rtol=1e-5, atol=1e-5)
+    ref_dh = before.float().index_add(0, rows, (dqg * keep) @ wT.float().t())
+    tol = 2e-2 if dt == torch.bfloat16 else 4e-3
+    assert float(((dh.float() - ref_dh).abs() / (ref_dh.abs() + 1)).max()) <= tol
+    other = torch.ones(B * Lp, dtype=torch.bool, device=dev)
+    other[rows[keep[:, 0] > 0]] = False
+    assert torch.equal(dh[other], before[other])
