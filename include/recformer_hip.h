@@ -168,6 +168,12 @@ int rf_drop_add_ln_fwd_t(int dtype, int M, int D, const void* t, int ldt, const 
 int rf_drop_add_ln_bwd_t(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
                          const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
                          void* dt, float* dw, float* db, void* workspace, rf_stream_t stream);
+/* rf_drop_add_ln_bwd_t that also writes dbias_t (D fp32) = the column sums of dt as stored (16-bit):
+ * the bias gradient of the Linear whose output t is (TF:1064-1071, 1123-1130), from the same pass (no
+ * separate read of dt for it). */
+int rf_drop_add_ln_bwd_tb(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
+                          const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
+                          void* dt, float* dw, float* db, float* dbias_t, void* workspace, rf_stream_t stream);
 /* Weight gradient of an nn.Linear, C (=|+=) X^T Y: C[n][k] = sum_m X[m][n] Y[m][k] over the M token
  * rows (X = dC (M x N), Y = A (M x K), 16-bit row-major; C fp32 N x K, the master weight's dtype) —
  * the dW = dC^T A of autograd through TF:504-514, 1064-1130 and the LM head (models.py:499-510).

@@ -51,6 +51,8 @@ SIGNATURES = {
                                      P, P, P, P]),
     "rf_drop_add_ln_bwd_t": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
                                      P]),
+    "rf_drop_add_ln_bwd_tb": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
+                                      P, P]),
     "rf_colsum_workspace": (ctypes.c_size_t, [c_int, c_int]),
     "rf_embed_ln_bwd_workspace": (ctypes.c_size_t, [c_int, c_int]),
     "rf_embed_ln_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, c_float, P, P, P, P, P, P]),

@@ -497,17 +497,19 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
                                                         const float* __restrict__ w, float* __restrict__ dx,
                                                         float* __restrict__ part, E* __restrict__ dt,
                                                         uint32_t thresh, float keep_scale, uint64_t seed,
-                                                        const uint64_t* seed_dev, const E* __restrict__ dy2) {
+                                                        const uint64_t* seed_dev, const E* __restrict__ dy2,
+                                                        int tb) {
   constexpr int D = 64 * VEC * NCH;
   if (thresh) seed = seed_resolve(seed, seed_dev);
-  __shared__ float red[4][2][D];
+  __shared__ float red[4][3][D];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float pw[NCH][VEC], pb[NCH][VEC], wr[NCH][VEC];
+  const int ns = tb ? 3 : 2;  // partial slots per block: dw, db (+ the column sums of dt)
+  float pw[NCH][VEC], pb[NCH][VEC], pt[NCH][VEC], wr[NCH][VEC];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     Vec<float, VEC>::load(w + c * 64 * VEC + lane * VEC, wr[c]);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) pw[c][j] = pb[c][j] = 0.f;
+    for (int j = 0; j < VEC; ++j) pw[c][j] = pb[c][j] = pt[c][j] = 0.f;
   }
   const int r0 = blockIdx.x * LNB_ROWS;
   for (int rr = wv; rr < LNB_ROWS; rr += 4) {
@@ -557,6 +559,10 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
         for (int j = 0; j < VEC; ++j)
           od[j] = (thresh == 0 || drop_keep(seed, (uint64_t)row * D + e + j, thresh)) ? o[j] * keep_scale : 0.f;
         Vec<E, VEC>::store(dt + (int64_t)row * D + e, od);
+        if (tb) {  // the dense branch's bias gradient: column sums of dt as stored (16-bit)
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) pt[c][j] += (float)(E)od[j];
+        }
       }
     }
   }
@@ -566,11 +572,12 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
     for (int j = 0; j < VEC; ++j) {
       red[wv][0][c * 64 * VEC + lane * VEC + j] = pw[c][j];
       red[wv][1][c * 64 * VEC + lane * VEC + j] = pb[c][j];
+      red[wv][2][c * 64 * VEC + lane * VEC + j] = pt[c][j];
     }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * D; i += 256) {
+  for (int i = threadIdx.x; i < ns * D; i += 256) {
     const int k = i / D, col = i - k * D;
-    part[((int64_t)blockIdx.x * 2 + k) * D + col] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
+    part[((int64_t)blockIdx.x * ns + k) * D + col] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
   }
 }
 
@@ -632,7 +639,7 @@ __global__ void __launch_bounds__(256) k_colsum_part(int M, int N, const T* __re
 
 // out[n] = sum_z part[z][n]: 64 slices x 4 columns per block, tree-reduced in LDS (fixed order)
 __global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* __restrict__ part, float* __restrict__ out,
-                                                     float* __restrict__ out2, int split) {
+                                                     float* __restrict__ out2, int split, float* __restrict__ out3) {
   __shared__ float red[64][5];
   const int z = threadIdx.x >> 2, k = threadIdx.x & 3;
   const int c = blockIdx.x * 4 + k;
@@ -643,19 +650,20 @@ __global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* _
     __syncthreads();
   }
   if (z == 0 && c < N) {
-    if (out2 && c >= split) out2[c - split] = red[0][k];
+    if (out3 && c >= 2 * split) out3[c - 2 * split] = red[0][k];
+    else if (out2 && c >= split) out2[c - split] = red[0][k];
     else out[c] = red[0][k];
   }
 }
 
 template <typename T>
 static void colsum(int M, int N, const T* x, int64_t ldx, float* part, float* out, float* out2, int split,
-                   hipStream_t s) {
+                   hipStream_t s, float* out3 = nullptr) {
   const int S = max(1, min(CS_SLICES, (M + 63) / 64));
   const bool vec = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(T))) == 0;
   if (vec) k_colsum_part<T, true><<<dim3((N + 255) / 256, S), 256, 0, s>>>(M, N, x, ldx, part);
   else k_colsum_part<T, false><<<dim3((N + 255) / 256, S), 256, 0, s>>>(M, N, x, ldx, part);
-  k_colsum_fin<<<(N + 3) / 4, 256, 0, s>>>(S, N, part, out, out2, split);
+  k_colsum_fin<<<(N + 3) / 4, 256, 0, s>>>(S, N, part, out, out2, split, out3);
 }
 
 template <typename T, int VEC, int NCH>
@@ -1016,7 +1024,7 @@ int rf_add_layernorm_split_fwd(int M, int D, const void* x, int ldx, const uint1
 
 size_t rf_layernorm_bwd_workspace(int M, int D) {
   if (M <= 0 || D <= 0) return 0;
-  return ((size_t)((M + LNB_ROWS - 1) / LNB_ROWS) + CS_SLICES) * 2 * D * sizeof(float);
+  return ((size_t)((M + LNB_ROWS - 1) / LNB_ROWS) + CS_SLICES) * 3 * D * sizeof(float);
 }
 
 size_t rf_colsum_workspace(int M, int N) { return (size_t)CS_SLICES * (N > 0 ? N : 0) * sizeof(float); }
@@ -1062,7 +1070,7 @@ template <typename E>
 static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                        const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                        E* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
-                       const E* dy2 = nullptr);
+                       const E* dy2 = nullptr, float* dbias_t = nullptr);
 }
 
 
@@ -1135,6 +1143,19 @@ int rf_drop_add_ln_bwd_t(int dtype, int M, int D, const float* dy, const void* d
                            1.0f / (1.0f - p), seed, stream, (const bf16*)dy16);
 }
 
+int rf_drop_add_ln_bwd_tb(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
+                          const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
+                          void* dt, float* dw, float* db, float* dbias_t, void* workspace, rf_stream_t stream) {
+  RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_drop_add_ln_bwd_tb: dtype must be bf16 or fp16");
+  RF_REQUIRE(M >= 0 && p >= 0.f && p < 1.f, "rf_drop_add_ln_bwd_tb: bad arguments");
+  RF_REQUIRE(M == 0 || (dt && dbias_t), "rf_drop_add_ln_bwd_tb: null dt / dbias_t");
+  if (dtype == RF_F16)
+    return ln_bwd_impl<f16>(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (f16*)dt, drop_thresh(p),
+                            1.0f / (1.0f - p), seed, stream, (const f16*)dy16, dbias_t);
+  return ln_bwd_impl<bf16>(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (bf16*)dt, drop_thresh(p),
+                           1.0f / (1.0f - p), seed, stream, (const bf16*)dy16, dbias_t);
+}
+
 int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                      const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                      rf_stream_t stream) {
@@ -1146,7 +1167,7 @@ template <typename E>
 static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                        const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                        E* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
-                       const E* dy2) {
+                       const E* dy2, float* dbias_t) {
   RF_REQUIRE(M >= 0 && ldx >= D, "rf_layernorm_bwd: bad shape");
   if (M == 0) return RF_OK;
   RF_REQUIRE((dy || dy2) && x && mean && rstd && w && dx && dw && db && workspace, "rf_layernorm_bwd: null pointer");
@@ -1154,10 +1175,13 @@ static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, c
   hipStream_t s = as_stream(stream);
   const int nb = (M + LNB_ROWS - 1) / LNB_ROWS;
   float* part = reinterpret_cast<float*>(workspace);
-#define L_(V, N) k_layernorm_bwd<E, V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, g_seed_dev, dy2)
+  const int tb = dt && dbias_t ? 1 : 0;
+  const int ns = 2 + tb;
+#define L_(V, N) k_layernorm_bwd<E, V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, g_seed_dev, dy2, tb)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
-  colsum<float>(nb, 2 * D, part, 2 * D, part + (size_t)nb * 2 * D, dw, db, D, s);  // [dw | db] columns
+  // [dw | db (| dbias_t)] columns
+  colsum<float>(nb, ns * D, part, ns * D, part + (size_t)nb * ns * D, dw, db, D, s, tb ? dbias_t : nullptr);
   RF_LAUNCH_CHECK("rf_layernorm_bwd");
 }
 }

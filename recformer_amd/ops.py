@@ -485,9 +485,10 @@ def drop_add_ln_fwd(t: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torc
 
 
 def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[torch.Tensor] = None,
-                    dtype: torch.dtype = torch.bfloat16):
+                    dtype: torch.dtype = torch.bfloat16, want_dbias: bool = False):
     """rf_drop_add_ln_bwd_t: (dres fp32, dt, dw, db) for the gradient dy (fp32) of y plus, when given,
-    dy16 of its 16-bit copy; either may be None (not both). dt and dy16 in `dtype` (bf16 / fp16)."""
+    dy16 of its 16-bit copy; either may be None (not both). dt and dy16 in `dtype` (bf16 / fp16).
+    want_dbias (rf_drop_add_ln_bwd_tb): also the column sums of dt (the dense branch's bias gradient)."""
     lib = _lib.load()
     _dev(x, mean, rstd, w)
     M, D = x.shape
@@ -503,6 +504,13 @@ def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[to
     dw = torch.empty(D, dtype=torch.float32, device=x.device)
     db = torch.empty_like(dw)
     ws = torch.empty(max(lib.rf_layernorm_bwd_workspace(M, D), 4), dtype=torch.uint8, device=x.device)
+    if want_dbias:
+        dbias = torch.empty_like(dw)
+        check(lib.rf_drop_add_ln_bwd_tb(dtype_code(dtype), M, D, _p(dy), _p(dy16), _p(x), _p(mean), _p(rstd),
+                                        _p(w.float().contiguous()), float(p), seed, _p(dres), _p(dt), _p(dw), _p(db),
+                                        _p(dbias), _p(ws), _stream(x)),
+              "rf_drop_add_ln_bwd_tb")
+        return dres, dt, dw, db, dbias
     check(lib.rf_drop_add_ln_bwd_t(dtype_code(dtype), M, D, _p(dy), _p(dy16), _p(x), _p(mean), _p(rstd),
                                    _p(w.float().contiguous()), float(p), seed, _p(dres), _p(dt), _p(dw), _p(db), _p(ws),
                                    _stream(x)),

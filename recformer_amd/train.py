@@ -60,6 +60,9 @@ EMBED_BWD_HIP = True
 # global rows' backward on rf_global_fold_bwd_full (one pass over h from the forward's fold workspace,
 # the per-head products with the key/value weights and the weight gradients inside)
 GLOBAL_BWD_HIP = True
+# the bias gradients of the attention-output and FFN2 Linears from the LayerNorm backward pass that
+# writes their dC (rf_drop_add_ln_bwd_tb) instead of a separate column-sum pass over dC
+LN_BIAS_GRAD = True
 # packed bf16 / fp16 training with the HIP global backward: the query_global projection of the global
 # rows runs inside _Attention, its backward on rf_global_query_bwd (dWqg, dbqg, and the rows' input
 # gradient added into the branch's dh in place: no gather backward, zero fill or extra dh sum)
@@ -152,13 +155,20 @@ class _Gemm(torch.autograd.Function):
             else:
                 da = dc @ wa
         dw = _weight_grad(dc, a).to(ctx.wdt) if ctx.needs_input_grad[1] else None
-        db = ops.colsum(dc) if ctx.needs_input_grad[3] else None  # deterministic HIP column sums
+        db = _bias_grad(dc) if ctx.needs_input_grad[3] else None  # deterministic HIP column sums
         if scaled:
             if dw is not None:
                 dw[:sc] *= s
             if db is not None:
                 db[:sc] *= s
         return da, dw, None, db, None, None
+
+
+def _bias_grad(dc):
+    """Column sums of dC (a Linear's bias gradient): the ones the LayerNorm backward computed with dC
+    (_DropAddLN, LN_BIAS_GRAD) when dc is that very tensor, else rf_colsum."""
+    cs = getattr(dc, "_rf_colsum", None)
+    return cs if cs is not None else ops.colsum(dc)
 
 
 class _GemmP(torch.autograd.Function):
@@ -186,7 +196,7 @@ class _GemmP(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             da = dc @ wt.t() if dc.shape[0] < SMALL_M else ops.gemm(dc, wt, None, ops.RF_EPI_NONE)
         dw = _weight_grad(dc, a).to(ctx.wdt) if any(ctx.needs_input_grad[6:]) else None
-        db = ops.colsum(dc) if ctx.needs_input_grad[1] else None
+        db = _bias_grad(dc) if ctx.needs_input_grad[1] else None
         if scaled:
             if dw is not None:
                 dw[:sc] *= s
@@ -324,7 +334,7 @@ class _FFN(torch.autograd.Function):
         dt2 = dt2.to(a.dtype).contiguous()
         dz = ops.gemm(dt2, w2t, None, ops.RF_EPI_DGELU, resid=z)
         dw2 = _weight_grad(dt2, u).to(ctx.wdt[1]) if ctx.needs_input_grad[4] else None
-        db2 = ops.colsum(dt2) if ctx.needs_input_grad[6] else None
+        db2 = _bias_grad(dt2) if ctx.needs_input_grad[6] else None
         da = ops.gemm(dz, w1t, None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
         dw1 = _weight_grad(dz, a).to(ctx.wdt[0]) if ctx.needs_input_grad[1] else None
         db1 = ops.colsum(dz) if ctx.needs_input_grad[3] else None
@@ -380,7 +390,14 @@ class _DropAddLN(torch.autograd.Function):
         if dy is None and dy16 is None:
             return None, None, None, None, None, None, None, None
         x, mean, rstd, w = ctx.saved_tensors
-        dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16, dtype=ctx.tdt)
+        if LN_BIAS_GRAD and ctx.needs_input_grad[0]:
+            # the dense branch's bias gradient (column sums of dt) from the same pass, handed to the
+            # producing Linear's backward with dt (_bias_grad)
+            dres, dt, dw, db, dbias = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16,
+                                                          dtype=ctx.tdt, want_dbias=True)
+            dt._rf_colsum = dbias
+        else:
+            dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16, dtype=ctx.tdt)
         return dt, dres, dw, db, None, None, None, None
 
 

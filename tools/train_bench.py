@@ -90,6 +90,30 @@ def main():
         opt.zero_grad(set_to_none=True)
         return loss
 
+    if a.graph and a.ab:
+        # captured A/B: one graph per value of the train.py switch, replays alternated in one process
+        from recformer_amd import train
+        from recformer_amd.graphs import CapturedTrainStep
+        graphs = {}
+        for val in (True, False):
+            setattr(train, a.ab, val)
+            graphs[val] = CapturedTrainStep(model, opt, dict(batch, labels=labels), autocast_dtype=dt,
+                                            warmup=a.warmup)
+        res = {True: [], False: []}
+        for rep in range(6):
+            for val in (True, False):
+                graphs[val]()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(a.steps):
+                    graphs[val]()
+                torch.cuda.synchronize()
+                res[val].append((time.perf_counter() - t0) / a.steps * 1e3)
+        for val in (True, False):
+            v = sorted(res[val])
+            print(f"captured {a.ab}={val}: ms/step median {v[len(v) // 2]:.2f} min {v[0]:.2f} all "
+                  f"{[round(x, 2) for x in res[val]]}")
+        return
     if a.graph:
         if scaler is not None:
             raise SystemExit("--graph: the bf16 step only (GradScaler's host-side inf check is not capturable)")
