@@ -1102,7 +1102,14 @@ __global__ void __launch_bounds__(256, 1)
   auto voffW = [&](int bn0) { return ((bn0 + wrow_l) * ldw + pch) * 2; };
   int vA = voffA(m0), vW = voffW(n0), vAn = vA, vWn = vW;
   auto launder = [&]() { asm volatile("" : "+v"(vA), "+v"(vW), "+v"(vAn), "+v"(vWn)); };
-  // piece p (0-7 A, 8-15 W) of virtual K-tile kv (>= nk: the next tile's K-tile kv - nk) into buffer buf
+  // The per-piece soffsets run as two chains (A: +8 rows per piece; W pieces issued in the order
+  // pp = 0,2,4,6,1,3,5,7, i.e. rows +0..3 then +64..67 (+32..35 fp32 out): +1 row, +61 (+29) once).
+  // Three row-step scalars stay live instead of 14 loop-invariant products, which hipcc spilled to
+  // VGPR lanes and reloaded with v_readlane inside phase B (one per piece).
+  const int stA = 8 * lda * 2, stW1 = ldw * 2, stWj = (OUT32 ? 29 : 61) * ldw * 2;
+  int sA = 0, sW = 0;
+  // piece p (0-7 A, 8-15 W) of virtual K-tile kv (>= nk: the next tile's K-tile kv - nk) into buffer
+  // buf; pieces 0 and 8 start their chain, so every K-tile issues p = 0..7 and 8..15 in order
   auto dma_piece = [&](int kv, int buf, int p) {
 #if defined(RF_W4_DIAG) && (RF_W4_DIAG & 2)  // timing diagnostic: no operand DMA in the K-loop
     if (kv >= 2) return;
@@ -1110,10 +1117,20 @@ __global__ void __launch_bounds__(256, 1)
     const bool nxt = kv >= nk;
     const int kt = nxt ? kv - nk : kv;
     const bool isA = p < 8;
-    const int pp = p & 7;
+    const int q = p & 7;
+    const int pp = isA ? q : (q < 4 ? 2 * q : 2 * (q - 4) + 1);
     char* dst = smem + buf * W4_BUF + (isA ? half : 2 + half) * PP_HALF + ((wave & 1) * 64 + 8 * pp) * 128;
+    if (p == 0) { sA = kt * 128; asm volatile("" : "+s"(sA)); }
+    if (p == 8) { sW = kt * 128; asm volatile("" : "+s"(sW)); }
+    const int soff = isA ? sA : sW;
+    {
+      int st = isA ? stA : (q == 3 ? stWj : stW1);
+      asm volatile("" : "+s"(st));  // no hoisting of per-piece products out of the K-loop
+      if (isA) sA += st; else sW += st;
+    }
+#if defined(RF_W4_DIAG) && (RF_W4_DIAG & 8)
     const int rstep = isA ? 8 * pp : (OUT32 ? 32 * (pp & 1) + (pp >> 1) : 64 * (pp & 1) + (pp >> 1));
-    const int soff = kt * 128 + rstep * (isA ? lda : ldw) * 2;
+#endif
     const int vo = isA ? (nxt ? vAn : vA) : (nxt ? vWn : vW);
 #if defined(RF_W4_DIAG) && (RF_W4_DIAG & 8)  // timing diagnostic: every DMA reads K-tile 0 (L2-hot)
     const int soffd = rstep * (isA ? lda : ldw) * 2;
