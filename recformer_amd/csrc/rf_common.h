@@ -174,14 +174,21 @@ __device__ __forceinline__ f32x2 gelu2_bf16out(f32x2 x) {
 // gelu_bf16out on 4 pairs, one stage at a time across the pairs (the same operations per value, so
 // bit-identical): the four chains interleave, so the transcendental and packed-op hazards fill with
 // the other chains' instructions instead of s_nop (the per-pair form compiled to a serial chain).
+// The clamp runs as one packed multiply with the VOP3P clamp bit: s = clamp(x (x / 64)) in [0, 1] =
+// min(x^2, 64) / 64, and the quadratic's coefficients are scaled by 64 and 4096 — powers of two, so
+// every rounding equals the unscaled form's (bit-identical to gelu2_bf16out) for two v_min_f32 less
+// per pair.
 __device__ __forceinline__ void gelu8_bf16out(f32x2 (&x)[4]) {
   f32x2 x2[4], t[4], d[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) x2[k] = __builtin_elementwise_min(x[k] * x[k], (f32x2){64.0f, 64.0f});
+  for (int k = 0; k < 4; ++k) {
+    const f32x2 x64 = x[k] * (f32x2){0.015625f, 0.015625f};
+    asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(x2[k]) : "v"(x[k]), "v"(x64));
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k)
-    t[k] = __builtin_elementwise_fma((f32x2){0.0010142630552196598f, 0.0010142630552196598f}, x2[k],
-                                     (f32x2){-0.1067757240026454f, -0.1067757240026454f});
+    t[k] = __builtin_elementwise_fma((f32x2){0.0010142630552196598f * 4096.0f, 0.0010142630552196598f * 4096.0f},
+                                     x2[k], (f32x2){-0.1067757240026454f * 64.0f, -0.1067757240026454f * 64.0f});
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     t[k] = __builtin_elementwise_fma(t[k], x2[k], (f32x2){-2.3011213394567367f, -2.3011213394567367f});

@@ -525,9 +525,13 @@ __device__ __forceinline__ int wperm(int rho) {
 // LN beta for those columns (hoisted by the caller). Mirrors epi_row16 / epi_store.
 // CHECK = false: interior tile (no bounds tests, EPI_COS row norm `rsc` from LDS), so the
 // epilogue holds no global load and hipcc places no vmcnt wait between its stores.
-template <typename E, int EPI, bool CF32, bool RF32, int NV, bool CHECK = true>
+// FS: the caller pre-scaled bv by this lane's column scale cs (its columns lie on one side of
+// scale_cols, a multiple of 16): v = fma(v, cs, bv) instead of (v + bv) * col_scale under a per-lane
+// branch — bit-identical for cs = 1 and for power-of-two scales (1/sqrt(64)).
+template <typename E, int EPI, bool CF32, bool RF32, int NV, bool CHECK = true, bool TB = false, bool FS = false>
 __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float* v, const float* bv,
-                                        const float* gm, const float* bt, float rsc = 0.f) {
+                                        const float* gm, const float* bt, float rsc = 0.f,
+                                        const void* tbase = nullptr, int tm0 = 0, float cs = 1.f) {
   if (CHECK && row >= e.M) return;
   if (CHECK && c0 + NV > e.N) {
 #pragma unroll
@@ -560,9 +564,9 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
     }
   } else if (EPI != RF_EPI_NONE) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] += bv[k];
+    for (int k = 0; k < NV; ++k) v[k] = FS ? fmaf(v[k], cs, bv[k]) : v[k] + bv[k];
   }
-  if (c0 < e.scale_cols) {
+  if (!FS && c0 < e.scale_cols) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] *= e.col_scale;
   }
@@ -637,14 +641,24 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
     for (int q = 0; q < NV / 4; ++q)
       *reinterpret_cast<f32x4*>(out + 4 * q) = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
   } else {
-    E* out = reinterpret_cast<E*>(e.C) + (int64_t)row * e.ldc + c0;
+    // TB (interior tiles): the tile's first output row as a wave-uniform base (tbase = row tm0): a
+    // 32-bit per-lane offset from it (one v_add per store, global_store's SGPR-base form) instead of
+    // 64-bit address arithmetic per store
+    E* out;
+    if constexpr (TB)
+      out = reinterpret_cast<E*>(const_cast<char*>(reinterpret_cast<const char*>(tbase)) +
+                                 (uint32_t)(((row - tm0) * e.ldc + c0) * (int)sizeof(E)));
+    else out = reinterpret_cast<E*>(e.C) + (int64_t)row * e.ldc + c0;
     if (NV == 8) {
       typename H16<E>::x8 x;
 #pragma unroll
       for (int k = 0; k < 8; ++k) x[k] = (E)v[k];
 #if !defined(RF_GEMM_PLAIN_STORE)
       // non-temporal: the tile's output is not re-read by this kernel; measured +0.8% per C2
-      // step (tools/gpu/gemm_var.sh: qkv -4%, FFN -1.5%)
+      // step (tools/gpu/gemm_var.sh: qkv -4%, FFN -1.5%). Plain stores for only the outputs the
+      // next kernel reads at once (out-proj / FFN2 -> LayerNorm, qkv -> band attention), for
+      // Infinity-Cache hits, measured slower too (same-process step A/B, round 3: LayerNorm
+      // unchanged, the GEMMs 1-3% slower)
       __builtin_nontemporal_store(x, reinterpret_cast<typename H16<E>::x8*>(out));
 #else
       *reinterpret_cast<typename H16<E>::x8*>(out) = x;
@@ -1344,6 +1358,15 @@ __global__ void __launch_bounds__(256, 1)
       }
     }
     const int em0 = m0;
+    const void* tbase = reinterpret_cast<const E*>(e.C) + (int64_t)m0 * e.ldc;
+    constexpr bool FSC = !OUT32 && (EPI == RF_EPI_BIAS || EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX ||
+                                    EPI == RF_EPI_BIAS_RESID);
+    float csc = 1.f;
+    if (FSC) {
+      csc = ecol < e.scale_cols ? e.col_scale : 1.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bv[k] *= csc;
+    }
     auto epilogue = [&](auto check) {
       constexpr bool CK = decltype(check)::value;
 #pragma unroll
@@ -1359,7 +1382,7 @@ __global__ void __launch_bounds__(256, 1)
             epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
             epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
           } else {
-            epi_seg<E, EPI, CF32, RF32, 8, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+            epi_seg<E, EPI, CF32, RF32, 8, CK, !CK, FSC>(e, row, ecol, vv, bv, gm, bt, rsc, tbase, em0, csc);
           }
         }
     };
