@@ -646,9 +646,9 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
     const int row = wave * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ (row & 7);
     const int p = row < gmax ? gidx[(int64_t)b * gmax + row] : -1;
-    const uint32_t off = __umul24(p >= 0 ? p : 0, ld) + ch * 8;
-    glds16(kb + off, smem + AP_KG + wave * 1024);
-    glds16(vb + off, smem + AP_VG + wave * 1024);
+    const uint32_t off = (__umul24(p >= 0 ? p : 0, ld) + ch * 8) * (uint32_t)sizeof(E);
+    glds16(reinterpret_cast<const char*>(kb) + off, smem + AP_KG + wave * 1024);
+    glds16(reinterpret_cast<const char*>(vb) + off, smem + AP_VG + wave * 1024);
     if (threadIdx.x < 32) gp[threadIdx.x] = (int)threadIdx.x < gmax ? gidx[(int64_t)b * gmax + threadIdx.x] : -1;
   }
   const int prow = 16 * wave + (lane >> 3);  // DMA piece rows prow, prow + 8 (pieces 2w, 2w+1)
@@ -658,15 +658,19 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int kp = min(max(64 * c - 32 + prow + 8 * j, 0), Lp - 1);
-      const uint32_t off = __umul24(kp, ld) + pch;
-      BAND_GLDS(kb + off, base + j * 1024);
-      BAND_GLDS(vb + off, base + 8192 + j * 1024);
+      // byte offsets in 32 bits from the wave-uniform (b, h) bases: the SGPR-base load form, no
+      // 64-bit address arithmetic per piece
+      const uint32_t off = (__umul24(kp, ld) + pch) * (uint32_t)sizeof(E);
+      BAND_GLDS(reinterpret_cast<const char*>(kb) + off, base + j * 1024);
+      BAND_GLDS(reinterpret_cast<const char*>(vb) + off, base + 8192 + j * 1024);
     }
   };
   auto dma_q = [&](int x) {
     char* base = smem + AP_Q + (x & 1) * 8192 + wave * 2048;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) BAND_GLDS(qb + __umul24(64 * x + prow + 8 * j, ld) + pch, base + j * 1024);
+    for (int j = 0; j < 2; ++j)
+      BAND_GLDS(reinterpret_cast<const char*>(qb) + (__umul24(64 * x + prow + 8 * j, ld) + pch) * (uint32_t)sizeof(E),
+                base + j * 1024);
   };
   dma_q(x0);
   dma_chunk(x0);
@@ -874,7 +878,8 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
 #pragma unroll
     for (int p2 = 0; p2 < 2; ++p2) {
       const int orow = 8 * p2 + (lane >> 3);
-      *reinterpret_cast<V8*>(ob + __umul24(i0 + 16 * wave + orow, ldo) + (lane & 7) * 8) = ov[p2];
+      *reinterpret_cast<V8*>(reinterpret_cast<char*>(ob) +
+                             (__umul24(i0 + 16 * wave + orow, ldo) + (lane & 7) * 8) * (uint32_t)sizeof(E)) = ov[p2];
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1430,6 +1435,8 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
   RF_REQUIRE(hd == 64, "rf_band_attn_fwd: head_dim must be 64 (got %d)", hd);
   RF_REQUIRE(B >= 0 && H > 0 && Lp >= 0 && gmax >= 0, "rf_band_attn_fwd: bad shape");
   RF_REQUIRE(ld_qkv >= H * hd && ld_out >= H * hd, "rf_band_attn_fwd: bad leading dims");
+  RF_REQUIRE((int64_t)Lp * (ld_qkv > ld_out ? ld_qkv : ld_out) * 4 < 0x7FFFFFFF,
+             "rf_band_attn_fwd: one sequence's rows must span < 2 GiB (32-bit offsets from the sequence base)");
   RF_REQUIRE(gmax == 0 || gidx, "rf_band_attn_fwd: gidx required");
   if (B == 0 || Lp == 0) return RF_OK;
   hipStream_t s = as_stream(stream);

@@ -516,7 +516,8 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
       const int seg = half * hseg + (p >> 3), row = (p & 7) * 8 + (lane >> 3);
       const int chk = (lane & 7) ^ (row & 7);
       const int jr = min(j0 + row, Lp - 1);
-      glds16(hb + (int64_t)jr * ldh + seg * 64 + chk * 8, smem + (seg * 64 + (p & 7) * 8) * 128);
+      glds16(reinterpret_cast<const char*>(hb) + (uint32_t)((jr * ldh + seg * 64 + chk * 8) * (int)sizeof(E)),
+             smem + (seg * 64 + (p & 7) * 8) * 128);
     }
   };
   // u fragments (B operand of S^T = H.U^T): hi and lo planes; heads >= H score 0
@@ -787,7 +788,8 @@ __global__ void __launch_bounds__(256) k_gfold_partial_ring(int Lp, int gmax, in
       const int seg = pc >> 2, row = (pc & 3) * 8 + (lane >> 3);
       const int chk = (lane & 7) ^ (row & 7);
       const int jr = min(j0 + row, Lp - 1);
-      glds16(hb + (int64_t)jr * ldh + seg * 64 + chk * 8, slot + (seg * 32 + (pc & 3) * 8) * 128);
+      glds16(reinterpret_cast<const char*>(hb) + (uint32_t)((jr * ldh + seg * 64 + chk * 8) * (int)sizeof(E)),
+             slot + (seg * 32 + (pc & 3) * 8) * 128);
     }
   };
   dma(0);
@@ -971,7 +973,8 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16_1(int Lp, int gmax, 
       const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
       const int chk = (lane & 7) ^ (row & 7);
       const int jr = min(j0 + row, Lp - 1);
-      glds16(hb + (int64_t)jr * ldh + seg * 64 + chk * 8, smem + (seg * 64 + (p & 7) * 8) * 128);
+      glds16(reinterpret_cast<const char*>(hb) + (uint32_t)((jr * ldh + seg * 64 + chk * 8) * (int)sizeof(E)),
+             smem + (seg * 64 + (p & 7) * 8) * 128);
     }
     wait_vmcnt0();
     __syncthreads();
@@ -1460,6 +1463,7 @@ extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int
   RF_REQUIRE(D == H * 64, "rf_global_attn_fold_fwd: D=%d must be H*64", D);
   RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_fwd: at most %d heads", GF_HP);
   RF_REQUIRE(ldh >= D && ld_qg >= D && ld_out >= D, "rf_global_attn_fold_fwd: dims");
+  RF_REQUIRE((int64_t)Lp * ldh * 4 < 0x7FFFFFFF, "rf_global_attn_fold: one sequence's rows must span < 2 GiB");
   RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16 || dtype == RF_F32, "rf_global_attn_fold_fwd: bad dtype %d", dtype);
   if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
   RF_REQUIRE(workspace && gidx && flags, "rf_global_attn_fold_fwd: null workspace/gidx/flags");
@@ -1528,6 +1532,7 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
   RF_REQUIRE(D == H * 64 && D <= 1024, "rf_global_attn_fold_h: D=%d must be H*64 <= 1024", D);
   RF_REQUIRE(H <= GF_HP, "rf_global_attn_fold_h: at most %d heads", GF_HP);
   RF_REQUIRE(ldh >= D && ld_out >= D, "rf_global_attn_fold_h: dims");
+  RF_REQUIRE((int64_t)Lp * ldh * 4 < 0x7FFFFFFF, "rf_global_attn_fold: one sequence's rows must span < 2 GiB");
   RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16 || dtype == RF_F32, "rf_global_attn_fold_h: bad dtype %d", dtype);
   if (B == 0 || Lp == 0 || gmax == 0) return RF_OK;
   RF_REQUIRE(workspace && gidx && flags && wqg && bqg, "rf_global_attn_fold_h: null pointer");
@@ -1736,7 +1741,8 @@ __global__ void __launch_bounds__(256) k_gbwd_main(int Lp, int gmax, int H, cons
     const int seg = p >> 3, row = (p & 7) * 8 + (lane >> 3);
     const int chk = (lane & 7) ^ (row & 7);
     const int jr = min(j0 + row, Lp - 1);
-    glds16(hb + (int64_t)jr * ldh + seg * 64 + chk * 8, himg + (seg * 64 + (p & 7) * 8) * 128);
+    glds16(reinterpret_cast<const char*>(hb) + (uint32_t)((jr * ldh + seg * 64 + chk * 8) * (int)sizeof(E)),
+           himg + (seg * 64 + (p & 7) * 8) * 128);
   }
   const int jv = j0 + lane;
   const bool okv = jv < Lp && flags[(int64_t)b * Lp + min(jv, Lp - 1)] != 0;
@@ -2178,6 +2184,7 @@ extern "C" int rf_global_fold_bwd(int dtype, int B, int Lp, int D, int H, const 
   RF_REQUIRE(h && flags && gidx && fwd_workspace && dw && dh && du && w && stats && workspace,
              "rf_global_fold_bwd: null pointer");
   RF_REQUIRE(ldh % 8 == 0 && lddh % 8 == 0 && ldh >= D && lddh >= D, "rf_global_fold_bwd: leading dims");
+  RF_REQUIRE((int64_t)Lp * ldh * 4 < 0x7FFFFFFF, "rf_global_attn_fold: one sequence's rows must span < 2 GiB");
   gbwd_run(dtype, B, Lp, D, H, h, ldh, flags, gidx, gmax, fwd_workspace, dw, cb, nullptr, 0, nullptr, nullptr,
            nullptr, p_drop, seed, dh, lddh, du, w, stats, workspace, as_stream(stream));
   RF_LAUNCH_CHECK("rf_global_fold_bwd");
@@ -2205,6 +2212,7 @@ extern "C" int rf_global_fold_bwd_full(int dtype, int B, int Lp, int D, int H, c
   RF_REQUIRE(ldh % 8 == 0 && lddh % 8 == 0 && ldh >= D && lddh >= D && lddout >= D && ldqg >= D,
              "rf_global_fold_bwd_full: leading dims");
   RF_REQUIRE(B * gmax <= 1024, "rf_global_fold_bwd_full: at most 1024 global rows");
+  RF_REQUIRE((int64_t)Lp * ldh * 4 < 0x7FFFFFFF, "rf_global_attn_fold: one sequence's rows must span < 2 GiB");
   const int R = B * gmax;
   char* p = reinterpret_cast<char*>(workspace) + gbwd_bytes(R, Lp, D);
   p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255);
