@@ -1280,9 +1280,6 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
         for (int p = 0; p < 16; ++p) dma_piece(t + 2, kb, p);
       }
-      // the next tile's column vectors into the other parity slot (last read by the previous
-      // tile's epilogue, before this tile's first barrier); repeated per K-tile to stay branch-free
-      dma_cols(nm0, nn0, (tix + 1) & 1);
       if (!IL) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) read0(kb ^ 1, i);
@@ -1389,6 +1386,10 @@ __global__ void __launch_bounds__(256, 1)
     if (interior) epilogue(std::false_type{});
     else epilogue(std::true_type{});
     asm volatile("" ::: "memory");
+    // the next tile's column vectors into the other parity slot, once per tile and outside the
+    // K-loop: that slot was last read by the previous tile's epilogue, which every wave finished
+    // before this tile's first barrier; the next tile's second mid-sync waits for it
+    if (has_next) dma_cols(nm0, nn0, (tix + 1) & 1);
     ++tix;
     if (!has_next) break;
     v += gridDim.x;
