@@ -337,6 +337,17 @@ int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, co
  * SeqRec): loss[m] = logsumexp(x[m, :N]) - x[m, label[m]] in fp32 (0 where label == ignore_index;
  * the caller divides the sum by the non-ignored count, as mean reduction does); optional
  * argmax[m] (first maximum, torch.argmax) for cl_correct_num (models.py:497). ldx in elements. */
+/* Backward of the cosine scoring head (Similarity, models.py:358-369; the CrossEntropyLoss over
+ * it, models.py:583-599): for logits s[b, c] = inv_temp (z_b . t_n) rz_b ri_n, n = c (cand == NULL,
+ * the full catalog) or n = cand[b * C + c] (sampled softmax), and their gradient g = dL/ds (B x C
+ * fp32), writes
+ *   dz_b = rz_b (inv_temp sum_c g_bc ri_n t_n - (sum_c g_bc s_bc) rz_b z_b)      (B x D fp32).
+ * z / items in dtype (fp32, bf16, fp16), rz / ri the inverse norms the forward used; ws holds
+ * rf_cos_score_bwd_workspace(B, C, D) bytes. Two launches, fixed-order sums (deterministic). */
+size_t rf_cos_score_bwd_workspace(int B, int C, int D);
+int rf_cos_score_bwd(int dtype, int B, int C, int D, const void* z, int ldz, const float* rz, const void* items,
+                     int ldi, const float* ri, const int64_t* cand, float inv_temp, const float* g, int64_t ldg,
+                     const float* s, int64_t lds, void* ws, float* dz, int64_t lddz, rf_stream_t stream);
 int rf_cross_entropy_fwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,
                          int64_t ignore_index, float* loss, int32_t* argmax, rf_stream_t stream);
 /* Its gradient w.r.t. the logits for the mean loss (the LM-head decoder's backward, models.py:499-510):
@@ -400,21 +411,33 @@ int rf_topk_merge(int B, int k0, const float* v0, const int32_t* i0, const float
  * with decay = 1 - lr weight_decay, w1 = 1 - beta1, w2 = 1 - beta2 (rounded from double on the host,
  * as torch passes them). step == NULL: step_size = lr / (1 - beta1^t) and bias_correction2_sqrt
  * are the host's (torch's non-capturable AdamW); otherwise both are computed on the device from the
- * step count *step (already advanced), so a captured optimizer step needs no host values. */
+ * step count *step (already advanced), so a captured optimizer step needs no host values.
+ * hyper != NULL (capturable groups): lr = hyper[0] and decay = hyper[1] are read on the device — the
+ * group's learning rate lives in device memory the host updates between graph replays (an LR
+ * scheduler's value reaches a captured step, as torch's capturable AdamW with a Tensor lr). */
 typedef struct rf_adamw_tensor {
   float* param;
-  const float* grad;
+  float* grad;
   float* exp_avg;
   float* exp_avg_sq;
   const float* step;
+  const float* hyper;
   int64_t numel;
   int64_t first_block;
   float decay, beta1, w1, beta2, w2, eps, lr, step_size, bias_correction2_sqrt;
   int32_t maximize;
-} rf_adamw_tensor; /* 96 bytes */
+} rf_adamw_tensor; /* 104 bytes */
 int rf_adamw_chunk(void);
 int rf_adamw_step(const rf_adamw_tensor* tensors, int ntensors, const int32_t* block_tensor, int nblocks,
                   rf_stream_t stream);
+/* The same under a gradient scaler (torch.amp.GradScaler driving an optimizer with
+ * _step_supports_amp_scaling, finetune.py:116-126 / lightning precision=16): grad_scale != NULL
+ * divides every gradient by *grad_scale before the update (the scaler's unscale, fused); found_inf
+ * != NULL and *found_inf != 0 skips the whole step — no parameter or moment is written, as
+ * GradScaler skips optimizer.step() on an inf/NaN gradient. Both are device scalars, so the step
+ * needs no host read and can be captured. */
+int rf_adamw_step_amp(const rf_adamw_tensor* tensors, int ntensors, const int32_t* block_tensor, int nblocks,
+                      const float* grad_scale, const float* found_inf, rf_stream_t stream);
 
 /* Training-step weight packing (autocast's per-op weight casts, finetune.py:106-110): every
  * descriptor's fp32 source (rows x cols, row-major, lda) rounded to the compute dtype (RF_BF16 /

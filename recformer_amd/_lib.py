@@ -72,6 +72,7 @@ SIGNATURES = {
     "rf_adamw_chunk": (c_int, []),
     "rf_set_seed_source": (P, [P]),
     "rf_adamw_step": (c_int, [P, c_int, P, c_int, P]),
+    "rf_adamw_step_amp": (c_int, [P, c_int, P, c_int, P, P, P]),
     "rf_weight_grad_workspace": (ctypes.c_size_t, [c_int, c_int, c_int]),
     "rf_weight_grad": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_int, c_int, P, ctypes.c_size_t,
                                P]),
@@ -104,6 +105,9 @@ SIGNATURES = {
     "rf_row_inv_norm": (c_int, [c_int, c_int, c_int, P, c_int, c_float, P, P]),
     "rf_cos_score_cand": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P,
                                   c_float, P, P]),
+    "rf_cos_score_bwd_workspace": (ctypes.c_size_t, [c_int, c_int, c_int]),
+    "rf_cos_score_bwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P, c_float, P,
+                                 ctypes.c_int64, P, ctypes.c_int64, P, P, ctypes.c_int64, P]),
     "rf_rank_accum": (c_int, [c_int, c_int, P, ctypes.c_int64, P, c_float, c_float, P, P, P, P]),
     "rf_label_scores": (c_int, [c_int, c_int, c_int, P, c_int, P, P, c_int, P, c_int, P, ctypes.c_int64, c_float, P,
                                 P]),

@@ -15,11 +15,13 @@
 namespace rf {
 
 constexpr int ADAM_CHUNK = 8192;  // elements per workgroup (256 threads x 8 float4)
+static_assert(sizeof(rf_adamw_tensor) == 104, "rf_adamw_tensor layout (recformer_amd/optim.py _DESC)");
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const rf_adamw_tensor& d,
-                                          float step_size, float bc2_sqrt) {
+                                          float decay, float step_size, float bc2_sqrt, float inv_scale) {
+  g = g * inv_scale;  // 1 unless a gradient scaler hands its scale (power of two: exact)
   if (d.maximize) g = -g;
-  p = p * d.decay;
+  p = p * decay;
   const float w = d.w1;
   m = w < 0.5f ? m + w * (g - m) : g - (g - m) * (1.0f - w);
   v = v * d.beta2 + d.w2 * g * g;
@@ -27,13 +29,23 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = p + (-step_size) * (m / denom);
 }
 
+// grad_scale / found_inf: device scalars of a gradient scaler (NULL: none). A step with an inf/NaN
+// gradient (found_inf != 0) writes nothing — every workgroup returns before its first load.
 __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict__ descs,
-                                               const int32_t* __restrict__ block_tensor) {
+                                               const int32_t* __restrict__ block_tensor,
+                                               const float* __restrict__ grad_scale,
+                                               const float* __restrict__ found_inf) {
+  if (found_inf && *found_inf != 0.0f) return;
+  const float inv_scale = grad_scale ? 1.0f / *grad_scale : 1.0f;
   const rf_adamw_tensor d = descs[block_tensor[blockIdx.x]];
-  float step_size = d.step_size, bc2_sqrt = d.bias_correction2_sqrt;
+  float step_size = d.step_size, bc2_sqrt = d.bias_correction2_sqrt, decay = d.decay, lr = d.lr;
+  if (d.hyper) {  // capturable group: lr and 1 - lr wd from device memory the host updates between replays
+    lr = d.hyper[0];
+    decay = d.hyper[1];
+  }
   if (d.step) {  // capturable: bias corrections from the device step count
     const float t = *d.step;
-    step_size = d.lr / (1.0f - powf(d.beta1, t));
+    step_size = lr / (1.0f - powf(d.beta1, t));
     bc2_sqrt = sqrtf(1.0f - powf(d.beta2, t));
   }
   const int64_t e0 = ((int64_t)blockIdx.x - d.first_block) * ADAM_CHUNK;
@@ -57,10 +69,10 @@ __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      adam_elem(p[i].x, g[i].x, m[i].x, v[i].x, d, step_size, bc2_sqrt);
-      adam_elem(p[i].y, g[i].y, m[i].y, v[i].y, d, step_size, bc2_sqrt);
-      adam_elem(p[i].z, g[i].z, m[i].z, v[i].z, d, step_size, bc2_sqrt);
-      adam_elem(p[i].w, g[i].w, m[i].w, v[i].w, d, step_size, bc2_sqrt);
+      adam_elem(p[i].x, g[i].x, m[i].x, v[i].x, d, decay, step_size, bc2_sqrt, inv_scale);
+      adam_elem(p[i].y, g[i].y, m[i].y, v[i].y, d, decay, step_size, bc2_sqrt, inv_scale);
+      adam_elem(p[i].z, g[i].z, m[i].z, v[i].z, d, decay, step_size, bc2_sqrt, inv_scale);
+      adam_elem(p[i].w, g[i].w, m[i].w, v[i].w, d, decay, step_size, bc2_sqrt, inv_scale);
       const int o = 4 * (threadIdx.x + 256 * i);
       *reinterpret_cast<float4*>(P + o) = p[i];
       *reinterpret_cast<float4*>(Mm + o) = m[i];
@@ -69,7 +81,7 @@ __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict
   } else {
     for (int64_t i = threadIdx.x; i < n; i += 256) {
       float p = P[i], m = Mm[i], v = Vv[i];
-      adam_elem(p, G[i], m, v, d, step_size, bc2_sqrt);
+      adam_elem(p, G[i], m, v, d, decay, step_size, bc2_sqrt, inv_scale);
       P[i] = p;
       Mm[i] = m;
       Vv[i] = v;
@@ -83,11 +95,16 @@ using namespace rf;
 
 extern "C" int rf_adamw_chunk(void) { return ADAM_CHUNK; }
 
-extern "C" int rf_adamw_step(const rf_adamw_tensor* tensors, int ntensors, const int32_t* block_tensor, int nblocks,
-                             rf_stream_t stream) {
+extern "C" int rf_adamw_step_amp(const rf_adamw_tensor* tensors, int ntensors, const int32_t* block_tensor,
+                                 int nblocks, const float* grad_scale, const float* found_inf, rf_stream_t stream) {
   RF_REQUIRE(ntensors >= 0 && nblocks >= 0, "rf_adamw_step: bad counts %d %d", ntensors, nblocks);
   if (nblocks == 0) return RF_OK;
   RF_REQUIRE(tensors && block_tensor, "rf_adamw_step: null pointer");
-  k_adamw<<<nblocks, 256, 0, as_stream(stream)>>>(tensors, block_tensor);
+  k_adamw<<<nblocks, 256, 0, as_stream(stream)>>>(tensors, block_tensor, grad_scale, found_inf);
   RF_LAUNCH_CHECK("rf_adamw_step");
+}
+
+extern "C" int rf_adamw_step(const rf_adamw_tensor* tensors, int ntensors, const int32_t* block_tensor, int nblocks,
+                             rf_stream_t stream) {
+  return rf_adamw_step_amp(tensors, ntensors, block_tensor, nblocks, nullptr, nullptr, stream);
 }

@@ -12,7 +12,7 @@
 namespace rf {
 
 static thread_local char g_err[512];
-int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8, -1};
+int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8, -1, 0};
 const uint64_t* g_seed_dev = nullptr;
 
 void set_error(const char* fmt, ...) {
@@ -713,6 +713,107 @@ __global__ void __launch_bounds__(256) k_cos_cand(int B, int C, int D, const T* 
   if (lane == 0) scores[idx] = s * rz[b] * ri[n] * inv_temp;
 }
 
+// Backward of the cosine scoring head (Similarity, models.py:358-369, trained through the
+// CrossEntropyLoss of models.py:583-599): logits s[b, c] = inv_temp (z_b . t_n) rz_b ri_n with
+// n = c (full catalog) or n = cand[b, c] (sampled softmax, models.py:592-597). With g = dL/ds:
+//   dz_b = rz_b (inv_temp sum_c g_bc ri_n t_n - (sum_c g_bc s_bc) rz_b z_b)
+// Pass 1 (k_cos_bwd_part): a workgroup takes COS_NCH columns of ROWS rows (16 for the full catalog —
+// the rows share every item row, so the table is read once — 1 for sampled rows, whose items differ),
+// thread t owns columns d = t + 256 k of the partial sum over its columns; the (g s) row sums too.
+// Pass 2 (k_cos_bwd_fin): the partials of a row summed in chunk order (deterministic), then dz.
+constexpr int COS_NCH = 64;
+
+template <typename T, int ROWS, int KD>
+__global__ void __launch_bounds__(256) k_cos_bwd_part(int B, int C, int D, const T* __restrict__ items, int ldi,
+                                                      const float* __restrict__ ri, const int64_t* __restrict__ cand,
+                                                      const float* __restrict__ g, int64_t ldg,
+                                                      const float* __restrict__ s, int64_t lds,
+                                                      float* __restrict__ part, float* __restrict__ partc) {
+  __shared__ float sg[ROWS][COS_NCH];
+  __shared__ float sgs[ROWS][COS_NCH];
+  __shared__ int64_t sidx[COS_NCH];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * COS_NCH, b0 = blockIdx.y * ROWS;
+  const int ncol = min(COS_NCH, C - c0);
+  for (int e = tid; e < ROWS * COS_NCH; e += 256) {
+    const int r = e / COS_NCH, c = e - r * COS_NCH;
+    const int b = b0 + r, col = c0 + c;
+    const bool ok = b < B && c < ncol;
+    const float gv = ok ? g[(int64_t)b * ldg + col] : 0.f;
+    sg[r][c] = gv;
+    sgs[r][c] = ok ? gv * s[(int64_t)b * lds + col] : 0.f;
+    if (ROWS == 1 && r == 0) sidx[c] = ok ? cand[(int64_t)b * C + col] : 0;
+  }
+  __syncthreads();
+  if (tid < ROWS && b0 + tid < B) {
+    float a = 0.f;
+    for (int c = 0; c < COS_NCH; ++c) a += sgs[tid][c];
+    partc[(int64_t)blockIdx.x * B + b0 + tid] = a;
+  }
+  float acc[ROWS][KD];
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+    for (int k = 0; k < KD; ++k) acc[r][k] = 0.f;
+  int c = 0;
+  for (; c + 4 <= ncol; c += 4) {  // 4 item rows in flight
+    float t[4][KD];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t n = ROWS == 1 ? sidx[c + u] : (int64_t)(c0 + c + u);
+      const float w = ri[n];
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int d = tid + 256 * k;
+        t[u][k] = d < D ? to_f32(items[n * ldi + d]) * w : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+        for (int k = 0; k < KD; ++k) acc[r][k] = fmaf(sg[r][c + u], t[u][k], acc[r][k]);
+  }
+  for (; c < ncol; ++c) {
+    const int64_t n = ROWS == 1 ? sidx[c] : (int64_t)(c0 + c);
+    const float w = ri[n];
+#pragma unroll
+    for (int k = 0; k < KD; ++k) {
+      const int d = tid + 256 * k;
+      const float t = d < D ? to_f32(items[n * ldi + d]) * w : 0.f;
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) acc[r][k] = fmaf(sg[r][c], t, acc[r][k]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    float* dst = part + ((int64_t)blockIdx.x * B + b0 + r) * D;
+#pragma unroll
+    for (int k = 0; k < KD; ++k) {
+      const int d = tid + 256 * k;
+      if (b0 + r < B && d < D) dst[d] = acc[r][k];
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_cos_bwd_fin(int B, int D, int nch, const T* __restrict__ z, int ldz,
+                                                     const float* __restrict__ rz, float inv_temp,
+                                                     const float* __restrict__ part, const float* __restrict__ partc,
+                                                     float* __restrict__ dz, int64_t lddz) {
+  const int b = blockIdx.y;
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= D) return;
+  float a = 0.f, cs = 0.f;
+  for (int ch = 0; ch < nch; ++ch) {
+    a += part[((int64_t)ch * B + b) * D + d];
+    cs += partc[(int64_t)ch * B + b];
+  }
+  const float r = rz[b];
+  dz[(int64_t)b * lddz + d] = r * (inv_temp * a - cs * r * to_f32(z[(int64_t)b * ldz + d]));
+}
+
 // ------------------------------------------------------------------------------------
 // D dispatch: 64*VEC*NCH == D
 #define RF_ROW_DISPATCH(D, LAUNCH)                                      \
@@ -899,7 +1000,7 @@ const char* rf_last_error(void) { return rf::g_err; }
 
 int rf_debug_set_knob(const char* name, int value) {
   static const char* names[rf::KNOB_COUNT] = {"gemm_gn", "gemm_variant", "band_qpb", "band_path", "gfold_path",
-                                              "gfold_qsplit", "gemm_pf"};
+                                              "gfold_qsplit", "gemm_pf", "gemm_mfma32"};
   for (int i = 0; i < rf::KNOB_COUNT; ++i)
     if (name && strcmp(name, names[i]) == 0) {
       const int old = rf::g_knob[i];
@@ -1245,6 +1346,60 @@ int rf_cos_score_cand(int dtype, int B, int C, int D, const void* z, int ldz, co
   else
     RF_REQUIRE(false, "rf_cos_score_cand: bad dtype %d", dtype);
   RF_LAUNCH_CHECK("rf_cos_score_cand");
+}
+
+size_t rf_cos_score_bwd_workspace(int B, int C, int D) {
+  const int64_t nch = (C + COS_NCH - 1) / COS_NCH;
+  return (size_t)(nch * B * ((int64_t)D + 1) * sizeof(float));
+}
+
+int rf_cos_score_bwd(int dtype, int B, int C, int D, const void* z, int ldz, const float* rz, const void* items,
+                     int ldi, const float* ri, const int64_t* cand, float inv_temp, const float* g, int64_t ldg,
+                     const float* s, int64_t lds, void* ws, float* dz, int64_t lddz, rf_stream_t stream) {
+  RF_REQUIRE(B >= 0 && C >= 0 && D > 0 && D <= 1024, "rf_cos_score_bwd: bad shape B=%d C=%d D=%d", B, C, D);
+  RF_REQUIRE(ldz >= D && ldi >= D && ldg >= C && lds >= C && lddz >= D, "rf_cos_score_bwd: bad leading dims");
+  if (B == 0) return RF_OK;
+  RF_REQUIRE(z && rz && items && ri && g && s && ws && dz, "rf_cos_score_bwd: null pointer");
+  const int nch = (C + COS_NCH - 1) / COS_NCH;
+  hipStream_t st = as_stream(stream);
+  float* part = reinterpret_cast<float*>(ws);
+  float* partc = part + (int64_t)nch * B * D;
+  if (C == 0) {
+    RF_REQUIRE(hipMemsetAsync(dz, 0, sizeof(float) * (size_t)lddz * (B - 1) + sizeof(float) * D, st) == hipSuccess,
+               "rf_cos_score_bwd: memset failed");
+    return RF_OK;
+  }
+  const int KD = (D + 255) / 256;
+#define COS_PART(T, ROWS, KDV)                                                                                  \
+  k_cos_bwd_part<T, ROWS, KDV><<<dim3(nch, (B + ROWS - 1) / ROWS), 256, 0, st>>>(                               \
+      B, C, D, (const T*)items, ldi, ri, cand, g, ldg, s, lds, part, partc)
+#define COS_KD(T, ROWS)                                   \
+  switch (KD) {                                           \
+    case 1: COS_PART(T, ROWS, 1); break;                  \
+    case 2: COS_PART(T, ROWS, 2); break;                  \
+    case 3: COS_PART(T, ROWS, 3); break;                  \
+    default: COS_PART(T, ROWS, 4); break;                 \
+  }
+#define COS_ROWS(T)                \
+  if (cand) { COS_KD(T, 1) }       \
+  else { COS_KD(T, 16) }
+  const dim3 fgrid((D + 255) / 256, B);
+  if (dtype == RF_F32) {
+    COS_ROWS(float)
+    k_cos_bwd_fin<float><<<fgrid, 256, 0, st>>>(B, D, nch, (const float*)z, ldz, rz, inv_temp, part, partc, dz, lddz);
+  } else if (dtype == RF_BF16) {
+    COS_ROWS(bf16)
+    k_cos_bwd_fin<bf16><<<fgrid, 256, 0, st>>>(B, D, nch, (const bf16*)z, ldz, rz, inv_temp, part, partc, dz, lddz);
+  } else if (dtype == RF_F16) {
+    COS_ROWS(f16)
+    k_cos_bwd_fin<f16><<<fgrid, 256, 0, st>>>(B, D, nch, (const f16*)z, ldz, rz, inv_temp, part, partc, dz, lddz);
+  } else {
+    RF_REQUIRE(false, "rf_cos_score_bwd: bad dtype %d", dtype);
+  }
+#undef COS_ROWS
+#undef COS_KD
+#undef COS_PART
+  RF_LAUNCH_CHECK("rf_cos_score_bwd");
 }
 
 int rf_cross_entropy_bwd(int dtype, int M, int N, const void* logits, int64_t ldx, const int64_t* labels,

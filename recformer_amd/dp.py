@@ -141,10 +141,19 @@ class GradBucketer:
 
     A second backward outside `no_sync()` before `finish()` (its buckets may already be reduced)
     raises instead of silently dropping that micro-batch.
+
+    Inside a captured training step (graphs.CapturedTrainStep(bucketer=...)) the hooks' flattening
+    and all-reduce launches and finish()'s waits and copies are recorded into the HIP graph, so each
+    replay runs the RCCL collectives with the backward. single_rank=True keeps the collectives at
+    world size 1 (a one-rank nccl group: the captured exchange on one GPU, tests).
     """
 
-    def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, group=None):
+    def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, group=None,
+                 single_rank: bool = False):
         self.rank, self.ws = world()
+        if group is not None:
+            self.rank, self.ws = dist.get_rank(group), dist.get_world_size(group)
+        self.active = self.ws > 1 or (single_rank and dist.is_available() and dist.is_initialized())
         self.average = average
         self.group = group
         self.params = [p for p in params if p.requires_grad]
@@ -152,7 +161,7 @@ class GradBucketer:
         self._handles = []
         self._sync = True
         self.collectives = 0  # collectives issued over the bucketer's lifetime (tests, logging)
-        if self.ws == 1:
+        if not self.active:
             return
         by = {}
         for p in reversed(self.params):
@@ -213,7 +222,7 @@ class GradBucketer:
     def finish(self) -> int:
         """Wait for the window's buckets (launching, in bucket order, any not launched during
         backward), average, write back; returns the number of collectives issued this window."""
-        if self.ws == 1:
+        if not self.active:
             return 0
         while self._next < len(self.buckets):
             self._launch(self._next)

@@ -17,6 +17,24 @@ import numpy as np
 import torch
 
 _M32 = 0xFFFFFFFF
+_MIX = 0x9E3779B97F4A7C15  # SEED_STEP_MIX of rf_common.h
+_seed_counter = None  # device int64 step counter of a captured step (set_seed_counter), or None
+
+
+def set_seed_counter(counter):
+    """Mirror of rf_set_seed_source for the torch-side masks: while a device step counter is set,
+    the seed of every mask drawn here is seed + counter * SEED_STEP_MIX (mod 2^64), computed on the
+    device, exactly as the kernels resolve theirs — so a captured step's torch-side dropout (the
+    non-fold global rows, the fp32 recompute) also draws fresh masks on each replay. Returns the
+    previous counter."""
+    global _seed_counter
+    old, _seed_counter = _seed_counter, counter
+    return old
+
+
+def _signed64(x: int) -> int:
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >= (1 << 63) else x
 
 
 def drop_params(p: float):
@@ -40,7 +58,12 @@ def _mul32(a: torch.Tensor, c: int) -> torch.Tensor:
 def keep(seed: int, idx: torch.Tensor, thresh: int) -> torch.Tensor:
     """drop_keep(seed, idx, thresh) of rf_common.h for an int64 index tensor (idx >= 0)."""
     idx = idx.to(torch.int64)
-    s_lo, s_hi = seed & _M32, (seed >> 32) & _M32
+    if _seed_counter is not None:
+        # seed + counter * MIX in wrapping int64 (= the kernels' uint64 arithmetic), on the device
+        sd = _seed_counter.to(device=idx.device, dtype=torch.int64).reshape(()) * _signed64(_MIX) + _signed64(seed)
+        s_lo, s_hi = sd & _M32, (sd >> 32) & _M32
+    else:
+        s_lo, s_hi = seed & _M32, (seed >> 32) & _M32
     h = _mul32(idx & _M32, 0x9E3779B1) ^ _mul32((idx >> 32) & _M32, 0x85EBCA77) ^ s_lo
     h = h ^ (h >> 16)
     h = _mul32(h, 0x85EBCA6B)

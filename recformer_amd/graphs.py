@@ -40,7 +40,7 @@ from typing import Callable, Dict, Optional
 
 import torch
 
-from . import _lib, models, train
+from . import _lib, dropout, models, train
 
 __all__ = ["GraphedForward", "CapturedTrainStep", "static_gmax"]
 
@@ -134,33 +134,79 @@ class CapturedTrainStep:
 
     optimizer: recformer_amd.optim.AdamW(..., capturable=True). loss_fn(model, batch) -> scalar
     loss (default: model(**batch), or its .loss). autocast_dtype: the autocast dtype of the step
-    (None: fp32). warmup eager steps run on a side stream first (they are real training steps)."""
+    (None: fp32). warmup eager optimizer steps run on a side stream first (they are real training
+    steps, with the same scaler / accumulation / clipping as the captured ones).
+
+    The reference drivers' full training mode (finetune.py:98-137; lightning_pretrain.py:134-145:
+    precision=16, accumulate_grad_batches, gradient_clip_val=1.0, data-parallel):
+      scaler: a torch.amp.GradScaler — the loss is scaled before backward, the inf/NaN check, the
+        AdamW's unscale and skip (optim.AdamW reads the scaler's device grad_scale / found_inf) and
+        the scale update (torch._amp_update_scale_) are all device work inside the graph; a step
+        with an inf gradient changes no parameter and backs the scale off on replay exactly as the
+        eager GradScaler loop does.
+      accumulation_steps k: each call runs ONE micro-batch (loss / k, as finetune.py:112-113); the
+        k-th call of a window also runs the optimizer. Two graphs share one memory pool: the first
+        k-1 micro-batches replay an accumulate-only graph (gradients added in place into .grad
+        buffers that persist across replays), the k-th replays a graph with the micro-batch, the
+        gradient exchange, clipping, the optimizer step and the in-place zeroing of the gradients.
+      max_grad_norm: torch.nn.utils.clip_grad_norm_ after unscaling (Lightning's
+        gradient_clip_val): device-side norm and scale, no host read.
+      bucketer: a dp.GradBucketer — its bucketed all-reduces are launched from the backward hooks
+        of the window's last micro-batch and captured with it (RCCL collectives inside the graph,
+        overlapped with that backward); the other micro-batches run under its no_sync().
+    After the window's last call, `found_inf` (device scalar, 1.0 when the step was skipped) and
+    `optimizer_was_run()` (host read) tell a driver whether to step its LR scheduler, as
+    finetune.py:119-125 does with the scaler's scale; the optimizer's learning rates are re-read
+    from its param_groups (optim.AdamW.sync_hyper) before every replay, so a host LR scheduler
+    works unchanged."""
 
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer, example: Dict[str, torch.Tensor],
                  loss_fn: Optional[Callable] = None, autocast_dtype: Optional[torch.dtype] = torch.bfloat16,
-                 warmup: int = 3, mlm_slack: float = 1.25):
+                 warmup: int = 3, mlm_slack: float = 1.25, scaler=None, accumulation_steps: int = 1,
+                 max_grad_norm: Optional[float] = None, bucketer=None):
         if not all(g.get("capturable", False) for g in optimizer.param_groups):
             raise ValueError("CapturedTrainStep needs an optimizer constructed with capturable=True")
+        if accumulation_steps < 1:
+            raise ValueError(f"accumulation_steps must be >= 1, got {accumulation_steps}")
+        if scaler is not None and not scaler.is_enabled():
+            scaler = None
         self.model, self.opt = model, optimizer
         self.loss_fn = loss_fn or _default_loss
         self.dtype = autocast_dtype
+        self.scaler, self.k, self.max_grad_norm, self.bucketer = scaler, int(accumulation_steps), max_grad_norm, bucketer
+        self.params = [p for g in optimizer.param_groups for p in g["params"]]
         dev = next(model.parameters()).device
         self.static = {k: (v.to(dev).clone() if torch.is_tensor(v) else v) for k, v in example.items()}
         self.gmax = static_gmax(self.static)
         n = mlm_rows(self.static)
         self.mlm_cap = ((int(n * mlm_slack) + 63) // 64) * 64 if n else None
         self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.found_inf = None
+        self._pos = 0  # micro-batches run in the current accumulation window
         lib = _lib.load()
 
-        def body():
+        def micro(last: bool):
+            """One micro-batch: forward, (scaled) backward; the last of a window also steps."""
             if self.dtype is None:
                 loss = self.loss_fn(self.model, self.static)
             else:
                 with torch.autocast("cuda", dtype=self.dtype, cache_enabled=False):
                     loss = self.loss_fn(self.model, self.static)
-            loss.backward()
-            self.opt.step()
+            out = loss / self.k if self.k > 1 else loss
+            if self.scaler is not None:
+                out = self.scaler.scale(out)
+            if self.bucketer is not None and not last:
+                with self.bucketer.no_sync():
+                    out.backward()
+            else:
+                out.backward()
+            if last:
+                self._optimizer_part()
             return loss
+
+        def window():
+            for i in range(self.k):
+                micro(i == self.k - 1)
 
         old_g, old_m = train._STATIC_GMAX, models._STATIC_MLM_ROWS
         train._STATIC_GMAX, models._STATIC_MLM_ROWS = self.gmax, self.mlm_cap
@@ -170,24 +216,71 @@ class CapturedTrainStep:
             with torch.cuda.stream(side):
                 for _ in range(warmup):
                     self.opt.zero_grad(set_to_none=True)
-                    body()
+                    window()
+                if self.k > 1:
+                    # persistent gradient buffers the accumulate graph adds into (zeroed by the last graph)
+                    for p in self.params:
+                        if p.requires_grad:
+                            if p.grad is None:
+                                p.grad = torch.zeros_like(p)
+                            else:
+                                p.grad.zero_()
+                if hasattr(self.opt, "sync_hyper"):
+                    self.opt.sync_hyper()
             torch.cuda.current_stream(dev).wait_stream(side)
-            self.opt.zero_grad(set_to_none=True)
-            self.graph = torch.cuda.CUDAGraph()
+            if self.k == 1:
+                self.opt.zero_grad(set_to_none=True)
             old_src = lib.rf_set_seed_source(self.counter.data_ptr())
+            old_py = dropout.set_seed_counter(self.counter)
             try:
-                with torch.cuda.graph(self.graph):
+                self.graph_acc = None
+                pool = None
+                if self.k > 1:
+                    self.graph_acc = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self.graph_acc):
+                        self.counter.add_(1)
+                        self.loss_acc = micro(False).detach()
+                    pool = self.graph_acc.pool()
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph, pool=pool):
                     self.counter.add_(1)
-                    self.loss = body().detach()
+                    self.loss = micro(True).detach()
             finally:
                 lib.rf_set_seed_source(old_src)
+                dropout.set_seed_counter(old_py)
         finally:
             train._STATIC_GMAX, models._STATIC_MLM_ROWS = old_g, old_m
         self.replays = 0
 
+    def _optimizer_part(self):
+        """Gradient exchange, unscale + clip, optimizer step, scale update, gradient zeroing."""
+        if self.bucketer is not None:
+            self.bucketer.finish()
+        sc = self.scaler
+        if self.max_grad_norm is not None:
+            if sc is not None:
+                sc.unscale_(self.opt)
+            torch.nn.utils.clip_grad_norm_([p for p in self.params if p.grad is not None], self.max_grad_norm,
+                                           foreach=True)
+        if sc is not None:
+            sc.step(self.opt)
+            st = sc._per_optimizer_states[id(self.opt)]["found_inf_per_device"]
+            self.found_inf = sum(v.to(sc._scale.device) for v in st.values())
+            sc.update()
+        else:
+            self.opt.step()
+        if self.k > 1:
+            torch._foreach_zero_([p.grad for p in self.params if p.grad is not None])
+
+    def optimizer_was_run(self) -> bool:
+        """Whether the last completed window's optimizer step was taken (host read; True without a
+        scaler)."""
+        return self.found_inf is None or float(self.found_inf) == 0.0
+
     def __call__(self, batch: Optional[Dict[str, torch.Tensor]] = None, check: bool = True) -> torch.Tensor:
-        """Copy batch (same shapes as the example) into the graph's inputs and replay one step;
-        returns the step's loss (a tensor the next replay overwrites)."""
+        """Copy batch (same shapes as the example) into the graph's inputs and replay one
+        micro-batch (with accumulation_steps = 1: one whole step); returns the micro-batch's loss (a
+        tensor the next replay overwrites)."""
         if batch is not None:
             if check:
                 g = static_gmax(batch)
@@ -202,6 +295,14 @@ class CapturedTrainStep:
                     if dst.shape != v.shape:
                         raise ValueError(f"{k}: shape {tuple(v.shape)} != captured {tuple(dst.shape)}")
                     dst.copy_(v, non_blocking=True)
+        self._pos += 1
+        if self._pos < self.k:
+            self.graph_acc.replay()
+            self.replays += 1
+            return self.loss_acc
+        self._pos = 0
+        if hasattr(self.opt, "sync_hyper"):
+            self.opt.sync_hyper()  # the host's current learning rates (an LR scheduler's) into the graph
         self.graph.replay()
         self.replays += 1
         return self.loss

@@ -225,6 +225,9 @@ def _cos_train(z: torch.Tensor, items: torch.Tensor, temp: float) -> torch.Tenso
         return (zn @ itn.t()) / temp
 
 
+# training scoring head (cosine scores + CrossEntropy, models.py:583-599) on the HIP kernels when
+# the item table is frozen; False: the torch ops (_cos_train, einsum, F.cross_entropy)
+SCORE_HEAD_HIP = True
 # bf16 path: keep the fp32 residual stream as split (hi, lo) 16-bit planes;
 # False = a plain fp32 tensor plus a separate bf16 GEMM operand (A/B tools, tests).
 SPLIT_STREAM = True
@@ -638,9 +641,26 @@ class RecformerForSeqRec(nn.Module):
                                   output_attentions=output_attentions,
                                   output_hidden_states=output_hidden_states, return_dict=True)
         pooler_output = outputs.pooler_output
+        if _needs_grad(self) and SCORE_HEAD_HIP and not self.item_embedding.weight.requires_grad and \
+                pooler_output.is_cuda:
+            # training head on HIP (models.py:583-599): fp32 cosine scores against the frozen table
+            # (from_pretrained(freeze=True), models.py:536) with its inverse norms cached once, the
+            # backward's dz on rf_cos_score_bwd, the CrossEntropy on rf_cross_entropy_fwd / _bwd
+            from . import train
+            table, rnorm = self._items(torch.float32)
+            inv_t = 1.0 / self.config.temp
+            if labels is None:
+                return train.cos_scores_train(pooler_output, table, rnorm, inv_t, candidates)
+            if self.config.finetune_negative_sample_size <= 0:
+                return train.cross_entropy_train(train.cos_scores_train(pooler_output, table, rnorm, inv_t), labels)
+            candidates = torch.cat((labels.unsqueeze(-1), torch.randint(
+                0, self.config.item_num, size=(batch_size, self.config.finetune_negative_sample_size)
+            ).to(labels.device)), dim=-1)
+            logits = train.cos_scores_train(pooler_output, table, rnorm, inv_t, candidates)
+            return train.cross_entropy_train(logits, torch.zeros_like(labels))
         if _needs_grad(self):
-            # training head: differentiable cosine scores + CrossEntropy (models.py:583-599);
-            # the item table is frozen (from_pretrained(freeze=True), models.py:536)
+            # training head: differentiable cosine scores + CrossEntropy (models.py:583-599) as torch
+            # ops — a trainable item table (init_item_embedding() without vectors)
             table = self.item_embedding.weight
             if labels is None:
                 items = table if candidates is None else table[candidates]

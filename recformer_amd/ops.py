@@ -21,6 +21,7 @@ __all__ = [
     "gemm", "weight_grad", "WeightPack", "embed_ln_bwd", "embedding_grad", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
+    "cos_scores_bwd",
     "RF_EPI_NONE", "RF_EPI_BIAS", "RF_EPI_BIAS_GELU", "RF_EPI_BIAS_GELU_AUX", "RF_EPI_BIAS_RESID", "RF_EPI_COS",
     "RF_EPI_DGELU",
 ]
@@ -880,6 +881,37 @@ def cos_scores_cand(z: torch.Tensor, items: torch.Tensor, cand: torch.Tensor, in
                                 _p(items), _rowmajor(items, "items"), _p(items_rnorm), _p(cand),
                                 float(inv_temp), _p(out), _stream(out)), "rf_cos_score_cand")
     return out
+
+
+def cos_scores_bwd(z: torch.Tensor, items: torch.Tensor, g: torch.Tensor, s: torch.Tensor, inv_temp: float,
+                   z_rnorm: torch.Tensor, items_rnorm: torch.Tensor,
+                   cand: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """rf_cos_score_bwd: dL/dz (B, D) fp32 of the cosine scores s = cos(z_b, items_n) * inv_temp
+    (n = column, or cand[b, c] for sampled candidates) from their gradient g (B, C) fp32 and s
+    itself; z_rnorm / items_rnorm are the forward's inverse norms (Similarity's backward,
+    models.py:358-369 under the CrossEntropyLoss of :583-599)."""
+    lib = _lib.load()
+    _dev(z, items, g, s, z_rnorm, items_rnorm)
+    B, D = z.shape
+    C = g.shape[1]
+    if items.dtype != z.dtype:
+        raise TypeError(f"cos_scores_bwd: items {items.dtype} vs z {z.dtype}")
+    for t, nm in ((g, "g"), (s, "s")):
+        if t.dtype != torch.float32 or tuple(t.shape) != (B, C):
+            raise ValueError(f"cos_scores_bwd: {nm} must be fp32 ({B}, {C})")
+    if cand is not None:
+        cand = cand.to(torch.int64).contiguous()
+        if tuple(cand.shape) != (B, C):
+            raise ValueError("cos_scores_bwd: cand must be (B, C)")
+    elif C > items.shape[0]:
+        raise ValueError("cos_scores_bwd: more score columns than items")
+    ws = torch.empty(max(int(lib.rf_cos_score_bwd_workspace(B, C, D)), 4), dtype=torch.uint8, device=z.device)
+    dz = torch.empty(B, D, dtype=torch.float32, device=z.device)
+    check(lib.rf_cos_score_bwd(dtype_code(z.dtype), B, C, D, _p(z), _rowmajor(z, "z"), _p(z_rnorm.contiguous()),
+                               _p(items), _rowmajor(items, "items"), _p(items_rnorm.contiguous()), _p(cand),
+                               float(inv_temp), _p(g), _rowmajor(g, "g"), _p(s), _rowmajor(s, "s"), _p(ws), _p(dz),
+                               D, _stream(dz)), "rf_cos_score_bwd")
+    return dz
 
 
 def cross_entropy_bwd(logits: torch.Tensor, labels: torch.Tensor, grad_scale: torch.Tensor,

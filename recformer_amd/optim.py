@@ -7,13 +7,24 @@ litmodels.py:42-56 for pretraining, stepped through GradScaler in fp16 runs, fin
 (amsgrad=False), with the update of every tensor fused into a single pass over
 (param, grad, exp_avg, exp_avg_sq) — 28 bytes of HBM traffic per fp32 element instead of
 torch's multi-tensor sequence of ~8 passes. Step counts and bias corrections stay on the host as
-in torch, so GradScaler uses its ordinary unscale-and-skip path (an inf step is never taken).
+in torch.
 
 capturable=True (as torch's flag): the step counts live on the device, are advanced by a
 foreach add and the bias corrections are computed in the kernel, so a whole training step including
-the optimizer can be captured in a HIP graph (recformer_amd.graphs). The hyperparameters (lr, betas,
-eps, weight_decay) are read when the descriptors are built: a captured graph keeps the values of its
-capture (re-capture after changing them).
+the optimizer can be captured in a HIP graph (recformer_amd.graphs). Each group's learning rate and
+decay factor (1 - lr * weight_decay) live in a device tensor that the kernel reads and that the host
+refreshes outside the graph (`sync_hyper()`, called by every uncaptured step and by
+CapturedTrainStep before each replay): an LR scheduler stepped on the host between replays
+(optimization.py:7-19's linear warmup/decay, litmodels.py:57-62) reaches the captured update, as
+torch's capturable AdamW with a Tensor lr. betas / eps / weight_decay changes after capture need a
+re-capture (the descriptors keep them).
+
+GradScaler (torch.amp): the optimizer sets `_step_supports_amp_scaling`, so `scaler.step(opt)` hands
+it the scaler's device `grad_scale` and `found_inf` instead of unscaling and reading found_inf on the
+host. The kernel divides each gradient by the scale and, when found_inf is set, writes nothing; the
+capturable step counts advanced before the launch are set back by found_inf after it (torch's fused
+AdamW does the same). The non-capturable form reads found_inf once on the host (as GradScaler's own
+skip does) so its host step counts stay exact.
 
 Parameters must be fp32 CUDA tensors with dense, contiguous gradients; anything else raises
 (there is no CPU fallback).
@@ -31,17 +42,19 @@ from .ops import check
 
 __all__ = ["AdamW"]
 
-# rf_adamw_tensor (include/recformer_hip.h): 5 pointers, numel, first_block, 9 floats, 1 int
+# rf_adamw_tensor (include/recformer_hip.h): 6 pointers, numel, first_block, 9 floats, 1 int
 _DESC = np.dtype([("param", "<u8"), ("grad", "<u8"), ("exp_avg", "<u8"), ("exp_avg_sq", "<u8"), ("step", "<u8"),
-                  ("numel", "<i8"), ("first_block", "<i8"), ("decay", "<f4"), ("beta1", "<f4"), ("w1", "<f4"),
+                  ("hyper", "<u8"), ("numel", "<i8"), ("first_block", "<i8"), ("decay", "<f4"), ("beta1", "<f4"), ("w1", "<f4"),
                   ("beta2", "<f4"), ("w2", "<f4"), ("eps", "<f4"), ("lr", "<f4"), ("step_size", "<f4"),
                   ("bc2_sqrt", "<f4"), ("maximize", "<i4")])
-assert _DESC.itemsize == 96
+assert _DESC.itemsize == 104
 
 
 class AdamW(torch.optim.Optimizer):
     """torch.optim.AdamW's interface (lr, betas, eps, weight_decay, amsgrad=False, maximize),
     one rf_adamw_step launch per step()."""
+
+    _step_supports_amp_scaling = True  # GradScaler hands grad_scale / found_inf (module docstring)
 
     def __init__(self, params: Iterable, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-2, amsgrad: bool = False, *, maximize: bool = False,
@@ -66,6 +79,9 @@ class AdamW(torch.optim.Optimizer):
         self._blob_key = None
         self._blob = None  # (pinned host copy, device copy) of the last descriptors
         self._spare = None  # pinned buffer reserved for a captured step's descriptors
+        self._graph_blobs = []  # descriptor blobs a captured graph reads: kept for the optimizer's lifetime
+        self._hyper = None  # device (groups, 2) fp32: lr, 1 - lr * weight_decay of each capturable group
+        self._hyper_vals = None  # the host values last uploaded into _hyper
         self._launches = 0
 
     def _state(self, p: torch.Tensor, capturable: bool) -> dict:
@@ -75,6 +91,33 @@ class AdamW(torch.optim.Optimizer):
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         return st
+
+    def _hyper_values(self):
+        out = []
+        for group in self.param_groups:
+            lr = group["lr"]
+            lr = float(lr) if isinstance(lr, torch.Tensor) else lr
+            out.append((float(np.float32(lr)), float(np.float32(1 - lr * group["weight_decay"]))))
+        return out
+
+    def sync_hyper(self, device=None) -> bool:
+        """Upload each group's (lr, 1 - lr * weight_decay) into the device tensor the capturable
+        kernel reads, if they changed since the last upload (stream-ordered, from pinned memory; no
+        host wait). Must not run while a stream captures; returns whether it copied."""
+        vals = self._hyper_values()
+        if self._hyper is not None and vals == self._hyper_vals:
+            return False
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("recformer_amd.optim.AdamW: the learning rate changed since the last uncaptured "
+                               "step; call sync_hyper() before capturing")
+        if device is None:
+            device = next(p.device for g in self.param_groups for p in g["params"])
+        if self._hyper is None or self._hyper.shape[0] != len(vals) or self._hyper.device != device:
+            self._hyper = torch.empty(len(vals), 2, dtype=torch.float32, device=device)
+        host = torch.tensor(vals, dtype=torch.float32).pin_memory()
+        self._hyper.copy_(host, non_blocking=True)
+        self._hyper_vals = vals
+        return True
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -86,8 +129,18 @@ class AdamW(torch.optim.Optimizer):
         if self._chunk is None:
             self._chunk = int(lib.rf_adamw_chunk())
         chunk = self._chunk
+        # GradScaler (torch.amp) with _step_supports_amp_scaling: device scale and inf flag
+        grad_scale = getattr(self, "grad_scale", None)
+        found_inf = getattr(self, "found_inf", None)
+        if not any(g.get("capturable", False) for g in self.param_groups) and found_inf is not None:
+            if float(found_inf) != 0.0:  # GradScaler's skip; host step counts must not advance
+                return loss
+            found_inf = None
         rows, device, dev_steps = [], None, []
-        for group in self.param_groups:
+        hyper_needed = any(g.get("capturable", False) for g in self.param_groups)
+        if hyper_needed:
+            self.sync_hyper()
+        for gi, group in enumerate(self.param_groups):
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             cap = group.get("capturable", False)
             if isinstance(lr, torch.Tensor):
@@ -112,25 +165,30 @@ class AdamW(torch.optim.Optimizer):
                     if not st["step"].is_cuda:
                         st["step"] = st["step"].to(p.device)
                     dev_steps.append(st["step"])
-                    step_ptr, step_size, bc2s = st["step"].data_ptr(), 0.0, 1.0
+                    # lr / decay from the device hyper slot: not part of the descriptor key, so a
+                    # scheduler's new value needs no descriptor upload
+                    step_ptr, hyper_ptr, step_size, bc2s, lr_d, dec_d = (st["step"].data_ptr(),
+                                                                         self._hyper[gi].data_ptr(), 0.0, 1.0, 0.0, 1.0)
                 else:
                     st["step"] += 1
                     step = float(st["step"])
-                    step_ptr, step_size, bc2s = 0, lr / (1 - b1 ** step), math.sqrt(1 - b2 ** step)
+                    step_ptr, hyper_ptr, step_size, bc2s = 0, 0, lr / (1 - b1 ** step), math.sqrt(1 - b2 ** step)
+                    lr_d, dec_d = lr, 1 - lr * wd
                 rows.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                             step_ptr, p.numel(), 1 - lr * wd, b1, 1 - b1, b2, 1 - b2, eps, lr, step_size, bc2s,
-                             1 if group["maximize"] else 0))
+                             step_ptr, hyper_ptr, p.numel(), dec_d, b1, 1 - b1, b2, 1 - b2, eps, lr_d, step_size,
+                             bc2s, 1 if group["maximize"] else 0))
         if not rows:
             return loss
         if dev_steps:
             torch._foreach_add_(dev_steps, 1.0)
-        numels = tuple(r[5] for r in rows)
+        numels = tuple(r[6] for r in rows)
         if numels != self._table_key:
             nblk = np.array([(n + chunk - 1) // chunk for n in numels], dtype=np.int64)
             self._first = np.concatenate([[0], np.cumsum(nblk)[:-1]]).astype(np.int64)
             self._table = np.repeat(np.arange(len(numels), dtype=np.int32), nblk)
             self._table_key = numels
         stream = torch.cuda.current_stream(device).cuda_stream
+        capturing = torch.cuda.is_current_stream_capturing()
         key = tuple(rows) if dev_steps else None
         if key is not None and key == self._blob_key:
             # capturable and nothing changed: the device descriptors of the last step stand (no copy,
@@ -139,8 +197,8 @@ class AdamW(torch.optim.Optimizer):
         else:
             d = np.zeros(len(rows), dtype=_DESC)
             cols = list(zip(*rows))
-            names = ("param", "grad", "exp_avg", "exp_avg_sq", "step", "numel", "decay", "beta1", "w1", "beta2",
-                     "w2", "eps", "lr", "step_size", "bc2_sqrt", "maximize")
+            names = ("param", "grad", "exp_avg", "exp_avg_sq", "step", "hyper", "numel", "decay", "beta1", "w1",
+                     "beta2", "w2", "eps", "lr", "step_size", "bc2_sqrt", "maximize")
             for name, col in zip(names, cols):
                 d[name] = col
             d["first_block"] = self._first
@@ -149,7 +207,7 @@ class AdamW(torch.optim.Optimizer):
             # allocated while a stream captures: uncaptured steps stage through a fresh pinned tensor
             # (torch's host allocator guards its reuse) and keep one spare, unused buffer for a capture.
             blob = np.concatenate([d.view(np.uint8), self._table.view(np.uint8)])
-            if torch.cuda.is_current_stream_capturing():
+            if capturing:
                 host = self._spare
                 if host is None or host.numel() < blob.size:
                     raise RuntimeError("recformer_amd.optim.AdamW: run one uncaptured step before capturing")
@@ -164,6 +222,20 @@ class AdamW(torch.optim.Optimizer):
             dev_blob.copy_(host, non_blocking=True)
             self._blob, self._blob_key = (host, dev_blob), key
             base, nd = dev_blob.data_ptr(), len(rows)
-        check(lib.rf_adamw_step(base, nd, base + nd * _DESC.itemsize, int(self._table.size), stream), "rf_adamw_step")
+        if capturing and not any(b is self._blob for b in self._graph_blobs):
+            # a graph replays from these (the pinned source of its descriptor copy, or the device
+            # descriptors it reuses): neither may return to torch's caching allocators while the
+            # optimizer lives, whatever later uncaptured steps do with _blob
+            self._graph_blobs.append(self._blob)
+        gs = grad_scale.data_ptr() if grad_scale is not None else 0
+        fi = found_inf.data_ptr() if found_inf is not None else 0
+        for t in (grad_scale, found_inf):
+            if t is not None and (t.dtype != torch.float32 or t.device != device or t.numel() != 1):
+                raise ValueError("recformer_amd.optim.AdamW: grad_scale / found_inf must be fp32 scalars on the "
+                                 "parameters' device")
+        check(lib.rf_adamw_step_amp(base, nd, base + nd * _DESC.itemsize, int(self._table.size), gs, fi, stream),
+              "rf_adamw_step")
+        if dev_steps and found_inf is not None:
+            torch._foreach_sub_(dev_steps, [found_inf] * len(dev_steps))  # a skipped step is not counted
         self._launches += 1
         return loss

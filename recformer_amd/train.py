@@ -43,7 +43,7 @@ import torch.nn.functional as F
 
 from . import dropout, ops
 
-__all__ = ["encode_train"]
+__all__ = ["encode_train", "cos_scores_train", "cross_entropy_train"]
 
 # the global rows' backward in closed form (_global_bwd); False: autograd over _global_torch
 GLOBAL_BWD_CLOSED_FORM = True
@@ -261,6 +261,64 @@ class _DecoderCE(torch.autograd.Function):
         dw = _weight_grad(dlog, x.contiguous()).to(ctx.wdt) if ctx.needs_input_grad[1] else None
         db = ops.colsum(dlog) if ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None
+
+
+class _CosScores(torch.autograd.Function):
+    """Similarity(z, items) / temp for training (models.py:358-369, used by :583-599) on HIP, in fp32
+    as the reference's autocast runs cosine_similarity: forward on rf_gemm's EPI_COS (exact fp32 MFMA,
+    the full catalog) or rf_cos_score_cand (sampled candidates, models.py:592-597), the backward's
+    dL/dz on rf_cos_score_bwd. The item table is frozen (nn.Embedding.from_pretrained(freeze=True),
+    models.py:536) and its inverse norms cached by the caller, so nothing flows to it and it is never
+    re-normalised per step."""
+
+    @staticmethod
+    def forward(ctx, zf, table, t_rnorm, cand, inv_t: float):
+        rz = ops.row_inv_norm(zf)
+        if cand is None:
+            s = ops.cos_scores(zf, table, inv_t, z_rnorm=rz, items_rnorm=t_rnorm)
+        else:
+            s = ops.cos_scores_cand(zf, table, cand, inv_t, z_rnorm=rz, items_rnorm=t_rnorm)
+        ctx.save_for_backward(zf, rz, table, t_rnorm, s, cand if cand is not None else torch.empty(0))
+        ctx.sampled = cand is not None
+        ctx.inv_t = inv_t
+        return s
+
+    @staticmethod
+    def backward(ctx, g):
+        zf, rz, table, t_rnorm, s, cand = ctx.saved_tensors
+        dz = ops.cos_scores_bwd(zf, table, g.float().contiguous(), s, ctx.inv_t, rz, t_rnorm,
+                                cand if ctx.sampled else None)
+        return dz, None, None, None, None
+
+
+class _CrossEntropy(torch.autograd.Function):
+    """torch.nn.functional.cross_entropy (mean over the non-ignored rows) of fp32 logits on
+    rf_cross_entropy_fwd / rf_cross_entropy_bwd (softmax - one-hot, scaled on the device): the
+    finetuning loss of models.py:589-597."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index: int = -100):
+        rows = ops.cross_entropy(logits, labels, ignore_index, reduction="none")
+        n = (labels.reshape(-1) != ignore_index).sum().to(torch.float32)
+        ctx.save_for_backward(logits, labels, n)
+        ctx.ign = ignore_index
+        return rows.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, labels, n = ctx.saved_tensors
+        dlog = ops.cross_entropy_bwd(logits, labels, (g.float() / n).reshape(1), ctx.ign)
+        return dlog, None, None
+
+
+def cos_scores_train(z: torch.Tensor, table: torch.Tensor, t_rnorm: torch.Tensor, inv_t: float,
+                     cand: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Differentiable fp32 cosine scores of z against a frozen fp32 table (inverse norms given)."""
+    return _CosScores.apply(z.float().contiguous(), table, t_rnorm, cand, float(inv_t))
+
+
+def cross_entropy_train(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    return _CrossEntropy.apply(logits, labels.reshape(-1).to(torch.int64).contiguous(), ignore_index)
 
 
 class _LMHeadTransform(torch.autograd.Function):
@@ -602,10 +660,12 @@ def _global_bwd(qg, h, wkg, wvg, flags, B: int, Lp: int, H: int, gout, z=None, b
 
 def _fold_ws(h, B: int, Lp: int, H: int, G: int):
     """A fold workspace the training forward keeps for the HIP global backward (16-bit, D a multiple
-    of 128 up to 768, at most 4 global rows per sequence), else None (a fresh one per call)."""
+    of 128 up to 768, at most 4 global rows per sequence, B * G <= 1024 global rows and Lp <= 4096 —
+    the limits rf_global_fold_bwd_full / rf_global_query_bwd require), else None: the closed-form
+    torch backward (_global_bwd) then handles the batch instead of the HIP entry points raising."""
     D = h.shape[1]
     if GLOBAL_BWD_HIP and h.is_cuda and h.dtype != torch.float32 and D % 128 == 0 and D <= 768 and G <= 4 \
-            and H <= 16 and D == 64 * H:
+            and H <= 16 and D == 64 * H and B * G <= 1024 and Lp <= 4096:
         return ops.global_fold_workspace(h, B, Lp, H, G)
     return None
 

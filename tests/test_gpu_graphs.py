@@ -144,3 +144,170 @@ def test_captured_pretrain_step_matches_eager(dev):
         assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-6), n
+
+
+def _lin_sched(opt, warm=2, total=12):
+    """The reference's linear warmup / decay schedule (optimization.py:7-19, litmodels.py:57-62):
+    lr = 0 when it is built, so a graph that froze the capture-time lr would never train."""
+    def lam(s):
+        return s / max(1, warm) if s < warm else max(0.0, 1 - s / max(1, total))
+    return torch.optim.lr_scheduler.LambdaLR(opt, lam)
+
+
+def test_captured_step_follows_lr_scheduler(dev):
+    """A host LR scheduler stepped between replays reaches the captured AdamW (device lr, synced
+    before each replay): parameters equal an eager run with the same schedule, and the first steps
+    (lr = 0) change nothing."""
+    batch = _batch(dev)
+    a, b = _model(dev), _model(dev)
+    oa = AdamW([p for p in a.parameters() if p.requires_grad], lr=1e-3, weight_decay=0.01, capturable=True)
+    ob = AdamW([p for p in b.parameters() if p.requires_grad], lr=1e-3, weight_decay=0.01, capturable=True)
+    sa, sb = _lin_sched(oa), _lin_sched(ob)
+    before = [p.detach().clone() for p in a.parameters()]
+    step = graphs.CapturedTrainStep(a, oa, batch, warmup=1)  # warmup runs at lr = 0: a no-op step
+    assert all(torch.equal(x, p) for x, p in zip(before, a.parameters()))
+    _eager_step(b, ob, batch, torch.bfloat16)
+    for _ in range(4):
+        sa.step()
+        sb.step()
+        la, lb = float(step()), _eager_step(b, ob, batch, torch.bfloat16)
+        assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    assert oa.param_groups[0]["lr"] == ob.param_groups[0]["lr"] > 0
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-6), n
+    assert not all(torch.equal(x, p) for x, p in zip(before, a.parameters()))
+
+
+def test_captured_step_survives_uncaptured_optimizer_steps(dev):
+    """The graph's AdamW descriptors stay valid after uncaptured optimizer steps that rebuild them
+    (another parameter subset, fresh pinned staging buffers reused by later host allocations)."""
+    batch = _batch(dev)
+    a, b = _model(dev), _model(dev)
+    pa_all = [p for p in a.parameters() if p.requires_grad]
+    pb_all = [p for p in b.parameters() if p.requires_grad]
+    oa = AdamW(pa_all, lr=1e-3, capturable=True)
+    ob = AdamW(pb_all, lr=1e-3, capturable=True)
+    step = graphs.CapturedTrainStep(a, oa, batch, warmup=1)
+    _eager_step(b, ob, batch, torch.bfloat16)
+    la = float(step())
+    lb = _eager_step(b, ob, batch, torch.bfloat16)
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb))
+    # an uncaptured step over half of the gradients (new descriptors, new pinned staging), on both
+    for opt, ps in ((oa, pa_all), (ob, pb_all)):
+        opt.zero_grad(set_to_none=True)
+        for i, p in enumerate(ps):
+            if i % 2 == 0:
+                p.grad = torch.full_like(p, 1e-3)
+        opt.step()
+    junk = [torch.full((1 << 16,), 0xAB, dtype=torch.uint8).pin_memory() for _ in range(8)]  # reuse the blocks
+    for _ in range(2):
+        la, lb = float(step()), _eager_step(b, ob, batch, torch.bfloat16)
+        assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    del junk
+    for (n, x), y in zip(a.named_parameters(), b.parameters()):
+        assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), n
+
+
+def _eager_window(m, opt, scaler, batches, k, clip):
+    """finetune.py:98-126 with Lightning's gradient_clip_val (lightning_pretrain.py:140): fp16
+    autocast, loss / k, GradScaler, unscale + clip, scaler.step / update, zero_grad."""
+    for i in range(k):
+        with torch.autocast("cuda", dtype=torch.float16):
+            loss = m(**batches[i])
+        scaler.scale(loss / k).backward()
+    scaler.unscale_(opt)
+    torch.nn.utils.clip_grad_norm_([p for p in m.parameters() if p.grad is not None], clip, foreach=True)
+    scaler.step(opt)
+    scaler.update()
+    opt.zero_grad(set_to_none=True)
+    return float(loss)
+
+
+def test_captured_fp16_gradscaler_accumulation_clip_matches_eager(dev):
+    """The reference drivers' training mode captured (finetune.py:106-126, lightning_pretrain.py:
+    137-142): fp16 autocast + GradScaler + 2 accumulated micro-batches + clip at 1.0. An initial
+    scale of 2^40 overflows the fp16 backward, so the first windows find inf gradients: the captured
+    step skips the update (parameters and AdamW step counts unchanged) and backs the scale off on
+    the device exactly as the eager GradScaler loop; then it trains and matches the eager loop."""
+    b0 = _batch(dev)
+    b1 = dict(b0)
+    b1["labels"] = torch.tensor([5, 1, 30, 2], device=dev)
+    mbs = [b0, b1]
+    a, b = _model(dev), _model(dev)
+    oa = AdamW([p for p in a.parameters() if p.requires_grad], lr=1e-3, weight_decay=0.01, capturable=True)
+    ob = AdamW([p for p in b.parameters() if p.requires_grad], lr=1e-3, weight_decay=0.01, capturable=True)
+    kw = dict(init_scale=2.0 ** 40, backoff_factor=2.0 ** -12, growth_interval=3)
+    sa, sb = torch.amp.GradScaler("cuda", **kw), torch.amp.GradScaler("cuda", **kw)
+    # the capture's eager warmup window runs at the overflowing scale (a skipped step), as eager
+    step = graphs.CapturedTrainStep(a, oa, b0, autocast_dtype=torch.float16, warmup=1, scaler=sa,
+                                    accumulation_steps=2, max_grad_norm=1.0)
+    # eager: the same warmup window (on b0 twice, as the capture's warmup replays the example batch)
+    _eager_window(b, ob, sb, [b0, b0], 2, 1.0)
+    assert float(sa.get_scale()) == float(sb.get_scale())
+    skipped = 0
+    for w in range(4):
+        pa0 = [p.detach().clone() for p in a.parameters()]
+        for i in range(2):
+            la = float(step(mbs[i]))
+        ran = step.optimizer_was_run()
+        lb = _eager_window(b, ob, sb, mbs, 2, 1.0)
+        assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (w, la, lb)
+        assert float(sa.get_scale()) == float(sb.get_scale()), (w, sa.get_scale(), sb.get_scale())
+        if not ran:
+            skipped += 1
+            assert all(torch.equal(x, p) for x, p in zip(pa0, a.parameters()))
+        st_a = float(next(iter(oa.state.values()))["step"])
+        st_b = float(next(iter(ob.state.values()))["step"])
+        assert st_a == st_b, (w, st_a, st_b)
+    assert skipped >= 1 and float(sa.get_scale()) <= 2.0 ** 17
+    assert float(next(iter(oa.state.values()))["step"]) >= 1  # it stepped after backing off
+    for (n, x), y in zip(a.named_parameters(), b.parameters()):
+        assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), n
+
+
+def test_captured_dp_step_nccl_single_rank(dev):
+    """The data-parallel step captured with its RCCL all-reduces (dp.GradBucketer launching bucketed
+    collectives from the backward hooks of the window's last micro-batch; the first micro-batch under
+    no_sync): a one-rank nccl group on the box, so the collectives really run inside the HIP graph;
+    the averaged gradients (world 1: the gradients) give the eager steps' parameters. The semantic
+    world-2 check is test_dp.py / test_gpu_pretrain.py (gloo)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from recformer_amd.dp import GradBucketer
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(dev))
+    try:
+        batch = _batch(dev)
+        a, b = _model(dev), _model(dev)
+        oa = AdamW([p for p in a.parameters() if p.requires_grad], lr=1e-3, capturable=True)
+        ob = AdamW([p for p in b.parameters() if p.requires_grad], lr=1e-3, capturable=True)
+        bk = GradBucketer([p for p in a.parameters()], bucket_bytes=1 << 20, single_rank=True)
+        assert len(bk.buckets) > 1
+        step = graphs.CapturedTrainStep(a, oa, batch, warmup=1, accumulation_steps=2, bucketer=bk)
+        n0 = bk.collectives
+
+        def eager():
+            for _ in range(2):
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = b(**batch) / 2
+                loss.backward()
+            ob.step()
+            ob.zero_grad(set_to_none=True)
+
+        eager()
+        for _ in range(2):
+            step(batch)
+            step(batch)
+            eager()
+        assert bk.collectives == n0 + len(bk.buckets)  # launched once, at capture; replays re-run them
+        for (n, x), y in zip(a.named_parameters(), b.parameters()):
+            assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), n
+    finally:
+        dist.destroy_process_group()

@@ -895,3 +895,93 @@ def test_weight_pack_matches_torch_casts(dev, dt):
                 w.mul_(1.5)
     with pytest.raises(ValueError):
         ops.WeightPack([dict(src=q.t(), dst=(qb, 0))], dt)
+
+
+@pytest.mark.parametrize("mfma32", [0, 1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (8192, 768, 3072), (4100, 2312, 768), (65536, 768, 768)])
+def test_gemm_four_wave_kernels_all_epilogues(dev, mfma32, dt, M, N, K):
+    """Both four-wave 256x256 kernels — k_gemm_w4 (v_mfma_f32_16x16x32) and k_gemm_w32
+    (v_mfma_f32_32x32x16, knob gemm_mfma32) — for every epilogue the encoder and its backward use
+    (none, bias with a q-column scale, GELU, GELU + pre-activation, the GELU-backward DGELU, fp32
+    output, cosine scores), including ragged M / N edges (4100 x 2312), against fp32 torch on the
+    same 16-bit operands."""
+    old = _lib.set_knob("gemm_mfma32", mfma32)
+    try:
+        a = _rand((M, K), dev, dt, 0.5, seed=91)
+        w = _rand((N, K), dev, dt, 0.05, seed=92)
+        b = _rand((N,), dev, torch.float32, seed=93)
+        prod = a.float() @ w.float().t()
+        sc = N // 3 // 16 * 16
+        tol = 4e-3 if dt == torch.float16 else 2e-2
+
+        def rel(x, ref):
+            return float((x.float() - ref).abs().max()) / max(1.0, float(ref.abs().max()))
+
+        out = ops.gemm(a, w, None, ops.RF_EPI_NONE)
+        assert rel(out, prod) <= tol
+        ref = prod + b
+        ref[:, :sc] *= 0.125
+        out = ops.gemm(a, w, b, ops.RF_EPI_BIAS, scale_cols=sc, col_scale=0.125)
+        assert rel(out, ref) <= tol
+        out32 = ops.gemm(a, w, b, ops.RF_EPI_BIAS, out_f32=True)
+        assert float((out32 - (prod + b)).abs().max()) <= 1e-3 * max(1.0, float(prod.abs().max()))
+        gl = ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU)
+        assert rel(gl, F.gelu(prod + b)) <= tol
+        z = torch.full((M, N), 7.0, device=dev, dtype=dt)
+        u = ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU_AUX, resid=z)
+        assert torch.equal(u, gl)
+        assert torch.equal(z, ops.gemm(a, w, b, ops.RF_EPI_BIAS))
+        zz = _rand((M, N), dev, dt, 2.0, seed=94)
+        dg = ops.gemm(a, w, None, ops.RF_EPI_DGELU, resid=zz)
+        ref = torch.ops.aten.gelu_backward(prod, zz.float())
+        assert float((dg.float() - ref).abs().max()) <= 1e-2 * max(float(ref.abs().max()), 1e-6)
+        ra = (1.0 / a.float().norm(dim=-1).clamp_min(1e-8)).contiguous()
+        rw = (1.0 / w.float().norm(dim=-1).clamp_min(1e-8)).contiguous()
+        cs = ops.cos_scores(a, w, 20.0, z_rnorm=ra, items_rnorm=rw)
+        ref = F.normalize(a.float(), dim=-1) @ F.normalize(w.float(), dim=-1).t() * 20.0
+        assert float((cs - ref).abs().max()) <= 2e-2
+    finally:
+        _lib.set_knob("gemm_mfma32", old)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,N,C", [(16, 10000, None), (16, 10000, 1001), (3, 700, None), (5, 200, 37), (40, 333, None)])
+def test_cos_scores_bwd_matches_autograd(dev, dt, B, N, C):
+    """rf_cos_score_bwd (the training scoring head's dL/dz, Similarity models.py:358-369 under the
+    CrossEntropyLoss of :583-599) against autograd through fp32 torch normalize + matmul / gather,
+    for the full catalog (C None: rows sharing the table, B > 16 in row groups) and sampled
+    candidates (cand (B, C) incl. repeats), with a CE-shaped upstream gradient."""
+    from recformer_amd import train
+    g = torch.Generator(device=dev).manual_seed(B * 7 + N)
+    z = torch.randn(B, 768, device=dev, generator=g).to(dt)
+    items = torch.randn(N, 768, device=dev, generator=g).to(dt)
+    items[3] *= 1e-3
+    inv_t = 20.0
+    cand = torch.randint(0, N, (B, C), device=dev, generator=g) if C else None
+    labels = torch.randint(0, C or N, (B,), device=dev, generator=g)
+    rt = ops.row_inv_norm(items)
+    zf = z.float().requires_grad_(True)
+    itf = items.float()
+    zn = zf / zf.norm(dim=-1, keepdim=True).clamp_min(1e-8)
+    itn = itf / itf.norm(dim=-1, keepdim=True).clamp_min(1e-8)
+    ref_s = zn @ itn.t() * inv_t if cand is None else torch.einsum("bd,bcd->bc", zn, itn[cand]) * inv_t
+    F.cross_entropy(ref_s, labels).backward()
+    zh = z.float().contiguous().requires_grad_(True)
+    if dt == torch.float32:
+        s = train.cos_scores_train(zh, items, rt, inv_t, cand)
+        loss = train.cross_entropy_train(s, labels)
+        loss.backward()
+        assert float((s - ref_s).abs().max()) <= 1e-4 * inv_t
+        dz = zh.grad
+    else:
+        s = ref_s.detach()
+        gs = torch.softmax(s, -1)
+        gs[torch.arange(B), labels] -= 1
+        gs /= B
+        dz = ops.cos_scores_bwd(z, items, gs.contiguous(), s.contiguous(), inv_t, ops.row_inv_norm(z), rt, cand)
+    err = float((dz - zf.grad).abs().max())
+    assert err <= 2e-3 * float(zf.grad.abs().max()) + 1e-7, err
+    if dt != torch.float32:  # fixed-order sums: bit-identical on a repeat
+        again = ops.cos_scores_bwd(z, items, gs.contiguous(), s.contiguous(), inv_t, ops.row_inv_norm(z), rt, cand)
+        assert torch.equal(dz, again)

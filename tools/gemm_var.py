@@ -13,6 +13,10 @@ from tools.gemm_ab import timeit  # noqa: E402
 
 
 def main():
+    from recformer_amd import _lib
+    for kv in filter(None, os.environ.get("RF_KNOBS", "").split(",")):  # e.g. RF_KNOBS=gemm_mfma32=1
+        k, v = kv.split("=")
+        _lib.set_knob(k, int(v))
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
     res = []
@@ -25,7 +29,8 @@ def main():
         t = timeit(lambda: ops.gemm(a, w, b, epi, out=out), iters=20, warm=5)
         h = hashlib.sha1(out.view(torch.int16).cpu().numpy().tobytes()).hexdigest()[:10]
         res.append(f"{name} {t * 1e6:6.1f}us {2 * M * N * K / t / 1e12:5.0f}TF {h}")
-    print(os.path.basename(os.environ.get("RF_HIP_LIB", "prod")), " | ".join(res), flush=True)
+    print(os.path.basename(os.environ.get("RF_HIP_LIB", "prod")), os.environ.get("RF_KNOBS", ""), " | ".join(res),
+          flush=True)
 
 
 if __name__ == "__main__":
