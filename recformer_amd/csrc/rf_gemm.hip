@@ -1449,79 +1449,6 @@ __device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// interior-tile epilogue of two output rows (row, row + 1) x 4 columns [col, col + 4): v[0..3] row,
-// v[4..7] row + 1; bv = the 4 columns' bias (pre-scaled by cs) or, for EPI_COS, item norms
-template <typename E, int EPI, bool CF32>
-__device__ __forceinline__ void w32_epi_pair(const EpiArgs& e, int row, int col, float (&v)[8], const float* bv,
-                                             float cs, float rs0, float rs1, const char* tbase, int tm0) {
-  typedef typename H16<E>::x4 V4;
-  if (EPI == RF_EPI_COS) {
-    const float s0 = rs0 * e.col_scale, s1 = rs1 * e.col_scale;
-    float* out = reinterpret_cast<float*>(const_cast<char*>(tbase) + (uint32_t)(((row - tm0) * e.ldc + col) * 4));
-    *reinterpret_cast<f32x4*>(out) = f32x4{v[0] * s0 * bv[0], v[1] * s0 * bv[1], v[2] * s0 * bv[2], v[3] * s0 * bv[3]};
-    out += e.ldc;
-    *reinterpret_cast<f32x4*>(out) = f32x4{v[4] * s1 * bv[0], v[5] * s1 * bv[1], v[6] * s1 * bv[2], v[7] * s1 * bv[3]};
-    return;
-  }
-  if (EPI == RF_EPI_DGELU) {
-    const E* z = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + col;
-    const V4 z0 = *reinterpret_cast<const V4*>(z);
-    const V4 z1 = *reinterpret_cast<const V4*>(z + e.ldr);
-    float zf[8], d[8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      zf[k] = (float)z0[k];
-      zf[4 + k] = (float)z1[k];
-    }
-    dgelu8_erf(zf, d);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= d[k];
-  } else if (EPI != RF_EPI_NONE) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], cs, bv[k & 3]);
-  } else if (!CF32) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= cs;
-  }
-  if (EPI == RF_EPI_BIAS_GELU_AUX) {
-    E* z = reinterpret_cast<E*>(const_cast<void*>(e.R)) + (int64_t)row * e.ldr + col;
-    V4 x0, x1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      x0[k] = (E)v[k];
-      x1[k] = (E)v[4 + k];
-    }
-    *reinterpret_cast<V4*>(z) = x0;
-    *reinterpret_cast<V4*>(z + e.ldr) = x1;
-  }
-  if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
-    f32x2 y[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) y[k] = (f32x2){v[2 * k], v[2 * k + 1]};
-    gelu8_bf16out(y);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[2 * k] = y[k].x;
-      v[2 * k + 1] = y[k].y;
-    }
-  }
-  if (CF32) {
-    float* out = reinterpret_cast<float*>(const_cast<char*>(tbase) + (uint32_t)(((row - tm0) * e.ldc + col) * 4));
-    *reinterpret_cast<f32x4*>(out) = f32x4{v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<f32x4*>(out + e.ldc) = f32x4{v[4], v[5], v[6], v[7]};
-  } else {
-    E* out = reinterpret_cast<E*>(const_cast<char*>(tbase) + (uint32_t)(((row - tm0) * e.ldc + col) * (int)sizeof(E)));
-    V4 x0, x1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      x0[k] = (E)v[k];
-      x1[k] = (E)v[4 + k];
-    }
-    __builtin_nontemporal_store(x0, reinterpret_cast<V4*>(out));
-    __builtin_nontemporal_store(x1, reinterpret_cast<V4*>(out + e.ldc));
-  }
-}
-
 template <typename E, int EPI, bool CF32>
 __global__ void __launch_bounds__(256, 1)
     k_gemm_w32(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e,
@@ -1724,47 +1651,135 @@ __global__ void __launch_bounds__(256, 1)
     // no accumulator copy-out may move into the MFMA stream (it would hold 256 VGPRs next to the next
     // tile's fragments); the epilogue streams 8 accumulators per row pair (sched_barrier per pair)
     __builtin_amdgcn_sched_barrier(0);
-    // epilogue: lane (c = l&31, g = l>>5): rows 32i + 8(r>>2) + 4g + (r&3), columns 4c .. 4c+3
-    const bool interior = (m0 + 256 <= e.M) && (n0 + 256 <= e.N);
+    // the accumulators are read below by inline asm, which the hazard recognizer does not see: 24 wait
+    // states cover the 32x32x16 MFMA's write -> VALU read distance (18) for the last MFMAs' blocks
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    // epilogue: lane (c = l&31, g = l>>5): rows 32i + 8(r>>2) + 4g + (r&3), columns 4c .. 4c+3.
+    // One branch-free path for every tile: outputs (and the DGELU / AUX pre-activation rows) go
+    // through buffer resources based at the tile's first row with num_records = its valid rows, so
+    // rows past M are dropped / read as zeros by the range check, and a lane whose 4 columns lie past
+    // N (N % 8 == 0: a 4-column group is all in or all out) gets a base offset >= 2^31, past any
+    // num_records. Each row pair's 8 accumulators stream out under a sched_barrier (no copy-out of all
+    // 256 next to the next tile's fragments); the DGELU pre-activations are loaded ZD pairs ahead.
     int el = lane;
     asm volatile("" : "+v"(el));
-    const int erow = m0 + wr * 128 + 4 * (el >> 5);
-    const int ecol = n0 + wc * 128 + 4 * (el & 31);
+    const int rowl = wr * 128 + 4 * (el >> 5);   // tile-relative row (+ 32i + 8(r>>2) + (r&3))
+    const int coll = wc * 128 + 4 * (el & 31);   // tile-relative column
+    const int ecol = n0 + coll;
+    const bool col_ok = ecol < e.N;
+    const int rows_valid = min(256, e.M - m0);
+    constexpr int CB = OUT32 ? 4 : (int)sizeof(E);
+    const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char*>(e.C) + (int64_t)m0 * e.ldc * CB, (short)0, rows_valid * e.ldc * CB, 0x00020000);
+    const uint32_t lbC = col_ok ? (uint32_t)((rowl * e.ldc + coll) * CB) : 0x80000000u;
+    const int rstepC = e.ldc * CB;
+    constexpr bool HAS_R = EPI == RF_EPI_DGELU || EPI == RF_EPI_BIAS_GELU_AUX;
+    __amdgpu_buffer_rsrc_t rsR = rsC;
+    uint32_t lbR = 0;
+    int rstepR = 0;
+    if (HAS_R) {
+      rsR = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char*>(reinterpret_cast<const char*>(e.R)) + (int64_t)m0 * e.ldr * (int)sizeof(E), (short)0,
+          rows_valid * e.ldr * (int)sizeof(E), 0x00020000);
+      lbR = col_ok ? (uint32_t)((rowl * e.ldr + coll) * (int)sizeof(E)) : 0x80000000u;
+      rstepR = e.ldr * (int)sizeof(E);
+    }
     float bv[4], gm[4], bt[4];
     const float* cb = reinterpret_cast<const float*>(smem + W4_CV + (tix & 1) * 3 * 1024);
-    lds_cols<EPI, 4>(cb, ecol - n0, bv, gm, bt);
+    lds_cols<EPI, 4>(cb, coll, bv, gm, bt);
     float csc = 1.f;
     if (!OUT32) {
       csc = ecol < e.scale_cols ? e.col_scale : 1.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) bv[k] *= csc;
     }
-    // one code path per row pair with the interior test inside it (a uniform branch): with a branch
-    // around two whole epilogues hipcc copies all 256 accumulators to VGPRs before it, next to the
-    // next tile's fragments, and spills
-    const char* tbase = reinterpret_cast<const char*>(e.C) + (int64_t)m0 * e.ldc * (OUT32 ? 4 : (int)sizeof(E));
+    typedef __attribute__((ext_vector_type(2))) unsigned int U2;
+    typedef __attribute__((ext_vector_type(4))) unsigned int U4;
+    constexpr int ZD = 8;  // DGELU pre-activation prefetch distance (row pairs)
+    U2 zr[ZD][2];
+    auto prow = [](int P) { return 32 * (P >> 3) + 8 * ((2 * (P & 7)) >> 2) + ((2 * (P & 7)) & 3); };
+    auto zload = [&](int P, U2 (&dst)[2]) {
+      const uint32_t o = lbR + (uint32_t)(prow(P) * rstepR);
+      dst[0] = __builtin_amdgcn_raw_buffer_load_b64(rsR, o, 0, 0);
+      dst[1] = __builtin_amdgcn_raw_buffer_load_b64(rsR, o + rstepR, 0, 0);
+    };
+    if (EPI == RF_EPI_DGELU) {
+#pragma unroll
+      for (int P = 0; P < ZD; ++P) zload(P, zr[P]);
+    }
+    auto pack4 = [](const float* x) {
+      typename H16<E>::x4 h;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) h[k] = (E)x[k];
+      return __builtin_bit_cast(U2, h);
+    };
     // compile-time pair index (a runtime loop here, which hipcc leaves for the long DGELU / AUX bodies,
     // indexes the accumulators dynamically and demotes them to scratch)
     static_for<32>([&](auto ir) {
-        constexpr int i = decltype(ir)::value >> 3, r = 2 * (decltype(ir)::value & 7);
-        float vv[8];
+      constexpr int P = decltype(ir)::value;
+      constexpr int i = P >> 3, r = 2 * (P & 7);
+      constexpr int pr = 32 * i + 8 * (r >> 2) + (r & 3);
+      float v[8];
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) {
-          vv[jb] = acc[i][jb][r];
-          vv[4 + jb] = acc[i][jb][r + 1];
+      for (int jb = 0; jb < 4; ++jb) {  // copy-out at the point of use (hipcc otherwise hoists all 256)
+        asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[jb]) : "a"(acc[i][jb][r]));
+        asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[4 + jb]) : "a"(acc[i][jb][r + 1]));
+      }
+      const uint32_t oC = lbC + (uint32_t)(pr * rstepC);
+      if (EPI == RF_EPI_COS) {
+        const float s0 = cb[256 + rowl + pr] * e.col_scale, s1 = cb[256 + rowl + pr + 1] * e.col_scale;
+        const U4 w0 = __builtin_bit_cast(U4, f32x4{v[0] * s0 * bv[0], v[1] * s0 * bv[1], v[2] * s0 * bv[2], v[3] * s0 * bv[3]});
+        const U4 w1 = __builtin_bit_cast(U4, f32x4{v[4] * s1 * bv[0], v[5] * s1 * bv[1], v[6] * s1 * bv[2], v[7] * s1 * bv[3]});
+        __builtin_amdgcn_raw_buffer_store_b128(w0, rsC, oC, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(w1, rsC, oC + rstepC, 0, 2);
+      } else {
+        if (EPI == RF_EPI_DGELU) {
+          const U2 z0 = zr[P % ZD][0], z1 = zr[P % ZD][1];
+          if (P + ZD < 32) zload(P + ZD, zr[P % ZD]);
+          const typename H16<E>::x4 h0 = __builtin_bit_cast(typename H16<E>::x4, z0);
+          const typename H16<E>::x4 h1 = __builtin_bit_cast(typename H16<E>::x4, z1);
+          float zf[8], d[8];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            zf[k] = (float)h0[k];
+            zf[4 + k] = (float)h1[k];
+          }
+          dgelu8_erf(zf, d);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] *= d[k];
+        } else if (EPI != RF_EPI_NONE) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], csc, bv[k & 3]);
+        } else if (!CF32) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] *= csc;
         }
-        const int row = erow + 32 * i + 8 * (r >> 2) + (r & 3);
-        if (interior) {
-          const float rs0 = EPI == RF_EPI_COS ? cb[256 + row - m0] : 0.f;
-          const float rs1 = EPI == RF_EPI_COS ? cb[256 + row + 1 - m0] : 0.f;
-          w32_epi_pair<E, EPI, CF32>(e, row, ecol, vv, bv, csc, rs0, rs1, tbase, m0);
+        if (EPI == RF_EPI_BIAS_GELU_AUX) {
+          const uint32_t oR = lbR + (uint32_t)(pr * rstepR);
+          __builtin_amdgcn_raw_buffer_store_b64(pack4(v), rsR, oR, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(pack4(v + 4), rsR, oR + rstepR, 0, 0);
+        }
+        if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
+          f32x2 y[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) y[k] = (f32x2){v[2 * k], v[2 * k + 1]};
+          gelu8_bf16out(y);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[2 * k] = y[k].x;
+            v[2 * k + 1] = y[k].y;
+          }
+        }
+        if (CF32) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, f32x4{v[0], v[1], v[2], v[3]}), rsC, oC, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, f32x4{v[4], v[5], v[6], v[7]}), rsC,
+                                                 oC + rstepC, 0, 2);
         } else {
-          float bvu[4], gu[4], tu[4];  // the unscaled bias: the generic path applies col_scale itself
-          load_cols<EPI, 4>(e, ecol, bvu, gu, tu);
-          epi_seg<E, EPI, CF32, false, 4, true>(e, row, ecol, vv, bvu, gu, tu, 0.f);
-          epi_seg<E, EPI, CF32, false, 4, true>(e, row + 1, ecol, vv + 4, bvu, gu, tu, 0.f);
+          __builtin_amdgcn_raw_buffer_store_b64(pack4(v), rsC, oC, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b64(pack4(v + 4), rsC, oC + rstepC, 0, 2);
         }
-        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     });
     asm volatile("" ::: "memory");
     if (has_next) dma_cols(nm0, nn0, (tix + 1) & 1);
@@ -1777,7 +1792,7 @@ __global__ void __launch_bounds__(256, 1)
     vAO = vAOn;
     vWE = vWEn;
     vWO = vWOn;
-    relax = interior ? S : 0;
+    relax = S;  // every tile issues its S stores (out-of-range ones are dropped, not skipped)
   }
   wait_vmcnt<0>();
 }
@@ -2105,7 +2120,10 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
     }
 #endif
     if constexpr (!RF32 && EPI != RF_EPI_BIAS_RESID && EPI != RF_EPI_BIAS_RESID_LN) {
-      if (w4_ok && g_knob[KNOB_GEMM_MFMA32] && N % 8 == 0) {
+      const int64_t cb = (CF32 || EPI == RF_EPI_COS) ? 4 : 2;
+      const bool w32_ok = N % 8 == 0 && (int64_t)256 * e.ldc * cb < 0x7FFFFFFF &&
+                          (int64_t)256 * (e.ldr > 0 ? e.ldr : 0) * 2 < 0x7FFFFFFF;
+      if (w4_ok && w32_ok && g_knob[KNOB_GEMM_MFMA32]) {
         launch_w32<E, EPI, CF32>(M, N, K, A, lda, W, ldw, e, s);
         return;
       }

@@ -36,6 +36,7 @@ Gradients are written (not accumulated) by each replay; the graph owns them.
 """
 from __future__ import annotations
 
+import dataclasses
 from typing import Callable, Dict, Optional
 
 import torch
@@ -125,15 +126,33 @@ def mlm_rows(batch: Dict[str, torch.Tensor]) -> int:
 
 
 def _default_loss(model, batch):
-    out = model(**batch)
-    return out if torch.is_tensor(out) else out.loss
+    return model(**batch)
+
+
+def _split_output(out):
+    """(loss, the model output object or None): loss_fn may return the loss or an output with .loss."""
+    return (out, None) if torch.is_tensor(out) else (out.loss, out)
+
+
+def _detached(obj):
+    """A copy of a model output whose tensor fields are detached: keeping the output object itself
+    would keep its autograd graph (and that graph's AccumulateGrad nodes, bound to the stream that
+    created them) alive into the next capture."""
+    if obj is None:
+        return None
+    if dataclasses.is_dataclass(obj):
+        return dataclasses.replace(obj, **{f.name: getattr(obj, f.name).detach() for f in dataclasses.fields(obj)
+                                           if torch.is_tensor(getattr(obj, f.name))})
+    return None
 
 
 class CapturedTrainStep:
     """step = CapturedTrainStep(model, optimizer, example_batch); loss = step(batch)
 
     optimizer: recformer_amd.optim.AdamW(..., capturable=True). loss_fn(model, batch) -> scalar
-    loss (default: model(**batch), or its .loss). autocast_dtype: the autocast dtype of the step
+    loss or an output with .loss (default: model(**batch)); `output` keeps the captured last
+    micro-batch's output object (e.g. RecformerForPretraining's cl_correct_num, a device tensor each
+    replay overwrites). autocast_dtype: the autocast dtype of the step
     (None: fp32). warmup eager optimizer steps run on a side stream first (they are real training
     steps, with the same scaler / accumulation / clipping as the captured ones).
 
@@ -182,16 +201,18 @@ class CapturedTrainStep:
         self.mlm_cap = ((int(n * mlm_slack) + 63) // 64) * 64 if n else None
         self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
         self.found_inf = None
+        self.output = None
         self._pos = 0  # micro-batches run in the current accumulation window
         lib = _lib.load()
 
         def micro(last: bool):
             """One micro-batch: forward, (scaled) backward; the last of a window also steps."""
             if self.dtype is None:
-                loss = self.loss_fn(self.model, self.static)
+                loss, obj = _split_output(self.loss_fn(self.model, self.static))
             else:
                 with torch.autocast("cuda", dtype=self.dtype, cache_enabled=False):
-                    loss = self.loss_fn(self.model, self.static)
+                    loss, obj = _split_output(self.loss_fn(self.model, self.static))
+            self.output = _detached(obj)  # the captured output (e.g. cl_correct_num): changes per replay
             out = loss / self.k if self.k > 1 else loss
             if self.scaler is not None:
                 out = self.scaler.scale(out)

@@ -2,6 +2,10 @@
 alternates blocks of steps between two settings of a models.py switch.
 
     python tools/ab_step.py [SWITCH] [B]      (default SWITCH=SPLIT_STREAM)
+
+SWITCH = knob:NAME alternates the library knob NAME between 1 and 0 (recformer_amd._lib.set_knob),
+e.g. knob:gemm_mfma32. AB_AUTOCAST=1: fp32 parameters under torch.autocast(bf16), bench.py's mode
+(default: bf16 weights).
 """
 import os
 import sys
@@ -10,7 +14,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from recformer_amd import RecformerConfig, RecformerForSeqRec, models  # noqa: E402
+from recformer_amd import RecformerConfig, RecformerForSeqRec, _lib, models  # noqa: E402
 from recformer_amd.synth import BASE, synth_batch  # noqa: E402
 
 
@@ -22,14 +26,21 @@ def main():
     torch.manual_seed(0)
     m = RecformerForSeqRec(cfg).eval()
     m.init_item_embedding(torch.randn(10000, cfg.hidden_size) * 0.5)
-    m = m.to(dev).to(torch.bfloat16)
+    autocast = os.environ.get("AB_AUTOCAST") == "1"
+    m = m.to(dev) if autocast else m.to(dev).to(torch.bfloat16)
+
+    def setv(val):
+        if switch.startswith("knob:"):
+            _lib.set_knob(switch[5:], 1 if val else 0)
+        else:
+            setattr(models, switch, val)
     batch = {k: v.to(dev) for k, v in synth_batch(B, 1024, cfg.vocab_size, seed=100, item_len=21).items()}
     res = {False: [], True: []}
     outs = {}
-    with torch.no_grad():
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
         for rep in range(6):
             for val in (True, False):
-                setattr(models, switch, val)
+                setv(val)
                 for _ in range(2):
                     outs[val] = m(**batch)
                 torch.cuda.synchronize()

@@ -1,0 +1,82 @@
+#!/bin/bash
+# One parametrised GPU driver (replaces the per-round one-off launchers).
+#   bash tools/gpu/run.sh <mode> [tag]      (inside gpurun; outputs under gpurun_out/<tag>/)
+# modes:
+#   suite      the whole -m gpu suite, then smoke() (the round-end gates)
+#   tests      pytest on $TESTS (default: the whole -m gpu suite), then a short bench line
+#   bench      the default bench.py line (N=1)
+#   profile    tools/profile_bench.sh: rocprofv3 kernel trace + FETCH / WRITE / MFMA-busy passes, then
+#              the default bench line from the same build
+#   gemm       GEMM shape timings, the four-wave kernels 16x16x32 vs 32x32x16 (knob gemm_mfma32),
+#              alternated twice (tools/gemm_var.py)
+#   lines      C3 (captured bf16 / fp16+GradScaler+accumulation+clip, eager), C4 (captured, 4 and 32 per
+#              rank) and C5 (retrieval, catalog encode) lines plus the retrieval kernel trace
+#   trainprof  rocprofv3 kernel trace of the captured C3 step ($TRAIN_ARGS)
+#   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3
+set -o pipefail
+MODE=${1:?mode}
+TAG=${2:-$MODE}
+O=gpurun_out/$TAG
+mkdir -p $O
+fail() { tail -${2:-30} "$1"; exit 1; }
+case $MODE in
+  suite)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ${SUITE_ARGS:-} \
+      > $O/pytest.log 2>&1 || { grep -E "^E  |FAILED" $O/pytest.log | cut -c1-300 | head -20; fail $O/pytest.log 5; }
+    tail -2 $O/pytest.log
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 \
+      || fail $O/smoke.log 5
+    tail -1 $O/smoke.log ;;
+  tests)
+    timeout -k 10 900 python -u -m pytest ${TESTS:-tests -m gpu} -x -v --timeout 300 --timeout-method thread \
+      > $O/pytest.log 2>&1 || { grep -E "^E  |FAILED" $O/pytest.log | cut -c1-300 | head -30; fail $O/pytest.log 5; }
+    grep -E "passed|failed" $O/pytest.log | tail -1
+    timeout -k 10 300 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 > $O/bench.log 2>&1 \
+      || fail $O/bench.log 20
+    tail -1 $O/bench.log | cut -c1-300 ;;
+  bench)
+    timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > $O/bench.log 2>&1 || fail $O/bench.log 20
+    tail -1 $O/bench.log | cut -c1-600 ;;
+  profile)
+    bash tools/profile_bench.sh $TAG > $O/profile.log 2>&1 || fail $O/profile.log
+    cat gpurun_out/prof_$TAG/summary.txt
+    timeout -k 10 400 python bench.py > $O/bench.log 2>&1 || fail $O/bench.log 20
+    tail -1 $O/bench.log | cut -c1-600 ;;
+  gemm)
+    for rep in 1 2; do
+      for k in gemm_mfma32=0 gemm_mfma32=1; do
+        RF_KNOBS=$k timeout -k 10 200 python3 tools/gemm_var.py >> $O/gemm.log 2>&1 || fail $O/gemm.log
+      done
+    done
+    cat $O/gemm.log ;;
+  ab32)
+    # the 32x32x16 four-wave GEMM vs the 16x16x32 one: C2 forward steps and captured C3 steps, each A/B
+    # alternated in one process (knob gemm_mfma32)
+    AB_AUTOCAST=1 timeout -k 10 400 python tools/ab_step.py knob:gemm_mfma32 64 > $O/ab_c2.log 2>&1 || fail $O/ab_c2.log
+    cat $O/ab_c2.log
+    timeout -k 10 500 python tools/train_bench.py --graph --steps 8 --warmup 2 --ab-knob gemm_mfma32 > $O/ab_c3.log 2>&1 \
+      || fail $O/ab_c3.log
+    tail -2 $O/ab_c3.log ;;
+  lines)
+    for args in "--graph" "--graph --dtype fp16 --accum 2 --clip 1.0" "--graph --negatives 1000" ""; do
+      timeout -k 10 300 python tools/train_bench.py --steps 8 --warmup 2 $args > $O/c3.log 2>&1 || fail $O/c3.log 20
+      tail -1 $O/c3.log | tee -a $O/c3_lines.jsonl
+    done
+    for b in 4 32; do
+      timeout -k 10 300 python tools/pretrain_bench.py --batch $b --steps 6 --warmup 2 --graph > $O/c4.log 2>&1 \
+        || fail $O/c4.log 20
+      tail -1 $O/c4.log | tee -a $O/c4_lines.jsonl
+    done
+    timeout -k 10 300 python tools/retrieval_bench.py > $O/retrieval.log 2>&1 || fail $O/retrieval.log 20
+    tail -4 $O/retrieval.log
+    cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/retrieval_trace -o r -- \
+      python3 tools/retrieval_bench.py > $O/retrieval_trace.log 2>&1 || fail $O/retrieval_trace.log 20
+    timeout -k 10 600 python tools/catalog_bench.py > $O/catalog.log 2>&1 || fail $O/catalog.log 20
+    tail -2 $O/catalog.log ;;
+  trainprof)
+    TRAIN_OUT=$TAG/trace TRAIN_ARGS=${TRAIN_ARGS:---graph} bash tools/gpu/trainprof.sh > $O/trainprof.txt 2>&1 \
+      || fail $O/trainprof.txt 20
+    head -30 $O/trainprof.txt ;;
+  *) echo "unknown mode $MODE"; exit 2 ;;
+esac

@@ -41,7 +41,8 @@ def main():
     ap.add_argument("--len-b", type=int, default=128)
     ap.add_argument("--no-share-casts", action="store_true", help="A/B: per-pass weight casts")
     ap.add_argument("--autograd-global-bwd", action="store_true", help="A/B: global rows' backward by autograd")
-    ap.add_argument("--graph", action="store_true", help="replay the step as one captured HIP graph (world 1)")
+    ap.add_argument("--graph", action="store_true", help="replay the step as one captured HIP graph (any world "
+                    "size: the bucketed all-reduce is captured with the backward)")
     ap.add_argument("--torch-adamw", action="store_true", help="A/B: torch.optim.AdamW instead of the HIP AdamW")
     ap.add_argument("--full-lm-head", action="store_true", help="A/B: LM head over every token")
     a = ap.parse_args()
@@ -87,17 +88,18 @@ def main():
         return out
 
     if a.graph:
-        if world > 1:
-            raise SystemExit("--graph: world 1 only (the bucketed all-reduce is not captured)")
+        # the bucketed RCCL all-reduces run inside the graph (launched from the backward hooks during
+        # capture, recorded with the backward they overlap); cl_correct_num from the captured output
         from recformer_amd.graphs import CapturedTrainStep
-        captured = CapturedTrainStep(model, opt, batch, warmup=a.warmup)
+        captured = CapturedTrainStep(model, opt, batch, warmup=a.warmup, bucketer=bucketer)
 
         class _Out:
-            cl_correct_num = -1
+            pass
 
         def step():  # noqa: F811 - the captured replay replaces the eager step
             o = _Out()
             o.loss = captured()
+            o.cl_correct_num = captured.output.cl_correct_num
             return o
     for _ in range(a.warmup):
         step()

@@ -43,6 +43,10 @@ def main():
     ap.add_argument("--ab-knob", default=None, help="A/B in one process: a library knob "
                     "(recformer_amd._lib.set_knob) at 1 / 0, or name=a,b for values a / b")
     ap.add_argument("--global-dh-f32", action="store_true", help="A/B: the global branch's dh as an fp32 product")
+    ap.add_argument("--accum", type=int, default=1, help="micro-batches per optimizer step (finetune.py "
+                    "gradient_accumulation_steps: loss / k, one optimizer step per k); a timed step = k micro-batches")
+    ap.add_argument("--clip", type=float, default=None, help="clip_grad_norm_ before the step (Lightning "
+                    "gradient_clip_val=1.0, lightning_pretrain.py:140); with fp16, after scaler.unscale_")
     a = ap.parse_args()
     if a.global_dh_f32:
         from recformer_amd import train
@@ -77,28 +81,42 @@ def main():
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
     scaler = torch.amp.GradScaler("cuda") if a.dtype == "fp16" else None
 
-    def step():
-        with torch.autocast("cuda", dtype=dt):
-            loss = model(**batch, labels=labels)
-        if scaler is not None:  # finetune.py:106-116 (fp16 autocast + GradScaler)
-            scaler.scale(loss).backward()
+    def step():  # one optimizer step: a.accum micro-batches (finetune.py:98-126)
+        for _ in range(a.accum):
+            with torch.autocast("cuda", dtype=dt):
+                loss = model(**batch, labels=labels)
+            out = loss / a.accum if a.accum > 1 else loss
+            if scaler is not None:  # finetune.py:106-116 (fp16 autocast + GradScaler)
+                scaler.scale(out).backward()
+            else:
+                out.backward()
+        if scaler is not None:
+            if a.clip is not None:
+                scaler.unscale_(opt)
+                torch.nn.utils.clip_grad_norm_(params, a.clip, foreach=True)
             scaler.step(opt)
             scaler.update()
         else:
-            loss.backward()
+            if a.clip is not None:
+                torch.nn.utils.clip_grad_norm_(params, a.clip, foreach=True)
             opt.step()
         opt.zero_grad(set_to_none=True)
         return loss
 
-    if a.graph and a.ab:
-        # captured A/B: one graph per value of the train.py switch, replays alternated in one process
-        from recformer_amd import train
+    if a.graph and (a.ab or a.ab_knob):
+        # captured A/B: one graph per value of the train.py switch (or library knob: the kernel choice
+        # is fixed at capture), replays alternated in one process
+        from recformer_amd import _lib, train
         from recformer_amd.graphs import CapturedTrainStep
         graphs = {}
         for val in (True, False):
-            setattr(train, a.ab, val)
+            if a.ab:
+                setattr(train, a.ab, val)
+            else:
+                _lib.set_knob(a.ab_knob, 1 if val else 0)
             graphs[val] = CapturedTrainStep(model, opt, dict(batch, labels=labels), autocast_dtype=dt,
-                                            warmup=a.warmup)
+                                            warmup=a.warmup, scaler=scaler, accumulation_steps=a.accum,
+                                            max_grad_norm=a.clip)
         res = {True: [], False: []}
         for rep in range(6):
             for val in (True, False):
@@ -111,17 +129,20 @@ def main():
                 res[val].append((time.perf_counter() - t0) / a.steps * 1e3)
         for val in (True, False):
             v = sorted(res[val])
-            print(f"captured {a.ab}={val}: ms/step median {v[len(v) // 2]:.2f} min {v[0]:.2f} all "
+            print(f"captured {a.ab or a.ab_knob}={val}: ms/step median {v[len(v) // 2]:.2f} min {v[0]:.2f} all "
                   f"{[round(x, 2) for x in res[val]]}")
         return
     if a.graph:
-        if scaler is not None:
-            raise SystemExit("--graph: the bf16 step only (GradScaler's host-side inf check is not capturable)")
+        # fp16 + GradScaler, accumulation and clipping are captured too (device-side inf check / skip /
+        # scale update, recformer_amd.graphs.CapturedTrainStep)
         from recformer_amd.graphs import CapturedTrainStep
-        captured = CapturedTrainStep(model, opt, dict(batch, labels=labels), autocast_dtype=dt, warmup=a.warmup)
+        captured = CapturedTrainStep(model, opt, dict(batch, labels=labels), autocast_dtype=dt, warmup=a.warmup,
+                                     scaler=scaler, accumulation_steps=a.accum, max_grad_norm=a.clip)
 
-        def step():  # noqa: F811 - the captured replay replaces the eager step
-            return captured()
+        def step():  # noqa: F811 - the captured replays replace the eager step
+            for _ in range(a.accum):
+                loss = captured()
+            return loss
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -156,9 +177,13 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     print(json.dumps({"workload": f"C3 finetune step (fwd+bwd+AdamW), 12L/768d, L=1024, {a.dtype} autocast, "
-                                  f"attention dropout {a.attn_dropout}",
-                      "batch": a.batch, "negatives": a.negatives, "catalog": a.catalog,
-                      "ms_per_step": round(1e3 * el / a.steps, 2), "seq_per_s": round(a.batch * a.steps / el, 2),
+                                  f"attention dropout {a.attn_dropout}"
+                                  + (", GradScaler" if scaler is not None else "")
+                                  + (f", {a.accum} micro-batches per step" if a.accum > 1 else "")
+                                  + (f", clip {a.clip}" if a.clip is not None else ""),
+                      "batch": a.batch, "accum": a.accum, "negatives": a.negatives, "catalog": a.catalog,
+                      "ms_per_step": round(1e3 * el / a.steps, 2),
+                      "seq_per_s": round(a.batch * a.accum * a.steps / el, 2),
                       "loss": float(loss.detach()), "optimizer": type(opt).__module__ + ".AdamW", "graph": a.graph,
                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}))
 
