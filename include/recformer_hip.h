@@ -379,6 +379,10 @@ int rf_rank_accum(int M, int N, const float* scores, int64_t ld, const float* s_
  * writes the scores to dense (B x ncols, ldd); mode 1 appends the scores s >= tau[b] with their item
  * ids to the row's list cval / cidx[b * capr + j], j < rcnt[b] (rcnt zeroed by the caller; it exceeds
  * capr when the list or a tile's 32-entry stage overflowed); mode 2 writes only the partials.
+ * D % 64 == 0 (D >= 128) with the knob rank_w32 on: both entry points run the 32x32x16 four-wave
+ * kernels (items as the MFMA A operand; k_rank_w32 / k_label_score32, still bit-identical to each
+ * other); then mode 0 needs ldd >= ncols rounded up to 256, and a lane with more than 4 candidates in
+ * a tile overflows its rows (rcnt > capr) instead of a 32-entry stage.
  * rf_rank_reduce: gt / valid / sexp per row = the partials summed over ntiles tile columns in order.
  * rf_topk_dense: top-k (k <= 256) of each row of a dense (B, n <= 2048) block, value descending, ties
  * by lower id (ids from idx (B, n) or idx_base + column).

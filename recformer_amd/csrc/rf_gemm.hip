@@ -23,6 +23,7 @@
 #include <utility>
 
 #include "rf_common.h"
+#include "rf_w32.h"
 
 namespace rf {
 
@@ -1418,109 +1419,12 @@ static void launch_w4(int M, int N, int K, const void* A, int lda, const void* W
 }
 
 
-// ---- 4-wave 256x256 GEMM on v_mfma_f32_32x32x16: one wave per SIMD, 4 x 4 blocks of 32 x 32 -----
-// k_gemm_w4's structure (256 x 256 tile, 4 waves x 128 x 128 accumulators = 256 AGPRs, two 64-KiB
-// K-tile buffers, one barrier per K-tile, the next tile's first two K-tiles fetched across the tile
-// boundary) with the 32x32x16 MFMA instead of 16x16x32: the same 2,048 MFMA cycles and 32
-// ds_read_b128 per wave and K-tile, but 64 instead of 128 MFMA issues, each holding the SIMD's
-// vector issue for 8 of its 32 cycles instead of 8 of 16 (MI355X_MICROARCH.md cycle table) — 1,536
-// instead of 1,024 free issue cycles per K-tile for the LDS reads and the 16 LDS-DMA pieces.
-// K-tile = 4 k-steps of 16: phase A runs k-steps 0, 1 (32 MFMAs) while the fragments of k-steps 2, 3
-// are read; phase B runs 2, 3 while the next K-tile's 0, 1 are read and the K-tile after it is
-// DMA'd into the buffer just released (one MFMA, one DMA piece, one MFMA, one read per group).
-// LDS image: 128-B rows, 16-B chunk c of row R at slot c ^ ((R >> 1) & 7) — the 32-row operand
-// read (lane l: row l & 31, chunk 2s + (l >> 5)) hits 16 distinct bank quads in each of
-// ds_read_b128's four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...).
-// Output: lane l holds column l & 31 of each 32 x 32 block and rows 8(r>>2) + 4(l>>5) + (r&3); the
-// W rows are permuted so lane c owns output columns 4c .. 4c+3 of the wave's 128 (LDS row
-// 32 jb + c holds W row 4c + jb): every store instruction writes two whole 256-B row segments.
-template <int N, typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
-}
-__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
-
+// ---- k_gemm_w32: the encoder GEMMs on w32_run (rf_w32.h) ----------------------------------------
 template <typename E, int EPI, bool CF32>
-__global__ void __launch_bounds__(256, 1)
-    k_gemm_w32(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e,
-               int nTm, int nTn) {
-  typedef typename H16<E>::x8 V8;
-  constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;
-  constexpr int S = 64;  // epilogue stores per wave (interior tile)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tiles = nTm * nTn;
-  int v = blockIdx.x;
-  if (v >= tiles) return;
-  const int GN = e.gn > 0 ? min(e.gn, nTn) : nTn;
-  auto tile_origin = [&](int vv, int& om0, int& on0) {
-    const int wg = xcd_remap(vv, tiles);
-    const int g = wg / (nTm * GN);
-    const int gw = min(GN, nTn - g * GN);
-    const int rem = wg - g * nTm * GN;
-    const int tm = rem / gw;
-    om0 = tm * 256;
-    on0 = (g * GN + rem - tm * gw) * 256;
-  };
-  int m0, n0, nm0 = 0, nn0 = 0;
-  tile_origin(v, m0, n0);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 1, wc = wave & 1;  // A half (rows 128 wr..) and W half (columns 128 wc..)
-  const int nk = K >> 6;
-  // Operand DMA (buffer_load ... lds, rows past M / N read as zeros): wave w stages LDS rows
-  // [64(w&1), +64) of A-half w>>1 and W-half w>>1 as 8 pieces pp of 8 rows; lane: LDS row
-  // 64(w&1) + 8pp + (l>>3), slot l&7, so it fetches chunk (l&7) ^ ((row>>1)&7) = (l&7) ^ (4(pp&1) + (l>>4)):
-  // two per-lane source offsets (even / odd pieces). W: LDS row rho holds W row 4(rho&31) + (rho>>5),
-  // i.e. per lane 4(l>>3) + 2(w&1) and per piece 32(pp&3) + (pp>>2) rows.
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)min((int64_t)e.M * lda * 2, (int64_t)0x7FFFFFFF), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsW =
-      __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)min((int64_t)e.N * ldw * 2, (int64_t)0x7FFFFFFF), 0x00020000);
-  const int half = wave >> 1;
-  const int pchE = ((lane & 7) ^ (lane >> 4)) * 8;
-  const int pchO = ((lane & 7) ^ (4 + (lane >> 4))) * 8;
-  const int arow_l = half * 128 + (wave & 1) * 64 + (lane >> 3);
-  const int wrow_l = half * 128 + 4 * (lane >> 3) + 2 * (wave & 1);
-  auto voffA = [&](int bm0, int pch) { return ((bm0 + arow_l) * lda + pch) * 2; };
-  auto voffW = [&](int bn0, int pch) { return ((bn0 + wrow_l) * ldw + pch) * 2; };
-  int vAE = voffA(m0, pchE), vAO = voffA(m0, pchO), vWE = voffW(n0, pchE), vWO = voffW(n0, pchO);
-  int vAEn = vAE, vAOn = vAO, vWEn = vWE, vWOn = vWO;
-  auto launder = [&]() {
-    asm volatile("" : "+v"(vAE), "+v"(vAO), "+v"(vWE), "+v"(vWO));
-    asm volatile("" : "+v"(vAEn), "+v"(vAOn), "+v"(vWEn), "+v"(vWOn));
-  };
-  // soffset chains: A +8 rows per piece; W pieces pp = 0..7 at rows +0, 32, 64, 96, 1, 33, 65, 97
-  const int stA = 8 * lda * 2, stW = 32 * ldw * 2, stWj = -95 * ldw * 2;
-  int sA = 0, sW = 0;
-  auto dma_piece = [&](int kv, int buf, int p) {
-    const bool nxt = kv >= nk;
-    const int kt = nxt ? kv - nk : kv;
-    const bool isA = p < 8;
-    const int pp = p & 7;
-    char* dst = smem + buf * W4_BUF + (isA ? half : 2 + half) * PP_HALF + ((wave & 1) * 64 + 8 * pp) * 128;
-    if (p == 0) { sA = kt * 128; asm volatile("" : "+s"(sA)); }
-    if (p == 8) { sW = kt * 128; asm volatile("" : "+s"(sW)); }
-    const int soff = isA ? sA : sW;
-    {
-      int st = isA ? stA : (pp == 3 ? stWj : stW);
-      asm volatile("" : "+s"(st));  // no hoisting of per-piece products out of the K-loop
-      if (isA) sA += st; else sW += st;
-    }
-    const int vo = isA ? ((pp & 1) ? (nxt ? vAOn : vAO) : (nxt ? vAEn : vAE))
-                       : ((pp & 1) ? (nxt ? vWOn : vWO) : (nxt ? vWEn : vWE));
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsW, (__attribute__((address_space(3))) void*)dst, 16, vo,
-                                             soff, 0, 0);
-  };
-  auto dma_cols = [&](int tm0, int tn0, int par) {
+struct W32GemmPol {
+  static constexpr int S = 64;  // 64 stores per wave (the DGELU / AUX extras only make the wait stricter)
+  EpiArgs e;
+  __device__ __forceinline__ void cols(char* slot, int wave, int lane, int tm0, int tn0) const {
     if (EPI == RF_EPI_NONE || EPI == RF_EPI_DGELU) return;
     const int vec = wave % 3;
     const float* src = EPI == RF_EPI_COS ? e.rw : e.bias;
@@ -1530,271 +1434,146 @@ __global__ void __launch_bounds__(256, 1)
       idx = min(tm0 + 4 * lane, e.M - 4);
     }
     if (EPI != RF_EPI_COS && vec != 0) return;
-    glds16(src + idx, smem + W4_CV + (par * 3 + vec) * 1024);
-  };
-  // fragment reads: k-step s of 32-row block f at LDS row 32f + (l&31), chunk 2s + (l>>5)
-  int offS[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    offS[s] = (lane & 31) * 128 + (((2 * s + (lane >> 5)) ^ ((lane >> 1) & 7)) << 4);
+    glds16(src + idx, slot + vec * 1024);
   }
-  const int aOff = wr * PP_HALF, bOff = (2 + wc) * PP_HALF;
-  V8 xa[2][4], xb[2][4], ya[2][4], yb[2][4];
-  f32x16 acc[4][4];
-  // set X = k-steps 0, 1; set Y = k-steps 2, 3; idx 0-3 A blocks, 4-7 W blocks; s = 0, 1 within the set
-  auto readX = [&](int buf, int s, int idx) {
-    const char* base = smem + buf * W4_BUF + (idx < 4 ? aOff : bOff) + (idx & 3) * 32 * 128 + offS[s];
-    if (idx < 4) xa[s][idx] = *reinterpret_cast<const V8*>(base);
-    else xb[s][idx - 4] = *reinterpret_cast<const V8*>(base);
-  };
-  auto readY = [&](int buf, int s, int idx) {
-    const char* base = smem + buf * W4_BUF + (idx < 4 ? aOff : bOff) + (idx & 3) * 32 * 128 + offS[2 + s];
-    if (idx < 4) ya[s][idx] = *reinterpret_cast<const V8*>(base);
-    else yb[s][idx - 4] = *reinterpret_cast<const V8*>(base);
-  };
-  auto bar = [&]() {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  const int pfd = e.pf & 0xff;
-  const int npf = pfd ? 1 + ((e.pf >> 8) & 1) : 0;
-  auto prefetch = [&](int kv) {
-    const bool nxt = kv >= nk;
-    const int kt = min(nxt ? kv - nk : kv, nk - 1);
-    const int prow = wave * 64 + lane;
-    auto* dst = (__attribute__((address_space(3))) void*)(smem + W4_PF + wave * 256);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 4, ((nxt ? nm0 : m0) + prow) * lda * 2, kt * 128, 0, 0);
-    if (npf == 2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, dst, 4, ((nxt ? nn0 : n0) + prow) * ldw * 2, kt * 128, 0, 0);
-  };
-
-  dma_cols(m0, n0, 0);
+  __device__ __forceinline__ void epilogue(f32x16 (&acc)[4][4], const W32Tile& t) const {
+    constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;
+  // epilogue: lane (c = l&31, g = l>>5): rows 32i + 8(r>>2) + 4g + (r&3), columns 4c .. 4c+3.
+  // One branch-free path for every tile: outputs (and the DGELU / AUX pre-activation rows) go
+  // through buffer resources based at the tile's first row with num_records = its valid rows, so
+  // rows past M are dropped / read as zeros by the range check, and a lane whose 4 columns lie past
+  // N (N % 8 == 0: a 4-column group is all in or all out) gets a base offset >= 2^31, past any
+  // num_records. Each row pair's 8 accumulators stream out under a sched_barrier (no copy-out of all
+  // 256 next to the next tile's fragments); the DGELU pre-activations are loaded ZD pairs ahead.
+  const int m0 = t.m0, n0 = t.n0, wr = t.wr, wc = t.wc;
+  const float* cb = t.cb;
+  int el = t.lane;
+  asm volatile("" : "+v"(el));
+  const int rowl = wr * 128 + 4 * (el >> 5);   // tile-relative row (+ 32i + 8(r>>2) + (r&3))
+  const int coll = wc * 128 + 4 * (el & 31);   // tile-relative column
+  const int ecol = n0 + coll;
+  const bool col_ok = ecol < e.N;
+  const int rows_valid = min(256, e.M - m0);
+  constexpr int CB = OUT32 ? 4 : (int)sizeof(E);
+  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<char*>(e.C) + (int64_t)m0 * e.ldc * CB, (short)0, rows_valid * e.ldc * CB, 0x00020000);
+  const uint32_t lbC = col_ok ? (uint32_t)((rowl * e.ldc + coll) * CB) : 0x80000000u;
+  const int rstepC = e.ldc * CB;
+  constexpr bool HAS_R = EPI == RF_EPI_DGELU || EPI == RF_EPI_BIAS_GELU_AUX;
+  __amdgpu_buffer_rsrc_t rsR = rsC;
+  uint32_t lbR = 0;
+  int rstepR = 0;
+  if (HAS_R) {
+    rsR = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(reinterpret_cast<const char*>(e.R)) + (int64_t)m0 * e.ldr * (int)sizeof(E), (short)0,
+        rows_valid * e.ldr * (int)sizeof(E), 0x00020000);
+    lbR = col_ok ? (uint32_t)((rowl * e.ldr + coll) * (int)sizeof(E)) : 0x80000000u;
+    rstepR = e.ldr * (int)sizeof(E);
+  }
+  float bv[4], gm[4], bt[4];
+  lds_cols<EPI, 4>(cb, coll, bv, gm, bt);
+  float csc = 1.f;
+  if (!OUT32) {
+    csc = ecol < e.scale_cols ? e.col_scale : 1.f;
 #pragma unroll
-  for (int p = 0; p < 16; ++p) dma_piece(0, 0, p);
+    for (int k = 0; k < 4; ++k) bv[k] *= csc;
+  }
+  typedef __attribute__((ext_vector_type(2))) unsigned int U2;
+  typedef __attribute__((ext_vector_type(4))) unsigned int U4;
+  constexpr int ZD = 8;  // DGELU pre-activation prefetch distance (row pairs)
+  U2 zr[ZD][2];
+  auto prow = [](int P) { return 32 * (P >> 3) + 8 * ((2 * (P & 7)) >> 2) + ((2 * (P & 7)) & 3); };
+  auto zload = [&](int P, U2 (&dst)[2]) {
+    const uint32_t o = lbR + (uint32_t)(prow(P) * rstepR);
+    dst[0] = __builtin_amdgcn_raw_buffer_load_b64(rsR, o, 0, 0);
+    dst[1] = __builtin_amdgcn_raw_buffer_load_b64(rsR, o + rstepR, 0, 0);
+  };
+  if (EPI == RF_EPI_DGELU) {
 #pragma unroll
-  for (int p = 0; p < 16; ++p) dma_piece(1, 1, p);
-  wait_vmcnt<16>();
-  bar();
+    for (int P = 0; P < ZD; ++P) zload(P, zr[P]);
+  }
+  auto pack4 = [](const float* x) {
+    typename H16<E>::x4 h;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) readX(0, i >> 3, i & 7);
-  int kb = 0, tix = 0, relax = 0;
-  for (;;) {
-    const bool has_next = v + (int)gridDim.x < tiles;
-    if (has_next) {
-      tile_origin(v + gridDim.x, nm0, nn0);
+    for (int k = 0; k < 4; ++k) h[k] = (E)x[k];
+    return __builtin_bit_cast(U2, h);
+  };
+  // compile-time pair index (a runtime loop here, which hipcc leaves for the long DGELU / AUX bodies,
+  // indexes the accumulators dynamically and demotes them to scratch)
+  static_for<32>([&](auto ir) {
+    constexpr int P = decltype(ir)::value;
+    constexpr int i = P >> 3, r = 2 * (P & 7);
+    constexpr int pr = 32 * i + 8 * (r >> 2) + (r & 3);
+    float v[8];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {  // copy-out at the point of use (hipcc otherwise hoists all 256)
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[jb]) : "a"(acc[i][jb][r]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[4 + jb]) : "a"(acc[i][jb][r + 1]));
+    }
+    const uint32_t oC = lbC + (uint32_t)(pr * rstepC);
+    if (EPI == RF_EPI_COS) {
+      const float s0 = cb[256 + rowl + pr] * e.col_scale, s1 = cb[256 + rowl + pr + 1] * e.col_scale;
+      const U4 w0 = __builtin_bit_cast(U4, f32x4{v[0] * s0 * bv[0], v[1] * s0 * bv[1], v[2] * s0 * bv[2], v[3] * s0 * bv[3]});
+      const U4 w1 = __builtin_bit_cast(U4, f32x4{v[4] * s1 * bv[0], v[5] * s1 * bv[1], v[6] * s1 * bv[2], v[7] * s1 * bv[3]});
+      __builtin_amdgcn_raw_buffer_store_b128(w0, rsC, oC, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(w1, rsC, oC + rstepC, 0, 2);
     } else {
-      nm0 = m0;
-      nn0 = n0;
-    }
-    vAEn = voffA(nm0, pchE);
-    vAOn = voffA(nm0, pchO);
-    vWEn = voffW(nn0, pchE);
-    vWOn = voffW(nn0, pchO);
-    // ---- phase A: k-steps 0, 1 of K-tile t on MFMA; k-steps 2, 3 of K-tile t from LDS ----
-    auto phaseA = [&](auto zero) {
+      if (EPI == RF_EPI_DGELU) {
+        const U2 z0 = zr[P % ZD][0], z1 = zr[P % ZD][1];
+        if (P + ZD < 32) zload(P + ZD, zr[P % ZD]);
+        const typename H16<E>::x4 h0 = __builtin_bit_cast(typename H16<E>::x4, z0);
+        const typename H16<E>::x4 h1 = __builtin_bit_cast(typename H16<E>::x4, z1);
+        float zf[8], d[8];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) readY(kb, i >> 3, ((i & 7) + 4) & 7);  // W blocks first
+        for (int k = 0; k < 4; ++k) {
+          zf[k] = (float)h0[k];
+          zf[4 + k] = (float)h1[k];
+        }
+        dgelu8_erf(zf, d);
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+        for (int k = 0; k < 8; ++k) v[k] *= d[k];
+      } else if (EPI != RF_EPI_NONE) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], csc, bv[k & 3]);
+      } else if (!CF32) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = mfma32(xa[s][i], xb[s][j], (decltype(zero)::value && s == 0) ? f32x16{} : acc[i][j]);
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        for (int k = 0; k < 8; ++k) v[k] *= csc;
       }
-    };
-    auto midsync = [&](int t) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (t == 0 && relax) wait_vmcnt<(S < 63 ? S : 63)>();
-      else if (t > 0 && npf == 1) wait_vmcnt<1>();
-      else if (t > 0 && npf == 2) wait_vmcnt<2>();
-      else wait_vmcnt<0>();
-      bar();
-    };
-    // ---- phase B: k-steps 2, 3 on MFMA; K-tile t+1's k-steps 0, 1 from LDS; DMA of K-tile t+2 ----
-    auto phaseB = [&](int t) {
-#pragma unroll
-      for (int p = 0; p < 16; ++p) {
-        dma_piece(t + 2, kb, p);
-        readX(kb ^ 1, p >> 3, ((p & 7) + 4) & 7);
+      if (EPI == RF_EPI_BIAS_GELU_AUX) {
+        const uint32_t oR = lbR + (uint32_t)(pr * rstepR);
+        __builtin_amdgcn_raw_buffer_store_b64(pack4(v), rsR, oR, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(pack4(v + 4), rsR, oR + rstepR, 0, 0);
       }
+      if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
+        f32x2 y[4];
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+        for (int k = 0; k < 4; ++k) y[k] = (f32x2){v[2 * k], v[2 * k + 1]};
+        gelu8_bf16out(y);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(ya[s][i], yb[s][j], acc[i][j]);
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 DMA piece
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] = y[k].x;
+          v[2 * k + 1] = y[k].y;
+        }
       }
-      if (npf && t + 1 < nk && t + 2 + pfd < 2 * nk) prefetch(t + 2 + pfd);
-      kb ^= 1;
-    };
-    launder();
-    phaseA(std::true_type{});
-    for (int t = 0; t + 1 < nk; ++t) {
-      midsync(t);
-      phaseB(t);
-      launder();
-      phaseA(std::false_type{});
-    }
-    midsync(nk - 1);
-    phaseB(nk - 1);
-    // no accumulator copy-out may move into the MFMA stream (it would hold 256 VGPRs next to the next
-    // tile's fragments); the epilogue streams 8 accumulators per row pair (sched_barrier per pair)
-    __builtin_amdgcn_sched_barrier(0);
-    // the accumulators are read below by inline asm, which the hazard recognizer does not see: 24 wait
-    // states cover the 32x32x16 MFMA's write -> VALU read distance (18) for the last MFMAs' blocks
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    // epilogue: lane (c = l&31, g = l>>5): rows 32i + 8(r>>2) + 4g + (r&3), columns 4c .. 4c+3.
-    // One branch-free path for every tile: outputs (and the DGELU / AUX pre-activation rows) go
-    // through buffer resources based at the tile's first row with num_records = its valid rows, so
-    // rows past M are dropped / read as zeros by the range check, and a lane whose 4 columns lie past
-    // N (N % 8 == 0: a 4-column group is all in or all out) gets a base offset >= 2^31, past any
-    // num_records. Each row pair's 8 accumulators stream out under a sched_barrier (no copy-out of all
-    // 256 next to the next tile's fragments); the DGELU pre-activations are loaded ZD pairs ahead.
-    int el = lane;
-    asm volatile("" : "+v"(el));
-    const int rowl = wr * 128 + 4 * (el >> 5);   // tile-relative row (+ 32i + 8(r>>2) + (r&3))
-    const int coll = wc * 128 + 4 * (el & 31);   // tile-relative column
-    const int ecol = n0 + coll;
-    const bool col_ok = ecol < e.N;
-    const int rows_valid = min(256, e.M - m0);
-    constexpr int CB = OUT32 ? 4 : (int)sizeof(E);
-    const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<char*>(e.C) + (int64_t)m0 * e.ldc * CB, (short)0, rows_valid * e.ldc * CB, 0x00020000);
-    const uint32_t lbC = col_ok ? (uint32_t)((rowl * e.ldc + coll) * CB) : 0x80000000u;
-    const int rstepC = e.ldc * CB;
-    constexpr bool HAS_R = EPI == RF_EPI_DGELU || EPI == RF_EPI_BIAS_GELU_AUX;
-    __amdgpu_buffer_rsrc_t rsR = rsC;
-    uint32_t lbR = 0;
-    int rstepR = 0;
-    if (HAS_R) {
-      rsR = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<char*>(reinterpret_cast<const char*>(e.R)) + (int64_t)m0 * e.ldr * (int)sizeof(E), (short)0,
-          rows_valid * e.ldr * (int)sizeof(E), 0x00020000);
-      lbR = col_ok ? (uint32_t)((rowl * e.ldr + coll) * (int)sizeof(E)) : 0x80000000u;
-      rstepR = e.ldr * (int)sizeof(E);
-    }
-    float bv[4], gm[4], bt[4];
-    const float* cb = reinterpret_cast<const float*>(smem + W4_CV + (tix & 1) * 3 * 1024);
-    lds_cols<EPI, 4>(cb, coll, bv, gm, bt);
-    float csc = 1.f;
-    if (!OUT32) {
-      csc = ecol < e.scale_cols ? e.col_scale : 1.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) bv[k] *= csc;
-    }
-    typedef __attribute__((ext_vector_type(2))) unsigned int U2;
-    typedef __attribute__((ext_vector_type(4))) unsigned int U4;
-    constexpr int ZD = 8;  // DGELU pre-activation prefetch distance (row pairs)
-    U2 zr[ZD][2];
-    auto prow = [](int P) { return 32 * (P >> 3) + 8 * ((2 * (P & 7)) >> 2) + ((2 * (P & 7)) & 3); };
-    auto zload = [&](int P, U2 (&dst)[2]) {
-      const uint32_t o = lbR + (uint32_t)(prow(P) * rstepR);
-      dst[0] = __builtin_amdgcn_raw_buffer_load_b64(rsR, o, 0, 0);
-      dst[1] = __builtin_amdgcn_raw_buffer_load_b64(rsR, o + rstepR, 0, 0);
-    };
-    if (EPI == RF_EPI_DGELU) {
-#pragma unroll
-      for (int P = 0; P < ZD; ++P) zload(P, zr[P]);
-    }
-    auto pack4 = [](const float* x) {
-      typename H16<E>::x4 h;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) h[k] = (E)x[k];
-      return __builtin_bit_cast(U2, h);
-    };
-    // compile-time pair index (a runtime loop here, which hipcc leaves for the long DGELU / AUX bodies,
-    // indexes the accumulators dynamically and demotes them to scratch)
-    static_for<32>([&](auto ir) {
-      constexpr int P = decltype(ir)::value;
-      constexpr int i = P >> 3, r = 2 * (P & 7);
-      constexpr int pr = 32 * i + 8 * (r >> 2) + (r & 3);
-      float v[8];
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb) {  // copy-out at the point of use (hipcc otherwise hoists all 256)
-        asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[jb]) : "a"(acc[i][jb][r]));
-        asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[4 + jb]) : "a"(acc[i][jb][r + 1]));
-      }
-      const uint32_t oC = lbC + (uint32_t)(pr * rstepC);
-      if (EPI == RF_EPI_COS) {
-        const float s0 = cb[256 + rowl + pr] * e.col_scale, s1 = cb[256 + rowl + pr + 1] * e.col_scale;
-        const U4 w0 = __builtin_bit_cast(U4, f32x4{v[0] * s0 * bv[0], v[1] * s0 * bv[1], v[2] * s0 * bv[2], v[3] * s0 * bv[3]});
-        const U4 w1 = __builtin_bit_cast(U4, f32x4{v[4] * s1 * bv[0], v[5] * s1 * bv[1], v[6] * s1 * bv[2], v[7] * s1 * bv[3]});
-        __builtin_amdgcn_raw_buffer_store_b128(w0, rsC, oC, 0, 2);
-        __builtin_amdgcn_raw_buffer_store_b128(w1, rsC, oC + rstepC, 0, 2);
+      if (CF32) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, f32x4{v[0], v[1], v[2], v[3]}), rsC, oC, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, f32x4{v[4], v[5], v[6], v[7]}), rsC,
+                                               oC + rstepC, 0, 2);
       } else {
-        if (EPI == RF_EPI_DGELU) {
-          const U2 z0 = zr[P % ZD][0], z1 = zr[P % ZD][1];
-          if (P + ZD < 32) zload(P + ZD, zr[P % ZD]);
-          const typename H16<E>::x4 h0 = __builtin_bit_cast(typename H16<E>::x4, z0);
-          const typename H16<E>::x4 h1 = __builtin_bit_cast(typename H16<E>::x4, z1);
-          float zf[8], d[8];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            zf[k] = (float)h0[k];
-            zf[4 + k] = (float)h1[k];
-          }
-          dgelu8_erf(zf, d);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] *= d[k];
-        } else if (EPI != RF_EPI_NONE) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], csc, bv[k & 3]);
-        } else if (!CF32) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] *= csc;
-        }
-        if (EPI == RF_EPI_BIAS_GELU_AUX) {
-          const uint32_t oR = lbR + (uint32_t)(pr * rstepR);
-          __builtin_amdgcn_raw_buffer_store_b64(pack4(v), rsR, oR, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(pack4(v + 4), rsR, oR + rstepR, 0, 0);
-        }
-        if (EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX) {
-          f32x2 y[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) y[k] = (f32x2){v[2 * k], v[2 * k + 1]};
-          gelu8_bf16out(y);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            v[2 * k] = y[k].x;
-            v[2 * k + 1] = y[k].y;
-          }
-        }
-        if (CF32) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, f32x4{v[0], v[1], v[2], v[3]}), rsC, oC, 0, 2);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, f32x4{v[4], v[5], v[6], v[7]}), rsC,
-                                                 oC + rstepC, 0, 2);
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b64(pack4(v), rsC, oC, 0, 2);
-          __builtin_amdgcn_raw_buffer_store_b64(pack4(v + 4), rsC, oC + rstepC, 0, 2);
-        }
+        __builtin_amdgcn_raw_buffer_store_b64(pack4(v), rsC, oC, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b64(pack4(v + 4), rsC, oC + rstepC, 0, 2);
       }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    asm volatile("" ::: "memory");
-    if (has_next) dma_cols(nm0, nn0, (tix + 1) & 1);
-    ++tix;
-    if (!has_next) break;
-    v += gridDim.x;
-    m0 = nm0;
-    n0 = nn0;
-    vAE = vAEn;
-    vAO = vAOn;
-    vWE = vWEn;
-    vWO = vWOn;
-    relax = S;  // every tile issues its S stores (out-of-range ones are dropped, not skipped)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  });
   }
-  wait_vmcnt<0>();
+};
+
+template <typename E, int EPI, bool CF32>
+__global__ void __launch_bounds__(256, 1)
+    k_gemm_w32(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e,
+               int nTm, int nTn) {
+  w32_run<E>(K, A, lda, W, ldw, e.M, e.N, e.gn, e.pf, nTm, nTn, W32GemmPol<E, EPI, CF32>{e});
 }
 
 template <typename E, int EPI, bool CF32>
@@ -1803,12 +1582,12 @@ static void launch_w32(int M, int N, int K, const void* A, int lda, const void* 
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)k_gemm_w32<E, EPI, CF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)W4_LDS);
+                              (int)W32_LDS);
     attr_set = true;
   }
   const int nTm = (M + 255) / 256, nTn = (N + 255) / 256;
   const int grid = min(nTm * nTn, num_cus());
-  k_gemm_w32<E, EPI, CF32><<<grid, 256, W4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
+  k_gemm_w32<E, EPI, CF32><<<grid, 256, W32_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
 }
 
 #if defined(RF_GEMM_EXPERIMENTS)  // retired main loop (tools/build_variant.sh builds only)

@@ -25,6 +25,10 @@
 //                   (the caller re-ranks those rows densely).
 // Element types: bf16 and fp16 operands (v_mfma_f32_16x16x32_bf16 / _f16), fp32 scores.
 #include "rf_common.h"
+#include "rf_w32.h"
+
+#include <algorithm>
+#include <cstddef>
 
 namespace rf {
 
@@ -43,6 +47,17 @@ template <> struct RtElt<f16> {
 };
 
 constexpr float RT_LOG2E = 1.4426950408889634f;
+
+static int num_cus_rt() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    n = c > 0 ? c : 256;
+  }
+  return n;
+}
 
 // the cosine score of one (query, item) pair from its fp32 dot product: one expression shared by
 // every kernel of this file (and by rf_gemm's EPI_COS epilogue)
@@ -324,6 +339,241 @@ __global__ void __launch_bounds__(512, 1) k_score_rank(int K, const T* __restric
   }
 }
 
+// ---- the same on the four-wave 32x32x16 main loop (rf_w32.h), catalog rows as the A operand ------
+// k_rank_w32: A = the shard's item rows [col0, col0 + ncols) (M), W = the queries (N), so a lane holds
+// 4 query columns x 64 item rows of every 256 x 256 tile: the per-query counts and exp-sums are
+// in-lane sums over items, one shuffle across the lane halves and one LDS exchange between the two
+// waves of a query half — no score matrix, no per-row cross-lane reductions. Candidates (MODE 1) go
+// straight to the query's global list with one atomic each (about k per row per column chunk), a
+// row whose list overflows is flagged by the merge as before; MODE 0 also stores the dense scores.
+// k_label_score32 computes the labels' own scores with the same MFMA (32x32x16, the same operand
+// roles, K ascending in 16-chunks, the chain starting from zero) and the same epilogue expression, so
+// the strict ranks compare bit-identical values. (The 16x16x32 kernels above are kept for D not a
+// multiple of 64 and as the knob-selected A/B path; label and rank kernels are always chosen by the
+// same predicate, rank_w32_ok.)
+struct RankW32Args {
+  int B, ncols, col0;
+  const float* rq;
+  const float* rc;
+  float scale, max_val, shift;
+  const float* s_label;
+  const float* tau;
+  float* dense;
+  int64_t ldd;
+  float* cval;
+  int32_t* cidx;
+  int32_t* rcnt;
+  int capr;
+  int32_t idx_base;
+  int32_t* part_cnt;
+  float* part_sexp;
+  int tn0;
+};
+
+// k_rank_w32's parameter list as a struct: the kernarg segment lays the arguments out this way
+constexpr int RK32_NS = 4;  // candidate slots per lane and tile (more: the lane's queries are re-ranked)
+
+struct RankKernArgs {
+  int K;
+  const void* items;
+  int ldi;
+  const void* Q;
+  int ldq, nTm, nTn;
+  RankW32Args a;
+};
+constexpr int RANK_KARG_OFF = (int)offsetof(RankKernArgs, a);
+
+template <int MODE>
+struct RankW32Pol {
+  static constexpr int S = 0;  // the epilogue's memory operations depend on the data: no relaxed wait
+  // the arguments stay in the kernarg segment and are re-read (scalar loads) in each epilogue through
+  // a laundered pointer: held in SGPRs across the K-loop they push the loop past the SGPR budget
+  // (spills into VGPR lanes)
+  typedef const __attribute__((address_space(4))) RankW32Args* KPtr;
+  __device__ __forceinline__ RankW32Args args() const {
+    // the kernel's `a` argument, read from the kernarg segment (its offset: RankKernArgs below)
+    KPtr p = (KPtr)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                    RANK_KARG_OFF);
+    asm volatile("" : "+s"(p));
+    RankW32Args r;  // field by field: scalar loads from the kernarg segment
+    r.B = p->B; r.ncols = p->ncols; r.col0 = p->col0;
+    r.rq = p->rq; r.rc = p->rc;
+    r.scale = p->scale; r.max_val = p->max_val; r.shift = p->shift;
+    r.s_label = p->s_label; r.tau = p->tau;
+    r.dense = p->dense; r.ldd = p->ldd;
+    r.cval = p->cval; r.cidx = p->cidx; r.rcnt = p->rcnt; r.capr = p->capr; r.idx_base = p->idx_base;
+    r.part_cnt = p->part_cnt; r.part_sexp = p->part_sexp; r.tn0 = p->tn0;
+    return r;
+  }
+  __device__ __forceinline__ void cols(char* slot, int wave, int lane, int tm0, int tn0) const {
+    const RankW32Args a = args();
+    // the tile's 256 item inverse norms, 4 B per lane (rows past ncols read as 0 by the range check)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.rc + a.col0), (short)0, a.ncols * 4, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + wave * 256), 4,
+                                             (tm0 + 64 * wave + lane) * 4, 0, 0, 0);
+  }
+  __device__ __forceinline__ void epilogue(f32x16 (&acc)[4][4], const W32Tile& t) const {
+    const RankW32Args a = args();
+    int el = t.lane;
+    asm volatile("" : "+v"(el));
+    const int c = el & 31, g = el >> 5;
+    const int q0 = t.n0 + t.wc * 128 + 4 * c;
+    float rs[4], sl[4], tau[4];
+    bool qok[4];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      qok[jb] = q0 + jb < a.B;
+      const int qq = min(q0 + jb, a.B - 1);
+      rs[jb] = a.rq[qq] * a.scale;
+      sl[jb] = a.s_label[qq];
+      tau[jb] = MODE == 1 ? a.tau[qq] : 0.f;
+    }
+    const int ib = t.wr * 128 + 4 * g;  // tile-relative item row of register 0 of block 0
+    int gt[4] = {0, 0, 0, 0}, vc[4] = {0, 0, 0, 0};
+    float se[4] = {0.f, 0.f, 0.f, 0.f};
+    // MODE 1: this lane's candidates, (score, jb << 8 | item row) in RK32_NS LDS slots (+ one trash slot)
+    float* cslot = reinterpret_cast<float*>(t.scr + 8192) + (t.wave * 64 + el) * 2 * (RK32_NS + 1);
+    int ncand = 0;
+    // MODE 0: dense scores through a buffer resource: a query past B is past num_records, an item past
+    // ncols gets an offset >= 2^31 (branch-free stores)
+    const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(MODE == 0 ? a.dense : nullptr), (short)0,
+        MODE == 0 ? (int)min((int64_t)a.B * a.ldd * 4, (int64_t)0x7FFFFFFF) : 0, 0x00020000);
+    const uint32_t lbD = (uint32_t)((q0 * (int)a.ldd + t.m0 + ib) * 4);
+    static_for<64>([&](auto ir) {
+      constexpr int i = decltype(ir)::value >> 4, r = decltype(ir)::value & 15;
+      constexpr int pr = 32 * i + 8 * (r >> 2) + (r & 3);
+      float v[4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[jb]) : "a"(acc[i][jb][r]) : "memory");
+      const int item = t.m0 + ib + pr;  // column of this launch's range [0, ncols)
+      const bool iok = item < a.ncols;
+      const float rcv = t.cb[ib + pr];
+      uint32_t cb4 = 0;
+      float svs[4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        // items past ncols score -inf: no count, exp2(-inf) = 0 — one select, no branch around the exp
+        const float sv = iok ? cos_score(v[jb], rs[jb], rcv) : -__builtin_inff();
+        gt[jb] += sv > sl[jb] ? 1 : 0;
+        vc[jb] += sv > -a.max_val ? 1 : 0;
+        se[jb] += __builtin_amdgcn_exp2f((sv - a.shift) * RT_LOG2E);
+        if (MODE == 0) {
+          // unconditional: the caller's row stride covers whole 256-column tiles (items past ncols land
+          // in the row's padding), queries past B are past num_records
+          uint32_t lb = lbD;
+          asm volatile("" : "+v"(lb));
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv), rsD, lb + (uint32_t)((jb * (int)a.ldd + pr) * 4),
+                                                0, 0);
+        }
+        if (MODE == 1) cb4 |= (qok[jb] && sv >= tau[jb]) ? (1u << jb) : 0u;
+        svs[jb] = sv;
+      }
+      if (MODE == 1) {
+        // every row writes its first candidate (or nothing: to the lane's trash slot) to the lane's next
+        // LDS slot — branch-free (branches here wreck the register allocation around the accumulators);
+        // two candidates in one row or more than RK32_NS in the tile count as an overflow
+        const int jb0 = cb4 & 1u ? 0 : (cb4 & 2u ? 1 : (cb4 & 4u ? 2 : 3));
+        const float sv0 = jb0 == 0 ? svs[0] : (jb0 == 1 ? svs[1] : (jb0 == 2 ? svs[2] : svs[3]));
+        const int pos = cb4 ? min(ncand, RK32_NS) : RK32_NS;
+        *reinterpret_cast<float2*>(cslot + 2 * pos) = make_float2(sv0, __int_as_float((jb0 << 8) | pr));
+        ncand += cb4 ? ((cb4 & (cb4 - 1)) ? RK32_NS + 1 : 1) : 0;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (MODE == 1 && ncand) {
+      // flush: one global atomic per candidate (about k per query per column chunk); a lane with more
+      // than RK32_NS poisons its queries' counts (> capr), which the merge flags for an exact re-rank
+      if (ncand > RK32_NS) {
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+          if (qok[jb]) atomicAdd(a.rcnt + q0 + jb, a.capr + 1);
+      } else {
+        for (int k = 0; k < ncand; ++k) {
+          const float sv = cslot[2 * k];
+          const int tag = __float_as_int(cslot[2 * k + 1]);
+          const int q = q0 + (tag >> 8);
+          const int pos = atomicAdd(a.rcnt + q, 1);
+          if (pos < a.capr) {
+            a.cval[(int64_t)q * a.capr + pos] = sv;
+            a.cidx[(int64_t)q * a.capr + pos] = a.idx_base + a.col0 + t.m0 + ib + (tag & 255);
+          }
+        }
+      }
+    }
+    // lane halves (item rows 4g..), then the two waves (wr) of this query half through LDS
+    int pk[4];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      pk[jb] = gt[jb] | (vc[jb] << 16);
+      pk[jb] += __shfl_xor(pk[jb], 32, 64);
+      se[jb] += __shfl_xor(se[jb], 32, 64);
+    }
+    int* xc = reinterpret_cast<int*>(t.scr) + t.wc * 512;      // [wc][4 c-quads][128]: counts
+    float* xs = reinterpret_cast<float*>(t.scr + 4096) + t.wc * 512;
+    if (t.wr == 1 && g == 0) {
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        xc[4 * c + jb] = pk[jb];
+        xs[4 * c + jb] = se[jb];
+      }
+    }
+    __syncthreads();
+    if (t.wr == 0 && g == 0) {
+      const int64_t o = (int64_t)(a.tn0 + t.m0 / 256) * a.B;
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        if (qok[jb]) {
+          a.part_cnt[o + q0 + jb] = pk[jb] + xc[4 * c + jb];
+          a.part_sexp[o + q0 + jb] = se[jb] + xs[4 * c + jb];
+        }
+      }
+    }
+  }
+};
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256, 1)
+    k_rank_w32(int K, const T* __restrict__ items, int ldi, const T* __restrict__ Q, int ldq, int nTm, int nTn,
+               RankW32Args a) {
+  w32_run<T>(K, items, ldi, Q, ldq, a.ncols, a.B, nTn, 0, nTm, nTn, RankW32Pol<MODE>{});
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) k_label_score32(int B, int K, const T* __restrict__ q, int ldq,
+                                                      const float* __restrict__ rq, const T* __restrict__ items,
+                                                      int ldi, const float* __restrict__ ri, int nshard,
+                                                      const int64_t* __restrict__ labels, int64_t label_base,
+                                                      float scale, float* __restrict__ s_label) {
+  typedef typename RtElt<T>::V8 V8;
+  const int lane = threadIdx.x;
+  const int n = lane & 31, g = lane >> 5;
+  const int qb = min((int)blockIdx.x * 32 + n, B - 1);
+  const int64_t lr = labels[qb] - label_base;
+  const bool mine = lr >= 0 && lr < nshard;
+  const T* ea = items + (mine ? lr : 0) * (int64_t)ldi + 8 * g;  // A: the label items (rows)
+  const T* qa = q + (int64_t)qb * ldq + 8 * g;                   // B: the queries (columns)
+  f32x16 acc = f32x16{};
+  for (int k0 = 0; k0 < K; k0 += 16)
+    acc = mfma32(*reinterpret_cast<const V8*>(ea + k0), *reinterpret_cast<const V8*>(qa + k0), acc);
+  // D[m][n] sits in lane n + 32 ((m >> 2) & 1), register 4 (m >> 3) + (m & 3): the diagonal m = n
+  if (g == ((n >> 2) & 1)) {
+    const int b = blockIdx.x * 32 + n;
+    if (b < B) {
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (r == 4 * (n >> 3) + (n & 3)) v = acc[r];
+      s_label[b] = mine ? cos_score(v, rq[b] * scale, ri[lr]) : 0.f;
+    }
+  }
+}
+
+static bool rank_w32_ok(int D, int ldq, int ldi) {
+  return g_knob[KNOB_RANK_W32] && D % 64 == 0 && D >= 128 && ldq % 8 == 0 && ldi % 8 == 0;
+}
+
 // 16 threads per row, each summing every 16th tile in order, then a fixed-order combine:
 // deterministic, and enough threads to hide the partials' load latency
 __global__ void __launch_bounds__(256) k_rank_reduce(int B, int ntiles, const int32_t* __restrict__ part_cnt,
@@ -582,6 +832,18 @@ extern "C" int rf_label_scores(int dtype, int B, int D, const void* q, int ldq, 
   RF_REQUIRE(ldq % 8 == 0 && ldi % 8 == 0, "rf_label_scores: leading dims must be multiples of 8");
   if (B == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
+  if (rank_w32_ok(D, ldq, ldi)) {
+    const int g32 = (B + 31) / 32;
+    if (dtype == RF_BF16)
+      k_label_score32<bf16><<<g32, 64, 0, s>>>(B, D, (const bf16*)q, ldq, rq, (const bf16*)items, ldi, ri, nshard,
+                                               labels, label_base, inv_temp, s_label);
+    else if (dtype == RF_F16)
+      k_label_score32<f16><<<g32, 64, 0, s>>>(B, D, (const f16*)q, ldq, rq, (const f16*)items, ldi, ri, nshard,
+                                              labels, label_base, inv_temp, s_label);
+    else
+      RF_REQUIRE(false, "rf_label_scores: dtype must be bf16 or fp16");
+    RF_LAUNCH_CHECK("rf_label_scores");
+  }
   const int grid = (B + 15) / 16;
   if (dtype == RF_BF16)
     k_label_score<bf16><<<grid, 64, 0, s>>>(B, D, (const bf16*)q, ldq, rq, (const bf16*)items, ldi, ri, nshard,
@@ -607,6 +869,48 @@ extern "C" int rf_score_rank(int dtype, int mode, int B, int D, const void* q, i
              "rf_score_rank: mode %d outputs missing or misaligned", mode);
   if (B == 0 || ncols == 0) return RF_OK;
   hipStream_t s = as_stream(stream);
+  if (rank_w32_ok(D, ldq, ldi)) {
+    static bool attr32 = false;
+    if (!attr32) {
+#define RK32_ATTR(T, M) \
+  (void)hipFuncSetAttribute((const void*)k_rank_w32<T, M>, hipFuncAttributeMaxDynamicSharedMemorySize, W32_LDS)
+      RK32_ATTR(bf16, 0); RK32_ATTR(bf16, 1); RK32_ATTR(bf16, 2);
+      RK32_ATTR(f16, 0); RK32_ATTR(f16, 1); RK32_ATTR(f16, 2);
+#undef RK32_ATTR
+      attr32 = true;
+    }
+    // launches of at most 2^31 bytes of item rows (the loop's buffer resources), 256-column aligned
+    const int64_t row_bytes = (int64_t)ldi * 2;
+    const int cap_cols = (int)std::min<int64_t>(ncols, (0x7FFFFFFF / row_bytes) / 256 * 256);
+    RF_REQUIRE(cap_cols > 0, "rf_score_rank: item rows too wide");
+    RF_REQUIRE(mode != 0 || ldd >= (ncols + 255) / 256 * 256,
+               "rf_score_rank: mode 0 needs ldd >= ncols rounded up to 256 (whole-tile rows)");
+    const int nTn = (B + 255) / 256;
+    for (int c0 = 0; c0 < ncols; c0 += cap_cols) {
+      const int nc = std::min(cap_cols, ncols - c0);
+      RankW32Args a{B, nc, col0 + c0, rq, ri, inv_temp, max_val, shift, s_label, tau,
+                    dense ? dense + c0 : nullptr, ldd, cval, cidx, rcnt, capr, idx_base, part_cnt, part_sexp,
+                    tn0 + c0 / 256};
+      const int nTm = (nc + 255) / 256;
+      const int grid = std::min(nTm * nTn, num_cus_rt());
+      const void* it = (const char*)items + (int64_t)(col0 + c0) * row_bytes;
+#define RK32_(T, M) \
+  k_rank_w32<T, M><<<grid, 256, W32_LDS, s>>>(D, (const T*)it, ldi, (const T*)q, ldq, nTm, nTn, a)
+      if (dtype == RF_BF16) {
+        if (mode == 0) RK32_(bf16, 0);
+        else if (mode == 1) RK32_(bf16, 1);
+        else RK32_(bf16, 2);
+      } else if (dtype == RF_F16) {
+        if (mode == 0) RK32_(f16, 0);
+        else if (mode == 1) RK32_(f16, 1);
+        else RK32_(f16, 2);
+      } else {
+        RF_REQUIRE(false, "rf_score_rank: dtype must be bf16 or fp16");
+      }
+#undef RK32_
+    }
+    RF_LAUNCH_CHECK("rf_score_rank");
+  }
   RankArgs a{B, ncols, col0, rq, ri, inv_temp, s_label, max_val, shift, tau, dense, ldd,
              cval, cidx, rcnt, capr, idx_base, part_cnt, part_sexp, tn0};
   const int nTm = (B + RK_BM - 1) / RK_BM, nTn = (ncols + RK_BN - 1) / RK_BN;

@@ -196,7 +196,7 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     part_sexp = torch.empty(ntiles, B, dtype=torch.float32, device=dev)
     topv = topi = None
     if k > 0:
-        dense = torch.empty(B, (s0 + 3) // 4 * 4, dtype=torch.float32, device=dev)
+        dense = torch.empty(B, (s0 + 255) // 256 * 256, dtype=torch.float32, device=dev)  # whole 256-col tiles
         _score_rank(q, qn, shard, s_label, inv_t, 0, 0, s0, part_cnt, part_sexp, 0, dense=dense, max_val=max_val)
         topv, topi = _topk_dense(dense[:, :s0], k, idx_base=shard.base)
         del dense

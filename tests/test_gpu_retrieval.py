@@ -167,3 +167,35 @@ def test_retrieval_scores_and_topk_vs_fp32_torch(dev, dt, B, N):
     for b in range(B):
         want = set(ri[b][clear[b]].tolist())
         assert want <= set(topi[b].tolist()), b
+
+
+@pytest.mark.parametrize("w32", [0, 1])
+@pytest.mark.parametrize("dt,B,N,cluster", [(torch.bfloat16, 300, 70001, 0), (torch.float16, 64, 12000, 200),
+                                            (torch.float16, 513, 33000, 0)])
+def test_rank_kernels_both_paths(dev, w32, dt, B, N, cluster):
+    """The 32x32x16 four-wave score + rank kernel (knob rank_w32: items as the MFMA A operand, per-query
+    counts as in-lane sums, candidates through per-lane slots) and the 16x16x32 kernel: on each path
+    the label scores are bit-identical to the path's dense scores, the strict ranks / valid counts equal
+    a count over those scores, and the top-50 equals a full sort of them (overflowing rows re-ranked);
+    the two paths' scores agree to fp32 rounding."""
+    old = _lib.set_knob("rank_w32", w32)
+    try:
+        q, items, labels = _case(dev, dt, B, N, B * 7 + N, cluster=cluster)
+        shard = CatalogShard(items)
+        sl = label_scores(q, shard, labels, 0.05)
+        dense = _dense_scores(q, shard, sl, 0.05)
+        assert torch.equal(sl, dense.gather(1, labels[:, None]).squeeze(1))
+        parts = shard_rank(q, shard, sl, 0.05, k=50)
+        assert torch.equal(parts["gt"].long(), (dense > sl[:, None]).sum(1))
+        assert torch.equal(parts["valid"].long(), torch.full((B,), N, dtype=torch.long, device=dev))
+        ref_se = torch.exp(dense.double() - parts["shift"]).sum(1)
+        assert torch.allclose(parts["sexp"].double(), ref_se, rtol=1e-4)
+        ids = torch.arange(N, device=dev, dtype=torch.int32).expand(B, N)
+        rv, ri = merge_topk(dense, ids, 50)
+        assert torch.equal(parts["topv"], rv)
+        assert torch.equal(parts["topi"], ri)
+        _lib.set_knob("rank_w32", 1 - w32)
+        other = _dense_scores(q, shard, label_scores(q, shard, labels, 0.05), 0.05)
+        assert float((other - dense).abs().max()) <= 1e-4 * 20
+    finally:
+        _lib.set_knob("rank_w32", old)

@@ -12,7 +12,8 @@
 #   lines      C3 (captured bf16 / fp16+GradScaler+accumulation+clip, eager), C4 (captured, 4 and 32 per
 #              rank) and C5 (retrieval, catalog encode) lines plus the retrieval kernel trace
 #   trainprof  rocprofv3 kernel trace of the captured C3 step ($TRAIN_ARGS)
-#   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3
+#   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3;
+#              C5 retrieval with the 32x32x16 rank kernel (knob rank_w32) alternated by process
 set -o pipefail
 MODE=${1:?mode}
 TAG=${2:-$MODE}
@@ -56,7 +57,12 @@ case $MODE in
     cat $O/ab_c2.log
     timeout -k 10 500 python tools/train_bench.py --graph --steps 8 --warmup 2 --ab-knob gemm_mfma32 > $O/ab_c3.log 2>&1 \
       || fail $O/ab_c3.log
-    tail -2 $O/ab_c3.log ;;
+    tail -2 $O/ab_c3.log
+    for k in rank_w32=0 rank_w32=1 rank_w32=0 rank_w32=1; do
+      RF_KNOBS=$k timeout -k 10 300 python tools/retrieval_bench.py >> $O/ab_c5.log 2>&1 || fail $O/ab_c5.log
+      echo "$k" >> $O/ab_c5.log
+    done
+    grep -E "rank_w32|ms" $O/ab_c5.log | cut -c1-250 ;;
   lines)
     for args in "--graph" "--graph --dtype fp16 --accum 2 --clip 1.0" "--graph --negatives 1000" ""; do
       timeout -k 10 300 python tools/train_bench.py --steps 8 --warmup 2 $args > $O/c3.log 2>&1 || fail $O/c3.log 20

@@ -35,6 +35,10 @@ def main():
     ap.add_argument("--dtype", type=str, default="fp16")
     ap.add_argument("--k", type=int, default=50)
     args = ap.parse_args()
+    from recformer_amd import _lib
+    for kv in filter(None, os.environ.get("RF_KNOBS", "").split(",")):  # e.g. RF_KNOBS=rank_w32=1
+        k, v = kv.split("=")
+        _lib.set_knob(k, int(v))
     dt = {"fp16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
