@@ -98,6 +98,38 @@ def _mm_f32(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return f(x, y).float()
 
 
+# weight gradients on a side stream beside the main stream's dA GEMM: the dA GEMMs of the N = 768
+# Linears at the reference's finetune batch (16 x 1024 tokens) have 192 tiles of 256^2 for 256 CUs, so
+# a quarter of the chip would idle; the independent dW = dC^T A work fills it (forked and joined with
+# stream events — graph-capturable)
+DW_SIDE_STREAM = True
+_SIDE_STREAMS = {}
+
+
+def _dw_async(fn, ref: torch.Tensor):
+    """Run fn() (weight-gradient work reading tensors the main stream produced) on a side stream
+    that first waits for the main stream; returns join(), which makes the main stream wait for the
+    side stream and returns fn's result (recorded on the main stream for the caching allocator)."""
+    if not (DW_SIDE_STREAM and ref.is_cuda):
+        r = fn()
+        return lambda: r
+    main = torch.cuda.current_stream(ref.device)
+    side = _SIDE_STREAMS.get(ref.device)
+    if side is None:
+        side = _SIDE_STREAMS[ref.device] = torch.cuda.Stream(ref.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        r = fn()
+
+    def join():
+        main.wait_stream(side)
+        for t in (r if isinstance(r, (list, tuple)) else (r,)):
+            if isinstance(t, torch.Tensor):
+                t.record_stream(main)
+        return r
+    return join
+
+
 def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
     """dW = dC^T A (N, K) in fp32 (the master weight's dtype), reduced over the M = B*Lp token
     rows. The layer weights are small (N*K <= 3072*768: at most 36 tiles of 256^2) against a long
@@ -193,10 +225,11 @@ class _GemmP(torch.autograd.Function):
         dc = dc.to(a.dtype).contiguous()
         scaled = sc > 0 and s != 1.0
         da = None
+        join = _dw_async(lambda: _weight_grad(dc, a).to(ctx.wdt), dc) if any(ctx.needs_input_grad[6:]) else None
         if ctx.needs_input_grad[0]:
             da = dc @ wt.t() if dc.shape[0] < SMALL_M else ops.gemm(dc, wt, None, ops.RF_EPI_NONE)
-        dw = _weight_grad(dc, a).to(ctx.wdt) if any(ctx.needs_input_grad[6:]) else None
         db = _bias_grad(dc) if ctx.needs_input_grad[1] else None
+        dw = join() if join is not None else None
         if scaled:
             if dw is not None:
                 dw[:sc] *= s
@@ -391,11 +424,14 @@ class _FFN(torch.autograd.Function):
         w2t = w2 if ctx.packed[1] else w2.t().contiguous()
         dt2 = dt2.to(a.dtype).contiguous()
         dz = ops.gemm(dt2, w2t, None, ops.RF_EPI_DGELU, resid=z)
-        dw2 = _weight_grad(dt2, u).to(ctx.wdt[1]) if ctx.needs_input_grad[4] else None
         db2 = _bias_grad(dt2) if ctx.needs_input_grad[6] else None
+        # both weight gradients on the side stream, beside da = dz.W1 (N = 768: a quarter of the CUs
+        # idle at 16k tokens); dw2 waits for nothing but dt2, dw1 for dz
+        join = _dw_async(lambda: (_weight_grad(dt2, u).to(ctx.wdt[1]) if ctx.needs_input_grad[4] else None,
+                                  _weight_grad(dz, a).to(ctx.wdt[0]) if ctx.needs_input_grad[1] else None), dz)
         da = ops.gemm(dz, w1t, None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
-        dw1 = _weight_grad(dz, a).to(ctx.wdt[0]) if ctx.needs_input_grad[1] else None
         db1 = ops.colsum(dz) if ctx.needs_input_grad[3] else None
+        dw2, dw1 = join()
         return da, dw1, None, db1, dw2, None, db2, None, None
 
 

@@ -58,6 +58,9 @@ case $MODE in
     timeout -k 10 500 python tools/train_bench.py --graph --steps 8 --warmup 2 --ab-knob gemm_mfma32 > $O/ab_c3.log 2>&1 \
       || fail $O/ab_c3.log
     tail -2 $O/ab_c3.log
+    timeout -k 10 500 python tools/train_bench.py --graph --steps 8 --warmup 2 --ab DW_SIDE_STREAM > $O/ab_c3_side.log 2>&1 \
+      || fail $O/ab_c3_side.log
+    tail -2 $O/ab_c3_side.log
     for k in rank_w32=0 rank_w32=1 rank_w32=0 rank_w32=1; do
       RF_KNOBS=$k timeout -k 10 300 python tools/retrieval_bench.py >> $O/ab_c5.log 2>&1 || fail $O/ab_c5.log
       echo "$k" >> $O/ab_c5.log
