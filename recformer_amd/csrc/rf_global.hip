@@ -1539,8 +1539,13 @@ extern "C" int rf_global_attn_fold_h_stage(int stage, int dtype, int B, int Lp, 
   RF_REQUIRE(dtype == RF_F32 || ldh % 8 == 0, "rf_global_attn_fold_h(16-bit): ldh must be a multiple of 8");
   RF_REQUIRE(dtype != RF_F32 || ldh % 4 == 0, "rf_global_attn_fold_h(f32): ldh must be a multiple of 4");
   const int R = B * gmax;
-  // fixed chunks here (inference): a sequence's result does not depend on the batch it is in
-  const int chr = dtype != RF_F32 ? GF_CH : GF_CHF;
+  // fixed chunks here (inference): a sequence's result does not depend on the batch it is in (knob
+  // gfold_chunk: 64 / 128 / 256 rows, at most 16 chunks per sequence; 0 = GF_CH)
+  int chr = dtype != RF_F32 ? GF_CH : GF_CHF;
+  if (dtype != RF_F32 && (g_knob[KNOB_GFOLD_CHUNK] == 64 || g_knob[KNOB_GFOLD_CHUNK] == 128)) {
+    chr = g_knob[KNOB_GFOLD_CHUNK];
+    while ((Lp + chr - 1) / chr > 16 && chr < GF_CH) chr *= 2;
+  }
   const int nch = (Lp + chr - 1) / chr;
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);

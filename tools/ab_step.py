@@ -30,8 +30,10 @@ def main():
     m = m.to(dev) if autocast else m.to(dev).to(torch.bfloat16)
 
     def setv(val):
-        if switch.startswith("knob:"):
-            _lib.set_knob(switch[5:], 1 if val else 0)
+        if switch.startswith("knob:"):  # knob:NAME (1 / 0) or knob:NAME=a,b (a / b)
+            name, _, vals = switch[5:].partition("=")
+            a, b = (int(x) for x in vals.split(",")) if vals else (1, 0)
+            _lib.set_knob(name, a if val else b)
         else:
             setattr(models, switch, val)
     batch = {k: v.to(dev) for k, v in synth_batch(B, 1024, cfg.vocab_size, seed=100, item_len=21).items()}

@@ -55,6 +55,9 @@ case $MODE in
     # alternated in one process (knob gemm_mfma32)
     AB_AUTOCAST=1 timeout -k 10 400 python tools/ab_step.py knob:gemm_mfma32 64 > $O/ab_c2.log 2>&1 || fail $O/ab_c2.log
     cat $O/ab_c2.log
+    AB_AUTOCAST=1 timeout -k 10 400 python tools/ab_step.py knob:gfold_chunk=128,0 64 > $O/ab_c2_gf.log 2>&1 \
+      || fail $O/ab_c2_gf.log
+    cat $O/ab_c2_gf.log
     timeout -k 10 500 python tools/train_bench.py --graph --steps 8 --warmup 2 --ab-knob gemm_mfma32 > $O/ab_c3.log 2>&1 \
       || fail $O/ab_c3.log
     tail -2 $O/ab_c3.log
