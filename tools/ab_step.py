@@ -27,6 +27,9 @@ def main():
     m = RecformerForSeqRec(cfg).eval()
     m.init_item_embedding(torch.randn(10000, cfg.hidden_size) * 0.5)
     autocast = os.environ.get("AB_AUTOCAST") == "1"
+    for kv in filter(None, os.environ.get("RF_KNOBS", "").split(",")):  # base knobs, e.g. gemm_mfma32=1
+        k, v = kv.split("=")
+        _lib.set_knob(k, int(v))
     m = m.to(dev) if autocast else m.to(dev).to(torch.bfloat16)
 
     def setv(val):

@@ -58,6 +58,10 @@ case $MODE in
     AB_AUTOCAST=1 timeout -k 10 400 python tools/ab_step.py knob:gfold_chunk=128,0 64 > $O/ab_c2_gf.log 2>&1 \
       || fail $O/ab_c2_gf.log
     cat $O/ab_c2_gf.log
+    # raster: every N-tile of an A row-panel on one XCD (gemm_gn 0 = full width) vs groups of 6, on w32
+    RF_KNOBS=gemm_mfma32=1 AB_AUTOCAST=1 timeout -k 10 400 python tools/ab_step.py knob:gemm_gn=0,6 64 \
+      > $O/ab_c2_gn.log 2>&1 || fail $O/ab_c2_gn.log
+    cat $O/ab_c2_gn.log
     timeout -k 10 500 python tools/train_bench.py --graph --steps 8 --warmup 2 --ab-knob gemm_mfma32 > $O/ab_c3.log 2>&1 \
       || fail $O/ab_c3.log
     tail -2 $O/ab_c3.log
