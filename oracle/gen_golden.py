@@ -7,6 +7,7 @@ fixtures are data (no reference source); weights are regenerated bit-exactly fro
 seed by the tests, and per-parameter checksums are stored to prove it.
 
     python oracle/gen_golden.py            # writes tests/golden/
+    python oracle/gen_golden.py attn       # only the output_attentions fixtures
 """
 from __future__ import annotations
 
@@ -47,9 +48,31 @@ def save(name, **arrays):
     print("wrote", path, os.path.getsize(path) // 1024, "KiB")
 
 
+def attention_fixtures(M):
+    """c1_attn_{ragged,l200}.npz: output_attentions=True of the reference on the c1_ragged / c1_l200
+    inputs (same batches, weight seed 1): per layer l, attentions `a{l}` (B,H,L,G+2w+1) and
+    global_attentions `g{l}` (B,H,Lp,G)."""
+    for name, v in (("ragged", dict(B=4, L=256, lens=[256, 200, 131, 77],
+                                    extra=((0, 5), (1, 100), (1, 150), (2, 140)))),
+                    ("l200", dict(B=4, L=200, lens=[200, 150, 64, 1], extra=()))):
+        batch = synth_batch(v["B"], v["L"], C1["vocab_size"], seed=11, lens=v["lens"],
+                            extra_globals=v["extra"])
+        ref = M.RecformerModel(make_reference_config(**C1)).eval()
+        hash_init_(ref, seed=1)
+        with torch.no_grad():
+            out = ref(**batch, output_attentions=True)
+        arrays = {}
+        for i, (a, g) in enumerate(zip(out.attentions, out.global_attentions)):
+            arrays[f"a{i}"], arrays[f"g{i}"] = a, g
+        save(f"c1_attn_{name}.npz", **arrays)
+
+
 def main():
     torch.set_num_threads(os.cpu_count())
     M = load_reference_models()
+    if sys.argv[1:] == ["attn"]:
+        attention_fixtures(M)
+        return
     manifest = {}
 
     # --- C1 variants -----------------------------------------------------------------
@@ -138,6 +161,8 @@ def main():
         m = getattr(M, cls)(make_reference_config(**C1))
         layout[cls] = {k: [list(v.shape), str(v.dtype)] for k, v in m.state_dict().items()}
     manifest["state_dict_layout_C1"] = layout
+
+    attention_fixtures(M)
 
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

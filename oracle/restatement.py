@@ -75,10 +75,18 @@ def _lin(x, sd, name):
     return F.linear(x, sd[name + ".weight"], sd[name + ".bias"])
 
 
-def band_global_attention(q, k, v, merged, half_w: int, qg=None, kg=None, vg=None):
+def band_global_attention(q, k, v, merged, half_w: int, qg=None, kg=None, vg=None, head_mask=None,
+                          probs_out=None):
     """q,k,v: (B,H,Lp,hd) (q pre-scaled). merged: (B,Lp) in {0,1,2}.
 
-    Returns ctx (B,H,Lp,hd). If qg/kg/vg given, global rows are overwritten.
+    Returns ctx (B,H,Lp,hd). If qg/kg/vg given, global rows are overwritten. `head_mask` (H,)
+    multiplies the local and the global probabilities per head, as transformers 4.28.0's
+    LongformerSelfAttention does with layer_head_mask (the version the reference pins; 5.15 has no
+    head_mask, so this step is restated from 4.28's published code and is parity unpinned).
+    `probs_out`, a list, receives (local, global) probabilities in the layout LongformerSelfAttention
+    returns for output_attentions (TF:593-640): local (B,H,Lp,G+2w+1) = [global-key columns, band
+    offsets -w..w], zero on padded and on global query rows (TF:626-629); global (B,H,G,Lp), the
+    row of an empty global slot uniform (its all-min score row, TF:990-1000).
     """
     B, H, Lp, hd = q.shape
     W = 2 * half_w
@@ -127,6 +135,8 @@ def band_global_attention(q, k, v, merged, half_w: int, qg=None, kg=None, vg=Non
         s = s_band
     p = torch.softmax(s.float(), dim=-1)
     p = torch.where(valid.view(B, 1, Lp, 1), p, torch.zeros_like(p))
+    if head_mask is not None:
+        p = p * head_mask.float().view(1, H, 1, 1)
     if G > 0:
         p_glob, p_band = p[..., :G], p[..., G:]
         ctx = torch.matmul(p_glob, vgl)
@@ -135,22 +145,39 @@ def band_global_attention(q, k, v, merged, half_w: int, qg=None, kg=None, vg=Non
         ctx = torch.zeros_like(q)
     pb = p_band.reshape(B, H, nb, blk, span)
     ctx = ctx + torch.matmul(pb, vw).reshape(B, H, Lp, hd)
+    if probs_out is not None:
+        # band column c of query qi in its block is span column qi + c
+        cols = (torch.arange(blk).view(blk, 1) + torch.arange(W + 1).view(1, W + 1))
+        band = torch.gather(pb, 4, cols.view(1, 1, 1, blk, W + 1).expand(B, H, nb, blk, W + 1))
+        local = band.reshape(B, H, Lp, W + 1)
+        if G > 0:
+            local = torch.cat([p_glob, local], dim=-1)
+        local = local.masked_fill(glob.view(B, 1, Lp, 1), 0.0)
 
     if G > 0 and qg is not None:
         # qg: (B,H,G,hd) (pre-scaled) for the G global rows; kg, vg: (B,H,Lp,hd)
         sg = torch.matmul(qg, kg.transpose(-1, -2))              # (B,H,G,Lp)
         sg = sg.masked_fill(~valid.view(B, 1, 1, Lp), float("-inf"))
         pg = torch.softmax(sg.float(), dim=-1)
+        if head_mask is not None:
+            pg = pg * head_mask.float().view(1, H, 1, 1)
         og = torch.matmul(pg, vg)                                # (B,H,G,hd)
+        if probs_out is not None:
+            pgo = torch.where(gval.view(B, 1, G, 1), pg, torch.full_like(pg, 1.0 / Lp))
+            if head_mask is not None:
+                pgo = torch.where(gval.view(B, 1, G, 1), pgo, pgo * head_mask.float().view(1, H, 1, 1))
+            probs_out.append((local, pgo))
         for b in range(B):
             n = int(gcount[b])
             if n:
                 pos = gidx[b, :n]
                 ctx[b, :, pos, :] = og[b, :, :n, :]
+    elif probs_out is not None:
+        probs_out.append((local, None))
     return ctx
 
 
-def layer_forward(sd, p: str, h, merged, H: int, half_w: int, eps: float):
+def layer_forward(sd, p: str, h, merged, H: int, half_w: int, eps: float, head_mask=None, probs_out=None):
     B, Lp, D = h.shape
     hd = D // H
     a = p + "attention.self."
@@ -172,7 +199,7 @@ def layer_forward(sd, p: str, h, merged, H: int, half_w: int, eps: float):
         qg = heads(_lin(hg, sd, a + "query_global") / math.sqrt(hd))
         kg = heads(_lin(h, sd, a + "key_global"))      # over ALL tokens, as TF:983-984
         vg = heads(_lin(h, sd, a + "value_global"))
-    ctx = band_global_attention(q, k, v, merged, half_w, qg, kg, vg)
+    ctx = band_global_attention(q, k, v, merged, half_w, qg, kg, vg, head_mask, probs_out)
     ctx = ctx.transpose(1, 2).reshape(B, Lp, D)
     o = p + "attention.output."
     x = F.layer_norm(_lin(ctx, sd, o + "dense") + h, (D,), sd[o + "LayerNorm.weight"], sd[o + "LayerNorm.bias"], eps)
@@ -184,8 +211,10 @@ def layer_forward(sd, p: str, h, merged, H: int, half_w: int, eps: float):
 
 def model_forward(sd: Dict[str, Tensor], cfg, input_ids, attention_mask=None, global_attention_mask=None,
                   token_type_ids=None, item_position_ids=None, prefix: str = "",
-                  return_all_layers: bool = False):
-    """RecformerModel.forward (models.py:274-356) -> (last_hidden_state, pooler_output)."""
+                  return_all_layers: bool = False, head_mask=None, probs_out=None):
+    """RecformerModel.forward (models.py:274-356) -> (last_hidden_state, pooler_output); with
+    `probs_out` (a list) also each layer's (local, global) attention probabilities over the padded
+    length (band_global_attention)."""
     windows = cfg.window_per_layer() if hasattr(cfg, "window_per_layer") else (
         cfg.attention_window if isinstance(cfg.attention_window, list) else [cfg.attention_window] * cfg.num_hidden_layers)
     wmax = max(windows)
@@ -197,7 +226,8 @@ def model_forward(sd: Dict[str, Tensor], cfg, input_ids, attention_mask=None, gl
     layers = [h]
     for i in range(cfg.num_hidden_layers):
         h = layer_forward(sd, f"{prefix}encoder.layer.{i}.", h, merged, cfg.num_attention_heads,
-                          windows[i] // 2, cfg.layer_norm_eps)
+                          windows[i] // 2, cfg.layer_norm_eps, None if head_mask is None else head_mask[i],
+                          probs_out)
         layers.append(h)
     h = h[:, :L]
     if cfg.pooler_type == "cls":

@@ -295,6 +295,40 @@ def _compute_dtype(param_dtype: torch.dtype) -> torch.dtype:
     return torch.float32
 
 
+def _embeds_as_table(inputs_embeds: torch.Tensor, position_ids, pad: int):
+    """`inputs_embeds` (B, L, d) as the word table of the embedding kernels: rows pad+1 .. pad+B*L
+    hold the vectors in token order and token t's id points at its own row, so rf_embed_ln adds the
+    position / type / item-position rows and normalises exactly as for token ids (models.py:106-136,
+    `inputs_embeds + position_embeddings + ...`). Rows 0..pad are zero: the padding id the prologue
+    writes into the window padding gathers a zero row (those rows are masked keys and are sliced
+    off). Gradients reach inputs_embeds through the table. Position ids default to pad+1 .. pad+L
+    (create_position_ids_from_inputs_embeds, models.py:140-153)."""
+    if inputs_embeds.dim() != 3:
+        raise ValueError(f"inputs_embeds must be (batch, seq, hidden), got {tuple(inputs_embeds.shape)}")
+    B, L, D = inputs_embeds.shape
+    dev = inputs_embeds.device
+    table = torch.cat([inputs_embeds.new_zeros(pad + 1, D, dtype=torch.float32),
+                       inputs_embeds.reshape(B * L, D).float()], 0)
+    ids = torch.arange(pad + 1, pad + 1 + B * L, dtype=torch.int64, device=dev).view(B, L)
+    if position_ids is None:
+        position_ids = torch.arange(pad + 1, pad + 1 + L, dtype=torch.int64, device=dev).unsqueeze(0).expand(B, L)
+    return ids, table, position_ids
+
+
+def _head_mask_columns(head_mask: Optional[torch.Tensor], cfg) -> Optional[torch.Tensor]:
+    """head_mask (num_layers, heads) as per-layer column scales (num_layers, hidden) of the attention
+    context: transformers 4.28's LongformerEncoder takes head_mask[layer] and LongformerSelfAttention
+    multiplies the local and the global attention probabilities by it per head (the reference passes
+    head_mask straight to the encoder, models.py:335-343), which scales that head's context columns."""
+    if head_mask is None:
+        return None
+    nl, H = cfg.num_hidden_layers, cfg.num_attention_heads
+    if head_mask.dim() != 2 or tuple(head_mask.shape) != (nl, H):
+        raise ValueError(f"head_mask must be (num_hidden_layers, num_attention_heads) = {(nl, H)}, "
+                         f"got {tuple(head_mask.shape)}")
+    return head_mask.float().repeat_interleave(cfg.hidden_size // H, dim=1)
+
+
 class _PackedWeights:
     """Compute-dtype copies of the layer weights in the layouts the kernels read.
 
@@ -411,33 +445,49 @@ class RecformerModel(nn.Module):
         return_dict = return_dict if return_dict is not None else cfg.use_return_dict
         if input_ids is not None and inputs_embeds is not None:
             raise ValueError("You cannot specify both input_ids and inputs_embeds at the same time")
-        if input_ids is None:
-            raise NotImplementedError("recformer_amd: inputs_embeds is not supported on the HIP path")
-        if head_mask is not None:
-            raise NotImplementedError("recformer_amd: head_mask is not supported (callers pass None)")
-        if output_attentions:
-            raise NotImplementedError("recformer_amd: output_attentions is not supported on the HIP path")
+        if input_ids is None and inputs_embeds is None:
+            raise ValueError("You have to specify either input_ids or inputs_embeds")
+        word = None
+        if inputs_embeds is not None:
+            input_ids, word, position_ids = _embeds_as_table(inputs_embeds, position_ids, cfg.pad_token_id)
+        head_cols = _head_mask_columns(head_mask, cfg)
+        # output_attentions: each layer appends (attentions, global_attentions) recomputed from its
+        # input (recformer_amd/probs.py); the kernels themselves never write probabilities
+        probe = [] if output_attentions else None
         if _train_path(self):
             # autograd path (recformer_amd/train.py): same kernels, explicit backward
             from .train import encode_train
             last, hidden_all = encode_train(self, input_ids, attention_mask, global_attention_mask,
                                             token_type_ids, position_ids, item_position_ids,
-                                            output_hidden_states)
+                                            output_hidden_states, word=word, head_cols=head_cols,
+                                            attn_probe=probe)
         else:
             last, hidden_all = self._encode(input_ids, attention_mask, global_attention_mask,
                                             token_type_ids, position_ids, item_position_ids,
-                                            output_hidden_states)
+                                            output_hidden_states, word=word, head_cols=head_cols,
+                                            attn_probe=probe)
+        attentions = global_attentions = None
+        if probe is not None:
+            attentions = tuple(a for a, _ in probe)
+            if any(g is not None for _, g in probe):
+                global_attentions = tuple(g for _, g in probe)
         pooled = self.pooler(attention_mask, last)
         if not return_dict:
             out = (last, pooled)
             if output_hidden_states:
                 out = out + (hidden_all,)
+            if attentions is not None:
+                out = out + (attentions,)
+            if global_attentions is not None:
+                out = out + (global_attentions,)
             return out
-        return RecformerModelOutput(last_hidden_state=last, pooler_output=pooled, hidden_states=hidden_all)
+        return RecformerModelOutput(last_hidden_state=last, pooler_output=pooled, hidden_states=hidden_all,
+                                    attentions=attentions, global_attentions=global_attentions)
 
     @torch.no_grad()
     def _encode(self, input_ids, attention_mask, global_attention_mask, token_type_ids,
-                position_ids, item_position_ids, output_hidden_states):
+                position_ids, item_position_ids, output_hidden_states, word=None, head_cols=None,
+                attn_probe=None):
         cfg = self.config
         B, L = input_ids.shape
         W = self._window()
@@ -490,12 +540,13 @@ class RecformerModel(nn.Module):
         # the split planes' hi half is a bf16 operand; fp16 keeps the fp32 stream plus an fp16 copy
         split = mixed and SPLIT_STREAM and dt == torch.bfloat16
         nl = len(pk["layers"])
+        word = pk["word"] if word is None else word
         if split:
-            h, h_lo = ops.embed_ln_split(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
+            h, h_lo = ops.embed_ln_split(ids, pos, tt, ip, word, pk["pos"], pk["type"], pk["ipos"],
                                          pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps)
             h32 = ops.join_split(h, h_lo) if (output_hidden_states or nl == 0) else None
         else:
-            h, h32 = ops.embed_ln(ids, pos, tt, ip, pk["word"], pk["pos"], pk["type"], pk["ipos"],
+            h, h32 = ops.embed_ln(ids, pos, tt, ip, word, pk["pos"], pk["type"], pk["ipos"],
                                   pk["ln_w"], pk["ln_b"], cfg.layer_norm_eps, out_dtype=dt, want_f32=mixed)
             if not mixed:
                 h32 = h
@@ -508,8 +559,14 @@ class RecformerModel(nn.Module):
         fold = getattr(cfg, "global_attention_fold", True)
         eps = cfg.layer_norm_eps
         gws = None
+        Lref = L + (W - L % W) % W
         for li, lw in enumerate(pk["layers"]):
             half_w = windows[li] // 2
+            if attn_probe is not None:
+                from .probs import layer_attention_probs
+                attn_probe.append(layer_attention_probs(
+                    h, self.encoder.layer[li].attention.self, flags, gidx, B, Lp, L, Lref, H, half_w, scale,
+                    None if head_cols is None else head_cols[li, ::hd]))
             nq = 5 * D if (gmax > 0 and not fold) else 3 * D
             gargs = (h, lw["w_qg"], lw["b_qg"], scale, lw["w_qkv"][3 * D:4 * D], lw["b_qkv"][3 * D:4 * D],
                      lw["w_qkv"][4 * D:5 * D], lw["b_qkv"][4 * D:5 * D], flags, gidx, B, Lp, H)
@@ -549,8 +606,13 @@ class RecformerModel(nn.Module):
                     qg = ops.gemm(hg, lw["w_qg"], lw["b_qg"], ops.RF_EPI_BIAS, scale_cols=D, col_scale=scale)
                     ops.global_attention(qg, qkv[:, 3 * D:4 * D], qkv[:, 4 * D:5 * D], flags, gidx,
                                          B, Lp, H, ctx, tag="global_attn")
+            w_o = lw["w_o"]
+            if head_cols is not None:
+                # head_mask (TF 4.28 LongformerSelfAttention: probs * layer_head_mask, local and global)
+                # scales each head's context columns: folded into the output projection's input columns
+                w_o = (w_o.float() * head_cols[li]).to(w_o.dtype).contiguous()
             if not mixed:
-                t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h32,
+                t = ops.gemm(ctx, w_o, lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=h32,
                              tag="gemm_out")
                 a = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], eps, out=t, tag="layernorm")
                 f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
@@ -563,7 +625,7 @@ class RecformerModel(nn.Module):
                 # the stream updated in place as planes (h = its hi plane); the last layer (and
                 # every layer when hidden states are returned) also writes the fp32 output.
                 last_layer = li == nl - 1
-                t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
+                t = ops.gemm(ctx, w_o, lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
                 ops.add_layernorm_split(t, h, h_lo, lw["ln1_w"], lw["ln1_b"], eps, tag="layernorm")
                 f = ops.gemm(h, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
                 t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS, tag="gemm_ffn2")
@@ -573,7 +635,7 @@ class RecformerModel(nn.Module):
                                                     tag="layernorm")
             else:
                 # the same with the fp32 stream as a plain fp32 tensor (SPLIT_STREAM = False)
-                t = ops.gemm(ctx, lw["w_o"], lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
+                t = ops.gemm(ctx, w_o, lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
                 a, a32 = ops.add_layernorm(t, h32, lw["ln1_w"], lw["ln1_b"], eps, out_dtype=dt,
                                            res_out=None if output_hidden_states else h32, tag="layernorm")
                 f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")

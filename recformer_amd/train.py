@@ -1122,9 +1122,12 @@ def _lin(a, lw, wkey: str, bkey: str, scale_cols: int, col_scale: float):
 
 
 def encode_train(model, input_ids, attention_mask, global_attention_mask, token_type_ids,
-                 position_ids, item_position_ids, output_hidden_states: bool
-                 ) -> Tuple[torch.Tensor, Optional[tuple]]:
-    """Autograd forward of RecformerModel (same outputs as RecformerModel._encode)."""
+                 position_ids, item_position_ids, output_hidden_states: bool, word=None, head_cols=None,
+                 attn_probe=None) -> Tuple[torch.Tensor, Optional[tuple]]:
+    """Autograd forward of RecformerModel (same outputs as RecformerModel._encode). `word` replaces the
+    word-embedding table (inputs_embeds, models._embeds_as_table); `head_cols` (layers, hidden) scales
+    each layer's attention context (head_mask, models._head_mask_columns); `attn_probe`, a list, receives
+    each layer's (attentions, global_attentions) (output_attentions, recformer_amd/probs.py)."""
     from .models import _compute_dtype
     cfg = model.config
     B, L = input_ids.shape
@@ -1149,7 +1152,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
         position_ids, Lp, cfg.pad_token_id, gmax)
     emb = model.embeddings
-    h32 = _EmbedLN.apply(ids, pos, tt, ip, emb.word_embeddings.weight.float(),
+    h32 = _EmbedLN.apply(ids, pos, tt, ip, emb.word_embeddings.weight.float() if word is None else word,
                          emb.position_embeddings.weight.float(), emb.token_type_embeddings.weight.float(),
                          emb.item_position_embeddings.weight.float(), emb.LayerNorm.weight.float(),
                          emb.LayerNorm.bias.float(), eps, cfg.pad_token_id)
@@ -1181,6 +1184,11 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     for li, lyr in enumerate(model.encoder.layer):
         lw = packed[li] if packed is not None else _layer_weights(li, lyr, dt)
         h = h16 if h16 is not None else h32.to(dt)
+        if attn_probe is not None:
+            from .probs import layer_attention_probs
+            attn_probe.append(layer_attention_probs(
+                h.detach(), lyr.attention.self, flags, gidx, B, Lp, L, Lp, H, windows[li] // 2, scale,
+                None if head_cols is None else head_cols[li, ::hd].detach()))
         qkv = _lin(h, lw, "w_qkv", "b_qkv", D, scale)
         qg = None
         qin = ()
@@ -1193,6 +1201,8 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
                                flags, gidx, B, Lp, H, windows[li] // 2, fold, grows, p_att, att_seeds[li],
                                lw.get("wkg_master"), lw.get("wvg_master"), *qin)
+        if head_cols is not None:
+            ctx = ctx * head_cols[li].to(ctx.dtype)
         ao = lyr.attention.output
         t = _lin(ctx, lw, "w_o", "b_o", 0, 1.0)
         if fused:

@@ -248,3 +248,151 @@ def test_graphed_forward_matches_eager(dev, B, L):
     b["global_attention_mask"][:, 1] = 1
     with pytest.raises(ValueError):
         g(**b)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast"])
+def test_inputs_embeds_matches_input_ids(dev, mode):
+    """inputs_embeds = Ew[input_ids] with the ids' position ids gives the input_ids outputs bit for
+    bit (the same fp32 rows summed in the same order, models.py:106-136); without position_ids the
+    positions are pad+1 .. pad+L (create_position_ids_from_inputs_embeds, models.py:140-153)."""
+    from recformer_amd import create_position_ids_from_input_ids
+    g = load_golden("c1_ragged")
+    m, ctx = _prep(hashed_model(C1, seed=1), dev, mode)
+    batch = {k: v.to(dev) for k, v in batch_of(g).items()}
+    ids = batch.pop("input_ids")
+    pad = m.config.pad_token_id
+    emb = m.embeddings.word_embeddings.weight.detach()[ids]
+    pos = create_position_ids_from_input_ids(ids, pad)
+    seq = torch.arange(pad + 1, pad + 1 + ids.shape[1], device=dev).expand_as(ids)
+    with torch.no_grad(), ctx:
+        a = m(input_ids=ids, **batch).last_hidden_state
+        b = m(inputs_embeds=emb, position_ids=pos, **batch).last_hidden_state
+        c = m(input_ids=ids, position_ids=seq, **batch).last_hidden_state
+        d = m(inputs_embeds=emb, **batch).last_hidden_state
+    assert torch.equal(a, b)
+    assert torch.equal(c, d)
+    with pytest.raises(ValueError):
+        m(input_ids=ids, inputs_embeds=emb, **batch)
+
+
+def test_inputs_embeds_gradient(dev):
+    """Training path: the gradient reaching inputs_embeds, summed over the tokens of each id, is the
+    word-embedding gradient of the input_ids run (rows other than the padding id)."""
+    from recformer_amd import create_position_ids_from_input_ids
+    g = load_golden("c1_ragged")
+    cfg = dict(C1, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m = hashed_model(cfg, seed=1).to(dev).train()
+    batch = {k: v.to(dev) for k, v in batch_of(g).items()}
+    ids = batch.pop("input_ids")
+    pad = m.config.pad_token_id
+    out = m(input_ids=ids, **batch)
+    out.last_hidden_state.square().mean().backward()
+    gw = m.embeddings.word_embeddings.weight.grad.clone()
+    m.zero_grad(set_to_none=True)
+    emb = m.embeddings.word_embeddings.weight.detach()[ids].clone().requires_grad_(True)
+    out2 = m(inputs_embeds=emb, position_ids=create_position_ids_from_input_ids(ids, pad), **batch)
+    assert torch.equal(out.last_hidden_state, out2.last_hidden_state)
+    out2.last_hidden_state.square().mean().backward()
+    assert m.embeddings.word_embeddings.weight.grad is None or not m.embeddings.word_embeddings.weight.grad.any()
+    ge = torch.zeros_like(gw).index_add_(0, ids.reshape(-1), emb.grad.reshape(-1, gw.shape[1]))
+    ge[pad] = 0
+    scale = max(float(gw.abs().max()), 1e-12)
+    assert float((ge - gw).abs().max()) <= 1e-5 * scale
+
+
+def _head_mask(cfg):
+    gen = torch.Generator().manual_seed(5)
+    hm = torch.rand(cfg["num_hidden_layers"], cfg["num_attention_heads"], generator=gen)
+    hm[0, 0] = 0.0
+    hm[-1, -1] = 0.0
+    hm[hm.shape[0] // 2] = 1.0
+    return hm
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
+@pytest.mark.parametrize("name", ["c1_full", "c1_ragged"])
+def test_head_mask_vs_oracle(dev, name, mode):
+    """head_mask (layers, heads) scales each head's local and global attention probabilities
+    (transformers 4.28 LongformerSelfAttention; oracle.restatement with head_mask, parity unpinned:
+    no reference fixture holds a head_mask run). All-ones equals no mask exactly."""
+    from oracle import restatement as R
+    g = load_golden(name)
+    lf = hashed_model(C1, seed=1)
+    hm = _head_mask(C1)
+    batch = batch_of(g)
+    with torch.no_grad():
+        ref, ref_pooled = R.model_forward(lf.state_dict(), lf.config, **batch, head_mask=hm)
+    m, ctx = _prep(lf, dev, mode)
+    bd = {k: v.to(dev) for k, v in batch.items()}
+    with torch.no_grad(), ctx:
+        out = m(**bd, head_mask=hm.to(dev))
+        plain = m(**bd).last_hidden_state
+        ones = m(**bd, head_mask=torch.ones_like(hm, device=dev)).last_hidden_state
+    assert torch.equal(plain, ones)
+    _check_e2e(mode, errs(out.last_hidden_state, ref), out.pooler_output, ref_pooled)
+    with pytest.raises(ValueError):
+        m(**bd, head_mask=hm[0].to(dev))
+
+
+def test_head_mask_training_grads_vs_oracle(dev):
+    """head_mask on the training path (fp32, dropout off): pooled-output loss and every parameter
+    gradient against autograd through the oracle with the same mask."""
+    from oracle import restatement as R
+    g = load_golden("c1_ragged")
+    cfg = dict(C1, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    lf = hashed_model(cfg, seed=1)
+    hm = _head_mask(cfg)
+    batch = batch_of(g)
+    sd = {k: v.detach().clone().requires_grad_(v.is_floating_point()) for k, v in lf.state_dict().items()}
+    _, p = R.model_forward(sd, lf.config, **batch, head_mask=hm)
+    ref_loss = p.square().sum()
+    ref_loss.backward()
+    m = lf.to(dev).train()
+    _, pooled = m(**{k: v.to(dev) for k, v in batch.items()}, head_mask=hm.to(dev), return_dict=False)
+    loss = pooled.square().sum()
+    loss.backward()
+    assert abs(float(loss) - float(ref_loss)) <= 1e-4 * max(1.0, abs(float(ref_loss)))
+    for k, prm in m.named_parameters():
+        gr = sd[k].grad
+        if gr is None:
+            continue
+        err = float((prm.grad.detach().cpu() - gr).abs().max())
+        assert err <= 2e-3 * max(float(gr.abs().max()), 1e-6), (k, err)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast"])
+@pytest.mark.parametrize("case", ["ragged", "l200"])
+@pytest.mark.parametrize("train", [False, True])
+def test_output_attentions_vs_reference(dev, case, mode, train):
+    """output_attentions=True (recformer_amd/probs.py) against the reference's own attentions /
+    global_attentions on the same inputs (tests/golden/c1_attn_*.npz): shapes, the zero rows and
+    columns, and values within 1e-4 (fp32) / 3e-2 max, 1e-3 mean (bf16 autocast, whose q/k are
+    bf16 as the reference's autocast ones are). The tuple form appends them after the hidden states."""
+    g = load_golden("c1_" + case)
+    a = load_golden("c1_attn_" + case)
+    cfg = dict(C1, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m, ctx = _prep(hashed_model(cfg, seed=1), dev, mode)
+    if train:
+        m.train()
+    batch = {k: v.to(dev) for k, v in batch_of(g).items()}
+    with torch.set_grad_enabled(train), ctx:
+        out = m(**batch, output_attentions=True)
+        tup = m(**batch, output_attentions=True, return_dict=False)
+    assert len(out.attentions) == len(out.global_attentions) == C1["num_hidden_layers"]
+    assert len(tup) == 4 and len(tup[2]) == C1["num_hidden_layers"]
+    for i in range(C1["num_hidden_layers"]):
+        ra, rg = a[f"a{i}"], a[f"g{i}"]
+        oa, og = out.attentions[i], out.global_attentions[i]
+        assert oa.shape == ra.shape and og.shape == rg.shape, (oa.shape, ra.shape, og.shape, rg.shape)
+        if mode == "fp32":
+            assert torch.equal(oa.float().cpu() == 0, ra == 0)
+        ea, eg = errs(oa, ra), errs(og, rg)
+        if mode == "fp32":
+            assert ea["max"] <= 1e-4 and eg["max"] <= 1e-4, (ea, eg)
+        else:
+            assert ea["max"] <= 3e-2 and ea["mean"] <= 1e-3, ea
+            assert eg["max"] <= 3e-2 and eg["mean"] <= 1e-3, eg
+    if not train:
+        with torch.no_grad(), ctx:
+            plain = m(**batch)
+        assert torch.equal(plain.last_hidden_state, out.last_hidden_state)

@@ -164,3 +164,35 @@ def test_package_exports_resolve():
     import recformer_amd
     for name in recformer_amd.__all__:
         assert getattr(recformer_amd, name) is not None, name
+
+
+def test_inputs_embeds_table_and_head_mask_host_logic():
+    """inputs_embeds becomes a word table whose rows the token ids index (zero rows up to the padding
+    id); head_mask (layers, heads) becomes per-layer context-column scales; the oracle's all-ones mask
+    is the identity."""
+    from oracle import restatement as R
+    from recformer_amd.models import _embeds_as_table, _head_mask_columns
+    from tests.common import batch_of, hashed_model, load_golden
+    x = torch.randn(2, 5, 8)
+    ids, table, pos = _embeds_as_table(x, None, 1)
+    assert table.shape == (2 + 10, 8) and not table[:2].any()
+    assert torch.equal(table[ids], x)
+    assert torch.equal(pos[1], torch.arange(2, 7))
+    cfg = RecformerConfig(**C1)
+    hm = torch.rand(cfg.num_hidden_layers, cfg.num_attention_heads)
+    cols = _head_mask_columns(hm, cfg)
+    hd = cfg.hidden_size // cfg.num_attention_heads
+    assert cols.shape == (cfg.num_hidden_layers, cfg.hidden_size)
+    assert torch.equal(cols[:, ::hd], hm)
+    with pytest.raises(ValueError):
+        _head_mask_columns(hm[0], cfg)
+    g = load_golden("c1_ragged")
+    lf = hashed_model(C1, seed=1)
+    with torch.no_grad():
+        a, _ = R.model_forward(lf.state_dict(), lf.config, **batch_of(g))
+        b, _ = R.model_forward(lf.state_dict(), lf.config, **batch_of(g), head_mask=torch.ones_like(hm))
+        hz = torch.ones_like(hm)
+        hz[0] = 0
+        c, _ = R.model_forward(lf.state_dict(), lf.config, **batch_of(g), head_mask=hz)
+    assert torch.equal(a, b)
+    assert not torch.allclose(a, c)

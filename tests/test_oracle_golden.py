@@ -79,3 +79,19 @@ def test_ranker_restatement_matches_reference(case):
     for a, b in zip(got[:-1], ref[:-1]):
         assert a == pytest.approx(b, abs=1e-7)
     assert got[-1] == pytest.approx(ref[-1], rel=1e-6)
+
+
+@pytest.mark.parametrize("case", ["ragged", "l200"])
+def test_attention_probs_match_reference(case):
+    """The restatement's attention probabilities (band_global_attention probs_out) against the
+    reference's output_attentions=True run (oracle/gen_golden.py attention_fixtures)."""
+    g = load_golden("c1_" + case)
+    a = load_golden("c1_attn_" + case)
+    m = hashed_model(C1, seed=1)
+    po = []
+    with torch.no_grad():
+        R.model_forward(m.state_dict(), m.config, **batch_of(g), probs_out=po)
+    L = g["input_ids"].shape[1]
+    for i, (local, glob) in enumerate(po):
+        assert errs(local[:, :, :L], a[f"a{i}"])["max"] <= 1e-6
+        assert errs(glob.transpose(2, 3), a[f"g{i}"])["max"] <= 1e-6
