@@ -267,6 +267,189 @@ __global__ void __launch_bounds__(256) k_band_attn_bf16(int Lp, const E* __restr
 }
 
 // ------------------------------------------------------------------------------------
+// Local branch, 16-bit, any window (k_band_attn_wide): the layout of k_band_attn_bf16 with
+// the key span of a 64-query block, rows [i0 - w, i0 + 63 + w], walked in 64-row chunks under
+// the online softmax (one more chunk per 64 of window), then the global-key chunks. Chunk c's
+// K/V rows are DMA'd to LDS once per workgroup; each wave skips the 16-key tiles outside its
+// own span [qw - w, qw + 15 + w]. Any half window and any Lp (query rows past Lp are not
+// stored). The window-64 kernels above stay the production path; this one serves the other
+// per-layer windows the reference accepts (models.py:179-187, e.g. the 512 offline preset).
+constexpr int AW_K = 0;        // 64 x 128 B
+constexpr int AW_V = 8192;     // 64 x 128 B
+constexpr int AW_KG = 16384;   // 32 x 128 B
+constexpr int AW_VG = 20480;   // 32 x 128 B
+constexpr int AW_FL = 24576;   // 64 chunk-row flags
+constexpr int AW_GP = 24640;   // 32 x int
+constexpr int AW_LDS = 24768;
+
+template <typename E>
+__global__ void __launch_bounds__(256) k_band_attn_wide(int Lp, int half_w, const E* __restrict__ q,
+                                                         const E* __restrict__ k,
+                                                         const E* __restrict__ v, int ld,
+                                                         const uint8_t* __restrict__ flags,
+                                                         const int32_t* __restrict__ gidx,
+                                                         int gmax, E* __restrict__ out,
+                                                         int ldo, int H) {
+  typedef typename H16<E>::x8 V8;
+  typedef typename H16<E>::x4 V4;
+  __shared__ __attribute__((aligned(16))) char smem[AW_LDS];
+  const int nqb = (Lp + 63) >> 6;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = wg % nqb, bh = wg / nqb;
+  const int i0 = qb * 64, h = bh % H, b = bh / H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t rb = (int64_t)b * Lp;
+  const int hoff = h * 64;
+  const int w = half_w;
+  int* gp = reinterpret_cast<int*>(smem + AW_GP);
+  uint8_t* fl = reinterpret_cast<uint8_t*>(smem + AW_FL);
+
+  const int qw = i0 + 16 * wave;
+  const int myq = qw + li;
+  const int qrow = min(myq, Lp - 1);
+  V8 qf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    qf[s] = *reinterpret_cast<const V8*>(q + (rb + qrow) * ld + hoff + 32 * s + 8 * g);
+  const bool qvalid = myq < Lp && flags[rb + qrow] != 0;
+
+  float m = RF_NEG_INF, lsum = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one segment of up to 64 keys (4 tiles of 16) against the wave's 16 queries: scores for the
+  // tiles in [t_lo, t_hi), masked by `ok(key tile row)`, online-softmax update, P.V
+  auto segment = [&](const char* kbase, const char* vbase, int ntile, auto ok) {
+    f32x4 st[4];
+    float cmx = RF_NEG_INF;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < ntile) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const V8 kf = *reinterpret_cast<const V8*>(kbase + swz128(16 * t + li, 4 * s + g));
+          st[t] = mfma16(kf, qf[s], st[t]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sv = (t < ntile && ok(16 * t + 4 * g + r)) ? st[t][r] : RF_NEG_INF;
+        st[t][r] = sv;
+        cmx = fmaxf(cmx, sv);
+      }
+    }
+    cmx = fmaxf(cmx, __shfl_xor(cmx, 16, 64));
+    cmx = fmaxf(cmx, __shfl_xor(cmx, 32, 64));
+    const float mn = fmaxf(m, cmx);
+    const float mu = (mn == RF_NEG_INF) ? 0.f : mn;
+    const float alpha = exp2f((m - mu) * LOG2E);
+    lsum *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f((st[t][r] - mu) * LOG2E);
+        st[t][r] = p;
+        lsum += p;
+      }
+    m = mn;
+    // PV: k-steps of 32 keys; key(g, j) = 32*s + 16*(j>>2) + 4*g + (j&3)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (2 * s < ntile) {
+        V8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (E)st[2 * s + (j >> 2)][j & 3];
+        const int r0 = 32 * s + 4 * g + (li >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int col = 16 * dt + 4 * (li & 3);
+          const V4 v0 = tr_read<E>(vbase, swz_el(r0, col));
+          const V4 v1 = tr_read<E>(vbase, swz_el(r0 + 16, col));
+          V8 vf;
+          vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v0[2]; vf[3] = v0[3];
+          vf[4] = v1[0]; vf[5] = v1[1]; vf[6] = v1[2]; vf[7] = v1[3];
+          o[dt] = mfma16(vf, pf, o[dt]);
+        }
+      }
+    }
+  };
+
+  // ---- window chunks ----
+  const int k_first = i0 - w;
+  const int nck = (64 + 2 * w + 63) / 64;
+  for (int c = 0; c < nck; ++c) {
+    const int kb0 = k_first + 64 * c;
+    __syncthreads();  // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cc = wave * 2 + i;
+      const int row = cc * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ (row & 7);
+      const int kp = min(max(kb0 + row, 0), Lp - 1);
+      const int64_t off = (rb + kp) * ld + hoff + ch * 8;
+      glds16(k + off, smem + AW_K + cc * 1024);
+      glds16(v + off, smem + AW_V + cc * 1024);
+    }
+    if (threadIdx.x < 64) {
+      const int kp = kb0 + threadIdx.x;
+      fl[threadIdx.x] = (kp >= 0 && kp < Lp) ? flags[rb + kp] : 0;
+    }
+    wait_vmcnt0();
+    __syncthreads();
+    // tiles of this chunk that meet the wave's span [qw - w, qw + 15 + w]
+    const int lo = qw - w - kb0, hi = qw + 15 + w - kb0;
+    if (hi < 0 || lo > 63) continue;
+    const int ntile = min(4, (hi >> 4) + 1);
+    segment(smem + AW_K, smem + AW_V, ntile, [&](int kr) {
+      const int kp = kb0 + kr;
+      return abs(kp - myq) <= w && fl[kr] == 1;
+    });
+  }
+
+  // ---- global-key chunks (local K/V at global positions) ----
+  const int nchunks = (gmax + 31) / 32;
+  for (int cg = 0; cg < nchunks; ++cg) {
+    __syncthreads();
+    {
+      const int row = wave * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ (row & 7);
+      const int gi = cg * 32 + row;
+      const int p = gi < gmax ? gidx[(int64_t)b * gmax + gi] : -1;
+      const int64_t off = (rb + (p >= 0 ? p : 0)) * ld + hoff + ch * 8;
+      glds16(k + off, smem + AW_KG + wave * 1024);
+      glds16(v + off, smem + AW_VG + wave * 1024);
+      if (threadIdx.x < 32) {
+        const int gj = cg * 32 + threadIdx.x;
+        gp[threadIdx.x] = gj < gmax ? gidx[(int64_t)b * gmax + gj] : -1;
+      }
+    }
+    wait_vmcnt0();
+    __syncthreads();
+    segment(smem + AW_KG, smem + AW_VG, 2, [&](int kr) { return gp[kr] >= 0; });
+  }
+
+  // ---- normalise and store O[q][16dt + 4g + r] ----
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (myq >= Lp) return;
+  const float inv = (qvalid && lsum > 0.f) ? 1.0f / lsum : 0.f;
+  E* orow = out + (rb + myq) * ldo + hoff + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    V4 wv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wv[r] = (E)(qvalid ? o[dt][r] * inv : 0.f);
+    *reinterpret_cast<V4*>(orow + 16 * dt) = wv;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Local branch, bf16, pipelined sliding window (k_band_attn_pipe): one workgroup walks a run
 // of consecutive 64-query blocks of one (sequence, head). Keys are staged in 64-row chunks
 // c = rows [64c-32, 64c+32): query block x needs chunks x and x+1, so each chunk is DMA'd
@@ -1442,7 +1625,21 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
   hipStream_t s = as_stream(stream);
   if (dtype == RF_BF16 || dtype == RF_F16) {
     const bool h16 = dtype == RF_F16;
-    RF_REQUIRE(half_w == 32, "rf_band_attn_fwd(bf16): window must be 64 (half 32), got half %d", half_w);
+    if (half_w != 32) {
+      // other windows: the chunked kernel (inference; the training path's other windows recompute
+      // the local branch in fp32, train._local_torch)
+      RF_REQUIRE(half_w > 0, "rf_band_attn_fwd: bad half window %d", half_w);
+      RF_REQUIRE(dr.thresh == 0, "rf_band_attn_fwd(16-bit): window %d runs without dropout", 2 * half_w);
+      RF_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0, "rf_band_attn_fwd(16-bit): alignment");
+      const int grid = ((Lp + 63) / 64) * H * B;
+      if (h16)
+        k_band_attn_wide<f16><<<grid, 256, 0, s>>>(Lp, half_w, (const f16*)q, (const f16*)k, (const f16*)v, ld_qkv,
+                                                   flags, gidx, gmax, (f16*)out, ld_out, H);
+      else
+        k_band_attn_wide<bf16><<<grid, 256, 0, s>>>(Lp, half_w, (const bf16*)q, (const bf16*)k, (const bf16*)v, ld_qkv,
+                                                    flags, gidx, gmax, (bf16*)out, ld_out, H);
+      RF_LAUNCH_CHECK("rf_band_attn_fwd");
+    }
     RF_REQUIRE(Lp % 64 == 0 || (Lp < 64 && Lp % 16 == 0 && dr.thresh == 0),
                "rf_band_attn_fwd(16-bit): Lp=%d must be a multiple of 64, or < 64 and a multiple of 16 "
                "(short sequences; no dropout)", Lp);

@@ -275,6 +275,41 @@ def test_band_and_global_attention(dev, dt, case):
     assert ctx.float().cpu()[pad_rows].abs().max().item() == 0.0 if pad_rows.any() else True
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", [
+    dict(half_w=256, B=2, Lp=1024, H=2, lens=[1024, 700], globals_=((0, 0), (1, 0), (1, 500))),
+    dict(half_w=64, B=2, Lp=384, H=3, lens=[384, 200], globals_=((0, 0),)),
+    dict(half_w=20, B=2, Lp=200, H=2, lens=[200, 57], globals_=((0, 0), (1, 3))),
+    dict(half_w=96, B=1, Lp=576, H=1, lens=[576], globals_=tuple((0, 13 * i) for i in range(40))),
+])
+def test_band_attention_other_windows(dev, dt, case):
+    """16-bit local attention at windows other than 64 (k_band_attn_wide: the reference accepts any
+    even per-layer window, models.py:179-187) against the oracle, incl. Lp not a multiple of 64 and
+    more than 32 global keys; then the global rows through rf_global_attn_fwd."""
+    B, Lp, H, hw = case["B"], case["Lp"], case["H"], case["half_w"]
+    D = H * 64
+    qkv, merged, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, case["lens"], case["globals_"], 17)
+    q, k, v, kg, vg = (qkv[:, i * D:(i + 1) * D] for i in range(5))
+    ctx = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, hw)
+    qg = None
+    if G:
+        qg_rows = _rand((B * G, D), dev, dt, 1.0, seed=18)
+        ops.global_attention(qg_rows, kg, vg, flags, gidx, B, Lp, H, ctx)
+        qg = qg_rows.float().cpu().view(B, G, H, 64).transpose(1, 2)
+
+    def hv(x):
+        return x.float().cpu().view(B, Lp, H, 64).transpose(1, 2)
+
+    ref = R.band_global_attention(hv(q), hv(k), hv(v), merged, hw, qg,
+                                  hv(kg) if G else None, hv(vg) if G else None)
+    ref = ref.transpose(1, 2).reshape(B * Lp, D)
+    err = (ctx.float().cpu() - ref).abs().max().item()
+    assert err <= 3e-2, err
+    pad_rows = merged.view(-1) == 0
+    if pad_rows.any():
+        assert ctx.float().cpu()[pad_rows].abs().max().item() == 0.0
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 def test_cos_scores(dev, dt):
     z = _rand((37, 768), dev, dt, seed=30)

@@ -396,3 +396,21 @@ def test_output_attentions_vs_reference(dev, case, mode, train):
         with torch.no_grad(), ctx:
             plain = m(**batch)
         assert torch.equal(plain.last_hidden_state, out.last_hidden_state)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
+def test_per_layer_windows_vs_oracle(dev, mode):
+    """Per-layer windows other than 64 ([128, 512], models.py:179-187) end to end against the oracle:
+    the 16-bit modes run k_band_attn_wide, fp32 the VALU kernel."""
+    from oracle import restatement as R
+    from recformer_amd.synth import synth_batch
+    cfg = dict(C1, attention_window=[128, 512])
+    batch = synth_batch(3, 300, C1["vocab_size"], seed=12, lens=[300, 211, 40], extra_globals=((1, 150),))
+    lf = hashed_model(cfg, seed=3)
+    with torch.no_grad():
+        ref, ref_pooled = R.model_forward(lf.state_dict(), lf.config, **batch)
+    m, ctx = _prep(lf, dev, mode)
+    with torch.no_grad(), ctx:
+        out = m(**{k: v.to(dev) for k, v in batch.items()})
+    assert out.last_hidden_state.shape == ref.shape
+    _check_e2e(mode, errs(out.last_hidden_state, ref), out.pooler_output, ref_pooled)
