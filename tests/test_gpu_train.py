@@ -725,3 +725,26 @@ def test_global_query_bwd_matches_torch(dev, dt):
     other = torch.ones(B * Lp, dtype=torch.bool, device=dev)
     other[rows[keep[:, 0] > 0]] = False
     assert torch.equal(dh[other], before[other])
+
+
+@pytest.mark.parametrize("kind", ["full", "sampled"])
+def test_hip_head_at_10k_items_matches_reference(dev, kind):
+    """The HIP training head (train.cos_scores_train on rf_cos_score_*, rf_cos_score_bwd and
+    train.cross_entropy_train on rf_cross_entropy_*) at C3's 10,000-item catalog against the
+    reference's own head (tests/golden/c3_head.npz): loss <= 1e-5 abs, dL/dz <= 1e-4 x max|dz|."""
+    from recformer_amd import train
+    from recformer_amd.hashinit import hash_tensor
+    g = load_golden("c3_head")
+    table = hash_tensor("catalog", (10000, 768), "weight", seed=4, std=1.0).to(dev).contiguous()
+    rnorm = ops.row_inv_norm(table)
+    z = hash_tensor("pooled", (16, 768), "weight", seed=9, std=1.0).to(dev).requires_grad_(True)
+    if kind == "full":
+        loss = train.cross_entropy_train(train.cos_scores_train(z, table, rnorm, 20.0), g["labels"].to(dev))
+    else:
+        logits = train.cos_scores_train(z, table, rnorm, 20.0, g["candidates"].to(dev).long())
+        loss = train.cross_entropy_train(logits, torch.zeros(16, dtype=torch.long, device=dev))
+    loss.backward()
+    assert abs(float(loss) - float(g["loss_" + kind])) <= 1e-5, (float(loss), float(g["loss_" + kind]))
+    ref = g["dz_" + kind]
+    err = float((z.grad.cpu() - ref).abs().max())
+    assert err <= 1e-4 * float(ref.abs().max()), (err, float(ref.abs().max()))

@@ -95,3 +95,23 @@ def test_attention_probs_match_reference(case):
     for i, (local, glob) in enumerate(po):
         assert errs(local[:, :, :L], a[f"a{i}"])["max"] <= 1e-6
         assert errs(glob.transpose(2, 3), a[f"g{i}"])["max"] <= 1e-6
+
+
+def test_head_at_10k_items_matches_reference():
+    """The restated scoring head (cosine / temp + CrossEntropy) against the reference's own
+    RecformerForSeqRec head on a 10,000-item frozen catalog (tests/golden/c3_head.npz,
+    oracle/gen_golden_head.py): full and sampled softmax, loss and dL/dz."""
+    from recformer_amd.hashinit import hash_tensor
+    g = load_golden("c3_head")
+    items = hash_tensor("catalog", (10000, 768), "weight", seed=4, std=1.0)
+    z0 = hash_tensor("pooled", (16, 768), "weight", seed=9, std=1.0)
+    for kind in ("full", "sampled"):
+        z = z0.clone().requires_grad_(True)
+        if kind == "full":
+            loss = R.seqrec_loss(R.cosine_scores(z, items, 0.05), g["labels"].long())
+        else:
+            cand = g["candidates"].long()
+            loss = R.seqrec_loss(R.cosine_scores(z, items[cand], 0.05), torch.zeros(16, dtype=torch.long))
+        loss.backward()
+        assert abs(float(loss) - float(g["loss_" + kind])) <= 1e-5
+        assert errs(z.grad, g["dz_" + kind])["max"] <= 1e-7
