@@ -1898,6 +1898,17 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
       default: break;
     }
 #endif
+    if constexpr (EPI == RF_EPI_DGELU || EPI == RF_EPI_BIAS_GELU_AUX) {
+      // A/B: smaller tiles with several workgroups per CU for the epilogue-heavy training shapes
+      if (g_knob[KNOB_EPI_TILE] == 1) {
+        launch_bf16<E, 128, 128, 64, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+        return;
+      }
+      if (g_knob[KNOB_EPI_TILE] == 2) {
+        launch_bf16<E, 256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+        return;
+      }
+    }
     if constexpr (!RF32 && EPI != RF_EPI_BIAS_RESID && EPI != RF_EPI_BIAS_RESID_LN) {
       const int64_t cb = (CF32 || EPI == RF_EPI_COS) ? 4 : 2;
       const bool w32_ok = N % 8 == 0 && (int64_t)256 * e.ldc * cb < 0x7FFFFFFF &&

@@ -12,6 +12,7 @@
 #   lines      C3 (captured bf16 / fp16+GradScaler+accumulation+clip, eager), C4 (captured, 4 and 32 per
 #              rank) and C5 (retrieval, catalog encode) lines plus the retrieval kernel trace
 #   trainprof  rocprofv3 kernel trace of the captured C3 step ($TRAIN_ARGS)
+#   abc3       captured-C3 A/Bs listed in $AB (knob:<name>[=a,b] or a Python flag), $TRAIN_ARGS appended
 #   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3;
 #              C5 retrieval with the 32x32x16 rank kernel (knob rank_w32) alternated by process
 set -o pipefail
@@ -73,6 +74,16 @@ case $MODE in
       echo "$k" >> $O/ab_c5.log
     done
     grep -E "rank_w32|ms" $O/ab_c5.log | cut -c1-250 ;;
+  abc3)
+    # captured C3 steps, one same-process A/B per entry of $AB: knob:<name>[=a,b] or a Python flag name
+    n=0
+    for x in ${AB:?AB}; do
+      n=$((n + 1))
+      case $x in knob:*) arg="--ab-knob ${x#knob:}" ;; *) arg="--ab $x" ;; esac
+      timeout -k 10 500 python tools/train_bench.py --graph --steps 8 --warmup 2 ${TRAIN_ARGS:-} $arg \
+        > $O/abc3_$n.log 2>&1 || fail $O/abc3_$n.log
+      echo "== $x"; tail -2 $O/abc3_$n.log
+    done ;;
   lines)
     for args in "--graph" "--graph --dtype fp16 --accum 2 --clip 1.0" "--graph --negatives 1000" ""; do
       timeout -k 10 300 python tools/train_bench.py --steps 8 --warmup 2 $args > $O/c3.log 2>&1 || fail $O/c3.log 20
