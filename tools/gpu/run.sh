@@ -11,6 +11,7 @@
 #              alternated twice (tools/gemm_var.py)
 #   lines      C3 (captured bf16 / fp16+GradScaler+accumulation+clip, eager), C4 (captured, 4 and 32 per
 #              rank) and C5 (retrieval, catalog encode) lines plus the retrieval kernel trace
+#   torchops   the Python lines that launch torch (non-HIP) kernels in one eager C3 step
 #   trainprof  rocprofv3 kernel trace of the captured C3 step ($TRAIN_ARGS)
 #   abc3       captured-C3 A/Bs listed in $AB (knob:<name>[=a,b] or a Python flag), $TRAIN_ARGS appended
 #   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3;
@@ -101,6 +102,9 @@ case $MODE in
       python3 tools/retrieval_bench.py > $O/retrieval_trace.log 2>&1 || fail $O/retrieval_trace.log 20
     timeout -k 10 600 python tools/catalog_bench.py > $O/catalog.log 2>&1 || fail $O/catalog.log 20
     tail -2 $O/catalog.log ;;
+  torchops)
+    timeout -k 10 300 python tools/torch_ops_trace.py > $O/torchops.txt 2>&1 || fail $O/torchops.txt 20
+    head -80 $O/torchops.txt ;;
   trainprof)
     TRAIN_OUT=$TAG/trace TRAIN_ARGS=${TRAIN_ARGS:---graph} bash tools/gpu/trainprof.sh > $O/trainprof.txt 2>&1 \
       || fail $O/trainprof.txt 20
