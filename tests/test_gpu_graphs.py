@@ -306,7 +306,9 @@ def test_captured_dp_step_nccl_single_rank(dev):
             step(batch)
             step(batch)
             eager()
-        assert bk.collectives == n0 + len(bk.buckets)  # launched once, at capture; replays re-run them
+        # launched from Python at warmup and at capture only (n0 counts them); replays re-run the captured ones
+        assert n0 >= 2 * len(bk.buckets)
+        assert bk.collectives == n0
         for (n, x), y in zip(a.named_parameters(), b.parameters()):
             assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), n
     finally:
