@@ -31,7 +31,7 @@ case $MODE in
       || fail $O/smoke.log 5
     tail -1 $O/smoke.log ;;
   tests)
-    timeout -k 10 900 python -u -m pytest ${TESTS:-tests -m gpu} -x -v --timeout 300 --timeout-method thread \
+    timeout -k 10 900 python -u -m pytest ${TESTS:-tests -m gpu} ${PYTEST_X--x} -v --timeout 300 --timeout-method thread \
       > $O/pytest.log 2>&1 || { grep -E "^E  |FAILED" $O/pytest.log | cut -c1-300 | head -30; fail $O/pytest.log 5; }
     grep -E "passed|failed" $O/pytest.log | tail -1
     timeout -k 10 300 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 > $O/bench.log 2>&1 \
