@@ -1457,7 +1457,7 @@ struct W32GemmPol {
   constexpr int CB = OUT32 ? 4 : (int)sizeof(E);
   const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<char*>(e.C) + (int64_t)m0 * e.ldc * CB, (short)0, rows_valid * e.ldc * CB, 0x00020000);
-  const uint32_t lbC = col_ok ? (uint32_t)((rowl * e.ldc + coll) * CB) : 0x80000000u;
+  const uint32_t lbC = col_ok ? (uint32_t)((rowl * e.ldc + ecol) * CB) : 0x80000000u;
   const int rstepC = e.ldc * CB;
   constexpr bool HAS_R = EPI == RF_EPI_DGELU || EPI == RF_EPI_BIAS_GELU_AUX;
   __amdgpu_buffer_rsrc_t rsR = rsC;
@@ -1467,7 +1467,7 @@ struct W32GemmPol {
     rsR = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>(reinterpret_cast<const char*>(e.R)) + (int64_t)m0 * e.ldr * (int)sizeof(E), (short)0,
         rows_valid * e.ldr * (int)sizeof(E), 0x00020000);
-    lbR = col_ok ? (uint32_t)((rowl * e.ldr + coll) * (int)sizeof(E)) : 0x80000000u;
+    lbR = col_ok ? (uint32_t)((rowl * e.ldr + ecol) * (int)sizeof(E)) : 0x80000000u;
     rstepR = e.ldr * (int)sizeof(E);
   }
   float bv[4], gm[4], bt[4];
