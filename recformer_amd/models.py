@@ -252,6 +252,9 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     if s is None:
         s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(dev)
     return s
+# inference callers that read only the pooled CLS vectors (RecformerForSeqRec scores, the catalog
+# encoder): the last layer on the CLS rows only when every CLS is a global token (_cls_last_layer)
+PRUNE_LAST_LAYER = True
 # training: RecformerForPretraining's four encoder passes share one autograd cast per weight
 SHARE_TRAIN_CASTS = True
 # set by graphs.GraphedForward during capture: the global-slot count of the captured shape
@@ -261,18 +264,18 @@ ASYNC_GLOBAL_COUNT = True
 
 
 def _async_count(t: torch.Tensor):
-    """Start copying a device integer scalar to pinned host memory (no host wait yet)."""
-    buf = torch.empty((), dtype=t.dtype, pin_memory=True)
+    """Start copying a device integer scalar (or small vector) to pinned host memory (no host wait yet)."""
+    buf = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
     buf.copy_(t, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
     return buf, ev
 
 
-def _read_count(p) -> int:
+def _read_count(p):
     buf, ev = p
     ev.synchronize()
-    return int(buf)
+    return int(buf) if buf.dim() == 0 else [int(x) for x in buf.tolist()]
 # pretraining training: the LM-head decoder + masked-LM cross entropy on the HIP kernels
 # (train._DecoderCE) for 16-bit compute; False = torch ops (F.linear + F.cross_entropy)
 DECODER_CE_HIP = True
@@ -437,7 +440,11 @@ class RecformerModel(nn.Module):
         output_attentions: Optional[bool] = None,
         output_hidden_states: Optional[bool] = None,
         return_dict: Optional[bool] = None,
+        _pooled_only: bool = False,
     ):
+        """models.py:274-356. `_pooled_only` (internal: RecformerForSeqRec and the catalog encoder, which
+        read pooler_output only) lets the inference path run the last layer on the CLS rows alone
+        (_cls_last_layer); last_hidden_state is then None."""
         cfg = self.config
         output_attentions = output_attentions if output_attentions is not None else cfg.output_attentions
         output_hidden_states = (output_hidden_states if output_hidden_states is not None
@@ -465,7 +472,9 @@ class RecformerModel(nn.Module):
             last, hidden_all = self._encode(input_ids, attention_mask, global_attention_mask,
                                             token_type_ids, position_ids, item_position_ids,
                                             output_hidden_states, word=word, head_cols=head_cols,
-                                            attn_probe=probe)
+                                            attn_probe=probe, pooled_only=_pooled_only)
+            if self._last_pruned:
+                return RecformerModelOutput(last_hidden_state=None, pooler_output=last)
         attentions = global_attentions = None
         if probe is not None:
             attentions = tuple(a for a, _ in probe)
@@ -487,8 +496,12 @@ class RecformerModel(nn.Module):
     @torch.no_grad()
     def _encode(self, input_ids, attention_mask, global_attention_mask, token_type_ids,
                 position_ids, item_position_ids, output_hidden_states, word=None, head_cols=None,
-                attn_probe=None):
+                attn_probe=None, pooled_only=False):
+        """(last_hidden_state, hidden_states); with `pooled_only` (callers that read the CLS rows only:
+        RecformerForSeqRec, the catalog encoder) it may return (pooled (B, d) fp32, None) instead —
+        see the last-layer note below; it says which through self._last_pruned."""
         cfg = self.config
+        self._last_pruned = False
         B, L = input_ids.shape
         W = self._window()
         Lp = L + (W - L % W) % W
@@ -506,6 +519,10 @@ class RecformerModel(nn.Module):
         # only after the token streams are prepared and the embedding + LayerNorm is queued, so the
         # GPU has work while the host reads (the global index table is prepared afterwards).
         pending = None
+        # pooled_only: whether every sequence's CLS (position 0) is a global token, read with the count
+        want_cls = (pooled_only and cfg.pooler_type == "cls" and PRUNE_LAST_LAYER and not output_hidden_states
+                    and attn_probe is None)
+        cls_global = False
         if _STATIC_GMAX is not None:
             gmax = _STATIC_GMAX
         elif global_attention_mask is not None and B > 0:
@@ -513,10 +530,12 @@ class RecformerModel(nn.Module):
             if attention_mask is not None:
                 gm = gm & (attention_mask > 0)
             if ASYNC_GLOBAL_COUNT:
-                pending = _async_count(gm.sum(1).max())
+                cnt = gm.sum(1).max()
+                pending = _async_count(torch.stack([cnt, gm[:, 0].all().to(cnt.dtype)]) if want_cls else cnt)
                 gmax = 0
             else:
                 gmax = int(gm.sum(1).max().item())
+                cls_global = want_cls and bool(gm[:, 0].all())
         else:
             gmax = 0
         ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
@@ -526,9 +545,11 @@ class RecformerModel(nn.Module):
         def _globals():
             # the global index table once the count is known (re-runs the prologue with gmax slots;
             # the token streams it rewrites are identical)
-            nonlocal gmax, flags, gidx
+            nonlocal gmax, flags, gidx, cls_global
             if pending is not None:
                 gmax = _read_count(pending)
+                if want_cls:
+                    gmax, cls_global = gmax[0], bool(gmax[1])
                 if gmax > 0:
                     _, _, _, _, flags, gidx = ops.prepare_inputs(
                         input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
@@ -571,6 +592,10 @@ class RecformerModel(nn.Module):
             gargs = (h, lw["w_qg"], lw["b_qg"], scale, lw["w_qkv"][3 * D:4 * D], lw["b_qkv"][3 * D:4 * D],
                      lw["w_qkv"][4 * D:5 * D], lw["b_qkv"][4 * D:5 * D], flags, gidx, B, Lp, H)
             early = gmax > 0 and fold and FOLD_EARLY
+            if li == nl - 1 and cls_global and gmax > 0 and fold and h.is_cuda:
+                self._last_pruned = True
+                return _cls_last_layer(self, lw, gargs, gws, h, h_lo if split else None, h32, head_cols, li,
+                                       B, Lp, D, H, dt, mixed), None
             side = early and FOLD_OVERLAP and h.is_cuda
             if early:
                 if gws is None:
@@ -650,6 +675,47 @@ class RecformerModel(nn.Module):
         return last, hidden_all
 
 
+def _cls_last_layer(model, lw, gargs, gws, h, h_lo, h32, head_cols, li, B, Lp, D, H, dt, mixed):
+    """The last layer on the CLS rows only (RecformerModel._encode with pooled_only).
+
+    The pooler reads row 0 of the last layer's output (models.py:160-171) and RecformerForSeqRec /
+    the catalog encoder read nothing else (similarity_score and the loss, models.py:539-599;
+    finetune.py:38-63). Each output row of a layer depends on the other rows only through attention;
+    a global token's attention output is the global path's (TF:612-629), which the fold computes from
+    the layer input h alone. So with every CLS global the last layer is: the fold, then the output
+    projection, residual LayerNorm, FFN and LayerNorm on the B CLS rows — the same arithmetic as the
+    full layer for those rows, without the qkv GEMM, the band attention and the other B(Lp-1) rows.
+    Returns the pooled vectors (B, d) fp32."""
+    eps = model.config.layer_norm_eps
+    dev = h.device
+    if gws is None:
+        gws = ops.global_fold_workspace(h, B, Lp, H, gargs[9].shape[1])  # gargs[9]: gidx
+    ctx = torch.empty(B * Lp, D, dtype=h.dtype, device=dev)  # the fold writes the global rows only
+    ops.global_attention_fold_h_stage(1, gws, *gargs, tag="global_attn")
+    ops.global_attention_fold_h_stage(2, gws, *gargs, out=ctx, tag="global_attn")
+    rows = torch.arange(B, device=dev) * Lp
+    c = ctx.index_select(0, rows)
+    if h_lo is not None:
+        res = ops.join_split(h.index_select(0, rows), h_lo.index_select(0, rows))
+    else:
+        res = h32.index_select(0, rows).float().contiguous()
+    w_o = lw["w_o"]
+    if head_cols is not None:
+        w_o = (w_o.float() * head_cols[li]).to(w_o.dtype).contiguous()
+    if not mixed:
+        t = ops.gemm(c, w_o, lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=res, tag="gemm_out")
+        a = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], eps, out=t, tag="layernorm")
+        f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
+        t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a, tag="gemm_ffn2")
+        return ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out=t2, tag="layernorm")
+    t = ops.gemm(c, w_o, lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
+    a, a32 = ops.add_layernorm(t, res, lw["ln1_w"], lw["ln1_b"], eps, out_dtype=dt, tag="layernorm")
+    f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
+    t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS, tag="gemm_ffn2")
+    _, y32 = ops.add_layernorm(t2, a32, lw["ln2_w"], lw["ln2_b"], eps, out_dtype=dt, tag="layernorm")
+    return y32
+
+
 class RecformerForSeqRec(nn.Module):
     """models.py:524-599 on HIP kernels (scores via normalize + MFMA GEMM, never the
     (B,N,d) broadcast of nn.CosineSimilarity)."""
@@ -701,7 +767,8 @@ class RecformerForSeqRec(nn.Module):
                                   token_type_ids=token_type_ids, position_ids=position_ids,
                                   item_position_ids=item_position_ids, inputs_embeds=inputs_embeds,
                                   output_attentions=output_attentions,
-                                  output_hidden_states=output_hidden_states, return_dict=True)
+                                  output_hidden_states=output_hidden_states, return_dict=True,
+                                  _pooled_only=True)
         pooler_output = outputs.pooler_output
         if _needs_grad(self) and SCORE_HEAD_HIP and not self.item_embedding.weight.requires_grad and \
                 pooler_output.is_cuda:

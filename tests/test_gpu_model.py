@@ -414,3 +414,28 @@ def test_per_layer_windows_vs_oracle(dev, mode):
         out = m(**{k: v.to(dev) for k, v in batch.items()})
     assert out.last_hidden_state.shape == ref.shape
     _check_e2e(mode, errs(out.last_hidden_state, ref), out.pooler_output, ref_pooled)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
+def test_cls_last_layer_matches_full(dev, monkeypatch, mode):
+    """RecformerForSeqRec's scores with the last layer on the CLS rows only (models._cls_last_layer:
+    the pooler reads row 0, a global token whose output is the fold's) equal the scores with every row
+    through the last layer; without a global CLS the full layer runs."""
+    from recformer_amd import models
+    g = load_golden("c2_12l")
+    m = hashed_model(BASE, seed=2, cls=RecformerForSeqRec, item_num=1000)
+    m.init_item_embedding(hash_tensor("catalog", (1000, 768), "weight", seed=3, std=1.0))
+    m, ctx = _prep(m, dev, mode)
+    batch = {k: v.to(dev) for k, v in batch_of(g).items()}
+    res = {}
+    for prune in (False, True):
+        monkeypatch.setattr(models, "PRUNE_LAST_LAYER", prune)
+        with torch.no_grad(), ctx:
+            res[prune] = m(**batch).float()
+            assert m.longformer._last_pruned == prune
+    tol = 1e-3 if mode == "fp32" else 2e-2
+    assert float((res[True] - res[False]).abs().max()) <= tol
+    nog = dict(batch, global_attention_mask=None)
+    with torch.no_grad(), ctx:
+        m(**nog)
+    assert not m.longformer._last_pruned

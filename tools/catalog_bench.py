@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--dtype", choices=["fp16", "bf16"], default="fp16")
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--pad64", action="store_true", help="pad L=33 to the 64-token window (no short path)")
+    ap.add_argument("--full-last-layer", action="store_true", help="A/B: every row through the last layer")
     a = ap.parse_args()
     if a.pad64:
         from recformer_amd import models
@@ -54,7 +55,9 @@ def main():
         t0 = time.perf_counter()
         for s in range(lo, hi, a.batch):
             n = min(a.batch, hi - s)
-            embs.append(model(**{k: v[:n] for k, v in tmpl.items()}).pooler_output.to(dt))
+            # pooler_output only (finetune.py:38-63): the last layer runs on the CLS rows (models._cls_last_layer)
+            embs.append(model(**{k: v[:n] for k, v in tmpl.items()}, _pooled_only=not a.full_last_layer)
+                        .pooler_output.to(dt))
         torch.cuda.synchronize()
         t_enc = time.perf_counter() - t0
     shard = CatalogShard(torch.cat(embs, 0), base=lo)
