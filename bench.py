@@ -54,6 +54,9 @@ def parse():
                     help="thread counts for the CPU baseline: 'all' = every CPU this process may use "
                          "(affinity capped by the cgroup CPU quota), 'omp' = OMP_NUM_THREADS, or integers")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--full-last-layer", action="store_true",
+                    help="every row through the last layer (default: the CLS rows only, which is all the "
+                         "scores read; recformer_amd.models._cls_last_layer)")
     ap.add_argument("--timing-steps", type=int, default=20,
                     help="steps of the separate HIP-event-instrumented pass (per-kernel times)")
     return ap.parse_args()
@@ -245,8 +248,10 @@ def main():
     dev = torch.device("cuda", local)
     coll_dev = None if rehearsal else dev
 
-    from recformer_amd import RecformerConfig, RecformerForSeqRec, dp, ops
+    from recformer_amd import RecformerConfig, RecformerForSeqRec, dp, models, ops
     from recformer_amd.synth import BASE, synth_batch
+    if args.full_last_layer:
+        models.PRUNE_LAST_LAYER = False
 
     L, B = args.seq_len, args.batch
     cfg = RecformerConfig(**dict(BASE, num_hidden_layers=args.layers,
@@ -359,6 +364,8 @@ def main():
                                    "window 64, CLS global, 10k-item cosine scoring",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": L,
                        "catalog": args.catalog, "layers": args.layers,
+                       "last_layer": ("all rows" if args.full_last_layer else
+                                      "CLS rows only (the scores read nothing else; same scores)"),
                        "parallelism": f"dp{world} (independent sequence shards, replicated catalog)",
                        **({"ranks_share_devices": ndev} if rehearsal else {})},
             "roofline": roofline,

@@ -703,16 +703,16 @@ def _cls_last_layer(model, lw, gargs, gws, h, h_lo, h32, head_cols, li, B, Lp, D
     if head_cols is not None:
         w_o = (w_o.float() * head_cols[li]).to(w_o.dtype).contiguous()
     if not mixed:
-        t = ops.gemm(c, w_o, lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=res, tag="gemm_out")
-        a = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], eps, out=t, tag="layernorm")
-        f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
-        t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a, tag="gemm_ffn2")
-        return ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out=t2, tag="layernorm")
-    t = ops.gemm(c, w_o, lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
-    a, a32 = ops.add_layernorm(t, res, lw["ln1_w"], lw["ln1_b"], eps, out_dtype=dt, tag="layernorm")
-    f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
-    t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS, tag="gemm_ffn2")
-    _, y32 = ops.add_layernorm(t2, a32, lw["ln2_w"], lw["ln2_b"], eps, out_dtype=dt, tag="layernorm")
+        t = ops.gemm(c, w_o, lw["b_o"], ops.RF_EPI_BIAS_RESID, resid=res, tag="cls_gemm_out")
+        a = ops.layernorm(t, lw["ln1_w"], lw["ln1_b"], eps, out=t, tag="cls_layernorm")
+        f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="cls_gemm_ffn1")
+        t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS_RESID, resid=a, tag="cls_gemm_ffn2")
+        return ops.layernorm(t2, lw["ln2_w"], lw["ln2_b"], eps, out=t2, tag="cls_layernorm")
+    t = ops.gemm(c, w_o, lw["b_o"], ops.RF_EPI_BIAS, tag="cls_gemm_out")
+    a, a32 = ops.add_layernorm(t, res, lw["ln1_w"], lw["ln1_b"], eps, out_dtype=dt, tag="cls_layernorm")
+    f = ops.gemm(a, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="cls_gemm_ffn1")
+    t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS, tag="cls_gemm_ffn2")
+    _, y32 = ops.add_layernorm(t2, a32, lw["ln2_w"], lw["ln2_b"], eps, out_dtype=dt, tag="cls_layernorm")
     return y32
 
 
