@@ -116,6 +116,22 @@ def static_gmax(batch: Dict[str, torch.Tensor]) -> int:
     return g
 
 
+def static_cls_global(batch: Dict[str, torch.Tensor]) -> bool:
+    """Whether position 0 is a (valid) global token in every sequence of every view (host read): the
+    condition for the CLS-only last layer (train._GlobalCLS)."""
+    seen = False
+    for k, v in batch.items():
+        if k.startswith("global_attention_mask") and torch.is_tensor(v):
+            am = batch.get("attention_mask" + k[len("global_attention_mask"):])
+            gm = v[:, 0] != 0
+            if am is not None:
+                gm = gm & (am[:, 0] > 0)
+            if not bool(gm.all()):
+                return False
+            seen = True
+    return seen
+
+
 def mlm_rows(batch: Dict[str, torch.Tensor]) -> int:
     """Largest number of labelled masked-LM tokens in any view of the batch (host read)."""
     n = 0
@@ -197,6 +213,7 @@ class CapturedTrainStep:
         dev = next(model.parameters()).device
         self.static = {k: (v.to(dev).clone() if torch.is_tensor(v) else v) for k, v in example.items()}
         self.gmax = static_gmax(self.static)
+        self.cls_global = static_cls_global(self.static)
         n = mlm_rows(self.static)
         self.mlm_cap = ((int(n * mlm_slack) + 63) // 64) * 64 if n else None
         self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -229,8 +246,8 @@ class CapturedTrainStep:
             for i in range(self.k):
                 micro(i == self.k - 1)
 
-        old_g, old_m = train._STATIC_GMAX, models._STATIC_MLM_ROWS
-        train._STATIC_GMAX, models._STATIC_MLM_ROWS = self.gmax, self.mlm_cap
+        old_g, old_m, old_c = train._STATIC_GMAX, models._STATIC_MLM_ROWS, train._STATIC_CLS
+        train._STATIC_GMAX, models._STATIC_MLM_ROWS, train._STATIC_CLS = self.gmax, self.mlm_cap, self.cls_global
         try:
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -270,7 +287,10 @@ class CapturedTrainStep:
                 lib.rf_set_seed_source(old_src)
                 dropout.set_seed_counter(old_py)
         finally:
-            train._STATIC_GMAX, models._STATIC_MLM_ROWS = old_g, old_m
+            train._STATIC_GMAX, models._STATIC_MLM_ROWS, train._STATIC_CLS = old_g, old_m, old_c
+        # the replay check on CLS-global batches only matters when the capture used the CLS-only layer
+        lf = getattr(self.model, "longformer", self.model)
+        self.cls_global = self.cls_global and bool(getattr(lf, "_last_pruned", False))
         self.replays = 0
 
     def _optimizer_part(self):
@@ -307,6 +327,9 @@ class CapturedTrainStep:
                 g = static_gmax(batch)
                 if g > self.gmax:
                     raise ValueError(f"batch has {g} global tokens in a sequence; the step was captured for {self.gmax}")
+                if self.cls_global and not static_cls_global(batch):
+                    raise ValueError("the step was captured with a global CLS token in every sequence (the "
+                                     "CLS-only last layer); this batch has a sequence without one")
                 n = mlm_rows(batch)
                 if n and (self.mlm_cap is None or n > self.mlm_cap):
                     raise ValueError(f"batch has {n} masked-LM labels in a view; the step was captured for {self.mlm_cap}")

@@ -467,7 +467,9 @@ class RecformerModel(nn.Module):
             last, hidden_all = encode_train(self, input_ids, attention_mask, global_attention_mask,
                                             token_type_ids, position_ids, item_position_ids,
                                             output_hidden_states, word=word, head_cols=head_cols,
-                                            attn_probe=probe)
+                                            attn_probe=probe, pooled_only=_pooled_only)
+            if self._last_pruned:
+                return RecformerModelOutput(last_hidden_state=None, pooler_output=last)
         else:
             last, hidden_all = self._encode(input_ids, attention_mask, global_attention_mask,
                                             token_type_ids, position_ids, item_position_ids,

@@ -1121,13 +1121,77 @@ def _lin(a, lw, wkey: str, bkey: str, scale_cols: int, col_scale: float):
     return _Gemm.apply(a, *lw[wkey], lw[bkey], scale_cols, col_scale)
 
 
+class _GlobalCLS(torch.autograd.Function):
+    """The last layer's attention output at the B CLS rows only (encode_train with pooled_only; the
+    training form of models._cls_last_layer): the global rows through the fold kernels (with the
+    attention-dropout mask of `seed`), the CLS rows returned; backward = rf_global_fold_bwd_full with
+    the CLS rows' gradient (nothing reads the other rows, so their gradient is zero) — no qkv GEMM and
+    no band attention either way. Inputs (qg, h, wkg, bkg, wvg, bvg) as _Attention's global part; with
+    the fp32 masters given, the key / value weight gradients go to them."""
+
+    @staticmethod
+    def forward(ctx, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, attn_p, seed, ws, wkg_master=None,
+                wvg_master=None):
+        D = h.shape[1]
+        out = torch.empty(B * Lp, D, dtype=h.dtype, device=h.device)
+        ops.global_attention_fold(qg.contiguous(), h.contiguous(), wkg.contiguous(), bkg, wvg.contiguous(), bvg,
+                                  flags, gidx, B, Lp, H, out, p_drop=attn_p, seed=seed, ws=ws)
+        rows = torch.arange(B, device=h.device) * Lp
+        ctx.save_for_backward(qg, h, wkg, wvg, bvg, flags, gidx, rows)
+        ctx.meta = (B, Lp, H, attn_p, seed, ws, wkg_master is not None)
+        return out.index_select(0, rows)
+
+    @staticmethod
+    def backward(ctx, dcls):
+        qg, h, wkg, wvg, bvg, flags, gidx, rows = ctx.saved_tensors
+        B, Lp, H, p, seed, ws, masters = ctx.meta
+        d16 = torch.zeros(B * Lp, h.shape[1], dtype=h.dtype, device=h.device)
+        d16.index_copy_(0, rows, dcls.to(h.dtype))
+        with torch.autocast("cuda", enabled=False):
+            dqg, dh, dwkg, dbkg, dwvg, dbvg = _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B, Lp, H, d16,
+                                                              ws, p, seed)
+        need = ctx.needs_input_grad
+        res = [dqg.to(qg.dtype) if need[0] else None, dh.to(h.dtype) if need[1] else None,
+               None if masters or not need[2] else dwkg.to(wkg.dtype), dbkg if need[3] else None,
+               None if masters or not need[4] else dwvg.to(wvg.dtype), dbvg if need[5] else None]
+        tail = [None] * 8
+        if masters:
+            tail[6] = dwkg.float() if need[14] else None
+            tail[7] = dwvg.float() if need[15] else None
+        return (*res, *tail)
+
+
+class _ZeroGrads(torch.autograd.Function):
+    """Identity on x whose backward also gives the listed parameters an all-zero gradient: the last
+    layer's local query / key / value projections do not reach the CLS rows (their gradient in the full
+    layer is exactly zero), and the optimizer must see a zero gradient — not None — to apply weight
+    decay to them as it does after the full layer's backward."""
+
+    @staticmethod
+    def forward(ctx, x, *params):
+        ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dx):
+        return (dx, *[torch.zeros(s, dtype=d, device=dv) for s, d, dv in ctx.shapes])
+
+
+# the CLS-global flag of a captured step's example batch (recformer_amd.graphs), as _STATIC_GMAX
+_STATIC_CLS: Optional[bool] = None
+
+
 def encode_train(model, input_ids, attention_mask, global_attention_mask, token_type_ids,
                  position_ids, item_position_ids, output_hidden_states: bool, word=None, head_cols=None,
-                 attn_probe=None) -> Tuple[torch.Tensor, Optional[tuple]]:
+                 attn_probe=None, pooled_only: bool = False) -> Tuple[torch.Tensor, Optional[tuple]]:
     """Autograd forward of RecformerModel (same outputs as RecformerModel._encode). `word` replaces the
     word-embedding table (inputs_embeds, models._embeds_as_table); `head_cols` (layers, hidden) scales
     each layer's attention context (head_mask, models._head_mask_columns); `attn_probe`, a list, receives
-    each layer's (attentions, global_attentions) (output_attentions, recformer_amd/probs.py)."""
+    each layer's (attentions, global_attentions) (output_attentions, recformer_amd/probs.py). With
+    `pooled_only` (RecformerForSeqRec: the loss reads the CLS rows only) and every CLS a global token,
+    the last layer runs on the CLS rows (_GlobalCLS) and (pooled (B, d) fp32, None) is returned, with
+    model._last_pruned set."""
+    model._last_pruned = False
     from .models import _compute_dtype
     cfg = model.config
     B, L = input_ids.shape
@@ -1146,8 +1210,18 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
         # a captured step (recformer_amd.graphs) fixes the global-slot count: no host sync, empty slots
         # (gidx < 0) are inert
         gmax = _STATIC_GMAX if _STATIC_GMAX is not None else (int(gm.sum(1).max().item()) if B > 0 else 0)
+        from . import models as _models
+        want = pooled_only and _models.PRUNE_LAST_LAYER and cfg.pooler_type == "cls" and not output_hidden_states \
+            and attn_probe is None and B > 0
+        if not want:
+            cls_global = False
+        elif _STATIC_GMAX is not None:
+            cls_global = bool(_STATIC_CLS)
+        else:
+            cls_global = bool(gm[:, 0].all())
     else:
         gmax = 0
+        cls_global = False
     ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
         input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
         position_ids, Lp, cfg.pad_token_id, gmax)
@@ -1184,6 +1258,13 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     for li, lyr in enumerate(model.encoder.layer):
         lw = packed[li] if packed is not None else _layer_weights(li, lyr, dt)
         h = h16 if h16 is not None else h32.to(dt)
+        if li == nl - 1 and cls_global and fold and fused and gmax > 0 and h.is_cuda:
+            ws = _fold_ws(h, B, Lp, H, gmax)
+            if ws is not None:
+                model._last_pruned = True
+                return _cls_last_layer_train(model, lyr, lw, h, h32, rows, gvalid, flags, gidx, B, Lp, H, D, dt,
+                                             scale, eps, p_hid, p_att, seeds[2 * li:2 * li + 2], att_seeds[li], ws,
+                                             head_cols, li), None
         if attn_probe is not None:
             from .probs import layer_attention_probs
             attn_probe.append(layer_attention_probs(
@@ -1240,3 +1321,38 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
     if output_hidden_states:
         hidden_all = tuple(x.view(B, Lp, D)[:, :L] for x in hidden_all)
     return last, hidden_all
+
+
+def _cls_last_layer_train(model, lyr, lw, h, h32, rows, gvalid, flags, gidx, B: int, Lp: int, H: int, D: int, dt,
+                          scale: float, eps: float, p_hid: float, p_att: float, seeds, att_seed: int, ws, head_cols,
+                          li: int) -> torch.Tensor:
+    """encode_train's last layer on the CLS rows (see _GlobalCLS): query_global on the global rows,
+    the fold at the CLS rows, then the output projection, residual LayerNorms and FFN on B rows.
+    Returns the pooled vectors (B, d) fp32 (differentiable)."""
+    hg = h[rows] * gvalid.to(h.dtype)
+    qg = _lin(hg, lw, "w_qg", "b_qg", D, scale)
+    c = _GlobalCLS.apply(qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"], flags, gidx, B, Lp, H, p_att,
+                         att_seed, ws, lw.get("wkg_master"), lw.get("wvg_master"))
+    if head_cols is not None:
+        c = c * head_cols[li].to(c.dtype)
+    cls = torch.arange(B, device=h.device) * Lp
+    res = h32.index_select(0, cls)
+    ao, fo = lyr.attention.output, lyr.output
+    t = _lin(c, lw, "w_o", "b_o", 0, 1.0)
+    a32, a16 = _DropAddLN.apply(t, res, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid, True, seeds[0])
+    if lw.get("packed"):
+        (w1,), w1_16, w1t = lw["w_1"]
+        (w2,), w2_16, w2t = lw["w_2"]
+        t2 = _FFN.apply(a16, w1, w1_16, lw["b_1"], w2, w2_16, lw["b_2"], w1t, w2t)
+    elif FFN_FUSED and D % 64 == 0 and lw["w_1"][1].shape[0] % 64 == 0:
+        t2 = _FFN.apply(a16, *lw["w_1"], lw["b_1"], *lw["w_2"], lw["b_2"])
+    else:
+        if dt == torch.bfloat16 and FUSED_GELU:
+            u = _GemmGelu.apply(a16, *lw["w_1"], lw["b_1"])
+        else:
+            u = F.gelu(_Gemm.apply(a16, *lw["w_1"], lw["b_1"], 0, 1.0))
+        t2 = _Gemm.apply(u, *lw["w_2"], lw["b_2"], 0, 1.0)
+    y = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, False, seeds[1])
+    sa = lyr.attention.self
+    local = [p for m in (sa.query, sa.key, sa.value) for p in (m.weight, m.bias) if p.requires_grad]
+    return _ZeroGrads.apply(y, *local) if local else y

@@ -748,3 +748,42 @@ def test_hip_head_at_10k_items_matches_reference(dev, kind):
     ref = g["dz_" + kind]
     err = float((z.grad.cpu() - ref).abs().max())
     assert err <= 1e-4 * float(ref.abs().max()), (err, float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_cls_last_layer_training_matches_full(dev, monkeypatch, dtype):
+    """RecformerForSeqRec training with the last layer on the CLS rows (train._GlobalCLS; dropout off):
+    the loss and every parameter gradient equal the full last layer's — including exact zeros (not
+    None) for the last layer's local query / key / value projections, which never reach the CLS rows."""
+    from recformer_amd import models
+    g = load_golden("c1_ragged")
+    batch = {k: v.to(dev) for k, v in batch_of(g).items()}
+    labels = torch.tensor([3, 17, 0, 39], device=dev)
+    torch.manual_seed(0)
+    items = torch.randn(40, CFG["hidden_size"]) * 0.5
+    res = {}
+    for prune in (False, True):
+        monkeypatch.setattr(models, "PRUNE_LAST_LAYER", prune)
+        lf = hashed_model(CFG, seed=1)
+        m = RecformerForSeqRec(lf.config)
+        m.longformer.load_state_dict(lf.state_dict())
+        m.config.finetune_negative_sample_size = 0
+        m.init_item_embedding(items.clone())
+        m = m.to(dev).train()
+        with torch.autocast("cuda", dtype=dtype):
+            loss = m(**batch, labels=labels)
+        loss.backward()
+        assert m.longformer._last_pruned == prune
+        res[prune] = (float(loss), {k: p.grad for k, p in m.longformer.named_parameters()})
+    assert abs(res[True][0] - res[False][0]) <= 2e-3 * max(1.0, abs(res[False][0]))
+    nl = CFG["num_hidden_layers"]
+    for k, gf in res[False][1].items():
+        gp = res[True][1][k]
+        assert gp is not None, k
+        if f"layer.{nl - 1}.attention.self." in k and k.split(".")[-2] in ("query", "key", "value"):
+            assert not gp.any() and not gf.any(), k
+            continue
+        if float(gf.abs().max()) < 1e-7:
+            continue
+        cos = F.cosine_similarity(gp.float().reshape(1, -1), gf.float().reshape(1, -1)).item()
+        assert cos >= 0.999, (k, cos)
