@@ -1154,10 +1154,10 @@ class _GlobalCLS(torch.autograd.Function):
         res = [dqg.to(qg.dtype) if need[0] else None, dh.to(h.dtype) if need[1] else None,
                None if masters or not need[2] else dwkg.to(wkg.dtype), dbkg if need[3] else None,
                None if masters or not need[4] else dwvg.to(wvg.dtype), dbvg if need[5] else None]
-        tail = [None] * 8
+        tail = [None] * 10  # flags, gidx, B, Lp, H, attn_p, seed, ws, then the two masters
         if masters:
-            tail[6] = dwkg.float() if need[14] else None
-            tail[7] = dwvg.float() if need[15] else None
+            tail[8] = dwkg.float() if need[14] else None
+            tail[9] = dwvg.float() if need[15] else None
         return (*res, *tail)
 
 

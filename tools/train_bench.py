@@ -103,17 +103,29 @@ def main():
         opt.zero_grad(set_to_none=True)
         return loss
 
+    def set_switch(val):
+        """A/B switch: a train.py flag (or models.<flag>) at True / False, or a library knob at 1 / 0
+        (name=a,b: values a / b)."""
+        from recformer_amd import _lib, models, train
+        if a.ab:
+            mod, name = (models, a.ab[len("models."):]) if a.ab.startswith("models.") else (train, a.ab)
+            if not hasattr(mod, name):
+                raise SystemExit(f"unknown switch {a.ab}")
+            setattr(mod, name, val)
+            return
+        kname, kvals = a.ab_knob, (1, 0)
+        if "=" in a.ab_knob:
+            kname, v = a.ab_knob.split("=")
+            kvals = tuple(int(x) for x in v.split(","))
+        _lib.set_knob(kname, kvals[0] if val else kvals[1])
+
     if a.graph and (a.ab or a.ab_knob):
-        # captured A/B: one graph per value of the train.py switch (or library knob: the kernel choice
-        # is fixed at capture), replays alternated in one process
-        from recformer_amd import _lib, train
+        # captured A/B: one graph per value of the switch (a library knob's kernel choice is fixed at
+        # capture), replays alternated in one process
         from recformer_amd.graphs import CapturedTrainStep
         graphs = {}
         for val in (True, False):
-            if a.ab:
-                setattr(train, a.ab, val)
-            else:
-                _lib.set_knob(a.ab_knob, 1 if val else 0)
+            set_switch(val)
             graphs[val] = CapturedTrainStep(model, opt, dict(batch, labels=labels), autocast_dtype=dt,
                                             warmup=a.warmup, scaler=scaler, accumulation_steps=a.accum,
                                             max_grad_norm=a.clip)
@@ -148,18 +160,10 @@ def main():
     torch.cuda.synchronize()
     if a.ab or a.ab_knob:
         # clocks differ across boxes and drift under load: alternate blocks in one process
-        from recformer_amd import _lib, train
         res = {True: [], False: []}
-        kname, kvals = a.ab_knob, (1, 0)
-        if a.ab_knob and "=" in a.ab_knob:
-            kname, v = a.ab_knob.split("=")
-            kvals = tuple(int(x) for x in v.split(","))
         for rep in range(6):
             for val in (True, False):
-                if a.ab:
-                    setattr(train, a.ab, val)
-                else:
-                    _lib.set_knob(kname, kvals[0] if val else kvals[1])
+                set_switch(val)
                 step()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
