@@ -14,6 +14,7 @@
 #   torchops   the Python lines that launch torch (non-HIP) kernels in one eager C3 step
 #   trainprof  rocprofv3 kernel trace of the captured C3 step ($TRAIN_ARGS)
 #   abc3       captured-C3 A/Bs listed in $AB (knob:<name>[=a,b] or a Python flag), $TRAIN_ARGS appended
+#   abc5       C5 retrieval, rank_w32 0 / 1 alternated by process
 #   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3;
 #              C5 retrieval with the 32x32x16 rank kernel (knob rank_w32) alternated by process
 set -o pipefail
@@ -85,6 +86,13 @@ case $MODE in
         > $O/abc3_$n.log 2>&1 || fail $O/abc3_$n.log
       echo "== $x"; tail -2 $O/abc3_$n.log
     done ;;
+  abc5)
+    # C5 retrieval with the 32x32x16 rank kernel (knob rank_w32) alternated by process
+    for k in rank_w32=0 rank_w32=1 rank_w32=0 rank_w32=1; do
+      RF_KNOBS=$k timeout -k 10 300 python tools/retrieval_bench.py >> $O/ab_c5.log 2>&1 || fail $O/ab_c5.log
+      echo "$k" >> $O/ab_c5.log
+    done
+    grep -E "rank_w32|ms" $O/ab_c5.log | cut -c1-250 ;;
   lines)
     for args in "--graph" "--graph --dtype fp16 --accum 2 --clip 1.0" "--graph --negatives 1000" ""; do
       timeout -k 10 300 python tools/train_bench.py --steps 8 --warmup 2 $args > $O/c3.log 2>&1 || fail $O/c3.log 20
