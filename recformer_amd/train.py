@@ -137,15 +137,16 @@ def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
     S chunks computed as one batched GEMM (S times the tiles) and the S fp32 partials summed."""
     M, N = dc.shape
     K = a.shape[1]
-    if M < SMALL_M and dc.is_cuda and dc.dtype != torch.float32:
-        # a few rows (the global query rows): one library GEMM with fp32 output (the big-tile
-        # kernels would run one mostly empty K-step per tile)
-        return _mm_f32(dc.t(), a)
     if (DW_HIP and dc.is_cuda and dc.dtype in (torch.bfloat16, torch.float16) and a.dtype == dc.dtype
             and N % 16 == 0 and K % 16 == 0 and dc.stride(1) == 1 and a.stride(1) == 1
             and dc.stride(0) % 8 == 0 and a.stride(0) % 8 == 0
             and dc.data_ptr() % 16 == 0 and a.data_ptr() % 16 == 0):
+        # any M, including a few rows (the global query rows, the CLS-only last layer): the buffer
+        # resources read rows past M as zeros — no library GEMM (and no library workspace on the
+        # weight-gradient side stream, which a captured graph would own)
         return ops.weight_grad(dc, a)
+    if M < SMALL_M and dc.is_cuda and dc.dtype != torch.float32:
+        return _mm_f32(dc.t(), a)
     S = 1
     if DW_SPLIT_K and M >= 8192 and N * K <= 4 * 1024 * 1024:
         S = 8
@@ -227,7 +228,7 @@ class _GemmP(torch.autograd.Function):
         da = None
         join = _dw_async(lambda: _weight_grad(dc, a).to(ctx.wdt), dc) if any(ctx.needs_input_grad[6:]) else None
         if ctx.needs_input_grad[0]:
-            da = dc @ wt.t() if dc.shape[0] < SMALL_M else ops.gemm(dc, wt, None, ops.RF_EPI_NONE)
+            da = ops.gemm(dc, wt, None, ops.RF_EPI_NONE)  # any M (a few rows: the small-tile kernel)
         db = _bias_grad(dc) if ctx.needs_input_grad[1] else None
         dw = join() if join is not None else None
         if scaled:
