@@ -755,7 +755,8 @@ def test_gemm_dgelu_epilogue(dev, dt, M, N, K):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,N,K,strided", [(16384, 2304, 768, False), (16384, 768, 3072, False),
                                            (16384, 3072, 768, False), (1000, 768, 768, True), (333, 64, 128, False),
-                                           (70000, 768, 768, False), (64, 256, 272, False)])
+                                           (70000, 768, 768, False), (64, 256, 272, False), (4, 768, 768, False),
+                                           (16, 3072, 768, False), (1, 64, 128, False)])
 def test_weight_grad_matches_fp32_matmul(dev, dt, M, N, K, strided):
     """rf_weight_grad (dW = dC^T A on MFMA with transposed LDS reads, rows split over workgroups and
     reduced in a fixed order) against torch's fp32 product of the same 16-bit operands: products of
