@@ -1848,6 +1848,65 @@ static void launch_bf16(int M, int N, int K, const void* A, int lda, const void*
       K, (const E*)A, lda, (const E*)W, ldw, e, nTn);
 }
 
+// ---- a few rows (M <= 64): k_gemm_skinny ----------------------------------------------------------
+// The CLS-only last layer (B rows: the batch's CLS vectors) and the global query rows: with 128 x 128
+// tiles a 64-row product has N / 128 workgroups, each walking all of K alone (FFN2's 64 x 768 x 3072:
+// 6 workgroups, ~44 us). Here a workgroup owns 16 output columns and all M (<= 64) rows; its four
+// waves split K into quarters (v_mfma_f32_16x16x32: A fragments = 16 rows, B = the 16 W rows), and
+// the four partial 64 x 16 tiles are summed in LDS in a fixed order, then the scalar epilogue
+// (epi_store: bias and column scale, GELU, the pre-activation output, the GELU backward) writes them.
+// Fragments come straight from HBM / L2 (16 B per lane per operand and k-step); N / 16 workgroups.
+template <typename E, int EPI, bool CF32>
+__global__ void __launch_bounds__(256) k_gemm_skinny(int M, int K, const E* __restrict__ A, int lda,
+                                                      const E* __restrict__ W, int ldw, EpiArgs e) {
+  typedef typename H16<E>::x8 V8;
+  __shared__ float red[4][64][17];
+  const int n0 = blockIdx.x * 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int nmb = (M + 15) >> 4;
+  const int kq = K >> 2;  // this wave's quarter of K (a multiple of 32)
+  const int k0 = wave * kq;
+  const E* wrow = W + (int64_t)(n0 + li) * ldw + k0 + 8 * g;
+  const E* arow[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) arow[mb] = A + (int64_t)min(16 * mb + li, M - 1) * lda + k0 + 8 * g;
+  f32x4 acc[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int k = 0; k < kq; k += 32) {
+    const V8 b = *reinterpret_cast<const V8*>(wrow + k);
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+      if (mb < nmb) acc[mb] = mfma16(*reinterpret_cast<const V8*>(arow[mb] + k), b, acc[mb]);
+  }
+  // D[row 4g + r][col li] of each 16-row block
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][16 * mb + 4 * g + r][li] = acc[mb][r];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + 256 * i, row = idx >> 4, col = idx & 15;
+    if (row < M) {
+      const float v = ((red[0][row][col] + red[1][row][col]) + red[2][row][col]) + red[3][row][col];
+      epi_store<E, EPI, CF32, false>(e, row, n0 + col, v);
+    }
+  }
+}
+
+template <typename E, int EPI, bool CF32>
+static bool launch_skinny(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
+                          hipStream_t s) {
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!(M >= 1 && M <= 64 && N % 16 == 0 && K % 128 == 0 && lda % 8 == 0 && ldw % 8 == 0 && al16(A) && al16(W)))
+    return false;
+  k_gemm_skinny<E, EPI, CF32><<<N / 16, 256, 0, s>>>(M, K, (const E*)A, lda, (const E*)W, ldw, e);
+  return true;
+}
+
 // Variant selector for A/B timing (knob gemm_variant), tools/gemm_gn.py with the bench epilogues:
 //   8 (default) four-wave, phase B DMA and LDS reads alternating, zero-C first MFMAs, W fragments
 //     read first; with the stage-wise GELU: qkv 198, out-proj 68.5, FFN1 285, FFN2 247 us
@@ -1880,6 +1939,10 @@ static bool pp_cols_ok(int M, int N, const EpiArgs& e) {
 template <typename E, int EPI, bool CF32, bool RF32>
 static void dispatch_tile(int M, int N, int K, const void* A, int lda, const void* W, int ldw,
                           const EpiArgs& e, hipStream_t s) {
+  if constexpr (!RF32 && (EPI == RF_EPI_NONE || EPI == RF_EPI_BIAS || EPI == RF_EPI_BIAS_GELU ||
+                          EPI == RF_EPI_BIAS_GELU_AUX || EPI == RF_EPI_DGELU)) {
+    if (M <= 64 && g_knob[KNOB_GEMM_SKINNY] && launch_skinny<E, EPI, CF32>(M, N, K, A, lda, W, ldw, e, s)) return;
+  }
   // 256x256 when the grid still covers the chip; 128x128 for skinny problems
   const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
   const bool w4_ok = pp_cols_ok(M, N, e) && K % 64 == 0 && K >= 128 && (int64_t)M * lda * 2 < 0x7FFFFFFF &&

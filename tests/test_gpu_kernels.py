@@ -1021,3 +1021,42 @@ def test_cos_scores_bwd_matches_autograd(dev, dt, B, N, C):
     if dt != torch.float32:  # fixed-order sums: bit-identical on a repeat
         again = ops.cos_scores_bwd(z, items, gs.contiguous(), s.contiguous(), inv_t, ops.row_inv_norm(z), rt, cand)
         assert torch.equal(dz, again)
+
+
+@pytest.mark.parametrize("skinny", [0, 1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(64, 3072, 768), (16, 768, 3072), (1, 2304, 768), (40, 768, 768)])
+def test_gemm_few_rows_all_epilogues(dev, skinny, dt, M, N, K):
+    """GEMMs with M <= 64 rows (the CLS-only last layer, the global query rows): k_gemm_skinny (knob
+    gemm_skinny, K split over the four waves and summed in LDS) and the 128 x 128 kernel, for the
+    epilogues those rows use, against fp32 torch on the same 16-bit operands."""
+    old = _lib.set_knob("gemm_skinny", skinny)
+    try:
+        a = _rand((M, K), dev, dt, 0.5, seed=71)
+        w = _rand((N, K), dev, dt, 0.05, seed=72)
+        b = _rand((N,), dev, torch.float32, seed=73)
+        prod = a.float() @ w.float().t()
+        tol = 4e-3 if dt == torch.float16 else 2e-2
+
+        def rel(x, ref):
+            return float((x.float() - ref).abs().max()) / max(1.0, float(ref.abs().max()))
+
+        assert rel(ops.gemm(a, w, None, ops.RF_EPI_NONE), prod) <= tol
+        sc = N // 3 // 16 * 16
+        ref = prod + b
+        ref[:, :sc] *= 0.125
+        assert rel(ops.gemm(a, w, b, ops.RF_EPI_BIAS, scale_cols=sc, col_scale=0.125), ref) <= tol
+        out32 = ops.gemm(a, w, b, ops.RF_EPI_BIAS, out_f32=True)
+        assert float((out32 - (prod + b)).abs().max()) <= 1e-3 * max(1.0, float(prod.abs().max()))
+        gl = ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU)
+        assert rel(gl, F.gelu(prod + b)) <= tol
+        z = torch.empty(M, N, device=dev, dtype=dt)
+        u = ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU_AUX, resid=z)
+        assert torch.equal(u, gl)
+        assert rel(z, prod + b) <= tol
+        zz = _rand((M, N), dev, dt, 2.0, seed=74)
+        dg = ops.gemm(a, w, None, ops.RF_EPI_DGELU, resid=zz)
+        ref = torch.ops.aten.gelu_backward(prod, zz.float())
+        assert float((dg.float() - ref).abs().max()) <= 1e-2 * max(float(ref.abs().max()), 1e-6)
+    finally:
+        _lib.set_knob("gemm_skinny", old)
