@@ -54,11 +54,14 @@ const char* rf_last_error(void);
  * forward's. Returns the previous counter. Process-wide; not thread-safe. */
 const uint64_t* rf_set_seed_source(const uint64_t* step_counter);
 int rf_abi_version(void);
-/* Diagnostics (A/B tools only, not used by the product path): set a launch-path tuning knob
- * ("gemm_gn", "gemm_variant", "band_qpb", "band_path", "gfold_path", "gfold_qsplit") for the
- * process; returns the previous value (INT32_MIN and rf_last_error() for an unknown name). The
- * compiled defaults are the measured choices; no launch reads the environment. */
+/* Diagnostics (A/B tools; the product never sets them): set a launch-path tuning knob ("gemm_gn",
+ * "gemm_variant", "band_qpb", "band_path", "gfold_path", "gfold_qsplit", "gemm_pf", "gemm_mfma32",
+ * "rank_w32", "gfold_chunk", "gemm_skinny", "epi_tile") for the process; returns the previous value
+ * (INT32_MIN and rf_last_error() for an unknown name). The compiled defaults are the measured choices;
+ * no launch reads the environment. The ranker reads rank_w32 to plan its seed block to match. */
 int rf_debug_set_knob(const char* name, int value);
+/* the knob's current value (INT32_MIN and rf_last_error for an unknown name) */
+int rf_debug_get_knob(const char* name);
 
 /* A2 — RecformerModel.forward prologue, models.py:306-329 (_merge_to_attention_mask
  * 262-272, _pad_to_window_size 210-260) + create_position_ids_from_input_ids 68-79.

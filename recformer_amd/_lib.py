@@ -25,6 +25,7 @@ SIGNATURES = {
     "rf_last_error": (ctypes.c_char_p, []),
     "rf_abi_version": (c_int, []),
     "rf_debug_set_knob": (c_int, [ctypes.c_char_p, c_int]),
+    "rf_debug_get_knob": (c_int, [ctypes.c_char_p]),
     "rf_prepare_inputs": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                   P, P, P, P, P, P, P]),
     "rf_embed_ln_fwd": (c_int, [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_float,
@@ -153,6 +154,14 @@ def set_knob(name: str, value: int) -> int:
     if old == -2 ** 31:
         raise RecformerHipError(load().rf_last_error().decode(errors="replace"))
     return old
+
+
+def get_knob(name: str) -> int:
+    """A launch-path knob's current value (the dispatch choices the Python side must mirror)."""
+    v = load().rf_debug_get_knob(name.encode())
+    if v == -2 ** 31:
+        raise RecformerHipError(load().rf_last_error().decode(errors="replace"))
+    return v
 
 
 def check(rc: int, what: str) -> None:

@@ -12,7 +12,7 @@
 namespace rf {
 
 static thread_local char g_err[512];
-int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8, -1, 0, 0, 0, 1, 0};
+int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8, -1, 0, 1, 0, 1, 0};
 const uint64_t* g_seed_dev = nullptr;
 
 void set_error(const char* fmt, ...) {
@@ -998,18 +998,27 @@ extern "C" {
 
 const char* rf_last_error(void) { return rf::g_err; }
 
-int rf_debug_set_knob(const char* name, int value) {
+static int knob_index(const char* name) {
   static const char* names[rf::KNOB_COUNT] = {"gemm_gn", "gemm_variant", "band_qpb", "band_path", "gfold_path",
                                               "gfold_qsplit", "gemm_pf", "gemm_mfma32", "rank_w32",
                                               "gfold_chunk", "gemm_skinny", "epi_tile"};
   for (int i = 0; i < rf::KNOB_COUNT; ++i)
-    if (name && strcmp(name, names[i]) == 0) {
-      const int old = rf::g_knob[i];
-      rf::g_knob[i] = value;
-      return old;
-    }
-  rf::set_error("rf_debug_set_knob: unknown knob '%s'", name ? name : "(null)");
-  return INT32_MIN;
+    if (name && strcmp(name, names[i]) == 0) return i;
+  rf::set_error("rf_debug_knob: unknown knob '%s'", name ? name : "(null)");
+  return -1;
+}
+
+int rf_debug_set_knob(const char* name, int value) {
+  const int i = knob_index(name);
+  if (i < 0) return INT32_MIN;
+  const int old = rf::g_knob[i];
+  rf::g_knob[i] = value;
+  return old;
+}
+
+int rf_debug_get_knob(const char* name) {
+  const int i = knob_index(name);
+  return i < 0 ? INT32_MIN : rf::g_knob[i];
 }
 int rf_abi_version(void) { return 1; }
 

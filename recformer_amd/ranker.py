@@ -75,6 +75,16 @@ TOPK_SAMPLE = 2048  # dense seed block that sets each row's first candidate thre
 TOPK_CAP = 1024     # candidate list per row and chunk
 TOPK_MAX_K = 256    # rf_topk_* limits (rf_retrieval.hip TK_KMAX, TK_DENSE_MAX)
 TOPK_MAX_SAMPLE = 2048
+# dense seed on the 32x32x16 rank kernel (shard_rank): with a 32k-item seed the first candidate chunk's
+# rate is <= k / 32768 per (query, item), under one candidate per lane and tile for k <= 100
+W32_DENSE_SEED = 32768
+
+
+def _rank_w32(q: torch.Tensor, shard) -> bool:
+    """Whether rf_score_rank takes the 32x32x16 kernel for these operands (rf_retrieval.hip rank_w32_ok)."""
+    D = q.shape[1]
+    return (_lib.get_knob("rank_w32") != 0 and D % 64 == 0 and D >= 128 and q.stride(0) % 8 == 0
+            and shard.items.stride(0) % 8 == 0)
 
 
 def _check_topk_args(k: int, sample: int, cap: int) -> None:
@@ -185,20 +195,36 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     inv_t = 1.0 / temp
     dev = q.device
     s0 = min(N, sample) if k > 0 else 0
-    # column chunks after the seed block: each as large as everything before it
-    plan, off = [], s0
+    # the dense seed: blocks of `sample` columns (their top-k merged block by block). One block, except
+    # on the 32x32x16 rank kernel (knob rank_w32), whose candidate slots are per lane (4 queries x 64
+    # items) rather than per query row: with a 2048-item seed the next chunks' candidate rate (about k
+    # per query per chunk) overflows most lanes, each overflow costing four queries a dense re-rank
+    seed_n = s0
+    if k > 0 and _rank_w32(q, shard):
+        seed_n = min(N, max(s0, W32_DENSE_SEED))
+    blocks = [(o, min(sample, seed_n - o)) for o in range(0, seed_n, sample)]
+    # column chunks after the seed: each as large as everything before it
+    plan, off = [], seed_n
     while k > 0 and off < N:
         plan.append((off, min(N - off, max(off, sample))))
         off += plan[-1][1]
-    nt0 = lib.rf_score_rank_tiles(s0 if k > 0 else N)
+    nt0 = sum(lib.rf_score_rank_tiles(n) for _, n in blocks) if k > 0 else lib.rf_score_rank_tiles(N)
     ntiles = nt0 + sum(lib.rf_score_rank_tiles(n) for _, n in plan)
     part_cnt = torch.empty(ntiles, B, dtype=torch.int32, device=dev)
     part_sexp = torch.empty(ntiles, B, dtype=torch.float32, device=dev)
     topv = topi = None
     if k > 0:
         dense = torch.empty(B, (s0 + 255) // 256 * 256, dtype=torch.float32, device=dev)  # whole 256-col tiles
-        _score_rank(q, qn, shard, s_label, inv_t, 0, 0, s0, part_cnt, part_sexp, 0, dense=dense, max_val=max_val)
-        topv, topi = _topk_dense(dense[:, :s0], k, idx_base=shard.base)
+        tb = 0
+        for o, n in blocks:
+            _score_rank(q, qn, shard, s_label, inv_t, 0, o, n, part_cnt, part_sexp, tb, dense=dense, max_val=max_val)
+            if topv is None:
+                topv, topi = _topk_dense(dense[:, :n], k, idx_base=shard.base + o)
+            else:
+                ids = (torch.arange(n, dtype=torch.int32, device=dev) + (shard.base + o)).expand(B, n)
+                topv, topi = _topk_dense(torch.cat([topv, dense[:, :n]], 1), k,
+                                         idx=torch.cat([topi, ids], 1).contiguous())
+            tb += lib.rf_score_rank_tiles(n)
         del dense
         # the rest in chunks that double with the items already seen: the running k-th score is a
         # lower bound of the final one, so only s >= it can enter the top-k (about k per row per
