@@ -14,6 +14,7 @@
 #   torchops   the Python lines that launch torch (non-HIP) kernels in one eager C3 step
 #   trainprof  rocprofv3 kernel trace of the captured C3 step ($TRAIN_ARGS)
 #   abc3       captured-C3 A/Bs listed in $AB (knob:<name>[=a,b] or a Python flag), $TRAIN_ARGS appended
+#   abc2       C2 forward-step A/Bs listed in $AB (tools/ab_step.py arguments)
 #   abc5       C5 retrieval, rank_w32 0 / 1 alternated by process
 #   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3;
 #              C5 retrieval with the 32x32x16 rank kernel (knob rank_w32) alternated by process
@@ -85,6 +86,14 @@ case $MODE in
       timeout -k 10 500 python tools/train_bench.py --graph --steps 8 --warmup 2 ${TRAIN_ARGS:-} $arg \
         > $O/abc3_$n.log 2>&1 || fail $O/abc3_$n.log
       echo "== $x"; tail -2 $O/abc3_$n.log
+    done ;;
+  abc2)
+    # C2 forward steps, one same-process A/B per entry of $AB (knob:<name>[=a,b] or a models / train flag)
+    n=0
+    for x in ${AB:?AB}; do
+      n=$((n + 1))
+      AB_AUTOCAST=1 timeout -k 10 400 python tools/ab_step.py $x 64 > $O/abc2_$n.log 2>&1 || fail $O/abc2_$n.log
+      echo "== $x"; grep -E "ms/step|diff" $O/abc2_$n.log
     done ;;
   abc5)
     # C5 retrieval with the 32x32x16 rank kernel (knob rank_w32) alternated by process
