@@ -21,7 +21,7 @@ EPI_TAG = {1: "gemm_qkv", 2: "gemm_ffn1", 3: "gemm_out", 4: "gemm_cos"}
 RENAME = {"k_add_ln_split": "layernorm"}  # split-stream residual LayerNorm = bench tag "layernorm"
 SIMPLE = ("k_band_attn", "k_gfold_partial", "k_gfold_qu", "k_gfold_u", "k_gfold_out", "k_layernorm",
           "k_embed_ln", "k_prepare", "k_gather_rows", "k_row_inv_norm", "k_cos_cand",
-          "k_global_attn", "k_gemm_f32")
+          "k_global_attn", "k_gemm_f32", "k_gemm_skinny", "k_band_attn_wide")
 
 
 def tagger():
