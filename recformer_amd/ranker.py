@@ -220,7 +220,10 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
             _score_rank(q, qn, shard, s_label, inv_t, 0, o, n, part_cnt, part_sexp, tb, dense=dense, max_val=max_val)
             if topv is None:
                 topv, topi = _topk_dense(dense[:, :n], k, idx_base=shard.base + o)
-            else:
+            elif n >= k:
+                v, i = _topk_dense(dense[:, :n], k, idx_base=shard.base + o)
+                topv, topi = _topk_dense(torch.cat([topv, v], 1), k, idx=torch.cat([topi, i], 1).contiguous())
+            else:  # a last block narrower than k
                 ids = (torch.arange(n, dtype=torch.int32, device=dev) + (shard.base + o)).expand(B, n)
                 topv, topi = _topk_dense(torch.cat([topv, dense[:, :n]], 1), k,
                                          idx=torch.cat([topi, ids], 1).contiguous())
