@@ -61,11 +61,15 @@ class GraphedForward:
         self.check = check
         self.static = {k: v.clone() for k, v in example.items()}
         self.gmax = self._global_count(self.static)
+        # the CLS-only last layer (models._cls_last_layer) of pooled-only callers is captured when the
+        # example has a global CLS in every sequence; replays are then checked for the same
+        self.cls_global = static_cls_global(self.static)
         stream = torch.cuda.Stream()
         stream.wait_stream(torch.cuda.current_stream())
-        old = models._STATIC_GMAX
+        old, old_c = models._STATIC_GMAX, models._STATIC_CLS
         try:
             models._STATIC_GMAX = self.gmax
+            models._STATIC_CLS = self.cls_global
             with torch.no_grad():
                 with torch.cuda.stream(stream):  # warm-up: caches, packed weights, kernel attributes
                     for _ in range(max(1, warmup)):
@@ -75,7 +79,9 @@ class GraphedForward:
                 with torch.cuda.graph(self.graph):
                     self.out = module(**self.static)
         finally:
-            models._STATIC_GMAX = old
+            models._STATIC_GMAX, models._STATIC_CLS = old, old_c
+        lf = getattr(module, "longformer", module)
+        self.cls_global = self.cls_global and bool(getattr(lf, "_last_pruned", False))
 
     @staticmethod
     def _global_count(b: Dict[str, torch.Tensor]) -> int:
@@ -98,6 +104,9 @@ class GraphedForward:
             self.static[k].copy_(v, non_blocking=True)
         if self.check and self._global_count(self.static) > self.gmax:
             raise ValueError(f"GraphedForward: more global tokens per sequence than captured ({self.gmax})")
+        if self.check and self.cls_global and not static_cls_global(self.static):
+            raise ValueError("GraphedForward: captured with a global CLS token in every sequence (the CLS-only "
+                             "last layer); this batch has a sequence without one")
         self.graph.replay()
         return self.out
 

@@ -257,8 +257,10 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
 PRUNE_LAST_LAYER = True
 # training: RecformerForPretraining's four encoder passes share one autograd cast per weight
 SHARE_TRAIN_CASTS = True
-# set by graphs.GraphedForward during capture: the global-slot count of the captured shape
+# set by graphs.GraphedForward during capture: the global-slot count of the captured shape, and whether
+# every sequence's CLS is global (the CLS-only last layer's condition, read on the host otherwise)
 _STATIC_GMAX = None
+_STATIC_CLS = None
 # read the global-token count after the embedding is queued (False: before the prologue)
 ASYNC_GLOBAL_COUNT = True
 
@@ -527,6 +529,7 @@ class RecformerModel(nn.Module):
         cls_global = False
         if _STATIC_GMAX is not None:
             gmax = _STATIC_GMAX
+            cls_global = want_cls and bool(_STATIC_CLS)
         elif global_attention_mask is not None and B > 0:
             gm = global_attention_mask != 0
             if attention_mask is not None:

@@ -248,6 +248,12 @@ def test_graphed_forward_matches_eager(dev, B, L):
     b["global_attention_mask"][:, 1] = 1
     with pytest.raises(ValueError):
         g(**b)
+    # captured with the CLS-only last layer (every CLS global): a batch without a global CLS is refused
+    assert g.cls_global
+    b2 = {k: v.to(dev) for k, v in synth_batch(B, L, BASE["vocab_size"], seed=5).items()}
+    b2["global_attention_mask"][0, 0] = 0
+    with pytest.raises(ValueError):
+        g(**b2)
 
 
 @pytest.mark.parametrize("mode", ["fp32", "autocast"])
