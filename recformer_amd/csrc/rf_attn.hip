@@ -1354,8 +1354,8 @@ __global__ void __launch_bounds__(256, 3) k_band_attn_pipe3(int Lp, int H, int q
 }
 
 // ------------------------------------------------------------------------------------
-// Short sequences (Lp <= 64, a multiple of 16: catalog items of <s> + up to 63 tokens, padded to
-// a multiple of 16 instead of the 64-token window; finetune.py:38-63): every key of the sequence
+// Short sequences (Lp < 64, any length: catalog items of <s> + up to 63 tokens, unpadded instead of
+// padded to the 64-token window; finetune.py:38-63): every key of the sequence
 // is in one 64-row tile, so one workgroup per (sequence, head) scores all of them. Same contract
 // as the band kernels: a local query i sees keys j with flag 1 and |i - j| <= 32, plus every global
 // key (flag 2, local K/V); padded query rows are written as 0. Keys / values DMA'd to LDS, Q^T
@@ -1640,9 +1640,9 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
                                                     flags, gidx, gmax, (bf16*)out, ld_out, H);
       RF_LAUNCH_CHECK("rf_band_attn_fwd");
     }
-    RF_REQUIRE(Lp % 64 == 0 || (Lp < 64 && Lp % 16 == 0 && dr.thresh == 0),
-               "rf_band_attn_fwd(16-bit): Lp=%d must be a multiple of 64, or < 64 and a multiple of 16 "
-               "(short sequences; no dropout)", Lp);
+    RF_REQUIRE(Lp % 64 == 0 || (Lp < 64 && dr.thresh == 0),
+               "rf_band_attn_fwd(16-bit): Lp=%d must be a multiple of 64, or < 64 (short sequences, any "
+               "length; no dropout)", Lp);
     RF_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0, "rf_band_attn_fwd(bf16): alignment");
     RF_REQUIRE(dr.thresh == 0 || gmax <= 32, "rf_band_attn_fwd(bf16): dropout needs gmax <= 32 (got %d)", gmax);
     if (Lp < 64) {

@@ -232,8 +232,10 @@ SCORE_HEAD_HIP = True
 # False = a plain fp32 tensor plus a separate bf16 GEMM operand (A/B tools, tests).
 SPLIT_STREAM = True
 # sequences shorter than the 64-token window (catalog items: <s> + <= 63 tokens, finetune.py:38-63)
-# padded to a multiple of 16 instead of 64 (rf_band_attn_fwd's short-sequence kernel): the valid
-# rows' outputs are the same (padding is masked), with up to 3/4 fewer rows through every GEMM
+# not padded at all instead of padded to 64 (rf_band_attn_fwd's short-sequence kernel takes any length
+# below the window): the valid rows' outputs are the same (padding is masked), and every GEMM /
+# LayerNorm runs on the real rows only (33-token items: 33 rows instead of 64, or 48 at the
+# multiple-of-16 padding of round 3)
 SHORT_SEQ = True
 # run the global fold's pass over h before the qkv GEMM (rf_global_attn_fold_h_stage)
 FOLD_EARLY = True
@@ -511,7 +513,7 @@ class RecformerModel(nn.Module):
         Lp = L + (W - L % W) % W
         windows_all = cfg.window_per_layer()
         if SHORT_SEQ and L < W and W == 64 and all(w == 64 for w in windows_all):
-            Lp = max(16, (L + 15) // 16 * 16)
+            Lp = L  # no padding rows at all (k_attn_short takes any length below the window)
         D, H = cfg.hidden_size, cfg.num_attention_heads
         hd = D // H
         dt = _compute_dtype(self.dtype)

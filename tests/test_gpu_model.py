@@ -207,8 +207,8 @@ def catalog_case():
 @pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
 @pytest.mark.parametrize("short", [True, False])
 def test_catalog_batch_vs_oracle(dev, catalog_case, monkeypatch, mode, short):
-    """Catalog encoding end to end against the oracle: the short-sequence path (L = 33 padded to
-    48, rf_band_attn_fwd's Lp < 64 kernel; models.SHORT_SEQ) and the window-padded one (Lp = 64)."""
+    """Catalog encoding end to end against the oracle: the short-sequence path (L = 33 unpadded,
+    rf_band_attn_fwd's Lp < 64 kernel; models.SHORT_SEQ) and the window-padded one (Lp = 64)."""
     from recformer_amd import models
     monkeypatch.setattr(models, "SHORT_SEQ", short)
     m, b, h_ref, p_ref = catalog_case
@@ -445,3 +445,30 @@ def test_cls_last_layer_matches_full(dev, monkeypatch, mode):
     with torch.no_grad(), ctx:
         m(**nog)
     assert not m.longformer._last_pruned
+
+
+@pytest.mark.parametrize("mode", ["fp32", "autocast", "autocast16"])
+@pytest.mark.parametrize("L", [1, 9, 33, 63])
+def test_short_sequences_unpadded_vs_oracle(dev, monkeypatch, mode, L):
+    """Sequences shorter than the 64-token window run unpadded (Lp = L, models.SHORT_SEQ and the
+    short-sequence attention kernel at any length) and match the oracle's window-padded run on the
+    valid rows, including a ragged item and the pooled CLS."""
+    from oracle import restatement as R
+    from recformer_amd import models
+    from recformer_amd.synth import synth_batch
+    monkeypatch.setattr(models, "SHORT_SEQ", True)
+    lf = hashed_model(C1, seed=1)
+    b = synth_batch(6, L, C1["vocab_size"], seed=L, item_len=max(1, L - 1))
+    if L > 4:
+        b["attention_mask"][2, L // 2:] = 0
+    with torch.no_grad():
+        h_ref, p_ref = R.model_forward(lf.state_dict(), lf.config, **b)
+    m, ctx = _prep(lf, dev, mode)
+    with torch.no_grad(), ctx:
+        out = m(**{k: v.to(dev) for k, v in b.items()})
+    valid = b["attention_mask"].bool()
+    e = errs(out.last_hidden_state[valid.to(dev)], h_ref[valid])
+    if mode == "fp32":
+        assert e["max"] <= 1e-3, e
+    else:
+        _check_e2e(mode, e, out.pooler_output, p_ref)

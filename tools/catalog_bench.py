@@ -1,6 +1,6 @@
 """C5 full-catalog retrieval (BASELINE configs[4]): encode a synthetic item catalog sharded over
 the ranks (<s> + 32 tokens per item, batches of `--batch`
-items, fp16 autocast by default; L=33 runs at Lp=48 through the short-sequence attention kernel unless
+items, fp16 autocast by default; L=33 runs unpadded (Lp=33) through the short-sequence attention kernel unless
 --pad64), keep each rank's embeddings as its CatalogShard (no gather of
 the table), all-gather the Q query vectors, and rank them against the whole catalog with the
 fused score + rank + top-50 kernels (recformer_amd.retrieve: per-shard counts and top-k,
@@ -79,7 +79,7 @@ def main():
     t_ret = dp.max_over_ranks(min(times), device=dev)
     t_enc = dp.max_over_ranks(t_enc, device=dev)
     if rank == 0:
-        print(json.dumps({"workload": "C5 retrieval: encode a catalog shard per GPU (L=33->" + ("64" if a.pad64 else "48") + "), fused score + rank + "
+        print(json.dumps({"workload": "C5 retrieval: encode a catalog shard per GPU (L=33->" + ("64" if a.pad64 else "33, unpadded") + "), fused score + rank + "
                                       f"top-{a.k} over the sharded catalog", "items": a.items, "queries": a.queries,
                           "gpus": world, "dtype": a.dtype, "encode_s": round(t_enc, 3),
                           "items_per_s": round(a.items / t_enc, 1), "retrieve_ms": round(1e3 * t_ret, 2),
