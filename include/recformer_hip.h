@@ -58,7 +58,7 @@ int rf_abi_version(void);
  * "gemm_variant", "band_qpb", "band_path", "gfold_path", "gfold_qsplit", "gemm_pf", "gemm_mfma32",
  * "rank_w32", "gfold_chunk", "gemm_skinny", "epi_tile") for the process; returns the previous value
  * (INT32_MIN and rf_last_error() for an unknown name). The compiled defaults are the measured choices;
- * no launch reads the environment. The ranker reads rank_w32 to plan its seed block to match. */
+ * no launch reads the environment. */
 int rf_debug_set_knob(const char* name, int value);
 /* the knob's current value (INT32_MIN and rf_last_error for an unknown name) */
 int rf_debug_get_knob(const char* name);

@@ -371,7 +371,6 @@ struct RankW32Args {
 };
 
 // k_rank_w32's parameter list as a struct: the kernarg segment lays the arguments out this way
-constexpr int RK32_NS = 4;  // candidate slots per lane and tile (more: the lane's queries are re-ranked)
 
 struct RankKernArgs {
   int K;
@@ -432,9 +431,6 @@ struct RankW32Pol {
     const int ib = t.wr * 128 + 4 * g;  // tile-relative item row of register 0 of block 0
     int gt[4] = {0, 0, 0, 0}, vc[4] = {0, 0, 0, 0};
     float se[4] = {0.f, 0.f, 0.f, 0.f};
-    // MODE 1: this lane's candidates, (score, jb << 8 | item row) in RK32_NS LDS slots (+ one trash slot)
-    float* cslot = reinterpret_cast<float*>(t.scr + 8192) + (t.wave * 64 + el) * 2 * (RK32_NS + 1);
-    int ncand = 0;
     // MODE 0: dense scores through a buffer resource: a query past B is past num_records, an item past
     // ncols gets an offset >= 2^31 (branch-free stores)
     const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(
@@ -471,37 +467,26 @@ struct RankW32Pol {
         svs[jb] = sv;
       }
       if (MODE == 1) {
-        // every row writes its first candidate (or nothing: to the lane's trash slot) to the lane's next
-        // LDS slot — branch-free (branches here wreck the register allocation around the accumulators);
-        // two candidates in one row or more than RK32_NS in the tile count as an overflow
-        const int jb0 = cb4 & 1u ? 0 : (cb4 & 2u ? 1 : (cb4 & 4u ? 2 : 3));
-        const float sv0 = jb0 == 0 ? svs[0] : (jb0 == 1 ? svs[1] : (jb0 == 2 ? svs[2] : svs[3]));
-        const int pos = cb4 ? min(ncand, RK32_NS) : RK32_NS;
-        *reinterpret_cast<float2*>(cslot + 2 * pos) = make_float2(sv0, __int_as_float((jb0 << 8) | pr));
-        ncand += cb4 ? ((cb4 & (cb4 - 1)) ? RK32_NS + 1 : 1) : 0;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    if (MODE == 1 && ncand) {
-      // flush: one global atomic per candidate (about k per query per column chunk); a lane with more
-      // than RK32_NS poisons its queries' counts (> capr), which the merge flags for an exact re-rank
-      if (ncand > RK32_NS) {
+        // candidates (about k per query and column chunk) go straight to the per-query lists: the write
+        // block runs only in the rows where some lane of the wave has one (a wave-uniform branch, exec
+        // masking inside), one global atomic per candidate; a list past capr flags its query for an
+        // exact re-rank (the merge)
+        if (__builtin_amdgcn_ballot_w64(cb4 != 0u)) {
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-          if (qok[jb]) atomicAdd(a.rcnt + q0 + jb, a.capr + 1);
-      } else {
-        for (int k = 0; k < ncand; ++k) {
-          const float sv = cslot[2 * k];
-          const int tag = __float_as_int(cslot[2 * k + 1]);
-          const int q = q0 + (tag >> 8);
-          const int pos = atomicAdd(a.rcnt + q, 1);
-          if (pos < a.capr) {
-            a.cval[(int64_t)q * a.capr + pos] = sv;
-            a.cidx[(int64_t)q * a.capr + pos] = a.idx_base + a.col0 + t.m0 + ib + (tag & 255);
+          for (int jb = 0; jb < 4; ++jb) {
+            if (cb4 & (1u << jb)) {
+              const int q = q0 + jb;
+              const int pos = atomicAdd(a.rcnt + q, 1);
+              if (pos < a.capr) {
+                a.cval[(int64_t)q * a.capr + pos] = svs[jb];
+                a.cidx[(int64_t)q * a.capr + pos] = a.idx_base + a.col0 + t.m0 + ib + pr;
+              }
+            }
           }
         }
       }
-    }
+      __builtin_amdgcn_sched_barrier(0);
+    });
     // lane halves (item rows 4g..), then the two waves (wr) of this query half through LDS
     int pk[4];
 #pragma unroll

@@ -75,16 +75,6 @@ TOPK_SAMPLE = 2048  # dense seed block that sets each row's first candidate thre
 TOPK_CAP = 1024     # candidate list per row and chunk
 TOPK_MAX_K = 256    # rf_topk_* limits (rf_retrieval.hip TK_KMAX, TK_DENSE_MAX)
 TOPK_MAX_SAMPLE = 2048
-# dense seed on the 32x32x16 rank kernel (shard_rank): with a 32k-item seed the first candidate chunk's
-# rate is <= k / 32768 per (query, item), under one candidate per lane and tile for k <= 100
-W32_DENSE_SEED = 32768
-
-
-def _rank_w32(q: torch.Tensor, shard) -> bool:
-    """Whether rf_score_rank takes the 32x32x16 kernel for these operands (rf_retrieval.hip rank_w32_ok)."""
-    D = q.shape[1]
-    return (_lib.get_knob("rank_w32") != 0 and D % 64 == 0 and D >= 128 and q.stride(0) % 8 == 0
-            and shard.items.stride(0) % 8 == 0)
 
 
 def _check_topk_args(k: int, sample: int, cap: int) -> None:
@@ -195,13 +185,9 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     inv_t = 1.0 / temp
     dev = q.device
     s0 = min(N, sample) if k > 0 else 0
-    # the dense seed: blocks of `sample` columns (their top-k merged block by block). One block, except
-    # on the 32x32x16 rank kernel (knob rank_w32), whose candidate slots are per lane (4 queries x 64
-    # items) rather than per query row: with a 2048-item seed the next chunks' candidate rate (about k
-    # per query per chunk) overflows most lanes, each overflow costing four queries a dense re-rank
+    # the dense seed: blocks of `sample` columns, their top-k merged block by block (one block at the
+    # default seed_n = s0; a larger seed_n would lower the first candidate chunks' rate)
     seed_n = s0
-    if k > 0 and _rank_w32(q, shard):
-        seed_n = min(N, max(s0, W32_DENSE_SEED))
     blocks = [(o, min(sample, seed_n - o)) for o in range(0, seed_n, sample)]
     # column chunks after the seed: each as large as everything before it
     plan, off = [], seed_n
