@@ -723,6 +723,17 @@ def _cls_last_layer(model, lw, gargs, gws, h, h_lo, h32, head_cols, li, B, Lp, D
     return y32
 
 
+def _negatives(cfg, batch_size: int, device) -> torch.Tensor:
+    """Sampled-softmax negatives (models.py:594): torch.randint on the CPU global RNG, as the reference,
+    then copied to the device; inside a HIP-graph capture (graphs.CapturedTrainStep) on the device's
+    generator instead (graph-safe philox offsets: fresh negatives on every replay), since a host tensor
+    cannot enter a captured graph."""
+    size = (batch_size, cfg.finetune_negative_sample_size)
+    if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        return torch.randint(0, cfg.item_num, size, device=device)
+    return torch.randint(0, cfg.item_num, size).to(device)
+
+
 class RecformerForSeqRec(nn.Module):
     """models.py:524-599 on HIP kernels (scores via normalize + MFMA GEMM, never the
     (B,N,d) broadcast of nn.CosineSimilarity)."""
@@ -789,9 +800,7 @@ class RecformerForSeqRec(nn.Module):
                 return train.cos_scores_train(pooler_output, table, rnorm, inv_t, candidates)
             if self.config.finetune_negative_sample_size <= 0:
                 return train.cross_entropy_train(train.cos_scores_train(pooler_output, table, rnorm, inv_t), labels)
-            candidates = torch.cat((labels.unsqueeze(-1), torch.randint(
-                0, self.config.item_num, size=(batch_size, self.config.finetune_negative_sample_size)
-            ).to(labels.device)), dim=-1)
+            candidates = torch.cat((labels.unsqueeze(-1), _negatives(self.config, batch_size, labels.device)), dim=-1)
             logits = train.cos_scores_train(pooler_output, table, rnorm, inv_t, candidates)
             return train.cross_entropy_train(logits, torch.zeros_like(labels))
         if _needs_grad(self):
@@ -805,9 +814,7 @@ class RecformerForSeqRec(nn.Module):
                                      F.normalize(items.float(), dim=-1, eps=1e-8)) / self.config.temp)
             if self.config.finetune_negative_sample_size <= 0:
                 return F.cross_entropy(_cos_train(pooler_output, table, self.config.temp), labels)
-            candidates = torch.cat((labels.unsqueeze(-1), torch.randint(
-                0, self.config.item_num, size=(batch_size, self.config.finetune_negative_sample_size)
-            ).to(labels.device)), dim=-1)
+            candidates = torch.cat((labels.unsqueeze(-1), _negatives(self.config, batch_size, labels.device)), dim=-1)
             items = table[candidates].float()
             zn = F.normalize(pooler_output.float(), dim=-1, eps=1e-8)
             logits = torch.einsum("bd,bcd->bc", zn, F.normalize(items, dim=-1, eps=1e-8)) / self.config.temp
@@ -818,9 +825,7 @@ class RecformerForSeqRec(nn.Module):
             logits = self.similarity_score(pooler_output)
             return ops.cross_entropy(logits, labels)  # CrossEntropyLoss, models.py:589-591
         # sampled softmax: candidates from the CPU global RNG as models.py:594
-        candidates = torch.cat((labels.unsqueeze(-1), torch.randint(
-            0, self.config.item_num, size=(batch_size, self.config.finetune_negative_sample_size)
-        ).to(labels.device)), dim=-1)
+        candidates = torch.cat((labels.unsqueeze(-1), _negatives(self.config, batch_size, labels.device)), dim=-1)
         logits = self.similarity_score(pooler_output, candidates)
         target = torch.zeros_like(labels, device=labels.device)
         return ops.cross_entropy(logits, target)  # models.py:595-597
