@@ -1079,9 +1079,16 @@ __global__ void __launch_bounds__(256) k_band_attn_pipe2(int Lp, int H, int qpb,
 // the chunk masks, the global positions) -> three workgroups per CU (VGPR budget <= 168).
 // (read-write operand: the load targets the registers the variable already lives in, so hipcc has
 // no reason to copy it between the load and the fence that follows the counted wait)
+// Non-temporal (the Q rows are read once, as pipe2's Q DMA: a temporal load left them in L2 / MALL
+// in place of the attention output the next GEMM reads — pipe3 ran faster itself but the out-proj
+// after it slower, round 3). RF_BAND_PLAIN_LOAD: the plain form, for A/B builds.
 template <typename V8>
 __device__ __forceinline__ void gload16(V8& dst, const void* p) {
+#if defined(RF_BAND_PLAIN_LOAD)
   asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(dst) : "v"(p) : "memory");
+#else
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "+v"(dst) : "v"(p) : "memory");
+#endif
 }
 
 constexpr int AQ_KV = 0;          // 3 x (K 64 x 128 B, V 64 x 128 B)
