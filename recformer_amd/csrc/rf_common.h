@@ -56,7 +56,8 @@ enum Knob {
   KNOB_GEMM_PF,         // four-wave GEMM L2 prefetch: -1 auto (2 for K >= 2048), else distance in K-tiles (0 = off), + 256: W rows too
   KNOB_GEMM_MFMA32,     // four-wave GEMM on v_mfma_f32_32x32x16 (k_gemm_w32): 1 on, 0 the 16x16x32 kernel (k_gemm_w4)
   KNOB_RANK_W32,        // catalog score + rank on the 32x32x16 four-wave loop (k_rank_w32 + k_label_score32): 1 on
-                        // (default: 1M x 4096 rank-only 6.9-7.0 vs 7.9 ms, r04f); 0 the 16x16x32 kernel
+                        // (0 by default; ranker.rank_catalog / retrieve(k=0) take it for their counts-only
+                        // pass: 1M x 4096 6.96 vs 7.89 ms; the top-k mode is faster on 16x16x32, r04h)
   KNOB_GFOLD_CHUNK,     // inference global fold: rows per chunk of the pass over h (0 = 256; 64 / 128)
   KNOB_GEMM_SKINNY,     // 16-bit GEMMs with M <= 64 rows on k_gemm_skinny (1, default) or the 128 x 128 kernel (0)
   KNOB_EPI_TILE,        // training GELU GEMMs (EPI_DGELU, EPI_BIAS_GELU_AUX): 0 the four-wave 256x256 kernel,

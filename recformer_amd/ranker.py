@@ -9,6 +9,7 @@ width (the counts accumulate), so a catalog can also be ranked block by block.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import List, Optional, Sequence
 
 import torch
@@ -75,6 +76,19 @@ TOPK_SAMPLE = 2048  # dense seed block that sets each row's first candidate thre
 TOPK_CAP = 1024     # candidate list per row and chunk
 TOPK_MAX_K = 256    # rf_topk_* limits (rf_retrieval.hip TK_KMAX, TK_DENSE_MAX)
 TOPK_MAX_SAMPLE = 2048
+
+
+@contextlib.contextmanager
+def _rank_family(topk: bool):
+    """The rank kernel family for one self-contained ranking (label scores + rank counts from the same
+    arithmetic, so the strict counts and exact ties stay the full-matrix Ranker's): the 32x32x16 loop
+    for counts only (1M x 4096: 6.96 vs 7.89 ms), the 16x16x32 one with a top-k (9.5 vs 10.5-10.8 ms;
+    gpurun_out/r04h/ab_c5.log). label_scores / shard_rank called directly follow the knob rank_w32."""
+    old = _lib.set_knob("rank_w32", 0 if topk else 1)
+    try:
+        yield
+    finally:
+        _lib.set_knob("rank_w32", old)
 
 
 def _check_topk_args(k: int, sample: int, cap: int) -> None:
@@ -296,10 +310,12 @@ def retrieve(queries: torch.Tensor, shard: CatalogShard, labels: torch.Tensor, m
     _check_topk_args(k, TOPK_SAMPLE, TOPK_CAP)
     q = _check_q(queries, shard)
     qn = ops.row_inv_norm(q)
-    sl = label_scores(q, shard, labels, temp, qn)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(sl, group=group)  # the owner's value plus zeros: exact
-    parts = combine_shards(shard_rank(q, shard, sl, temp, k, qn), k, group)
+    with _rank_family(k > 0):
+        sl = label_scores(q, shard, labels, temp, qn)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(sl, group=group)  # the owner's value plus zeros: exact
+        part = shard_rank(q, shard, sl, temp, k, qn)
+    parts = combine_shards(part, k, group)
     loss = float((torch.log(parts["sexp"]) + parts["shift"] - sl).mean())
     return _metrics(parts["gt"], parts["valid"], loss, metrics_ks), parts["topv"], parts["topi"]
 
@@ -322,8 +338,9 @@ def rank_catalog(queries: torch.Tensor, items: torch.Tensor, labels: torch.Tenso
         shard = CatalogShard(items, 0, items_rnorm)
         q = _check_q(queries, shard)
         qn = ops.row_inv_norm(q)
-        sl = label_scores(q, shard, labels, temp, qn)
-        parts = shard_rank(q, shard, sl, temp, 0, qn)
+        with _rank_family(False):
+            sl = label_scores(q, shard, labels, temp, qn)
+            parts = shard_rank(q, shard, sl, temp, 0, qn)
         loss = float((torch.log(parts["sexp"]) + parts["shift"] - sl).mean())
         return _metrics(parts["gt"], parts["valid"], loss, metrics_ks)
     return _rank_catalog_blocks(queries.float().contiguous(), items.float().contiguous(), labels, metrics_ks, temp,
