@@ -181,10 +181,13 @@ int rf_drop_add_ln_bwd_tb(int dtype, int M, int D, const float* dy, const void* 
  * rows (X = dC (M x N), Y = A (M x K), 16-bit row-major; C fp32 N x K, the master weight's dtype) —
  * the dW = dC^T A of autograd through TF:504-514, 1064-1130 and the LM head (models.py:499-510).
  * MFMA with transposed LDS reads; the rows split over workgroups into fp32 slabs reduced in a fixed
- * order (deterministic); accumulate != 0 adds into C. Workspace: rf_weight_grad_workspace bytes. */
+ * order (deterministic); accumulate != 0 adds into C. Rows n < scale_rows of the product are
+ * multiplied by row_scale before they are stored / added (a Linear whose first outputs carry a column
+ * scale: the query's 1/sqrt(head_dim), TF:504-514; 0 = none). Workspace: rf_weight_grad_workspace bytes. */
 size_t rf_weight_grad_workspace(int M, int N, int K);
 int rf_weight_grad(int dtype, int M, int N, int K, const void* X, int ldx, const void* Y, int ldy, float* C, int ldc,
-                   int accumulate, void* workspace, size_t ws_bytes, rf_stream_t stream);
+                   int accumulate, int scale_rows, float row_scale, void* workspace, size_t ws_bytes,
+                   rf_stream_t stream);
 /* Backward of the fused embedding + LayerNorm (RecformerEmbeddings, models.py:108-138): from dh (M x D
  * fp32) the row gradient dx = dL/d(Ew[id] + Ep[pos] + Et[tt] + Ei[ip]) (M x D fp32; the pre-LN sum is
  * regathered from the fp32 tables, not stored) and dgamma / dbeta (deterministic, fixed-order sums).
@@ -204,9 +207,11 @@ int rf_segment_rows_sum(int M, int D, const float* src, const int32_t* perm, con
                         float* dst, int V, void* workspace, rf_stream_t stream);
 /* Column sums out[n] = sum_m x[m][n] (fp32 out; x in dtype, row-major, leading dim ldx), two
  * deterministic stages through rf_colsum_workspace(M, N) bytes — the bias gradient of the
- * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias). */
+ * training path's linears (db = sum_rows dC, the autograd of TF:504-1130's nn.Linear bias); columns
+ * n < scale_cols multiplied by col_scale (the query's bias under its 1/sqrt(head_dim) scale; 0 = none). */
 size_t rf_colsum_workspace(int M, int N);
-int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, void* workspace, rf_stream_t stream);
+int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, int scale_cols, float col_scale,
+              void* workspace, rf_stream_t stream);
 /* dst[rows[r]] += src[r] (r < R; rows[r] < 0 skipped) for one or two (src, dst) pairs of the
  * same shape (src1 = dst1 = null: one); repeated rows add in row order. The training path's
  * global-key gradient columns added into dk / dv at the global positions (the reduction of

@@ -75,10 +75,10 @@ SIGNATURES = {
     "rf_adamw_step": (c_int, [P, c_int, P, c_int, P]),
     "rf_adamw_step_amp": (c_int, [P, c_int, P, c_int, P, P, P]),
     "rf_weight_grad_workspace": (ctypes.c_size_t, [c_int, c_int, c_int]),
-    "rf_weight_grad": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_int, c_int, P, ctypes.c_size_t,
-                               P]),
+    "rf_weight_grad": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_float, P,
+                               ctypes.c_size_t, P]),
     "rf_scatter_add_rows": (c_int, [c_int, c_int, c_int, P, P, P, c_int, P, P, c_int, P]),
-    "rf_colsum": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, P, P]),
+    "rf_colsum": (c_int, [c_int, c_int, c_int, P, ctypes.c_int64, P, c_int, c_float, P, P]),
     "rf_layernorm_bwd": (c_int, [c_int, c_int, P, P, c_int, P, P, P, P, P, P, P, P]),
     "rf_band_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
                                  c_int, P, c_int, P]),

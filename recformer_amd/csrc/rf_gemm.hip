@@ -530,10 +530,13 @@ __device__ __forceinline__ int wperm(int rho) {
 // FS: the caller pre-scaled bv by this lane's column scale cs (its columns lie on one side of
 // scale_cols, a multiple of 16): v = fma(v, cs, bv) instead of (v + bv) * col_scale under a per-lane
 // branch — bit-identical for cs = 1 and for power-of-two scales (1/sqrt(64)).
-template <typename E, int EPI, bool CF32, bool RF32, int NV, bool CHECK = true, bool TB = false, bool FS = false>
+// ZV (EPI_DGELU, NV = 8): the pre-activations come in zv, loaded by the caller ahead of use
+template <typename E, int EPI, bool CF32, bool RF32, int NV, bool CHECK = true, bool TB = false, bool FS = false,
+          bool ZV = false>
 __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float* v, const float* bv,
                                         const float* gm, const float* bt, float rsc = 0.f,
-                                        const void* tbase = nullptr, int tm0 = 0, float cs = 1.f) {
+                                        const void* tbase = nullptr, int tm0 = 0, float cs = 1.f,
+                                        typename H16<E>::x8 zv = {}) {
   if (CHECK && row >= e.M) return;
   if (CHECK && c0 + NV > e.N) {
 #pragma unroll
@@ -553,7 +556,7 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
   if (EPI == RF_EPI_DGELU) {
     const E* z = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
     if (NV == 8) {
-      const typename H16<E>::x8 x = *reinterpret_cast<const typename H16<E>::x8*>(z);
+      const typename H16<E>::x8 x = ZV ? zv : *reinterpret_cast<const typename H16<E>::x8*>(z);
       float zf[8], d[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) zf[k] = (float)x[k];
@@ -1079,7 +1082,8 @@ __global__ void __launch_bounds__(256, 1)
               int nTm, int nTn) {
   typedef typename H16<E>::x8 V8;
   constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;
-  constexpr int S = OUT32 ? 64 : 32;  // epilogue stores per wave (interior tile)
+  // epilogue stores per wave (interior tile); EPI_BIAS_GELU_AUX stores the pre-activation too
+  constexpr int S = (OUT32 || EPI == RF_EPI_BIAS_GELU_AUX) ? 64 : 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles = nTm * nTn;
   int v = blockIdx.x;
@@ -1368,22 +1372,50 @@ __global__ void __launch_bounds__(256, 1)
     }
     auto epilogue = [&](auto check) {
       constexpr bool CK = decltype(check)::value;
+      // interior EPI_DGELU tiles: the lane's pre-activation rows stream ZD rows ahead of their use
+      // (row k + ZD is loaded before row k is computed), so a row's wait covers one load issued ZD
+      // rows earlier instead of a memory round trip per row (a load next to its use made hipcc wait
+      // vmcnt(0), draining the row's previous store and the next tile's operand DMA with it)
+      constexpr bool ZP = !CK && !OUT32 && EPI == RF_EPI_DGELU;
+      if constexpr (ZP) {
+        constexpr int ZD = 16;  // rows in flight (4 VGPRs each)
+        const char* zbase = reinterpret_cast<const char*>(e.R) + (int64_t)em0 * e.ldr * (int)sizeof(E);
+        auto zload = [&](int k) {
+          const int row = erow + (k >> 2) * 16 + (k & 3);
+          return *reinterpret_cast<const V8*>(zbase + (uint32_t)(((row - em0) * e.ldr + ecol) * (int)sizeof(E)));
+        };
+        V8 zv[ZD];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+        for (int k = 0; k < ZD; ++k) zv[k] = zload(k);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int k = 0; k < 32; ++k) {
+          const int i = k >> 2, r = k & 3;
+          const V8 z = zv[k % ZD];
+          if (k + ZD < 32) zv[k % ZD] = zload(k + ZD);
           float vv[8];
 #pragma unroll
           for (int f = 0; f < 8; ++f) vv[f] = acc[i][f][r];
-          const int row = erow + i * 16 + r;
-          const float rsc = EPI == RF_EPI_COS ? cb[256 + row - em0] : 0.f;
-          if (OUT32) {
-            epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
-            epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
-          } else {
-            epi_seg<E, EPI, CF32, RF32, 8, CK, !CK, FSC>(e, row, ecol, vv, bv, gm, bt, rsc, tbase, em0, csc);
-          }
+          epi_seg<E, EPI, CF32, RF32, 8, CK, true, FSC, true>(e, erow + i * 16 + r, ecol, vv, bv, gm, bt, 0.f, tbase,
+                                                              em0, csc, z);
         }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float vv[8];
+#pragma unroll
+            for (int f = 0; f < 8; ++f) vv[f] = acc[i][f][r];
+            const int row = erow + i * 16 + r;
+            const float rsc = EPI == RF_EPI_COS ? cb[256 + row - em0] : 0.f;
+            if (OUT32) {
+              epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+              epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
+            } else {
+              epi_seg<E, EPI, CF32, RF32, 8, CK, !CK, FSC>(e, row, ecol, vv, bv, gm, bt, rsc, tbase, em0, csc);
+            }
+          }
+      }
     };
     if (interior) epilogue(std::false_type{});
     else epilogue(std::true_type{});

@@ -225,10 +225,11 @@ __global__ void __launch_bounds__(256, 1)
   tn_wait_vm<0>();  // the (unused) DMA of the last phase B has landed before the workgroup exits
 }
 
-// C (=|+=) sum_s slabs[s]: fixed order over s, 4 consecutive floats per thread
+// C (=|+=) sum_s slabs[s]: fixed order over s, 4 consecutive floats per thread; rows n < scale_n of the
+// sum multiplied by scale first (a Linear's output-column scale, e.g. the query's 1/8: its dW rows)
 __global__ void __launch_bounds__(256) k_tn_reduce(int N, int K, const float* __restrict__ slabs, int ld_slab,
                                                    int64_t slab_stride, int S, float* __restrict__ C, int ldc,
-                                                   int accumulate) {
+                                                   int accumulate, int scale_n, float scale) {
   const int kq = K >> 2;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)N * kq) return;
@@ -238,6 +239,9 @@ __global__ void __launch_bounds__(256) k_tn_reduce(int N, int K, const float* __
   for (int s = 1; s < S; ++s) {
     const float4 b = *reinterpret_cast<const float4*>(s0 + s * slab_stride);
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  if (n < scale_n) {
+    a.x *= scale; a.y *= scale; a.z *= scale; a.w *= scale;
   }
   float* c = C + (int64_t)n * ldc + k;
   if (accumulate) {
@@ -273,7 +277,7 @@ static void tn_plan(int M, int N, int K, int& S, int& mchunk) {
 
 template <typename E>
 static int launch_tn(int M, int N, int K, const void* X, int ldx, const void* Y, int ldy, float* C, int ldc,
-                     int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
+                     int accumulate, int scale_n, float scale, void* ws, size_t ws_bytes, hipStream_t s) {
   int S, mchunk;
   tn_plan(M, N, K, S, mchunk);
   const int nTn = (N + 255) / 256, nTk = (K + 255) / 256;
@@ -288,7 +292,8 @@ static int launch_tn(int M, int N, int K, const void* X, int ldx, const void* Y,
   k_gemm_tn<E><<<nTn * nTk * S, 256, TN_LDS, s>>>(M, N, K, (const E*)X, ldx, (const E*)Y, ldy, (float*)ws, K, slab,
                                                   mchunk, nTn, nTk, S);
   const int64_t work = (int64_t)N * (K / 4);
-  k_tn_reduce<<<(unsigned)((work + 255) / 256), 256, 0, s>>>(N, K, (const float*)ws, K, slab, S, C, ldc, accumulate);
+  k_tn_reduce<<<(unsigned)((work + 255) / 256), 256, 0, s>>>(N, K, (const float*)ws, K, slab, S, C, ldc, accumulate,
+                                                                 scale_n, scale);
   return RF_OK;
 }
 
@@ -304,9 +309,9 @@ extern "C" size_t rf_weight_grad_workspace(int M, int N, int K) {
 }
 
 extern "C" int rf_weight_grad(int dtype, int M, int N, int K, const void* X, int ldx, const void* Y, int ldy,
-                              float* C, int ldc, int accumulate, void* workspace, size_t ws_bytes,
-                              rf_stream_t stream) {
-  RF_REQUIRE(M >= 0 && N > 0 && K > 0, "rf_weight_grad: bad shape M=%d N=%d K=%d", M, N, K);
+                              float* C, int ldc, int accumulate, int scale_rows, float row_scale, void* workspace,
+                              size_t ws_bytes, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && N > 0 && K > 0 && scale_rows >= 0, "rf_weight_grad: bad shape M=%d N=%d K=%d", M, N, K);
   RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_weight_grad: 16-bit operands only (dtype %d)", dtype);
   RF_REQUIRE(N % 16 == 0 && K % 16 == 0, "rf_weight_grad: N=%d and K=%d must be multiples of 16", N, K);
   RF_REQUIRE(ldx >= N && ldy >= K && ldx % 8 == 0 && ldy % 8 == 0 && ldc >= K && ldc % 4 == 0,
@@ -323,8 +328,9 @@ extern "C" int rf_weight_grad(int dtype, int M, int N, int K, const void* X, int
     }
     RF_LAUNCH_CHECK("rf_weight_grad");
   }
-  int rc = dtype == RF_BF16 ? launch_tn<bf16>(M, N, K, X, ldx, Y, ldy, C, ldc, accumulate, workspace, ws_bytes, s)
-                            : launch_tn<f16>(M, N, K, X, ldx, Y, ldy, C, ldc, accumulate, workspace, ws_bytes, s);
+  int rc = dtype == RF_BF16
+               ? launch_tn<bf16>(M, N, K, X, ldx, Y, ldy, C, ldc, accumulate, scale_rows, row_scale, workspace, ws_bytes, s)
+               : launch_tn<f16>(M, N, K, X, ldx, Y, ldy, C, ldc, accumulate, scale_rows, row_scale, workspace, ws_bytes, s);
   if (rc != RF_OK) return rc;
   RF_LAUNCH_CHECK("rf_weight_grad");
 }

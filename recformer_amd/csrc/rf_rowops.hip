@@ -638,8 +638,10 @@ __global__ void __launch_bounds__(256) k_colsum_part(int M, int N, const T* __re
 }
 
 // out[n] = sum_z part[z][n]: 64 slices x 4 columns per block, tree-reduced in LDS (fixed order)
+// scale_n > 0: out[c] for c < scale_n multiplied by scale (a Linear's column scale, e.g. the query's 1/8)
 __global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* __restrict__ part, float* __restrict__ out,
-                                                     float* __restrict__ out2, int split, float* __restrict__ out3) {
+                                                     float* __restrict__ out2, int split, float* __restrict__ out3,
+                                                     int scale_n = 0, float scale = 1.f) {
   __shared__ float red[64][5];
   const int z = threadIdx.x >> 2, k = threadIdx.x & 3;
   const int c = blockIdx.x * 4 + k;
@@ -652,18 +654,18 @@ __global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* _
   if (z == 0 && c < N) {
     if (out3 && c >= 2 * split) out3[c - 2 * split] = red[0][k];
     else if (out2 && c >= split) out2[c - split] = red[0][k];
-    else out[c] = red[0][k];
+    else out[c] = c < scale_n ? red[0][k] * scale : red[0][k];
   }
 }
 
 template <typename T>
 static void colsum(int M, int N, const T* x, int64_t ldx, float* part, float* out, float* out2, int split,
-                   hipStream_t s, float* out3 = nullptr) {
+                   hipStream_t s, float* out3 = nullptr, int scale_n = 0, float scale = 1.f) {
   const int S = max(1, min(CS_SLICES, (M + 63) / 64));
   const bool vec = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(T))) == 0;
   if (vec) k_colsum_part<T, true><<<dim3((N + 255) / 256, S), 256, 0, s>>>(M, N, x, ldx, part);
   else k_colsum_part<T, false><<<dim3((N + 255) / 256, S), 256, 0, s>>>(M, N, x, ldx, part);
-  k_colsum_fin<<<(N + 3) / 4, 256, 0, s>>>(S, N, part, out, out2, split, out3);
+  k_colsum_fin<<<(N + 3) / 4, 256, 0, s>>>(S, N, part, out, out2, split, out3, scale_n, scale);
 }
 
 template <typename T, int VEC, int NCH>
@@ -1161,17 +1163,20 @@ int rf_scatter_add_rows(int dtype, int R, int D, const int32_t* rows, const void
   RF_LAUNCH_CHECK("rf_scatter_add_rows");
 }
 
-int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, void* workspace, rf_stream_t stream) {
-  RF_REQUIRE(M >= 0 && N > 0 && ldx >= N, "rf_colsum: bad shape");
+int rf_colsum(int dtype, int M, int N, const void* x, int64_t ldx, float* out, int scale_cols, float col_scale,
+              void* workspace, rf_stream_t stream) {
+  RF_REQUIRE(M >= 0 && N > 0 && ldx >= N && scale_cols >= 0, "rf_colsum: bad shape");
   RF_REQUIRE(out && workspace && (M == 0 || x), "rf_colsum: null pointer");
   hipStream_t s = as_stream(stream);
   if (M == 0) {
     (void)hipMemsetAsync(out, 0, (size_t)N * sizeof(float), s);
     RF_LAUNCH_CHECK("rf_colsum");
   }
-  if (dtype == RF_BF16) colsum<bf16>(M, N, (const bf16*)x, ldx, (float*)workspace, out, nullptr, N, s);
-  else if (dtype == RF_F16) colsum<f16>(M, N, (const f16*)x, ldx, (float*)workspace, out, nullptr, N, s);
-  else if (dtype == RF_F32) colsum<float>(M, N, (const float*)x, ldx, (float*)workspace, out, nullptr, N, s);
+  float* ws = (float*)workspace;
+  if (dtype == RF_BF16) colsum<bf16>(M, N, (const bf16*)x, ldx, ws, out, nullptr, N, s, nullptr, scale_cols, col_scale);
+  else if (dtype == RF_F16) colsum<f16>(M, N, (const f16*)x, ldx, ws, out, nullptr, N, s, nullptr, scale_cols, col_scale);
+  else if (dtype == RF_F32)
+    colsum<float>(M, N, (const float*)x, ldx, ws, out, nullptr, N, s, nullptr, scale_cols, col_scale);
   else RF_REQUIRE(false, "rf_colsum: bad dtype %d", dtype);
   RF_LAUNCH_CHECK("rf_colsum");
 }

@@ -310,23 +310,26 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
     return dx, dw, db
 
 
-def colsum(x: torch.Tensor, tag: Optional[str] = None) -> torch.Tensor:
-    """rf_colsum: fp32 column sums of a row-major (M, N) bf16 / fp32 matrix (bias gradients)."""
+def colsum(x: torch.Tensor, scale_cols: int = 0, col_scale: float = 1.0, tag: Optional[str] = None) -> torch.Tensor:
+    """rf_colsum: fp32 column sums of a row-major (M, N) bf16 / fp32 matrix (bias gradients); the first
+    scale_cols sums multiplied by col_scale."""
     lib = _lib.load()
     _dev(x)
     M, N = x.shape
     out = torch.empty(N, dtype=torch.float32, device=x.device)
     ws = torch.empty(max(lib.rf_colsum_workspace(M, N), 4), dtype=torch.uint8, device=x.device)
     with _region(tag):
-        rc = lib.rf_colsum(dtype_code(x.dtype), M, N, _p(x), _rowmajor(x, "x"), _p(out), _p(ws), _stream(x))
+        rc = lib.rf_colsum(dtype_code(x.dtype), M, N, _p(x), _rowmajor(x, "x"), _p(out), int(scale_cols),
+                           float(col_scale), _p(ws), _stream(x))
     check(rc, "rf_colsum")
     return out
 
 
 def weight_grad(dc: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False,
-                tag: Optional[str] = None) -> torch.Tensor:
+                scale_rows: int = 0, row_scale: float = 1.0, tag: Optional[str] = None) -> torch.Tensor:
     """rf_weight_grad: dW = dc^T a in fp32 (N, K) for 16-bit dc (M, N) and a (M, K) row-major views (the
-    weight gradient of a Linear); `out` given with accumulate=True adds into it."""
+    weight gradient of a Linear), its first scale_rows rows multiplied by row_scale; `out` given with
+    accumulate=True adds into it."""
     lib = _lib.load()
     _dev(dc, a)
     M, N = dc.shape
@@ -342,7 +345,8 @@ def weight_grad(dc: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] =
     ws = torch.empty(max(lib.rf_weight_grad_workspace(M, N, K), 16), dtype=torch.uint8, device=dc.device)
     with _region(tag):
         rc = lib.rf_weight_grad(dtype_code(dc.dtype), M, N, K, _p(dc), _rowmajor(dc, "dc"), _p(a), _rowmajor(a, "a"),
-                                _p(out), _rowmajor(out, "out"), int(accumulate), _p(ws), ws.numel(), _stream(dc))
+                                _p(out), _rowmajor(out, "out"), int(accumulate), int(scale_rows), float(row_scale),
+                                _p(ws), ws.numel(), _stream(dc))
     check(rc, "rf_weight_grad")
     return out
 

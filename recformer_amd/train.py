@@ -130,21 +130,24 @@ def _dw_async(fn, ref: torch.Tensor):
     return join
 
 
-def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+def _weight_grad(dc: torch.Tensor, a: torch.Tensor, scale=(0, 1.0)) -> torch.Tensor:
     """dW = dC^T A (N, K) in fp32 (the master weight's dtype), reduced over the M = B*Lp token
-    rows. The layer weights are small (N*K <= 3072*768: at most 36 tiles of 256^2) against a long
+    rows, its first scale[0] rows multiplied by scale[1] (a column-scaled Linear: the query's 1/8).
+    The layer weights are small (N*K <= 3072*768: at most 36 tiles of 256^2) against a long
     reduction, so one GEMM leaves most of the chip idle; with DW_SPLIT_K the rows are split into
     S chunks computed as one batched GEMM (S times the tiles) and the S fp32 partials summed."""
+    sc, s = scale
+    if sc > 0 and s != 1.0 and not _dw_hip_ok(dc, a):
+        dw = _weight_grad(dc, a)
+        dw[:sc].mul_(s)
+        return dw
     M, N = dc.shape
     K = a.shape[1]
-    if (DW_HIP and dc.is_cuda and dc.dtype in (torch.bfloat16, torch.float16) and a.dtype == dc.dtype
-            and N % 16 == 0 and K % 16 == 0 and dc.stride(1) == 1 and a.stride(1) == 1
-            and dc.stride(0) % 8 == 0 and a.stride(0) % 8 == 0
-            and dc.data_ptr() % 16 == 0 and a.data_ptr() % 16 == 0):
+    if _dw_hip_ok(dc, a):
         # any M, including a few rows (the global query rows, the CLS-only last layer): the buffer
         # resources read rows past M as zeros — no library GEMM (and no library workspace on the
         # weight-gradient side stream, which a captured graph would own)
-        return ops.weight_grad(dc, a)
+        return ops.weight_grad(dc, a, scale_rows=sc, row_scale=s)
     if M < SMALL_M and dc.is_cuda and dc.dtype != torch.float32:
         return _mm_f32(dc.t(), a)
     S = 1
@@ -156,6 +159,14 @@ def _weight_grad(dc: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
         return _mm_f32(dc.t(), a)
     part = _mm_f32(dc.reshape(S, M // S, N).transpose(1, 2), a.reshape(S, M // S, K))  # (S, N, K)
     return part.sum(0)
+
+
+def _dw_hip_ok(dc: torch.Tensor, a: torch.Tensor) -> bool:
+    N, K = dc.shape[1], a.shape[1]
+    return (DW_HIP and dc.is_cuda and dc.dtype in (torch.bfloat16, torch.float16) and a.dtype == dc.dtype
+            and N % 16 == 0 and K % 16 == 0 and dc.stride(1) == 1 and a.stride(1) == 1
+            and dc.stride(0) % 8 == 0 and a.stride(0) % 8 == 0
+            and dc.data_ptr() % 16 == 0 and a.data_ptr() % 16 == 0)
 
 
 class _Gemm(torch.autograd.Function):
@@ -187,21 +198,24 @@ class _Gemm(torch.autograd.Function):
                 da = ops.gemm(dc.contiguous(), wa.t().contiguous(), None, ops.RF_EPI_NONE)  # rf_gemm, W^T copy
             else:
                 da = dc @ wa
-        dw = _weight_grad(dc, a).to(ctx.wdt) if ctx.needs_input_grad[1] else None
-        db = _bias_grad(dc) if ctx.needs_input_grad[3] else None  # deterministic HIP column sums
-        if scaled:
-            if dw is not None:
-                dw[:sc] *= s
-            if db is not None:
-                db[:sc] *= s
+        # the dW rows and db entries of the scaled outputs scaled inside the reduction kernels
+        dw = _weight_grad(dc, a, (sc, s)).to(ctx.wdt) if ctx.needs_input_grad[1] else None
+        db = _bias_grad(dc, (sc, s)) if ctx.needs_input_grad[3] else None  # deterministic HIP column sums
         return da, dw, None, db, None, None
 
 
-def _bias_grad(dc):
-    """Column sums of dC (a Linear's bias gradient): the ones the LayerNorm backward computed with dC
-    (_DropAddLN, LN_BIAS_GRAD) when dc is that very tensor, else rf_colsum."""
+def _bias_grad(dc, scale=(0, 1.0)):
+    """Column sums of dC (a Linear's bias gradient), the first scale[0] multiplied by scale[1]: the ones
+    the LayerNorm backward computed with dC (_DropAddLN, LN_BIAS_GRAD) when dc is that very tensor,
+    else rf_colsum."""
+    sc, s = scale
     cs = getattr(dc, "_rf_colsum", None)
-    return cs if cs is not None else ops.colsum(dc)
+    if cs is None:
+        return ops.colsum(dc, sc, s)
+    if sc > 0 and s != 1.0:
+        cs = cs.clone()
+        cs[:sc].mul_(s)
+    return cs
 
 
 class _GemmP(torch.autograd.Function):
@@ -226,16 +240,14 @@ class _GemmP(torch.autograd.Function):
         dc = dc.to(a.dtype).contiguous()
         scaled = sc > 0 and s != 1.0
         da = None
-        join = _dw_async(lambda: _weight_grad(dc, a).to(ctx.wdt), dc) if any(ctx.needs_input_grad[6:]) else None
+        # the dW rows and db entries of the scaled outputs scaled inside the reduction kernels
+        scl = (sc, s) if scaled else (0, 1.0)
+        join = (_dw_async(lambda: _weight_grad(dc, a, scl).to(ctx.wdt), dc) if any(ctx.needs_input_grad[6:])
+                else None)
         if ctx.needs_input_grad[0]:
             da = ops.gemm(dc, wt, None, ops.RF_EPI_NONE)  # any M (a few rows: the small-tile kernel)
-        db = _bias_grad(dc) if ctx.needs_input_grad[1] else None
+        db = _bias_grad(dc, scl) if ctx.needs_input_grad[1] else None
         dw = join() if join is not None else None
-        if scaled:
-            if dw is not None:
-                dw[:sc] *= s
-            if db is not None:
-                db[:sc] *= s
         dws = [None] * len(ctx.rows)
         if dw is not None:
             r0 = 0
@@ -791,8 +803,10 @@ class _Attention(torch.autograd.Function):
         ctx.q_scale = q_scale
         if ctx.qin:
             D0 = qkv.shape[1] // 3
-            qg = ops.gemm(h.index_select(0, grows[0]), wqg16, bqg, ops.RF_EPI_BIAS, scale_cols=D0,
-                          col_scale=q_scale)
+            # the global rows of h (rf_gather_global_rows; an empty slot gathers a zero row, whose
+            # qg no output reads)
+            hg = ops.gather_global_rows(h, gidx, B, Lp)
+            qg = ops.gemm(hg, wqg16, bqg, ops.RF_EPI_BIAS, scale_cols=D0, col_scale=q_scale)
             ctx.qw = (wqg16, wqgT16)
         ctx.fold_ws = None  # the forward fold's workspace when the HIP global backward can use it
         D = qkv.shape[1] // 3

@@ -587,6 +587,11 @@ def test_colsum(dev, dt, M, N):
         ref = x.float().sum(0)  # strided rows: vector path (ld % 4 == 0) and scalar path
         out = ops.colsum(x)
         assert (out - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item()) + 1e-3
+        # the first columns under a power-of-two scale (the query's 1/8): exactly the scaled sums
+        sc = (N + 1) // 2
+        exp = out.clone()
+        exp[:sc] *= 0.125
+        assert torch.equal(ops.colsum(x, sc, 0.125), exp)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
@@ -779,6 +784,14 @@ def test_weight_grad_matches_fp32_matmul(dev, dt, M, N, K, strided):
     acc = base.clone()
     ops.weight_grad(dc, a, out=acc, accumulate=True)
     assert float((acc - (base + ref)).abs().max()) <= 1e-4 * float(ref.abs().max()) + 1e-5
+    # the first rows under a power-of-two scale (the query's 1/8, TF:504-514): exactly the scaled rows
+    sr = min(N, 16 * ((N // 3 + 15) // 16))
+    exp = got.clone()
+    exp[:sr] *= 0.125
+    assert torch.equal(ops.weight_grad(dc, a, scale_rows=sr, row_scale=0.125), exp)
+    acc2 = base.clone()
+    ops.weight_grad(dc, a, out=acc2, accumulate=True, scale_rows=sr, row_scale=0.125)
+    assert torch.equal(acc2, base + exp)
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])

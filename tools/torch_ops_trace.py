@@ -1,8 +1,8 @@
 """Which Python lines launch the torch (non-HIP) kernels of the C3 training step.
 
-Runs one eager C3 step (tools/train_bench.py's model, batch and optimizer) under torch.profiler with
-Python stacks and prints, per aten op that launches a device kernel (fill_/zero_/zeros, add, copy_,
-index_select, cat, sort, ...), the call count per step and the innermost recformer_amd frames that
+Runs one eager C3 step (tools/train_bench.py's model, batch and optimizer) under a TorchDispatchMode
+that records the Python stack of every aten op on a device tensor and prints, per aten op that
+launches a device kernel (fill_/zero_/zeros, add, copy_, index_select, cat, sort, ...), the count per step and the innermost recformer_amd frames that
 issued it — the list of torch launches left to fold into the HIP kernels or remove.
 
     python tools/torch_ops_trace.py [--batch 16]
@@ -11,10 +11,11 @@ import argparse
 import collections
 import os
 import sys
+import traceback
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
-from torch.profiler import ProfilerActivity, profile  # noqa: E402
+from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
 
 from recformer_amd import RecformerConfig, RecformerForSeqRec  # noqa: E402
 from recformer_amd.optim import AdamW  # noqa: E402
@@ -23,7 +24,7 @@ from recformer_amd.synth import BASE, synth_batch  # noqa: E402
 OPS = ("aten::fill_", "aten::zero_", "aten::zeros", "aten::zeros_like", "aten::add", "aten::add_", "aten::copy_",
        "aten::index_select", "aten::index", "aten::cat", "aten::sort", "aten::mul", "aten::mul_", "aten::where",
        "aten::clamp", "aten::sum", "aten::arange", "aten::masked_fill", "aten::to", "aten::_to_copy",
-       "aten::index_add_", "aten::scatter_add_", "aten::embedding_dense_backward", "aten::div", "aten::neg")
+       "aten::index_add_", "aten::index_add", "aten::index_put_", "aten::scatter_add_", "aten::embedding_dense_backward", "aten::div", "aten::neg")
 
 
 def main():
@@ -52,25 +53,31 @@ def main():
     for _ in range(2):
         step()
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=False) as prof:
-        step()
-        torch.cuda.synchronize()
+    # aten-level interception (below autograd, so the engine's own gradient accumulations show up
+    # too); the Python stack at dispatch time names the recformer_amd line that issued each op
     per = collections.Counter()
     where = collections.defaultdict(collections.Counter)
-    for ev in prof.events():
-        if ev.name not in OPS:
-            continue
-        # only the outermost aten op of a chain (a zeros that calls fill_ counts once)
-        if ev.cpu_parent is not None and ev.cpu_parent.name.startswith("aten::"):
-            continue
-        frames = [f for f in (ev.stack or []) if "recformer_amd" in f or "torch/autograd" in f]
-        key = " < ".join(f.split("/")[-1] for f in frames[:a.frames]) or "(no recformer_amd frame)"
-        per[ev.name] += 1
-        where[ev.name][key] += 1
-    print(f"torch ops in one eager C3 step (batch {a.batch}): {sum(per.values())}")
+    names = {n.split("::")[1] for n in OPS}
+
+    class Rec(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            name = func.overloadpacket.__name__
+            if name in names and any(torch.is_tensor(x) and x.is_cuda for x in args):
+                st = traceback.extract_stack(limit=40)
+                fr = [f"{os.path.basename(f.filename)}:{f.lineno}" for f in st
+                      if "recformer_amd" in f.filename or "autograd" in f.filename]
+                key = " < ".join(reversed(fr[-a.frames:])) or "(autograd engine)"
+                per[name] += 1
+                where[name][key] += 1
+            return func(*args, **(kwargs or {}))
+
+    with Rec():
+        step()
+        torch.cuda.synchronize()
+    print(f"aten ops on device tensors in one eager C3 step (batch {a.batch}): {sum(per.values())}")
     for name, n in per.most_common():
         print(f"{n:5d}  {name}")
-        for key, m in where[name].most_common(8):
+        for key, m in where[name].most_common(10):
             print(f"         {m:4d}  {key}")
 
 
