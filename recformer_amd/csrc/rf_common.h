@@ -63,6 +63,7 @@ enum Knob {
   KNOB_EPI_TILE,        // training GELU GEMMs (EPI_DGELU, EPI_BIAS_GELU_AUX): 0 the four-wave 256x256 kernel,
                         // 1 the 128x128 tile kernel, 2 the 256x128 tile kernel (several workgroups per CU,
                         // so one's epilogue overlaps another's MFMAs)
+  KNOB_TN_WGS,          // weight-gradient GEMM: workgroups its row split aims at (0 = one per CU)
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];

@@ -235,9 +235,23 @@ __global__ void __launch_bounds__(256) k_tn_reduce(int N, int K, const float* __
   if (idx >= (int64_t)N * kq) return;
   const int n = (int)(idx / kq), k = (int)(idx - (int64_t)n * kq) * 4;
   const float* s0 = slabs + (int64_t)n * ld_slab + k;
-  float4 a = *reinterpret_cast<const float4*>(s0);
-  for (int s = 1; s < S; ++s) {
-    const float4 b = *reinterpret_cast<const float4*>(s0 + s * slab_stride);
+  auto ld = [&](int s) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s0 + s * slab_stride));
+    return make_float4(v[0], v[1], v[2], v[3]);
+  };
+  float4 a = ld(0);
+  int s = 1;
+  // four slabs' loads in flight per step (the adds keep the order s = 1, 2, ...: same sums as one
+  // at a time, which waited one memory round trip per slab)
+  for (; s + 4 <= S; s += 4) {
+    const float4 b0 = ld(s), b1 = ld(s + 1), b2 = ld(s + 2), b3 = ld(s + 3);
+    a.x += b0.x; a.y += b0.y; a.z += b0.z; a.w += b0.w;
+    a.x += b1.x; a.y += b1.y; a.z += b1.z; a.w += b1.w;
+    a.x += b2.x; a.y += b2.y; a.z += b2.z; a.w += b2.w;
+    a.x += b3.x; a.y += b3.y; a.z += b3.z; a.w += b3.w;
+  }
+  for (; s < S; ++s) {
+    const float4 b = ld(s);
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
   }
   if (n < scale_n) {
@@ -267,7 +281,7 @@ static int tn_cus() {
 // into a second round that doubled the kernel's time; each split at least 512 rows
 static void tn_plan(int M, int N, int K, int& S, int& mchunk) {
   const int T = ((N + 255) / 256) * ((K + 255) / 256);
-  const int cus = tn_cus();
+  const int cus = g_knob[KNOB_TN_WGS] > 0 ? g_knob[KNOB_TN_WGS] : tn_cus();
   int s = cus / T;
   const int max_s = max(1, M / 512);
   s = max(1, min(s, max_s));
