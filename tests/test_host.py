@@ -59,6 +59,20 @@ def test_library_exports_every_header_symbol():
     assert lib.rf_abi_version() == 1
 
 
+def test_every_documented_knob_is_readable():
+    """The knob names the header documents (rf_debug_set_knob) all resolve, and set / get round-trip;
+    an unknown name is an error message, not a crash. Host-side table only (no GPU)."""
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "recformer_hip.h")).read()
+    m = re.search(r"knobs? \(([^)]*)\)", hdr.replace("\n *", " "))
+    names = re.findall(r'"([a-z0-9_]+)"', m.group(1)) if m else []
+    assert "tn_wgs" in names and "gemm_mfma32" in names, names
+    for n in names:
+        v = _lib.get_knob(n)
+        assert _lib.set_knob(n, v) == v and _lib.get_knob(n) == v
+    with pytest.raises(_lib.RecformerHipError):
+        _lib.get_knob("no_such_knob")
+
+
 def test_argument_errors_come_back_as_messages():
     lib = _lib.load()
     # bad shape is rejected host-side before any launch (no GPU needed)
