@@ -4,7 +4,9 @@ score + rank + top-50 kernels (recformer_amd.ranker.shard_rank), one GPU.
     python tools/retrieval_bench.py [--queries 4096] [--items 125000,1000000] [--dtype fp16]
 
 Prints per shard size: ms per call, query-item pairs/s, TFLOP/s of the score GEMM (2*Q*N*d) and
-its fraction of the 2.5 PF dense fp16/bf16 MFMA peak; the counts-only mode (rank_catalog) too."""
+its fraction of the 2.5 PF dense fp16/bf16 MFMA peak; the counts-only mode (rank_catalog) too. Each mode
+runs on the kernel family the product path picks for it (ranker._rank_family: the 16x16x32 rank loop
+with a top-k, the 32x32x16 one for counts only) unless RF_KNOBS pins rank_w32."""
 import argparse
 import json
 import os
@@ -14,7 +16,9 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from recformer_amd.ranker import CatalogShard, label_scores, shard_rank  # noqa: E402
+import contextlib  # noqa: E402
+
+from recformer_amd.ranker import CatalogShard, _rank_family, label_scores, shard_rank  # noqa: E402
 
 
 def timeit(fn, iters=10, warm=3):
@@ -36,9 +40,12 @@ def main():
     ap.add_argument("--k", type=int, default=50)
     args = ap.parse_args()
     from recformer_amd import _lib
+    pinned = False
     for kv in filter(None, os.environ.get("RF_KNOBS", "").split(",")):  # e.g. RF_KNOBS=rank_w32=1
         k, v = kv.split("=")
         _lib.set_knob(k, int(v))
+        pinned = pinned or k == "rank_w32"
+    family = (lambda topk: contextlib.nullcontext()) if pinned else _rank_family
     dt = {"fp16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -48,9 +55,12 @@ def main():
         items = torch.randn(N, d, device=dev, generator=g).to(dt)
         labels = torch.randint(0, N, (Q,), device=dev, generator=g)
         shard = CatalogShard(items)
-        sl = label_scores(q, shard, labels, 0.05)
-        t_top = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=args.k))
-        t_cnt = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=0))
+        with family(True):  # label scores from the same family as the ranking (exact strict counts)
+            sl = label_scores(q, shard, labels, 0.05)
+            t_top = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=args.k))
+        with family(False):
+            sl = label_scores(q, shard, labels, 0.05)
+            t_cnt = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=0))
         fl = 2.0 * Q * N * d
         for name, t in (("rank+top%d" % args.k, t_top), ("rank only", t_cnt)):
             print(json.dumps({"items": N, "queries": Q, "dtype": args.dtype, "mode": name, "ms": round(t * 1e3, 3),
