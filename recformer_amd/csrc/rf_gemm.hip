@@ -530,7 +530,8 @@ __device__ __forceinline__ int wperm(int rho) {
 // FS: the caller pre-scaled bv by this lane's column scale cs (its columns lie on one side of
 // scale_cols, a multiple of 16): v = fma(v, cs, bv) instead of (v + bv) * col_scale under a per-lane
 // branch — bit-identical for cs = 1 and for power-of-two scales (1/sqrt(64)).
-// ZV (EPI_DGELU, NV = 8): the pre-activations come in zv, loaded by the caller ahead of use
+// ZV (NV = 8): EPI_DGELU's pre-activations / EPI_BIAS_RESID's 16-bit residual come in zv, loaded by
+// the caller ahead of use
 template <typename E, int EPI, bool CF32, bool RF32, int NV, bool CHECK = true, bool TB = false, bool FS = false,
           bool ZV = false>
 __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float* v, const float* bv,
@@ -618,6 +619,9 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
         const float4 x = *reinterpret_cast<const float4*>(r + 4 * q);
         v[4 * q] += x.x; v[4 * q + 1] += x.y; v[4 * q + 2] += x.z; v[4 * q + 3] += x.w;
       }
+    } else if (ZV && NV == 8) {  // the caller's prefetched residual row segment
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += (float)zv[k];
     } else {
       const E* r = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
 #pragma unroll
@@ -1376,7 +1380,9 @@ __global__ void __launch_bounds__(256, 1)
       // (row k + ZD is loaded before row k is computed), so a row's wait covers one load issued ZD
       // rows earlier instead of a memory round trip per row (a load next to its use made hipcc wait
       // vmcnt(0), draining the row's previous store and the next tile's operand DMA with it)
-      constexpr bool ZP = !CK && !OUT32 && EPI == RF_EPI_DGELU;
+      // (the same for a 16-bit residual row, EPI_BIAS_RESID: the training dA GEMM that adds the other
+      // consumer's gradient, train._GradMailbox)
+      constexpr bool ZP = !CK && !OUT32 && (EPI == RF_EPI_DGELU || (EPI == RF_EPI_BIAS_RESID && !RF32));
       if constexpr (ZP) {
         constexpr int ZD = 16;  // rows in flight (4 VGPRs each)
         const char* zbase = reinterpret_cast<const char*>(e.R) + (int64_t)em0 * e.ldr * (int)sizeof(E);

@@ -103,6 +103,9 @@ def _mm_f32(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
 # a quarter of the chip would idle; the independent dW = dC^T A work fills it (forked and joined with
 # stream events — graph-capturable)
 DW_SIDE_STREAM = True
+# the attention's gradient of a layer's input added inside the q|k|v projection's dA GEMM (_GradMailbox)
+# instead of autograd's separate bf16 sum
+GRAD_MAILBOX = True
 _SIDE_STREAMS = {}
 
 
@@ -218,6 +221,28 @@ def _bias_grad(dc, scale=(0, 1.0)):
     return cs
 
 
+class _GradMailbox:
+    """One layer's hand-off of h's gradient from the attention's backward to the q|k|v projection's
+    backward: h (the LayerNorm output) feeds both, so autograd would add their two bf16 gradients in a
+    separate pass over (M, d); instead _Attention.backward leaves its part here and _GemmP.backward (which
+    runs after it: it needs the attention's dq|dk|dv) adds it in the dA GEMM's epilogue (EPI_BIAS_RESID
+    with a zero bias; one rounding to bf16 instead of two)."""
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
+_ZERO_BIAS = {}
+
+
+def _zero_bias(n: int, device) -> torch.Tensor:
+    t = _ZERO_BIAS.get((n, device))
+    if t is None:
+        t = _ZERO_BIAS[(n, device)] = torch.zeros(n, dtype=torch.float32, device=device)
+    return t
+
+
 class _GemmP(torch.autograd.Function):
     """_Gemm over packed weights (ops.WeightPack, one rf_pack_weights launch per forward): the forward
     reads the compute-dtype copy w16, the backward's dA = dC.W the packed transposed copy w16t (its
@@ -226,8 +251,9 @@ class _GemmP(torch.autograd.Function):
     one rf_weight_grad result, with no concatenation in the forward and no split copy."""
 
     @staticmethod
-    def forward(ctx, a, b, w16, w16t, scale_cols: int, col_scale: float, *masters):
+    def forward(ctx, a, b, w16, w16t, scale_cols: int, col_scale: float, mb, *masters):
         ctx.save_for_backward(a, w16t)
+        ctx.mb = mb  # a _GradMailbox (or None): another consumer's gradient of a, added into dA
         ctx.sc = (scale_cols, col_scale)
         ctx.rows = [m.shape[0] for m in masters]
         ctx.wdt = masters[0].dtype
@@ -242,19 +268,24 @@ class _GemmP(torch.autograd.Function):
         da = None
         # the dW rows and db entries of the scaled outputs scaled inside the reduction kernels
         scl = (sc, s) if scaled else (0, 1.0)
-        join = (_dw_async(lambda: _weight_grad(dc, a, scl).to(ctx.wdt), dc) if any(ctx.needs_input_grad[6:])
+        join = (_dw_async(lambda: _weight_grad(dc, a, scl).to(ctx.wdt), dc) if any(ctx.needs_input_grad[7:])
                 else None)
         if ctx.needs_input_grad[0]:
-            da = ops.gemm(dc, wt, None, ops.RF_EPI_NONE)  # any M (a few rows: the small-tile kernel)
+            other = ctx.mb.g if ctx.mb is not None else None
+            if other is not None:  # dA + the attention's gradient of the same input, in the epilogue
+                ctx.mb.g = None
+                da = ops.gemm(dc, wt, _zero_bias(wt.shape[0], dc.device), ops.RF_EPI_BIAS_RESID, resid=other)
+            else:
+                da = ops.gemm(dc, wt, None, ops.RF_EPI_NONE)  # any M (a few rows: the small-tile kernel)
         db = _bias_grad(dc, scl) if ctx.needs_input_grad[1] else None
         dw = join() if join is not None else None
         dws = [None] * len(ctx.rows)
         if dw is not None:
             r0 = 0
             for i, n in enumerate(ctx.rows):
-                dws[i] = dw[r0:r0 + n] if ctx.needs_input_grad[6 + i] else None
+                dws[i] = dw[r0:r0 + n] if ctx.needs_input_grad[7 + i] else None
                 r0 += n
-        return (da, db, None, None, None, None, *dws)
+        return (da, db, None, None, None, None, None, *dws)
 
 
 class _GemmGelu(torch.autograd.Function):
@@ -793,7 +824,9 @@ class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, half_w, fold, grows=None,
                 attn_p: float = 0.0, seed: int = 0, wkg_master=None, wvg_master=None, wqg16=None, wqgT16=None,
-                bqg=None, wqg_master=None, q_scale: float = 1.0):
+                bqg=None, wqg_master=None, q_scale: float = 1.0, mb=None):
+        # mb: a _GradMailbox shared with the q|k|v projection of h (h's gradient from here goes there)
+        ctx.mb = mb
         # wkg / wvg: the global key / value weights in the compute dtype; with the masters given
         # (packed copies, not tracked) their gradients go to the fp32 masters directly.
         # wqg16 given (GLOBAL_QG_INSIDE): qg = (h[global rows] Wqg^T + bqg) * q_scale is computed here
@@ -924,13 +957,24 @@ class _Attention(torch.autograd.Function):
                     res[2], qtail = _Attention._qg_backward(ctx, grads[0], res[2], h, gidx, B, Lp, hip_bwd)
         if ctx.needs_input_grad[0]:
             res[0] = dqkv.to(qkv.dtype)
-        tail = [None] * 17  # the forward's non-tensor inputs, the two masters, the query weights
+        tail = [None] * 18  # the forward's non-tensor inputs, the two masters, the query weights, mb
         if ctx.masters and gmax > 0 and (any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]) or
                                          ctx.qin):
             tail[10:12] = extra
         if ctx.qin and gmax > 0:
             tail[12:17] = qtail
-        return (*res, *tail)
+        return (*_Attention._post_h(ctx, res, h), *tail)
+
+    @staticmethod
+    def _post_h(ctx, res, h):
+        """h's gradient into the mailbox (the q|k|v projection's dA adds it) instead of to autograd."""
+        dh = res[2]
+        if (ctx.mb is not None and dh is not None and dh.dtype == h.dtype and dh.shape == h.shape
+                and dh.is_contiguous()):
+            ctx.mb.g = dh
+            res = list(res)
+            res[2] = None
+        return res
 
     @staticmethod
     def _qg_backward(ctx, dqg, dh, h, gidx, B: int, Lp: int, hip: bool):
@@ -984,7 +1028,7 @@ class _Attention(torch.autograd.Function):
             res = [torch.cat(z, 1)] + res[3:]
         else:
             res = [None] + res[3:]
-        tail = [None] * 17  # the forward's non-tensor inputs, the two masters, the query weights
+        tail = [None] * 18  # the forward's non-tensor inputs, the two masters, the query weights, mb
         if ctx.masters:
             g_k, g_v = res[3], res[5]
             res[3] = res[5] = None
@@ -994,7 +1038,7 @@ class _Attention(torch.autograd.Function):
             res[1] = None
             B, Lp = ctx.dims[0], ctx.dims[1]
             res[2], tail[12:17] = _Attention._qg_backward(ctx, dqg, res[2], h, gidx, B, Lp, False)
-        return (*res, *tail)
+        return (*_Attention._post_h(ctx, res, h), *tail)
 
 
 # ------------------------------------------------------------------------------------------
@@ -1128,11 +1172,12 @@ def _packed_layer_weights(model, dt: torch.dtype, scale: float):
     return _cast(("pack", id(model), dt, scale), make)
 
 
-def _lin(a, lw, wkey: str, bkey: str, scale_cols: int, col_scale: float):
-    """One of the layer's Linears: _GemmP over the packed weights, or _Gemm (master, w16)."""
+def _lin(a, lw, wkey: str, bkey: str, scale_cols: int, col_scale: float, mb=None):
+    """One of the layer's Linears: _GemmP over the packed weights (mb: a _GradMailbox through which
+    another consumer of `a` hands over its gradient), or _Gemm (master, w16)."""
     if lw.get("packed"):
         masters, w16, w16t = lw[wkey]
-        return _GemmP.apply(a, lw[bkey], w16, w16t, scale_cols, col_scale, *masters)
+        return _GemmP.apply(a, lw[bkey], w16, w16t, scale_cols, col_scale, mb, *masters)
     return _Gemm.apply(a, *lw[wkey], lw[bkey], scale_cols, col_scale)
 
 
@@ -1285,7 +1330,10 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
             attn_probe.append(layer_attention_probs(
                 h.detach(), lyr.attention.self, flags, gidx, B, Lp, L, Lp, H, windows[li] // 2, scale,
                 None if head_cols is None else head_cols[li, ::hd].detach()))
-        qkv = _lin(h, lw, "w_qkv", "b_qkv", D, scale)
+        # the attention's gradient of h joins the q|k|v projection's dA in its epilogue (packed weights,
+        # 16-bit h: the residual form of the GEMM)
+        mb = _GradMailbox() if (lw.get("packed") and GRAD_MAILBOX and h.dtype != torch.float32) else None
+        qkv = _lin(h, lw, "w_qkv", "b_qkv", D, scale, mb)
         qg = None
         qin = ()
         if gmax > 0 and qg_inside:
@@ -1296,7 +1344,7 @@ def encode_train(model, input_ids, attention_mask, global_attention_mask, token_
             qg = _lin(hg, lw, "w_qg", "b_qg", D, scale)
         ctx = _Attention.apply(qkv, qg, h, lw["w_kg"], lw["b_kg"], lw["w_vg"], lw["b_vg"],
                                flags, gidx, B, Lp, H, windows[li] // 2, fold, grows, p_att, att_seeds[li],
-                               lw.get("wkg_master"), lw.get("wvg_master"), *qin)
+                               lw.get("wkg_master"), lw.get("wvg_master"), *(qin or (None, None, None, None, 1.0)), mb)
         if head_cols is not None:
             ctx = ctx * head_cols[li].to(ctx.dtype)
         ao = lyr.attention.output
