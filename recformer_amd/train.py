@@ -106,6 +106,9 @@ DW_SIDE_STREAM = True
 # the attention's gradient of a layer's input added inside the q|k|v projection's dA GEMM (_GradMailbox)
 # instead of autograd's separate bf16 sum
 GRAD_MAILBOX = True
+# the bias gradients' column sums on the weight-gradient side stream too: measured slower (captured C3
+# 16.48 vs 16.38 ms in one process, gpurun_out/r04s: that stream is the step's critical path), so off
+BIAS_GRAD_SIDE = False
 _SIDE_STREAMS = {}
 
 
@@ -268,8 +271,9 @@ class _GemmP(torch.autograd.Function):
         da = None
         # the dW rows and db entries of the scaled outputs scaled inside the reduction kernels
         scl = (sc, s) if scaled else (0, 1.0)
-        join = (_dw_async(lambda: _weight_grad(dc, a, scl).to(ctx.wdt), dc) if any(ctx.needs_input_grad[7:])
-                else None)
+        side_b = BIAS_GRAD_SIDE and ctx.needs_input_grad[1] and any(ctx.needs_input_grad[7:])
+        join = (_dw_async(lambda: (_weight_grad(dc, a, scl).to(ctx.wdt), _bias_grad(dc, scl) if side_b else None),
+                          dc) if any(ctx.needs_input_grad[7:]) else None)
         if ctx.needs_input_grad[0]:
             other = ctx.mb.g if ctx.mb is not None else None
             if other is not None:  # dA + the attention's gradient of the same input, in the epilogue
@@ -277,8 +281,11 @@ class _GemmP(torch.autograd.Function):
                 da = ops.gemm(dc, wt, _zero_bias(wt.shape[0], dc.device), ops.RF_EPI_BIAS_RESID, resid=other)
             else:
                 da = ops.gemm(dc, wt, None, ops.RF_EPI_NONE)  # any M (a few rows: the small-tile kernel)
-        db = _bias_grad(dc, scl) if ctx.needs_input_grad[1] else None
-        dw = join() if join is not None else None
+        db = _bias_grad(dc, scl) if ctx.needs_input_grad[1] and not side_b else None
+        dw = None
+        if join is not None:
+            dw, dbs = join()
+            db = dbs if side_b else db
         dws = [None] * len(ctx.rows)
         if dw is not None:
             r0 = 0
@@ -471,11 +478,14 @@ class _FFN(torch.autograd.Function):
         db2 = _bias_grad(dt2) if ctx.needs_input_grad[6] else None
         # both weight gradients on the side stream, beside da = dz.W1 (N = 768: a quarter of the CUs
         # idle at 16k tokens); dw2 waits for nothing but dt2, dw1 for dz
+        side_b = BIAS_GRAD_SIDE and ctx.needs_input_grad[3]
         join = _dw_async(lambda: (_weight_grad(dt2, u).to(ctx.wdt[1]) if ctx.needs_input_grad[4] else None,
-                                  _weight_grad(dz, a).to(ctx.wdt[0]) if ctx.needs_input_grad[1] else None), dz)
+                                  _weight_grad(dz, a).to(ctx.wdt[0]) if ctx.needs_input_grad[1] else None,
+                                  ops.colsum(dz) if side_b else None), dz)
         da = ops.gemm(dz, w1t, None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
-        db1 = ops.colsum(dz) if ctx.needs_input_grad[3] else None
-        dw2, dw1 = join()
+        db1 = ops.colsum(dz) if ctx.needs_input_grad[3] and not side_b else None
+        dw2, dw1, db1s = join()
+        db1 = db1s if side_b else db1
         return da, dw1, None, db1, dw2, None, db2, None, None
 
 
