@@ -582,7 +582,8 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
       typename H16<E>::x8 x;
 #pragma unroll
       for (int k = 0; k < 8; ++k) x[k] = (E)v[k];
-      *reinterpret_cast<typename H16<E>::x8*>(z) = x;
+      // non-temporal: read again only by the backward's GELU-derivative GEMM, a whole pass later
+      __builtin_nontemporal_store(x, reinterpret_cast<typename H16<E>::x8*>(z));
     } else {
 #pragma unroll
       for (int k = 0; k < NV; ++k) z[k] = (E)v[k];
