@@ -240,9 +240,14 @@ _ZERO_BIAS = {}
 
 
 def _zero_bias(n: int, device) -> torch.Tensor:
+    """A zero bias vector for the residual-form GEMM. Cached only when made outside a graph capture: a
+    tensor allocated while capturing lives in that graph's private pool and is freed with the graph,
+    so a cached one would dangle for every later step."""
     t = _ZERO_BIAS.get((n, device))
     if t is None:
-        t = _ZERO_BIAS[(n, device)] = torch.zeros(n, dtype=torch.float32, device=device)
+        t = torch.zeros(n, dtype=torch.float32, device=device)
+        if not torch.cuda.is_current_stream_capturing():
+            _ZERO_BIAS[(n, device)] = t
     return t
 
 
