@@ -64,6 +64,8 @@ enum Knob {
                         // 1 the 128x128 tile kernel, 2 the 256x128 tile kernel (several workgroups per CU,
                         // so one's epilogue overlaps another's MFMAs)
   KNOB_TN_WGS,          // weight-gradient GEMM: workgroups its row split aims at (0 = one per CU)
+  KNOB_MID_TILE,        // EPI_NONE / EPI_BIAS GEMMs whose 256x256 grid leaves CUs idle: 0 the four-wave kernel,
+                        // 1 the 128x128 tile kernel, 2 the 256x128 one
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];

@@ -2011,6 +2011,18 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
         return;
       }
     }
+    if constexpr (!RF32 && (EPI == RF_EPI_NONE || EPI == RF_EPI_BIAS)) {
+      // A/B: the N = 768 GEMMs at the training batch (16k rows: 192 tiles of 256^2 for 256 CUs) on
+      // smaller tiles that cover the chip
+      if (g_knob[KNOB_MID_TILE] && tiles256 < num_cus()) {
+        if (g_knob[KNOB_MID_TILE] == 1) {
+          launch_bf16<E, 128, 128, 64, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+          return;
+        }
+        launch_bf16<E, 256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+        return;
+      }
+    }
     if constexpr (!RF32 && EPI != RF_EPI_BIAS_RESID && EPI != RF_EPI_BIAS_RESID_LN) {
       const int64_t cb = (CF32 || EPI == RF_EPI_COS) ? 4 : 2;
       const bool w32_ok = N % 8 == 0 && (int64_t)256 * e.ldc * cb < 0x7FFFFFFF &&
