@@ -65,7 +65,8 @@ enum Knob {
                         // so one's epilogue overlaps another's MFMAs)
   KNOB_TN_WGS,          // weight-gradient GEMM: workgroups its row split aims at (0 = one per CU)
   KNOB_MID_TILE,        // EPI_NONE / EPI_BIAS GEMMs whose 256x256 grid leaves CUs idle: 0 the four-wave kernel,
-                        // 1 the 128x128 tile kernel, 2 the 256x128 one
+                        // 1 the 128x128 tile kernel, 2 the 256x128 one (captured C3: 17.77 / 18.20 vs
+                        // 16.26 / 16.36 ms, r04z: the older tile kernels lose more than the idle CUs cost)
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];
