@@ -270,13 +270,25 @@ def test_captured_dp_step_nccl_single_rank(dev):
     collectives from the backward hooks of the window's last micro-batch; the first micro-batch under
     no_sync): a one-rank nccl group on the box, so the collectives really run inside the HIP graph;
     the averaged gradients (world 1: the gradients) give the eager steps' parameters. The semantic
-    world-2 check is test_dp.py / test_gpu_pretrain.py (gloo)."""
+    world-2 check is test_dp.py / test_gpu_pretrain.py (gloo). Runs in a child process: a failure
+    inside RCCL during graph capture aborts its process (it did once, on one box, in capture_end),
+    which would otherwise take the rest of the suite with it."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import torch\nfrom tests.test_gpu_graphs import _captured_dp_step_nccl_single_rank as f\n"
+            "f(torch.device('cuda'))\nprint('child ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "child ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+
+
+def _captured_dp_step_nccl_single_rank(dev):
     import os
     import socket
     import torch.distributed as dist
     from recformer_amd.dp import GradBucketer
-    if dist.is_initialized():
-        pytest.skip("a process group is already initialised")
+    assert not dist.is_initialized()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
