@@ -278,7 +278,7 @@ def test_captured_dp_step_nccl_single_rank(dev):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = ("import torch\nfrom tests.test_gpu_graphs import _captured_dp_step_nccl_single_rank as f\n"
-            "f(torch.device('cuda'))\nprint('child ok')\n")
+            "f(torch.device('cuda', 0))\nprint('child ok')\n")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "child ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
