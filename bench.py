@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--full-last-layer", action="store_true",
                     help="every row through the last layer (default: the CLS rows only, which is all the "
                          "scores read; recformer_amd.models._cls_last_layer)")
+    ap.add_argument("--no-full-leg", action="store_true",
+                    help="skip the second timed leg with every row through the last layer (reported next to "
+                         "the headline value so kernel progress stays comparable round over round)")
     ap.add_argument("--timing-steps", type=int, default=20,
                     help="steps of the separate HIP-event-instrumented pass (per-kernel times)")
     return ap.parse_args()
@@ -70,13 +73,29 @@ def gemm_flops_per_seq(L, d, ffn, layers, gmax=1, fold=True):
     return per_layer * layers
 
 
-def e2e_floor_us(L, d, ffn, layers, catalog, w=64, gmax=1):
-    """SURVEY §8d end-to-end MFMA bound per sequence: the GEMMs (folded global projections), the
-    exact band attention (4*d*sum|keys_i| + 4*G*L*d per layer, |keys_i| = w + 1 + G) and the
-    catalog scoring (2*N*d), at 2.5 PF dense bf16."""
-    attn = layers * (4 * d * L * (w + 1 + gmax) + 4 * gmax * L * d)
-    flops = gemm_flops_per_seq(L, d, ffn, layers, gmax) + attn + 2 * catalog * d
-    return flops / (BF16_PEAK_TFLOPS * 1e12) * 1e6
+def step_flops_per_seq(L, d, ffn, layers, catalog, w=64, gmax=1, cls_last=True):
+    """Algorithmic flops per sequence of the step as it runs (SURVEY §8d counting: the GEMMs with the
+    global projections folded, the exact band attention 4*d*sum|keys_i| + 4*G*L*d per layer with
+    |keys_i| = w + 1 + G, the catalog scoring 2*N*d). cls_last: the last layer on the CLS rows only
+    (models._cls_last_layer, what RecformerForSeqRec runs when every CLS is global) — its q_g projection
+    on the G global rows, the global rows' attention over all L keys, and out-proj + FFN on the one CLS
+    row; its local q|k|v projection, band attention and L-row GEMMs are not run."""
+    full = layers - 1 if cls_last else layers
+    gemm = gemm_flops_per_seq(L, d, ffn, full, gmax)
+    attn = full * (4 * d * L * (w + 1 + gmax) + 4 * gmax * L * d)
+    if cls_last:
+        gemm += 2 * gmax * d * d + 2 * d * d + 2 * 2 * d * ffn
+        attn += 4 * gmax * L * d
+    score = 2 * catalog * d
+    return {"gemm": gemm, "attn": attn, "score": score, "total": gemm + attn + score}
+
+
+def e2e_floor_us(L, d, ffn, layers, catalog, w=64, gmax=1, cls_last=True):
+    """End-to-end MFMA bound per sequence of the step as it runs, at 2.5 PF dense bf16:
+    176.5 GFLOP -> 70.6 us/seq with every row through the last layer, 161.8 GFLOP -> 64.7 us/seq with
+    the CLS-only last layer."""
+    f = step_flops_per_seq(L, d, ffn, layers, catalog, w, gmax, cls_last)["total"]
+    return f / (BF16_PEAK_TFLOPS * 1e12) * 1e6
 
 
 def committed_profile(B, L, layers):
@@ -291,6 +310,27 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        # second leg: the same step with every row through the last layer (the kernels' work of a
+        # 12-full-layer encode; comparable with rounds before the CLS-only last layer)
+        elapsed_full = None
+        if not args.full_last_layer and not args.no_full_leg:
+            models.PRUNE_LAST_LAYER = False
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            elapsed_full = time.perf_counter() - t1
+            models.PRUNE_LAST_LAYER = True
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
         # per-kernel breakdown from a separate instrumented pass (HIP events around every
         # launch), so the event records never sit inside the timed steps
         kt, inst_steps, inst_s = {}, 0, 0.0
@@ -309,6 +349,7 @@ def main():
     tmax = dp.max_over_ranks(elapsed, device=coll_dev)
     total_seqs = B * world * args.steps
     value = total_seqs / tmax
+    tmax_full = dp.max_over_ranks(elapsed_full, device=coll_dev) if elapsed_full is not None else None
 
     out = None
     if rank == 0:
@@ -353,7 +394,9 @@ def main():
                              "traffic_unit": "HBM bytes per launch (PMC)", "profile_source": prof_src,
                              "profile_us": prof.get("band_attn", {}).get("median_us"),
                              "algorithmic_per_launch": f"{nbytes / 1e6:.1f} MB (8*B*L*d bytes)"}
-        flops_seq = gemm_flops_per_seq(L, d, ffn, args.layers, fold=getattr(cfg, "global_attention_fold", True))
+        cls_last = not args.full_last_layer
+        fl = step_flops_per_seq(L, d, ffn, args.layers, args.catalog, cls_last=cls_last)
+        floor = e2e_floor_us(L, d, ffn, args.layers, args.catalog, cls_last=cls_last)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "user-seq/s",
             "n_gpus": dist.get_world_size() if world > 1 else 1,
@@ -370,18 +413,29 @@ def main():
                        **({"ranks_share_devices": ndev} if rehearsal else {})},
             "roofline": roofline,
             "attention_roofline": attn_roof,
-            "model_tflops": round(value / world * flops_seq / 1e12, 1),
-            # end to end against the MFMA bound of the algorithm (GEMMs + exact band
-            # attention + scoring = 176.5 GFLOP/seq at C2 -> 70.6 us/seq at 2.5 PF dense bf16)
-            "e2e_roofline": {"bound": "mfma", "us_per_seq_floor": round(e2e_floor_us(L, d, ffn, args.layers,
-                                                                                      args.catalog), 2),
-                             "frac": round(value / world * e2e_floor_us(L, d, ffn, args.layers, args.catalog) * 1e-6, 4),
-                             "note": "per-GPU seq/s x the MFMA-bound us per sequence"},
+            # the algorithmic flops of the step as it runs (GEMMs + band attention + scoring)
+            "model_tflops": round(value / world * fl["total"] / 1e12, 1),
+            "gflop_per_seq": {k: round(v / 1e9, 3) for k, v in fl.items()},
+            # end to end against the MFMA bound of the algorithm as run
+            "e2e_roofline": {"bound": "mfma", "us_per_seq_floor": round(floor, 2),
+                             "frac": round(value / world * floor * 1e-6, 4),
+                             "note": "per-GPU seq/s x the MFMA-bound us per sequence of the step as run"},
+        }
+        if tmax_full is not None:
+            v_full = total_seqs / tmax_full
+            floor_full = e2e_floor_us(L, d, ffn, args.layers, args.catalog, cls_last=False)
+            out["value_full_last_layer"] = round(v_full, 2)
+            out["full_last_layer"] = {"ms_per_step": round(1e3 * tmax_full / args.steps, 3), "steps": args.steps,
+                                      "e2e_frac": round(v_full / world * floor_full * 1e-6, 4),
+                                      "us_per_seq_floor": round(floor_full, 2),
+                                      "note": "same process, same batch, every row through the last layer "
+                                              "(models.PRUNE_LAST_LAYER=False)"}
+        out.update({
             "kernels": kernels,
             "kernels_pass": ({"steps": inst_steps, "ms_per_step": round(1e3 * inst_s / inst_steps, 3),
                               "note": "separate HIP-event-instrumented steps after the timed ones"}
                              if inst_steps else None),
-        }
+        })
         if want_cpu:
             items_cpu = items.float()
             out["cpu_baseline"] = cpu_baseline(sd_cpu, cfg, items_cpu, L, args.cpu_baseline_seconds,

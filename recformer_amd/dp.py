@@ -117,16 +117,31 @@ class GradBucketer:
     gradients in ~25-50 MB buckets launched in reverse layer order during backward).
 
     Parameters are grouped, in reverse registration order (the order backward produces their
-    gradients), into buckets of <= bucket_bytes per (dtype, device). A post-accumulate-grad hook
-    counts each bucket's ready gradients; once a bucket is complete AND every lower-numbered bucket
-    has been launched, it is flattened and its all-reduce launched asynchronously, so communication
-    of late layers overlaps the backward of early ones. Launches are strictly in bucket order on
-    every rank — a bucket whose parameters got no gradient on one rank (e.g. the global-attention
-    projections of a batch without global tokens) holds the later buckets back until `finish()`
-    instead of letting ranks pair different buckets in the collective. `finish()` launches what is
-    left, waits, divides by the world size (average: the mean of the ranks' gradients, as
-    DistributedDataParallel) and copies back into each .grad; parameters without a gradient are
-    reduced as zeros. With one rank it does nothing.
+    gradients), into buckets of <= bucket_bytes per (dtype, device). Each bucket owns one persistent
+    flat buffer and every parameter's .grad is a view into it (DDP's gradient_as_bucket_view): backward
+    accumulates straight into the bucket, so there is no flattening copy before the collective and no
+    copy back after it. A post-accumulate-grad hook counts each bucket's ready gradients; once a bucket
+    is complete AND every lower-numbered bucket has been launched, its all-reduce is launched
+    asynchronously, so communication of late layers overlaps the backward of early ones. Launches are
+    strictly in bucket order on every rank — a bucket whose parameters got no gradient on one rank (e.g.
+    the global-attention projections of a batch without global tokens) holds the later buckets back
+    until `finish()` instead of letting ranks pair different buckets in the collective. `finish()`
+    launches what is left, waits and averages (the mean of the ranks' gradients, as
+    DistributedDataParallel); a parameter without a gradient on a rank contributes zeros. With one rank
+    it does nothing (unless single_rank).
+
+    comm_dtype: the dtype on the wire. None = the gradients' own (fp32 master gradients: 4 bytes per
+    parameter, 592 MB per exchange at 148M parameters, averaged by the collective itself on RCCL);
+    torch.bfloat16 / torch.float16 = a 16-bit exchange, as the reference's DeepSpeed precision=16 step
+    (lightning_pretrain.py:134-145): each complete bucket is packed once into a 16-bit buffer, pre-divided
+    by the world size (fp32 arithmetic, one rounding), all-reduced (296 MB per exchange), and unpacked
+    into the fp32 bucket — fp32 master accumulation, a 16-bit exchange.
+
+    Gradient storage: the bucket views are installed at construction and re-installed by zero_grad()
+    (which zeroes the flat buffers: one fill per bucket). A driver that sets gradients to None
+    (optimizer.zero_grad()) still works: the hook then copies the gradient autograd produced into its
+    view once and re-binds .grad; a parameter that got no gradient in the window is zeroed in its view
+    when its bucket is launched.
 
     Gradient accumulation (the reference accumulates 8 micro-batches per optimizer step under DDP,
     finetune.py:112-126, lightning_pretrain.py:137): run the first k-1 backward passes inside
@@ -137,30 +152,35 @@ class GradBucketer:
         for i, batch in enumerate(micro_batches):
             with b.no_sync() if i < len(micro_batches) - 1 else contextlib.nullcontext():
                 model(**batch).backward()
-        b.finish(); opt.step()
+        b.finish(); opt.step(); b.zero_grad()
 
     A second backward outside `no_sync()` before `finish()` (its buckets may already be reduced)
     raises instead of silently dropping that micro-batch.
 
-    Inside a captured training step (graphs.CapturedTrainStep(bucketer=...)) the hooks' flattening
-    and all-reduce launches and finish()'s waits and copies are recorded into the HIP graph, so each
-    replay runs the RCCL collectives with the backward. single_rank=True keeps the collectives at
-    world size 1 (a one-rank nccl group: the captured exchange on one GPU, tests).
+    Inside a captured training step (graphs.CapturedTrainStep(bucketer=...)) the hooks' packs and
+    all-reduce launches and finish()'s waits and unpacks are recorded into the HIP graph, so each
+    replay runs the RCCL collectives with the backward; the graph zeroes the buckets after the
+    optimizer. single_rank=True keeps the collectives at world size 1 (a one-rank nccl group: the
+    captured exchange on one GPU, tests).
     """
 
     def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, group=None,
-                 single_rank: bool = False):
+                 single_rank: bool = False, comm_dtype: torch.dtype = None):
         self.rank, self.ws = world()
         if group is not None:
             self.rank, self.ws = dist.get_rank(group), dist.get_world_size(group)
         self.active = self.ws > 1 or (single_rank and dist.is_available() and dist.is_initialized())
         self.average = average
         self.group = group
+        self.comm_dtype = comm_dtype
+        if comm_dtype is not None and comm_dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError(f"comm_dtype must be None, torch.bfloat16 or torch.float16, got {comm_dtype}")
         self.params = [p for p in params if p.requires_grad]
         self.buckets = []
         self._handles = []
         self._sync = True
         self.collectives = 0  # collectives issued over the bucketer's lifetime (tests, logging)
+        self.wire_bytes = 0   # bytes handed to the collectives over the bucketer's lifetime
         if not self.active:
             return
         by = {}
@@ -177,18 +197,58 @@ class GradBucketer:
                 size += nb
             if cur:
                 self.buckets.append(cur)
+        # one flat buffer per bucket, the .grad views into it, and the 16-bit wire buffer
+        self._flat, self._views, self._wire = [], [], []
         self._of = {}
         for bi, ps in enumerate(self.buckets):
+            flat = torch.zeros(sum(p.numel() for p in ps), dtype=ps[0].dtype, device=ps[0].device)
+            views, off = [], 0
             for p in ps:
-                self._of[id(p)] = bi
+                views.append(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+                self._of[id(p)] = (bi, len(views) - 1)
                 p.register_post_accumulate_grad_hook(self._hook)
+            self._flat.append(flat)
+            self._views.append(views)
+            self._wire.append(torch.empty(flat.numel(), dtype=comm_dtype, device=flat.device)
+                              if comm_dtype is not None and comm_dtype != flat.dtype else None)
+        # average inside the collective where the backend has it (RCCL's ncclAvg), else divide after
+        self._avg_op = None
+        if average and self.ws > 1:
+            try:
+                if dist.get_backend(group) == "nccl":
+                    self._avg_op = dist.ReduceOp.AVG
+            except (RuntimeError, ValueError):
+                self._avg_op = None
+        self.zero_grad()
         self._reset()
 
     def _reset(self):
         self._ready = [0] * len(self.buckets)
-        self._flat = [None] * len(self.buckets)
         self._next = 0  # lowest bucket not yet launched
         self._seen = set()  # parameters whose gradient arrived in this window's synced backward
+
+    def zero_grad(self):
+        """Zero every bucket (one fill each) and bind each parameter's .grad to its bucket view — the
+        optimizer.zero_grad() of a bucketed step (in-place, so the views stay the gradients)."""
+        if not self.active:
+            for p in self.params:
+                if p.grad is not None:
+                    p.grad.zero_()
+            return
+        for flat in self._flat:
+            flat.zero_()
+        for ps, views in zip(self.buckets, self._views):
+            for p, v in zip(ps, views):
+                if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                    p.grad = v
+
+    def bucket_bytes_on_wire(self) -> int:
+        """Bytes one exchange hands to the collectives (all buckets)."""
+        if not self.active:
+            return 0
+        return sum(f.numel() * (w.element_size() if w is not None else f.element_size())
+                   for f, w in zip(self._flat, self._wire))
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -199,10 +259,26 @@ class GradBucketer:
         finally:
             self._sync = prev
 
+    def _bind(self, bi):
+        """Make every .grad of bucket bi its view: a gradient autograd put elsewhere (after a
+        zero_grad(set_to_none=True)) is copied in once; a missing one is zero in the view."""
+        for p, v in zip(self.buckets[bi], self._views[bi]):
+            g = p.grad
+            if g is None:
+                v.zero_()
+                p.grad = v
+            elif g.data_ptr() != v.data_ptr():
+                v.copy_(g)
+                p.grad = v
+
     def _hook(self, p):
+        bi, j = self._of[id(p)]
         if not self._sync:
+            g, v = p.grad, self._views[bi][j]
+            if g is not None and g.data_ptr() != v.data_ptr():
+                v.copy_(g)  # keep accumulating in the bucket view across no_sync micro-batches
+                p.grad = v
             return
-        bi = self._of[id(p)]
         if id(p) in self._seen:
             raise RuntimeError("GradBucketer: a second backward reached an already reduced bucket before finish(); "
                                "run all but the last micro-batch of an accumulation window under no_sync()")
@@ -213,15 +289,32 @@ class GradBucketer:
             self._next += 1
 
     def _launch(self, bi):
-        ps = self.buckets[bi]
-        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps])
-        self._flat[bi] = flat
-        self._handles.append((bi, dist.all_reduce(flat, group=self.group, async_op=True)))
+        self._bind(bi)
+        flat, wire = self._flat[bi], self._wire[bi]
+        if wire is not None:
+            # pack: fp32 -> 16 bit, pre-divided by the world size (the mean's division before the sum)
+            if self.average and self.ws > 1:
+                torch.mul(flat, 1.0 / self.ws, out=wire)
+            else:
+                wire.copy_(flat)
+            buf, op = wire, dist.ReduceOp.SUM
+        else:
+            buf, op = flat, (self._avg_op or dist.ReduceOp.SUM)
+        self._handles.append((bi, dist.all_reduce(buf, op=op, group=self.group, async_op=True)))
         self.collectives += 1
+        self.wire_bytes += buf.numel() * buf.element_size()
+
+    def discard(self):
+        """Forget this window's launched buckets without waiting (the work handles): a captured step's
+        close() drops what its capture left behind."""
+        self._handles = []
+        if self.active:
+            self._reset()
 
     def finish(self) -> int:
         """Wait for the window's buckets (launching, in bucket order, any not launched during
-        backward), average, write back; returns the number of collectives issued this window."""
+        backward), average, unpack a 16-bit exchange into the fp32 buckets; returns the number of
+        collectives issued this window."""
         if not self.active:
             return 0
         while self._next < len(self.buckets):
@@ -230,17 +323,11 @@ class GradBucketer:
         n = len(self._handles)
         for bi, h in self._handles:
             h.wait()
-            flat = self._flat[bi]
-            if self.average:
-                flat /= self.ws
-            off = 0
-            for p in self.buckets[bi]:
-                g = flat[off:off + p.numel()].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
-                off += p.numel()
+            flat, wire = self._flat[bi], self._wire[bi]
+            if wire is not None:
+                flat.copy_(wire)
+            elif self.average and self.ws > 1 and self._avg_op is None:
+                flat.div_(self.ws)
         self._handles = []
         self._reset()
         return n

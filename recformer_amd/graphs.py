@@ -32,7 +32,8 @@ What capture needs from the step, and how the build provides it:
   * an optimizer without host state: recformer_amd.optim.AdamW(capturable=True) (device step
     counts, bias corrections in the kernel);
   * static inputs: the batch is copied into the graph's input buffers before each replay.
-Gradients are written (not accumulated) by each replay; the graph owns them.
+Gradients are written (not accumulated) by each replay; the graph owns them (with a dp.GradBucketer the
+bucket views are the gradients: accumulated into by the backward and zeroed after the optimizer).
 """
 from __future__ import annotations
 
@@ -44,6 +45,15 @@ import torch
 from . import _lib, dropout, models, train
 
 __all__ = ["GraphedForward", "CapturedTrainStep", "static_gmax"]
+
+# Stream-capture mode of every graph captured here. "thread_local" restricts the capture-unsafe HIP calls
+# to the capturing thread only: in "global" mode (torch's default) a capture-unsafe call from ANY thread
+# fails and invalidates the capture — and ProcessGroupNCCL's watchdog thread polls the events of the
+# collectives launched before the capture (the captured step's eager warmup windows) with
+# hipEventQuery until it reaps them. When that poll fell inside the capture, the query failed, the
+# watchdog thread raised, and its exception terminated the process while the main thread sat in
+# capture_end (the round-4 abort of the captured one-rank RCCL step, gpurun_out/r04f2/pytest.log).
+CAPTURE_MODE = "thread_local"
 
 
 class GraphedForward:
@@ -76,7 +86,8 @@ class GraphedForward:
                         module(**self.static)
                 torch.cuda.current_stream().wait_stream(stream)
                 self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph):
+                torch.cuda.synchronize()
+                with torch.cuda.graph(self.graph, capture_error_mode=CAPTURE_MODE):
                     self.out = module(**self.static)
         finally:
             models._STATIC_GMAX, models._STATIC_CLS = old, old_c
@@ -262,9 +273,13 @@ class CapturedTrainStep:
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 for _ in range(warmup):
-                    self.opt.zero_grad(set_to_none=True)
+                    self._zero_grads(set_to_none=True)
                     window()
-                if self.k > 1:
+                if self.bucketer is not None and self.bucketer.active:
+                    # the bucket views are the persistent gradients the graphs accumulate into (zeroed
+                    # by the step's graph after the optimizer, one fill per bucket)
+                    self.bucketer.zero_grad()
+                elif self.k > 1:
                     # persistent gradient buffers the accumulate graph adds into (zeroed by the last graph)
                     for p in self.params:
                         if p.requires_grad:
@@ -275,8 +290,11 @@ class CapturedTrainStep:
                 if hasattr(self.opt, "sync_hyper"):
                     self.opt.sync_hyper()
             torch.cuda.current_stream(dev).wait_stream(side)
-            if self.k == 1:
+            if self.k == 1 and not self._bucket_views():
                 self.opt.zero_grad(set_to_none=True)
+            # drain: every warmup kernel and collective finished before the capture starts (finish()
+            # waited for the bucketer's handles on the stream; this waits for the device)
+            torch.cuda.synchronize(dev)
             old_src = lib.rf_set_seed_source(self.counter.data_ptr())
             old_py = dropout.set_seed_counter(self.counter)
             try:
@@ -284,12 +302,12 @@ class CapturedTrainStep:
                 pool = None
                 if self.k > 1:
                     self.graph_acc = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(self.graph_acc):
+                    with torch.cuda.graph(self.graph_acc, capture_error_mode=CAPTURE_MODE):
                         self.counter.add_(1)
                         self.loss_acc = micro(False).detach()
                     pool = self.graph_acc.pool()
                 self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph, pool=pool):
+                with torch.cuda.graph(self.graph, pool=pool, capture_error_mode=CAPTURE_MODE):
                     self.counter.add_(1)
                     self.loss = micro(True).detach()
             finally:
@@ -319,8 +337,42 @@ class CapturedTrainStep:
             sc.update()
         else:
             self.opt.step()
-        if self.k > 1:
+        if self._bucket_views():
+            self.bucketer.zero_grad()
+        elif self.k > 1:
             torch._foreach_zero_([p.grad for p in self.params if p.grad is not None])
+
+    def _bucket_views(self) -> bool:
+        return self.bucketer is not None and self.bucketer.active
+
+    def _zero_grads(self, set_to_none: bool):
+        if self._bucket_views():
+            self.bucketer.zero_grad()
+        else:
+            self.opt.zero_grad(set_to_none=set_to_none)
+
+    def close(self):
+        """Release the captured graphs (and the tensors they own) now, after the device has finished
+        any replay: a graph with captured RCCL kernels must be torn down while its process group
+        still exists, so a driver calls close() before dist.destroy_process_group() instead of
+        leaving the graphs to the garbage collector. The step cannot be replayed afterwards."""
+        if getattr(self, "graph", None) is None:
+            return
+        torch.cuda.synchronize(self.counter.device)
+        for g in (self.graph_acc, self.graph):
+            if g is not None:
+                g.reset()
+        self.graph = self.graph_acc = None
+        self.loss = self.loss_acc = self.output = self.found_inf = None
+        if self.bucketer is not None:
+            self.bucketer.discard()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     def optimizer_was_run(self) -> bool:
         """Whether the last completed window's optimizer step was taken (host read; True without a
@@ -348,6 +400,8 @@ class CapturedTrainStep:
                     if dst.shape != v.shape:
                         raise ValueError(f"{k}: shape {tuple(v.shape)} != captured {tuple(dst.shape)}")
                     dst.copy_(v, non_blocking=True)
+        if self.graph is None:
+            raise RuntimeError("CapturedTrainStep: replay after close()")
         self._pos += 1
         if self._pos < self.k:
             self.graph_acc.replay()

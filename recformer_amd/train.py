@@ -105,10 +105,11 @@ def _mm_f32(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
 DW_SIDE_STREAM = True
 # the attention's gradient of a layer's input added inside the q|k|v projection's dA GEMM (_GradMailbox)
 # instead of autograd's separate bf16 sum: -0.4% per captured C3 step (16.55 vs 16.62 ms, gpurun_out/r04r),
-# but the whole -m gpu suite faulted with it on (an illegal address in the first training test after the
-# graph tests; the training, graph and kernel files passed on their own, in another order) — off until
-# that is understood
-GRAD_MAILBOX = False
+# The round-4 suite fault with it on (an illegal address in the first training test after the graph tests,
+# gpurun_out/r04v) was _zero_bias caching a zero vector allocated during a graph capture: it lived in that
+# graph's private pool, which was freed with the graph, and every later uncaptured mailbox GEMM read it
+# (fixed in _zero_bias: nothing made during a capture is cached)
+GRAD_MAILBOX = True
 # the bias gradients' column sums on the weight-gradient side stream too: measured slower (captured C3
 # 16.48 vs 16.38 ms in one process, gpurun_out/r04s: that stream is the step's critical path), so off
 BIAS_GRAD_SIDE = False

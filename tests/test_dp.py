@@ -301,6 +301,78 @@ def test_gradbucketer_accumulation_world2():
         assert torch.allclose(g, p.grad, atol=1e-6, rtol=1e-5)
 
 
+def _wire_net():
+    torch.manual_seed(3)
+    return torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 64),
+                               torch.nn.GELU(), torch.nn.Linear(64, 8))
+
+
+def _wire_worker(rank, ws, port, out_q):
+    """Two windows per wire dtype: GradBucketer with .grad as bucket views, fp32 / bf16 / fp16 on the
+    wire; the second window after optimizer-style zero_grad(set_to_none=True) (the hook re-binds)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        g = torch.Generator().manual_seed(9)
+        xs = torch.randn(2, 16, 64, generator=g)
+        res = {}
+        for name, cd in (("fp32", None), ("bf16", torch.bfloat16), ("fp16", torch.float16)):
+            net = _wire_net()
+            b = dp.GradBucketer(net.parameters(), bucket_bytes=16 << 10, comm_dtype=cd)
+            flats = [(f.data_ptr(), f.data_ptr() + f.numel() * f.element_size()) for f in b._flat]
+            grads = []
+            for w in range(2):
+                if w == 1:
+                    for p in net.parameters():
+                        p.grad = None  # optimizer.zero_grad(set_to_none=True)
+                x = xs[w, rank * 8:(rank + 1) * 8]
+                net(x).pow(2).mean().backward()
+                b.finish()
+                aliased = all(any(a <= p.grad.data_ptr() < e for a, e in flats) for p in net.parameters())
+                grads.append(([p.grad.clone() for p in net.parameters()], aliased))
+                b.zero_grad()
+            res[name] = (grads, b.bucket_bytes_on_wire(), len(b.buckets))
+        out_q.put(_plain((rank, res)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradbucketer_16bit_wire_world2():
+    """world-2 gloo: the 16-bit exchange (DeepSpeed precision=16's reduce, lightning_pretrain.py:134-145)
+    averages the gradients to the 16-bit contract of the fp32 exchange, which equals the full-batch
+    gradient; .grad stays a view into the bucket buffers (no flatten / copy-back), also after a
+    set-to-None zero_grad; the wire carries half the bytes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_wire_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(_unplain(q.get(timeout=300)) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    xs = torch.randn(2, 16, 64, generator=torch.Generator().manual_seed(9))
+    for w in range(2):
+        net = _wire_net()
+        net(xs[w]).pow(2).mean().backward()
+        full = [p.grad for p in net.parameters()]
+        for r in (0, 1):
+            res = got[r]
+            g32, al32 = res["fp32"][0][w]
+            assert al32
+            for a, ref in zip(g32, full):
+                assert torch.allclose(a, ref, atol=1e-6, rtol=1e-5)
+            for name, eps in (("bf16", 2 ** -8), ("fp16", 2 ** -11)):
+                g16, al = res[name][0][w]
+                assert al
+                for a, b32 in zip(g16, g32):
+                    # pre-divide + 16-bit rounding of each rank's half + the 16-bit sum: <= 3 roundings
+                    assert (a - b32).abs().max() <= 3 * eps * b32.abs().max() + 1e-12, name
+    n32, n16 = got[0]["fp32"][1], got[0]["bf16"][1]
+    assert n16 * 2 == n32 and got[0]["fp32"][2] >= 2
+
+
 def _combine_worker(rank, ws, port, out_q):
     """One rank's shard result for C5 retrieval (what rf_score_rank + rf_topk_* produce on the
     device): counts over its catalog shard and its top-k with global ids; combined over ranks."""

@@ -45,6 +45,9 @@ def main():
                     "size: the bucketed all-reduce is captured with the backward)")
     ap.add_argument("--torch-adamw", action="store_true", help="A/B: torch.optim.AdamW instead of the HIP AdamW")
     ap.add_argument("--full-lm-head", action="store_true", help="A/B: LM head over every token")
+    ap.add_argument("--comm-dtype", choices=["fp32", "bf16", "fp16"], default="bf16",
+                    help="gradient exchange on the wire (dp.GradBucketer comm_dtype; bf16/fp16 = 16-bit, "
+                         "as DeepSpeed precision=16)")
     a = ap.parse_args()
     if a.full_lm_head:
         from recformer_amd import models
@@ -75,7 +78,8 @@ def main():
     batch.update(mlm_input_ids_a=mlm_a, mlm_labels_a=lab_a, mlm_input_ids_b=mlm_b, mlm_labels_b=lab_b)
     batch = {k: v.to(dev) for k, v in batch.items()}
 
-    bucketer = dp.GradBucketer(model.parameters()) if world > 1 else None
+    wire = {"fp32": None, "bf16": torch.bfloat16, "fp16": torch.float16}[a.comm_dtype]
+    bucketer = dp.GradBucketer(model.parameters(), comm_dtype=wire) if world > 1 else None
 
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -84,7 +88,10 @@ def main():
         if bucketer is not None:  # buckets were launched during backward; wait + average
             bucketer.finish()
         opt.step()
-        opt.zero_grad(set_to_none=True)
+        if bucketer is not None:
+            bucketer.zero_grad()  # the bucket views stay the gradients
+        else:
+            opt.zero_grad(set_to_none=True)
         return out
 
     if a.graph:
@@ -120,6 +127,9 @@ def main():
                           "ms_per_step": round(1e3 * dt / a.steps, 2),
                           "seq_per_s": round(world * a.batch * a.steps / dt, 2),
                           "loss": float(out.loss.detach()), "cl_correct": int(out.cl_correct_num), "graph": a.graph,
+                          "grad_wire": a.comm_dtype if bucketer is not None else None,
+                          "wire_mb_per_step": (round(bucketer.bucket_bytes_on_wire() / 1e6, 1)
+                                               if bucketer is not None else None),
                           "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
