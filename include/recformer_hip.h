@@ -22,6 +22,7 @@
 #ifndef RECFORMER_HIP_H
 #define RECFORMER_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -164,19 +165,23 @@ int rf_drop_add_ln_bwd_dual(int M, int D, const float* dy, const void* dy16, con
                             const float* rstd, const float* w, float p, uint64_t seed, float* dres, void* dt,
                             float* dw, float* db, void* workspace, rf_stream_t stream);
 /* The same pair with the dense output t / y16 / dt / dy16 in dtype (RF_BF16 or RF_F16: the fp16
- * autocast path, finetune.py:106-110). */
+ * autocast path, finetune.py:106-110). mask_row_mul (>= 1): the keep mask of row r is that of row
+ * r * mask_row_mul, i.e. the hash index is (r * mask_row_mul * D + col) — the training path's CLS-only
+ * last layer runs the B CLS rows compacted and passes Lp, so each draws the mask of its full-layer row
+ * b * Lp (1: the plain row-major index). */
 int rf_drop_add_ln_fwd_t(int dtype, int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
                          const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,
-                         void* y16, rf_stream_t stream);
+                         void* y16, int mask_row_mul, rf_stream_t stream);
 int rf_drop_add_ln_bwd_t(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
                          const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
-                         void* dt, float* dw, float* db, void* workspace, rf_stream_t stream);
+                         void* dt, float* dw, float* db, void* workspace, int mask_row_mul, rf_stream_t stream);
 /* rf_drop_add_ln_bwd_t that also writes dbias_t (D fp32) = the column sums of dt as stored (16-bit):
  * the bias gradient of the Linear whose output t is (TF:1064-1071, 1123-1130), from the same pass (no
  * separate read of dt for it). */
 int rf_drop_add_ln_bwd_tb(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
                           const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
-                          void* dt, float* dw, float* db, float* dbias_t, void* workspace, rf_stream_t stream);
+                          void* dt, float* dw, float* db, float* dbias_t, void* workspace, int mask_row_mul,
+                          rf_stream_t stream);
 /* Weight gradient of an nn.Linear, C (=|+=) X^T Y: C[n][k] = sum_m X[m][n] Y[m][k] over the M token
  * rows (X = dC (M x N), Y = A (M x K), 16-bit row-major; C fp32 N x K, the master weight's dtype) —
  * the dW = dC^T A of autograd through TF:504-514, 1064-1130 and the LM head (models.py:499-510).
@@ -389,8 +394,9 @@ int rf_rank_accum(int M, int N, const float* scores, int64_t ld, const float* s_
  * capr when the list or a tile's 32-entry stage overflowed); mode 2 writes only the partials.
  * D % 64 == 0 (D >= 128) with the knob rank_w32 on: both entry points run the 32x32x16 four-wave
  * kernels (items as the MFMA A operand; k_rank_w32 / k_label_score32, still bit-identical to each
- * other); then mode 0 needs ldd >= ncols rounded up to 256, and a lane with more than 4 candidates in
- * a tile overflows its rows (rcnt > capr) instead of a 32-entry stage.
+ * other); then mode 0 needs ldd >= ncols rounded up to 256, and mode 1 appends each candidate straight
+ * to its row's list with one atomic (no per-tile stage): a row overflows only when its list passes
+ * capr (rcnt > capr).
  * rf_rank_reduce: gt / valid / sexp per row = the partials summed over ntiles tile columns in order.
  * rf_topk_dense: top-k (k <= 256) of each row of a dense (B, n <= 2048) block, value descending, ties
  * by lower id (ids from idx (B, n) or idx_base + column).

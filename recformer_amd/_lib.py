@@ -49,11 +49,11 @@ SIGNATURES = {
     "rf_drop_add_ln_bwd_dual": (c_int, [c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
                                         P]),
     "rf_drop_add_ln_fwd_t": (c_int, [c_int, c_int, c_int, P, c_int, P, c_float, ctypes.c_uint64, P, P, c_float, P, P,
-                                     P, P, P, P]),
+                                     P, P, P, c_int, P]),
     "rf_drop_add_ln_bwd_t": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
-                                     P]),
+                                     c_int, P]),
     "rf_drop_add_ln_bwd_tb": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_float, ctypes.c_uint64, P, P, P, P, P,
-                                      P, P]),
+                                      P, c_int, P]),
     "rf_colsum_workspace": (ctypes.c_size_t, [c_int, c_int]),
     "rf_embed_ln_bwd_workspace": (ctypes.c_size_t, [c_int, c_int]),
     "rf_embed_ln_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, c_float, P, P, P, P, P, P]),

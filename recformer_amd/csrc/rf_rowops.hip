@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const E* __restr
                                                           const float* __restrict__ lw, const float* __restrict__ lb,
                                                           float eps, float* __restrict__ xo, float* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                          E* __restrict__ y16) {
+                                                          E* __restrict__ y16, int mrow) {
   constexpr int D = 64 * VEC * NCH;
   if (thresh) seed = seed_resolve(seed, seed_dev);
   const int lane = threadIdx.x & 63;
@@ -446,7 +446,7 @@ __global__ void __launch_bounds__(256) k_drop_add_ln_fwd(int M, const E* __restr
     Vec<float, VEC>::load(res + (int64_t)row * D + e, rv);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      const bool keep = thresh == 0 || drop_keep(seed, (uint64_t)row * D + e + j, thresh);
+      const bool keep = thresh == 0 || drop_keep(seed, (uint64_t)row * mrow * D + e + j, thresh);
       xv[c][j] = (keep ? tv[j] * keep_scale : 0.f) + rv[j];
       s += xv[c][j];
     }
@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
                                                         float* __restrict__ part, E* __restrict__ dt,
                                                         uint32_t thresh, float keep_scale, uint64_t seed,
                                                         const uint64_t* seed_dev, const E* __restrict__ dy2,
-                                                        int tb) {
+                                                        int tb, int mrow) {
   constexpr int D = 64 * VEC * NCH;
   if (thresh) seed = seed_resolve(seed, seed_dev);
   __shared__ float red[4][3][D];
@@ -557,7 +557,8 @@ __global__ void __launch_bounds__(256) k_layernorm_bwd(int M, const float* __res
         float od[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j)
-          od[j] = (thresh == 0 || drop_keep(seed, (uint64_t)row * D + e + j, thresh)) ? o[j] * keep_scale : 0.f;
+          od[j] = (thresh == 0 || drop_keep(seed, (uint64_t)row * mrow * D + e + j, thresh)) ? o[j] * keep_scale
+                                                                                             : 0.f;
         Vec<E, VEC>::store(dt + (int64_t)row * D + e, od);
         if (tb) {  // the dense branch's bias gradient: column sums of dt as stored (16-bit)
 #pragma unroll
@@ -1186,7 +1187,7 @@ template <typename E>
 static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                        const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                        E* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
-                       const E* dy2 = nullptr, float* dbias_t = nullptr);
+                       const E* dy2 = nullptr, float* dbias_t = nullptr, int mrow = 1);
 }
 
 
@@ -1205,13 +1206,13 @@ int rf_drop_add_ln_fwd(int M, int D, const void* t, int ldt, const float* res, f
 int rf_drop_add_ln_fwd_dual(int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
                             const float* w, const float* b, float eps, float* x, float* y, float* mean,
                             float* rstd, void* y16, rf_stream_t stream) {
-  return rf_drop_add_ln_fwd_t(RF_BF16, M, D, t, ldt, res, p, seed, w, b, eps, x, y, mean, rstd, y16, stream);
+  return rf_drop_add_ln_fwd_t(RF_BF16, M, D, t, ldt, res, p, seed, w, b, eps, x, y, mean, rstd, y16, 1, stream);
 }
 int rf_drop_add_ln_fwd_t(int dtype, int M, int D, const void* t, int ldt, const float* res, float p, uint64_t seed,
                          const float* w, const float* b, float eps, float* x, float* y, float* mean, float* rstd,
-                         void* y16, rf_stream_t stream) {
+                         void* y16, int mask_row_mul, rf_stream_t stream) {
   RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_drop_add_ln_fwd: dtype must be bf16 or fp16");
-  RF_REQUIRE(M >= 0 && ldt >= D && p >= 0.f && p < 1.f, "rf_drop_add_ln_fwd: bad arguments");
+  RF_REQUIRE(M >= 0 && ldt >= D && p >= 0.f && p < 1.f && mask_row_mul >= 1, "rf_drop_add_ln_fwd: bad arguments");
   if (M == 0) return RF_OK;
   RF_REQUIRE(t && res && w && b && x && y && mean && rstd, "rf_drop_add_ln_fwd: null pointer");
   RF_REQUIRE(ldt % 4 == 0, "rf_drop_add_ln_fwd: ldt must be a multiple of 4");
@@ -1221,7 +1222,7 @@ int rf_drop_add_ln_fwd_t(int dtype, int M, int D, const void* t, int ldt, const 
   dim3 grid((M + 3) / 4);
 #define L_(V, N)                                                                                   \
   k_drop_add_ln_fwd<E, V, N><<<grid, 256, 0, s>>>(M, (const E*)t, ldt, res, th, ks, seed, g_seed_dev, w, b, eps, x, y, \
-                                                  mean, rstd, (E*)y16)
+                                                  mean, rstd, (E*)y16, mask_row_mul)
   if (dtype == RF_F16) {
     typedef f16 E;
     RF_ROW_DISPATCH(D, L_);
@@ -1243,33 +1244,34 @@ int rf_drop_add_ln_bwd(int M, int D, const float* dy, const float* x, const floa
 int rf_drop_add_ln_bwd_dual(int M, int D, const float* dy, const void* dy16, const float* x, const float* mean,
                             const float* rstd, const float* w, float p, uint64_t seed, float* dres, void* dt,
                             float* dw, float* db, void* workspace, rf_stream_t stream) {
-  return rf_drop_add_ln_bwd_t(RF_BF16, M, D, dy, dy16, x, mean, rstd, w, p, seed, dres, dt, dw, db, workspace,
+  return rf_drop_add_ln_bwd_t(RF_BF16, M, D, dy, dy16, x, mean, rstd, w, p, seed, dres, dt, dw, db, workspace, 1,
                               stream);
 }
 int rf_drop_add_ln_bwd_t(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
                          const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
-                         void* dt, float* dw, float* db, void* workspace, rf_stream_t stream) {
+                         void* dt, float* dw, float* db, void* workspace, int mask_row_mul, rf_stream_t stream) {
   RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_drop_add_ln_bwd: dtype must be bf16 or fp16");
-  RF_REQUIRE(M >= 0 && p >= 0.f && p < 1.f, "rf_drop_add_ln_bwd: bad arguments");
+  RF_REQUIRE(M >= 0 && p >= 0.f && p < 1.f && mask_row_mul >= 1, "rf_drop_add_ln_bwd: bad arguments");
   RF_REQUIRE(M == 0 || dt, "rf_drop_add_ln_bwd: null dt");
   if (dtype == RF_F16)
     return ln_bwd_impl<f16>(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (f16*)dt, drop_thresh(p),
-                            1.0f / (1.0f - p), seed, stream, (const f16*)dy16);
+                            1.0f / (1.0f - p), seed, stream, (const f16*)dy16, nullptr, mask_row_mul);
   return ln_bwd_impl<bf16>(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (bf16*)dt, drop_thresh(p),
-                           1.0f / (1.0f - p), seed, stream, (const bf16*)dy16);
+                           1.0f / (1.0f - p), seed, stream, (const bf16*)dy16, nullptr, mask_row_mul);
 }
 
 int rf_drop_add_ln_bwd_tb(int dtype, int M, int D, const float* dy, const void* dy16, const float* x,
                           const float* mean, const float* rstd, const float* w, float p, uint64_t seed, float* dres,
-                          void* dt, float* dw, float* db, float* dbias_t, void* workspace, rf_stream_t stream) {
+                          void* dt, float* dw, float* db, float* dbias_t, void* workspace, int mask_row_mul,
+                          rf_stream_t stream) {
   RF_REQUIRE(dtype == RF_BF16 || dtype == RF_F16, "rf_drop_add_ln_bwd_tb: dtype must be bf16 or fp16");
-  RF_REQUIRE(M >= 0 && p >= 0.f && p < 1.f, "rf_drop_add_ln_bwd_tb: bad arguments");
+  RF_REQUIRE(M >= 0 && p >= 0.f && p < 1.f && mask_row_mul >= 1, "rf_drop_add_ln_bwd_tb: bad arguments");
   RF_REQUIRE(M == 0 || (dt && dbias_t), "rf_drop_add_ln_bwd_tb: null dt / dbias_t");
   if (dtype == RF_F16)
     return ln_bwd_impl<f16>(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (f16*)dt, drop_thresh(p),
-                            1.0f / (1.0f - p), seed, stream, (const f16*)dy16, dbias_t);
+                            1.0f / (1.0f - p), seed, stream, (const f16*)dy16, dbias_t, mask_row_mul);
   return ln_bwd_impl<bf16>(M, D, dy, x, D, mean, rstd, w, dres, dw, db, workspace, (bf16*)dt, drop_thresh(p),
-                           1.0f / (1.0f - p), seed, stream, (const bf16*)dy16, dbias_t);
+                           1.0f / (1.0f - p), seed, stream, (const bf16*)dy16, dbias_t, mask_row_mul);
 }
 
 int rf_layernorm_bwd(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
@@ -1283,7 +1285,7 @@ template <typename E>
 static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, const float* mean,
                        const float* rstd, const float* w, float* dx, float* dw, float* db, void* workspace,
                        E* dt, uint32_t thresh, float keep_scale, uint64_t seed, rf_stream_t stream,
-                       const E* dy2, float* dbias_t) {
+                       const E* dy2, float* dbias_t, int mrow) {
   RF_REQUIRE(M >= 0 && ldx >= D, "rf_layernorm_bwd: bad shape");
   if (M == 0) return RF_OK;
   RF_REQUIRE((dy || dy2) && x && mean && rstd && w && dx && dw && db && workspace, "rf_layernorm_bwd: null pointer");
@@ -1293,7 +1295,7 @@ static int ln_bwd_impl(int M, int D, const float* dy, const float* x, int ldx, c
   float* part = reinterpret_cast<float*>(workspace);
   const int tb = dt && dbias_t ? 1 : 0;
   const int ns = 2 + tb;
-#define L_(V, N) k_layernorm_bwd<E, V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, g_seed_dev, dy2, tb)
+#define L_(V, N) k_layernorm_bwd<E, V, N><<<nb, 256, 0, s>>>(M, dy, x, ldx, mean, rstd, w, dx, part, dt, thresh, keep_scale, seed, g_seed_dev, dy2, tb, mrow)
   RF_ROW_DISPATCH(D, L_);
 #undef L_
   // [dw | db (| dbias_t)] columns

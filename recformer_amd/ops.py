@@ -470,9 +470,10 @@ def embedding_grad(src: torch.Tensor, index: torch.Tensor, num_rows: int, pad: O
 
 
 def drop_add_ln_fwd(t: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float, p: float,
-                    seed: int, want_bf16: bool = False):
-    """rf_drop_add_ln_fwd(_dual): (x, y, mean, rstd) with x = dropout_p(t) + res, y = LN(x), all
-    fp32; with want_bf16 also y16 = bf16(y) (rf_drop_add_ln_fwd_dual), appended."""
+                    seed: int, want_bf16: bool = False, mask_row_mul: int = 1):
+    """rf_drop_add_ln_fwd_t: (x, y, mean, rstd) with x = dropout_p(t) + res, y = LN(x), all fp32; with
+    want_bf16 also y16 = bf16(y), appended. mask_row_mul: row r draws the mask of row r * mask_row_mul
+    (the CLS-only last layer's compacted rows pass Lp: the full layer's row b * Lp)."""
     lib = _lib.load()
     _dev(t, res, w, b)
     M, D = t.shape
@@ -485,12 +486,13 @@ def drop_add_ln_fwd(t: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torc
     y16 = torch.empty(M, D, dtype=t.dtype, device=t.device) if want_bf16 else None
     check(lib.rf_drop_add_ln_fwd_t(dtype_code(t.dtype), M, D, _p(t), _rowmajor(t, "t"), _p(res), float(p), seed,
                                    _p(w.float().contiguous()), _p(b.float().contiguous()), float(eps), _p(x),
-                                   _p(y), _p(mean), _p(rstd), _p(y16), _stream(t)), "rf_drop_add_ln_fwd")
+                                   _p(y), _p(mean), _p(rstd), _p(y16), int(mask_row_mul), _stream(t)),
+          "rf_drop_add_ln_fwd")
     return (x, y, mean, rstd, y16) if want_bf16 else (x, y, mean, rstd)
 
 
 def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[torch.Tensor] = None,
-                    dtype: torch.dtype = torch.bfloat16, want_dbias: bool = False):
+                    dtype: torch.dtype = torch.bfloat16, want_dbias: bool = False, mask_row_mul: int = 1):
     """rf_drop_add_ln_bwd_t: (dres fp32, dt, dw, db) for the gradient dy (fp32) of y plus, when given,
     dy16 of its 16-bit copy; either may be None (not both). dt and dy16 in `dtype` (bf16 / fp16).
     want_dbias (rf_drop_add_ln_bwd_tb): also the column sums of dt (the dense branch's bias gradient)."""
@@ -513,12 +515,12 @@ def drop_add_ln_bwd(dy, x, mean, rstd, w, p: float, seed: int, dy16: Optional[to
         dbias = torch.empty_like(dw)
         check(lib.rf_drop_add_ln_bwd_tb(dtype_code(dtype), M, D, _p(dy), _p(dy16), _p(x), _p(mean), _p(rstd),
                                         _p(w.float().contiguous()), float(p), seed, _p(dres), _p(dt), _p(dw), _p(db),
-                                        _p(dbias), _p(ws), _stream(x)),
+                                        _p(dbias), _p(ws), int(mask_row_mul), _stream(x)),
               "rf_drop_add_ln_bwd_tb")
         return dres, dt, dw, db, dbias
     check(lib.rf_drop_add_ln_bwd_t(dtype_code(dtype), M, D, _p(dy), _p(dy16), _p(x), _p(mean), _p(rstd),
                                    _p(w.float().contiguous()), float(p), seed, _p(dres), _p(dt), _p(dw), _p(db), _p(ws),
-                                   _stream(x)),
+                                   int(mask_row_mul), _stream(x)),
           "rf_drop_add_ln_bwd")
     return dres, dt, dw, db
 

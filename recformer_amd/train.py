@@ -531,13 +531,16 @@ class _DropAddLN(torch.autograd.Function):
     (no separate cast, cast-backward and gradient add per LayerNorm)."""
 
     @staticmethod
-    def forward(ctx, t, res, w, b, eps: float, p: float, dual: bool = False, seed: Optional[int] = None):
+    def forward(ctx, t, res, w, b, eps: float, p: float, dual: bool = False, seed: Optional[int] = None,
+                mask_row_mul: int = 1):
+        # mask_row_mul: rows drawn as row * mask_row_mul of the mask (the CLS-only last layer's compacted
+        # CLS rows pass Lp: each gets the mask of its row b * Lp in the full layer)
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
-        out = ops.drop_add_ln_fwd(t, res.contiguous(), w, b, eps, p, seed, want_bf16=dual)
+        out = ops.drop_add_ln_fwd(t, res.contiguous(), w, b, eps, p, seed, want_bf16=dual, mask_row_mul=mask_row_mul)
         x, y, mean, rstd = out[:4]
         ctx.save_for_backward(x, mean, rstd, w)
-        ctx.p, ctx.seed = p, seed
+        ctx.p, ctx.seed, ctx.mrow = p, seed, mask_row_mul
         ctx.tdt = t.dtype
         ctx.set_materialize_grads(False)
         return (y, out[4]) if dual else y
@@ -545,17 +548,18 @@ class _DropAddLN(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, dy16=None):
         if dy is None and dy16 is None:
-            return None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, None
         x, mean, rstd, w = ctx.saved_tensors
         if LN_BIAS_GRAD and ctx.needs_input_grad[0]:
             # the dense branch's bias gradient (column sums of dt) from the same pass, handed to the
             # producing Linear's backward with dt (_bias_grad)
             dres, dt, dw, db, dbias = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16,
-                                                          dtype=ctx.tdt, want_dbias=True)
+                                                          dtype=ctx.tdt, want_dbias=True, mask_row_mul=ctx.mrow)
             dt._rf_colsum = dbias
         else:
-            dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16, dtype=ctx.tdt)
-        return dt, dres, dw, db, None, None, None, None
+            dres, dt, dw, db = ops.drop_add_ln_bwd(dy, x, mean, rstd, w, ctx.p, ctx.seed, dy16=dy16, dtype=ctx.tdt,
+                                                   mask_row_mul=ctx.mrow)
+        return dt, dres, dw, db, None, None, None, None, None
 
 
 class _EmbedLN(torch.autograd.Function):
@@ -1421,7 +1425,8 @@ def _cls_last_layer_train(model, lyr, lw, h, h32, rows, gvalid, flags, gidx, B: 
     res = h32.index_select(0, cls)
     ao, fo = lyr.attention.output, lyr.output
     t = _lin(c, lw, "w_o", "b_o", 0, 1.0)
-    a32, a16 = _DropAddLN.apply(t, res, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid, True, seeds[0])
+    # the compacted CLS rows draw the hidden-dropout masks of their full-layer rows b * Lp
+    a32, a16 = _DropAddLN.apply(t, res, ao.LayerNorm.weight, ao.LayerNorm.bias, eps, p_hid, True, seeds[0], Lp)
     if lw.get("packed"):
         (w1,), w1_16, w1t = lw["w_1"]
         (w2,), w2_16, w2t = lw["w_2"]
@@ -1434,7 +1439,7 @@ def _cls_last_layer_train(model, lyr, lw, h, h32, rows, gvalid, flags, gidx, B: 
         else:
             u = F.gelu(_Gemm.apply(a16, *lw["w_1"], lw["b_1"], 0, 1.0))
         t2 = _Gemm.apply(u, *lw["w_2"], lw["b_2"], 0, 1.0)
-    y = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, False, seeds[1])
+    y = _DropAddLN.apply(t2, a32, fo.LayerNorm.weight, fo.LayerNorm.bias, eps, p_hid, False, seeds[1], Lp)
     sa = lyr.attention.self
     local = [p for m in (sa.query, sa.key, sa.value) for p in (m.weight, m.bias) if p.requires_grad]
     return _ZeroGrads.apply(y, *local) if local else y

@@ -750,11 +750,15 @@ def test_hip_head_at_10k_items_matches_reference(dev, kind):
     assert err <= 1e-4 * float(ref.abs().max()), (err, float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_cls_last_layer_training_matches_full(dev, monkeypatch, dtype):
-    """RecformerForSeqRec training with the last layer on the CLS rows (train._GlobalCLS; dropout off):
-    the loss and every parameter gradient equal the full last layer's — including exact zeros (not
-    None) for the last layer's local query / key / value projections, which never reach the CLS rows."""
+def test_cls_last_layer_training_matches_full(dev, monkeypatch, dtype, p_drop):
+    """RecformerForSeqRec training with the last layer on the CLS rows (train._GlobalCLS): the loss and
+    every parameter gradient equal the full last layer's — including exact zeros (not None) for the last
+    layer's local query / key / value projections, which never reach the CLS rows. With hidden and
+    attention dropout on (the reference finetune's 0.1, same torch seed): the compacted CLS rows draw
+    the hidden-dropout masks of their full-layer rows b * Lp (mask_row_mul) and the fold the global
+    rows' attention masks, so both paths train on the same masks."""
     from recformer_amd import models
     g = load_golden("c1_ragged")
     batch = {k: v.to(dev) for k, v in batch_of(g).items()}
@@ -764,12 +768,13 @@ def test_cls_last_layer_training_matches_full(dev, monkeypatch, dtype):
     res = {}
     for prune in (False, True):
         monkeypatch.setattr(models, "PRUNE_LAST_LAYER", prune)
-        lf = hashed_model(CFG, seed=1)
+        lf = hashed_model(dict(CFG, hidden_dropout_prob=p_drop, attention_probs_dropout_prob=p_drop), seed=1)
         m = RecformerForSeqRec(lf.config)
         m.longformer.load_state_dict(lf.state_dict())
         m.config.finetune_negative_sample_size = 0
         m.init_item_embedding(items.clone())
         m = m.to(dev).train()
+        torch.manual_seed(123)  # the pass's dropout seeds
         with torch.autocast("cuda", dtype=dtype):
             loss = m(**batch, labels=labels)
         loss.backward()

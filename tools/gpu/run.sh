@@ -16,6 +16,10 @@
 #   abc3       captured-C3 A/Bs listed in $AB (knob:<name>[=a,b] or a Python flag), $TRAIN_ARGS appended
 #   abc2       C2 forward-step A/Bs listed in $AB (tools/ab_step.py arguments)
 #   abc5       C5 retrieval, rank_w32 0 / 1 alternated by process
+#   abtree     same-box A/B of library generations: abtree/<name> trees (tools/abtree.sh, $TREES, default
+#              "r03 r04") against the working tree, every row through the last layer, order A B C C B A
+#   gemmpmc    the four C2 GEMMs alone (tools/gemm_pmc.py): kernel trace + SQ wait / instruction / LDS and
+#              HBM-byte PMC passes, one rocprofv3 run per pass
 #   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3;
 #              C5 retrieval with the 32x32x16 rank kernel (knob rank_w32) alternated by process
 set -o pipefail
@@ -77,6 +81,35 @@ case $MODE in
       echo "$k" >> $O/ab_c5.log
     done
     grep -E "rank_w32|ms" $O/ab_c5.log | cut -c1-250 ;;
+  abtree)
+    trees="${TREES:-r03 r04} cur"
+    order="$trees $(echo $trees | tr ' ' '\n' | tac | tr '\n' ' ')"
+    for t in $order; do
+      if [ "$t" = cur ]; then dir=.; extra="--full-last-layer --no-full-leg"; else dir=abtree/$t; extra=""; fi
+      [ "$t" != cur ] && grep -q full-last-layer $dir/bench.py && extra="--full-last-layer"
+      (cd $dir && timeout -k 10 300 python bench.py --steps 80 --warmup 10 --cpu-baseline-seconds 0 $extra) \
+        > $O/ab_$t.log 2>&1 || fail $O/ab_$t.log
+      tail -1 $O/ab_$t.log | python3 -c "
+import json, sys
+d = json.loads(sys.stdin.read())
+k = d.get('kernels', {})
+print(json.dumps({'tree': '$t', 'value': d['value'], 'ms_per_step': d['ms_per_step'],
+                  **{n: round(k[n]['avg_us'], 1) for n in ('gemm_qkv', 'gemm_out', 'gemm_ffn1', 'gemm_ffn2', 'band_attn')
+                     if n in k}}))" | tee -a $O/abtree.jsonl
+    done ;;
+  gemmpmc)
+    cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o g -- \
+      python3 tools/gemm_pmc.py 40 > $O/trace.log 2>&1 || fail $O/trace.log
+    i=0
+    for ctrs in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_WAVES" \
+                "FETCH_SIZE" "WRITE_SIZE" ${EXTRA_PMC:-}; do
+      timeout -s KILL 90 rocprofv3 --pmc $ctrs --output-format csv -d $O/pmc$i -o p -- python3 tools/gemm_pmc.py 10 \
+        > $O/pmc$i.log 2>&1 || fail $O/pmc$i.log
+      i=$((i+1))
+    done
+    python3 tools/summarize_pmc.py $O | tee $O/summary.txt ;;
   abc3)
     # captured C3 steps, one same-process A/B per entry of $AB: knob:<name>[=a,b] or a Python flag name
     n=0
