@@ -1668,7 +1668,10 @@ __global__ void __launch_bounds__(256) k_gbwd_prep(int D, int H, int nch, int Lp
       const int d = t - 64;
       const float v = live ? to_f32(dout[((int64_t)(r / gmax) * Lp + pos) * ldd + h * 64 + d]) : 0.f;
       dos[d] = v;
-      if (drop) c = wave_sum(v * bvg[h * 64 + d]);
+      // bvg holds H * 64 values: the padding heads h >= H (the grid covers GF_HP) must not read it (they
+      // once did, 4 KiB past the bias at C1's H = 2 — an illegal address whenever the bias sat at the end of
+      // a mapped block: the round-4/5 suite fault first blamed on the gradient mailbox)
+      if (drop) c = wave_sum(live ? v * bvg[h * 64 + d] : 0.f);
     } else if (live && cb) {
       c = cb[r * GF_HP + h];
     }

@@ -782,6 +782,7 @@ def test_cls_last_layer_training_matches_full(dev, monkeypatch, dtype, p_drop):
         res[prune] = (float(loss), {k: p.grad for k, p in m.longformer.named_parameters()})
     assert abs(res[True][0] - res[False][0]) <= 2e-3 * max(1.0, abs(res[False][0]))
     nl = CFG["num_hidden_layers"]
+    gmax = max(float(g.abs().max()) for g in res[False][1].values() if g is not None)
     for k, gf in res[False][1].items():
         gp = res[True][1][k]
         assert gp is not None, k
@@ -789,6 +790,11 @@ def test_cls_last_layer_training_matches_full(dev, monkeypatch, dtype, p_drop):
             assert not gp.any() and not gf.any(), k
             continue
         if float(gf.abs().max()) < 1e-7:
+            continue
+        if k.endswith("key.bias") or k.endswith("key_global.bias"):
+            # mathematically zero (a key bias shifts every score of a softmax row equally): rounding noise
+            # on both paths, so bounded instead of correlated
+            assert float(gp.abs().max()) <= 1e-3 * gmax and float(gf.abs().max()) <= 1e-3 * gmax, k
             continue
         cos = F.cosine_similarity(gp.float().reshape(1, -1), gf.float().reshape(1, -1)).item()
         assert cos >= 0.999, (k, cos)

@@ -14,7 +14,9 @@ import torch  # noqa: E402
 from recformer_amd import ops  # noqa: E402
 
 SHAPES = {"qkv": (65536, 2304, 768, ops.RF_EPI_BIAS, 768), "out": (65536, 768, 768, ops.RF_EPI_BIAS, 0),
-          "ffn1": (65536, 3072, 768, ops.RF_EPI_BIAS_GELU, 0), "ffn2": (65536, 768, 3072, ops.RF_EPI_BIAS, 0)}
+          "ffn1": (65536, 3072, 768, ops.RF_EPI_BIAS_GELU, 0), "ffn2": (65536, 768, 3072, ops.RF_EPI_BIAS, 0),
+          # FFN1's shape with the plain bias epilogue: the GELU's share of FFN1 by difference
+          "ffn1b": (65536, 3072, 768, ops.RF_EPI_BIAS, 0)}
 
 
 def main():

@@ -15,7 +15,8 @@ import json
 import os
 import sys
 
-ALG = {"qkv": (65536, 2304, 768), "out": (65536, 768, 768), "ffn1": (65536, 3072, 768), "ffn2": (65536, 768, 3072)}
+ALG = {"qkv": (65536, 2304, 768), "out": (65536, 768, 768), "ffn1": (65536, 3072, 768), "ffn2": (65536, 768, 3072),
+       "ffn1b": (65536, 3072, 768)}
 
 
 def rows(pattern):
