@@ -76,6 +76,10 @@ TOPK_SAMPLE = 2048  # dense seed block that sets each row's first candidate thre
 TOPK_CAP = 1024     # candidate list per row and chunk
 TOPK_MAX_K = 256    # rf_topk_* limits (rf_retrieval.hip TK_KMAX, TK_DENSE_MAX)
 TOPK_MAX_SAMPLE = 2048
+# column chunks after the seed: each TOPK_GROWTH - 1 times the columns already seen (2: doubling). A larger
+# factor means fewer launches and merges but a lower threshold relative to each chunk (about
+# k * (TOPK_GROWTH - 1) candidates per row and chunk)
+TOPK_GROWTH = 2
 
 
 @contextlib.contextmanager
@@ -203,10 +207,11 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     # default seed_n = s0; a larger seed_n would lower the first candidate chunks' rate)
     seed_n = s0
     blocks = [(o, min(sample, seed_n - o)) for o in range(0, seed_n, sample)]
-    # column chunks after the seed: each as large as everything before it
+    # column chunks after the seed: each (TOPK_GROWTH - 1) times everything before it
     plan, off = [], seed_n
+    grow = max(2, int(TOPK_GROWTH))
     while k > 0 and off < N:
-        plan.append((off, min(N - off, max(off, sample))))
+        plan.append((off, min(N - off, max(off * (grow - 1), sample))))
         off += plan[-1][1]
     nt0 = sum(lib.rf_score_rank_tiles(n) for _, n in blocks) if k > 0 else lib.rf_score_rank_tiles(N)
     ntiles = nt0 + sum(lib.rf_score_rank_tiles(n) for _, n in plan)

@@ -21,6 +21,16 @@ import contextlib  # noqa: E402
 from recformer_amd.ranker import CatalogShard, _rank_family, label_scores, shard_rank  # noqa: E402
 
 
+@contextlib.contextmanager
+def _knob_ctx(name, value):
+    from recformer_amd import _lib
+    old = _lib.set_knob(name, value)
+    try:
+        yield
+    finally:
+        _lib.set_knob(name, old)
+
+
 def timeit(fn, iters=10, warm=3):
     for _ in range(warm):
         fn()
@@ -38,7 +48,12 @@ def main():
     ap.add_argument("--items", type=str, default="125000,1000000")
     ap.add_argument("--dtype", type=str, default="fp16")
     ap.add_argument("--k", type=int, default=50)
+    ap.add_argument("--growth", type=str, default="",
+                    help="comma list of ranker.TOPK_GROWTH values to time the top-k mode at (A/B); default: the "
+                         "module's")
+    ap.add_argument("--family", type=str, default="", help="A/B: 'w16,w32' times the top-k mode on both families")
     args = ap.parse_args()
+    import recformer_amd.ranker as RK
     from recformer_amd import _lib
     pinned = False
     for kv in filter(None, os.environ.get("RF_KNOBS", "").split(",")):  # e.g. RF_KNOBS=rank_w32=1
@@ -58,6 +73,23 @@ def main():
         with family(True):  # label scores from the same family as the ranking (exact strict counts)
             sl = label_scores(q, shard, labels, 0.05)
             t_top = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=args.k))
+            ref = shard_rank(q, shard, sl, 0.05, k=args.k)
+        # A/B of the top-k plan (the same result required): growth factors x kernel families
+        for fam in filter(None, args.family.split(",")) or ([""] if args.growth else []):
+            for gr in filter(None, args.growth.split(",")) or [str(RK.TOPK_GROWTH)]:
+                old_g = RK.TOPK_GROWTH
+                RK.TOPK_GROWTH = int(gr)
+                ctx = (contextlib.nullcontext() if not fam else
+                       _knob_ctx("rank_w32", 1 if fam == "w32" else 0))
+                with ctx:
+                    slf = label_scores(q, shard, labels, 0.05)
+                    t = timeit(lambda: shard_rank(q, shard, slf, 0.05, k=args.k))
+                    r = shard_rank(q, shard, slf, 0.05, k=args.k)
+                RK.TOPK_GROWTH = old_g
+                same = bool(torch.equal(r["topi"], ref["topi"]) and torch.equal(r["gt"], ref["gt"]))
+                print(json.dumps({"items": N, "ab": f"growth={gr} family={fam or 'default'}", "ms": round(t * 1e3, 3),
+                                  "frac_of_2.5PF": round(2.0 * Q * N * d / t / 2.5e15, 3), "same_result": same}),
+                      flush=True)
         with family(False):
             sl = label_scores(q, shard, labels, 0.05)
             t_cnt = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=0))
