@@ -638,6 +638,38 @@ __global__ void __launch_bounds__(256) k_colsum_part(int M, int N, const T* __re
     part[(int64_t)blockIdx.y * N + cc] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
+// 16-bit x with 16-B rows (N % 8 == 0, ldx % 8 == 0, 16-B aligned): one 16-B load per lane and row (8
+// columns), 512 columns per block, the same slice / phase split and the same per-column order of the
+// additions as k_colsum_part (rows r0 + ph, r0 + ph + 4, ... per phase, then the 4 phases in order), so the
+// partials are bit-identical to it; the 8-B loads of k_colsum_part moved the training bias-gradient sums
+// at ~3.6 TB/s
+template <typename E>
+__global__ void __launch_bounds__(256) k_colsum_part16(int M, int N, const E* __restrict__ x, int64_t ldx,
+                                                        float* __restrict__ part) {
+  typedef typename H16<E>::x8 V8;
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 512 + 8 * lane;
+  const int per = (M + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(M, r0 + per);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+#pragma unroll 8
+    for (int r = r0 + ph; r < r1; r += 4) {
+      const V8 v = *reinterpret_cast<const V8*>(x + (int64_t)r * ldx + c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += (float)v[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[ph][8 * lane + k] = a[k];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int cc = blockIdx.x * 512 + i;
+    if (cc < N) part[(int64_t)blockIdx.y * N + cc] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
 // out[n] = sum_z part[z][n]: 64 slices x 4 columns per block, tree-reduced in LDS (fixed order)
 // scale_n > 0: out[c] for c < scale_n multiplied by scale (a Linear's column scale, e.g. the query's 1/8)
 __global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* __restrict__ part, float* __restrict__ out,
@@ -664,6 +696,13 @@ static void colsum(int M, int N, const T* x, int64_t ldx, float* part, float* ou
                    hipStream_t s, float* out3 = nullptr, int scale_n = 0, float scale = 1.f) {
   const int S = max(1, min(CS_SLICES, (M + 63) / 64));
   const bool vec = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(T))) == 0;
+  if constexpr (sizeof(T) == 2) {
+    if (N % 8 == 0 && ldx % 8 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) {
+      k_colsum_part16<T><<<dim3((N + 511) / 512, S), 256, 0, s>>>(M, N, x, ldx, part);
+      k_colsum_fin<<<(N + 3) / 4, 256, 0, s>>>(S, N, part, out, out2, split, out3, scale_n, scale);
+      return;
+    }
+  }
   if (vec) k_colsum_part<T, true><<<dim3((N + 255) / 256, S), 256, 0, s>>>(M, N, x, ldx, part);
   else k_colsum_part<T, false><<<dim3((N + 255) / 256, S), 256, 0, s>>>(M, N, x, ldx, part);
   k_colsum_fin<<<(N + 3) / 4, 256, 0, s>>>(S, N, part, out, out2, split, out3, scale_n, scale);

@@ -58,12 +58,16 @@ def test_label_scores_bit_identical_to_ranking_kernel(dev, dt):
     assert torch.equal(s_half[labels >= 2500], torch.zeros_like(s_half[labels >= 2500]))
 
 
+@pytest.mark.parametrize("growth", [2, 8])
 @pytest.mark.parametrize("dt,B,N,cluster", [(torch.bfloat16, 37, 20011, 0), (torch.float16, 300, 33000, 0),
                                             (torch.bfloat16, 64, 12000, 200)])
-def test_shard_rank_matches_restated_ranker_and_sort(dev, dt, B, N, cluster):
+def test_shard_rank_matches_restated_ranker_and_sort(dev, monkeypatch, dt, B, N, cluster, growth):
     """Strict ranks, valid lengths and the Ranker metrics equal the restated Ranker on the same
     scores; the top-50 equals a full stable sort; a row whose candidate slots overflow (cluster of
-    near-copies in one tile) is re-ranked exactly."""
+    near-copies in one tile) is re-ranked exactly. growth: the candidate chunks' growth factor
+    (ranker.TOPK_GROWTH; 2 = each chunk as large as everything before it)."""
+    import recformer_amd.ranker as RK
+    monkeypatch.setattr(RK, "TOPK_GROWTH", growth)
     q, items, labels = _case(dev, dt, B, N, B + N, cluster=cluster)
     shard = CatalogShard(items)
     sl = label_scores(q, shard, labels, 0.05)
