@@ -31,7 +31,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--infer", action="store_true",
+                    help="the C2 inference step instead (bench.py: B=64 encode + score, fp32 parameters under autocast)")
     a = ap.parse_args()
+    if a.infer:
+        a.batch = 64 if a.batch == 16 else a.batch
     dev = torch.device("cuda")
     cfg = RecformerConfig(**dict(BASE, item_num=10000, finetune_negative_sample_size=0))
     torch.manual_seed(0)
@@ -50,6 +54,13 @@ def main():
         opt.step()
         opt.zero_grad(set_to_none=True)
 
+    if a.infer:
+        model.eval()
+
+        def step():  # noqa: F811 - bench.py's step
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+                return model(**batch)
+
     for _ in range(2):
         step()
     torch.cuda.synchronize()
@@ -62,7 +73,16 @@ def main():
     class Rec(TorchDispatchMode):
         def __torch_dispatch__(self, func, types, args=(), kwargs=None):
             name = func.overloadpacket.__name__
-            if name in names and any(torch.is_tensor(x) and x.is_cuda for x in args):
+            kw = kwargs or {}
+            on_dev = any(torch.is_tensor(x) and x.is_cuda for x in list(args) + list(kw.values()))
+            dv = kw.get("device")
+            on_dev = on_dev or (dv is not None and torch.device(dv).type == "cuda")
+            # every op on (or creating) a device tensor — factories (zeros, full, arange, empty) included
+            if on_dev and name not in ("empty", "empty_strided", "view", "_unsafe_view", "t", "transpose",
+                                       "slice", "select", "as_strided", "detach", "alias", "expand",
+                                       "unsqueeze", "squeeze", "permute", "reshape", "_reshape_alias",
+                                       "split", "unbind", "diagonal", "set_", "resize_", "lift_fresh",
+                                       "is_same_size", "_local_scalar_dense"):
                 st = traceback.extract_stack(limit=40)
                 fr = [f"{os.path.basename(f.filename)}:{f.lineno}" for f in st
                       if "recformer_amd" in f.filename or "autograd" in f.filename]
@@ -74,7 +94,8 @@ def main():
     with Rec():
         step()
         torch.cuda.synchronize()
-    print(f"aten ops on device tensors in one eager C3 step (batch {a.batch}): {sum(per.values())}")
+    print(f"aten ops on device tensors in one eager {'C2 inference' if a.infer else 'C3'} step (batch {a.batch}): "
+          f"{sum(per.values())}")
     for name, n in per.most_common():
         print(f"{n:5d}  {name}")
         for key, m in where[name].most_common(10):
