@@ -134,28 +134,45 @@ __device__ __forceinline__ float dgelu_erf(float z) {
   const float erf = copysignf(fmaf(-p * t, e, 1.0f), z);
   return fmaf(0.5f, erf, 0.5f) + z * 0.3989422804014327f * e;
 }
-// the same on 8 values, one stage at a time across them (independent chains fill the
-// transcendental hazards; see gelu8_bf16out)
+// the same on 8 values, one stage at a time across 4 pairs (independent chains fill the transcendental
+// hazards; see gelu8_bf16out), the multiplies, FMAs and adds as packed-fp32 (v_pk_*) pairs: the same
+// operations per value in the same order, so bit-identical to dgelu_erf (hipcc left this scalar: ~13
+// VALU + 2 transcendentals per value, a third of the GELU-backward GEMM's tile time at 16k x 3072 x 768)
 __device__ __forceinline__ void dgelu8_erf(const float (&z)[8], float (&d)[8]) {
-  float ax[8], t[8], p[8], e[8];
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 c0 = {0.70710678118654752f, 0.70710678118654752f};
+  f2 zz[4], ax[4], t[4], p[4], e[4];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) ax[k] = fabsf(z[k]) * 0.70710678118654752f;
+  for (int k = 0; k < 4; ++k) zz[k] = (f2){z[2 * k], z[2 * k + 1]};
 #pragma unroll
-  for (int k = 0; k < 8; ++k) t[k] = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax[k], 1.0f));
+  for (int k = 0; k < 4; ++k) ax[k] = __builtin_elementwise_abs(zz[k]) * c0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) e[k] = __expf(-ax[k] * ax[k]);
+  for (int k = 0; k < 4; ++k) {
+    const f2 q = __builtin_elementwise_fma((f2){0.3275911f, 0.3275911f}, ax[k], (f2){1.0f, 1.0f});
+    t[k] = (f2){__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+  }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) p[k] = fmaf(t[k], 1.061405429f, -1.453152027f);
+  for (int k = 0; k < 4; ++k) {
+    const f2 a2 = -ax[k] * ax[k];
+    e[k] = (f2){__expf(a2.x), __expf(a2.y)};
+  }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) p[k] = fmaf(t[k], p[k], 1.421413741f);
+  for (int k = 0; k < 4; ++k) p[k] = __builtin_elementwise_fma(t[k], (f2){1.061405429f, 1.061405429f},
+                                                               (f2){-1.453152027f, -1.453152027f});
 #pragma unroll
-  for (int k = 0; k < 8; ++k) p[k] = fmaf(t[k], p[k], -0.284496736f);
+  for (int k = 0; k < 4; ++k) p[k] = __builtin_elementwise_fma(t[k], p[k], (f2){1.421413741f, 1.421413741f});
 #pragma unroll
-  for (int k = 0; k < 8; ++k) p[k] = fmaf(t[k], p[k], 0.254829592f);
+  for (int k = 0; k < 4; ++k) p[k] = __builtin_elementwise_fma(t[k], p[k], (f2){-0.284496736f, -0.284496736f});
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float erf = copysignf(fmaf(-p[k] * t[k], e[k], 1.0f), z[k]);
-    d[k] = fmaf(0.5f, erf, 0.5f) + z[k] * 0.3989422804014327f * e[k];
+  for (int k = 0; k < 4; ++k) p[k] = __builtin_elementwise_fma(t[k], p[k], (f2){0.254829592f, 0.254829592f});
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f2 y = __builtin_elementwise_fma(-p[k] * t[k], e[k], (f2){1.0f, 1.0f});
+    const f2 erf = __builtin_elementwise_copysign(y, zz[k]);
+    const f2 r = __builtin_elementwise_fma((f2){0.5f, 0.5f}, erf, (f2){0.5f, 0.5f}) +
+                 zz[k] * (f2){0.3989422804014327f, 0.3989422804014327f} * e[k];
+    d[2 * k] = r.x;
+    d[2 * k + 1] = r.y;
   }
 }
 
