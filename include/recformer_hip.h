@@ -70,13 +70,16 @@ int rf_debug_get_knob(const char* name);
  * position_ids may be NULL = reference defaults). Outputs (B,Lp) int32 ids/pos/type/
  * item-pos, uint8 flags {0 pad, 1 local, 2 global}, and gidx (B,gmax) int32 = the
  * positions of each row's global tokens in order, -1 padded (replaces the nonzero()
- * bookkeeping of TF:869-896 without a host sync). */
+ * bookkeeping of TF:869-896 without a host sync). gstat (B,2) int32, optional (NULL: not
+ * written): per sequence its number of global tokens and whether position 0 (the CLS) is one —
+ * what the caller reads back once to size gidx (the global-slot count) and to pick the
+ * CLS-only last layer, instead of reducing the masks with separate device ops. */
 int rf_prepare_inputs(const int64_t* input_ids, const int64_t* attention_mask,
                       const int64_t* global_attention_mask, const int64_t* token_type_ids,
                       const int64_t* item_position_ids, const int64_t* position_ids,
                       int B, int L, int Lp, int pad_id, int gmax,
                       int32_t* ids, int32_t* pos, int32_t* tt, int32_t* ip, uint8_t* flags,
-                      int32_t* gidx, rf_stream_t stream);
+                      int32_t* gidx, int32_t* gstat, rf_stream_t stream);
 
 /* A3 — RecformerEmbeddings.forward, models.py:108-138: LN(Ew[id] + Ep[pos] + Et[tt] +
  * Ei[ip]) for M tokens, one fused pass. Tables in table_dtype, LN params fp32, output in

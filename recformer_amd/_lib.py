@@ -27,7 +27,7 @@ SIGNATURES = {
     "rf_debug_set_knob": (c_int, [ctypes.c_char_p, c_int]),
     "rf_debug_get_knob": (c_int, [ctypes.c_char_p]),
     "rf_prepare_inputs": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
-                                  P, P, P, P, P, P, P]),
+                                  P, P, P, P, P, P, P, P]),
     "rf_embed_ln_fwd": (c_int, [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_float,
                                 P, P, P]),
     "rf_gemm": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, P, c_int, P, c_int,

@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(256) k_prepare(
     const int64_t* __restrict__ ip_in, const int64_t* __restrict__ pos_in, int L, int Lp,
     int pad_id, int gmax, int32_t* __restrict__ ids, int32_t* __restrict__ pos,
     int32_t* __restrict__ tt, int32_t* __restrict__ ip, uint8_t* __restrict__ flags,
-    int32_t* __restrict__ gidx) {
+    int32_t* __restrict__ gidx, int32_t* __restrict__ gstat) {
   __shared__ int scan_lds[8];
   const int b = blockIdx.x;
   const int per = (Lp + 255) / 256;
@@ -222,6 +222,14 @@ __global__ void __launch_bounds__(256) k_prepare(
     flags[o] = f;
   }
   for (int g = tot_glob + threadIdx.x; g < gmax; g += 256) gidx[(int64_t)b * gmax + g] = -1;
+  if (gstat && threadIdx.x == 0) {
+    // per sequence: its number of global tokens and whether position 0 (the CLS) is one — the same
+    // flag rule as above, so the host's global-slot count matches the flags exactly
+    const int64_t am0 = am_in ? am_in[(int64_t)b * L] : 1;
+    const int64_t m0 = gm_in ? am0 * (gm_in[(int64_t)b * L] + 1) : am0;
+    gstat[2 * b] = tot_glob;
+    gstat[2 * b + 1] = m0 > 1 ? 1 : 0;
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1068,7 +1076,7 @@ int rf_prepare_inputs(const int64_t* input_ids, const int64_t* attention_mask,
                       const int64_t* global_attention_mask, const int64_t* token_type_ids,
                       const int64_t* item_position_ids, const int64_t* position_ids, int B,
                       int L, int Lp, int pad_id, int gmax, int32_t* ids, int32_t* pos,
-                      int32_t* tt, int32_t* ip, uint8_t* flags, int32_t* gidx,
+                      int32_t* tt, int32_t* ip, uint8_t* flags, int32_t* gidx, int32_t* gstat,
                       rf_stream_t stream) {
   RF_REQUIRE(input_ids && item_position_ids && ids && pos && tt && ip && flags,
              "rf_prepare_inputs: null pointer");
@@ -1077,7 +1085,7 @@ int rf_prepare_inputs(const int64_t* input_ids, const int64_t* attention_mask,
   k_prepare<<<B, 256, 0, as_stream(stream)>>>(input_ids, attention_mask, global_attention_mask,
                                                token_type_ids, item_position_ids, position_ids,
                                                L, Lp, pad_id, gmax, ids, pos, tt, ip, flags,
-                                               gidx);
+                                               gidx, gstat);
   RF_LAUNCH_CHECK("rf_prepare_inputs");
 }
 

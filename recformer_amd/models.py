@@ -279,7 +279,7 @@ def _async_count(t: torch.Tensor):
 def _read_count(p):
     buf, ev = p
     ev.synchronize()
-    return int(buf) if buf.dim() == 0 else [int(x) for x in buf.tolist()]
+    return int(buf) if buf.dim() == 0 else buf.tolist()
 # pretraining training: the LM-head decoder + masked-LM cross entropy on the HIP kernels
 # (train._DecoderCE) for 16-bit compute; False = torch ops (F.linear + F.cross_entropy)
 DECODER_CE_HIP = True
@@ -529,34 +529,39 @@ class RecformerModel(nn.Module):
         want_cls = (pooled_only and cfg.pooler_type == "cls" and PRUNE_LAST_LAYER and not output_hidden_states
                     and attn_probe is None)
         cls_global = False
+        gstat = None
         if _STATIC_GMAX is not None:
             gmax = _STATIC_GMAX
             cls_global = want_cls and bool(_STATIC_CLS)
         elif global_attention_mask is not None and B > 0:
-            gm = global_attention_mask != 0
-            if attention_mask is not None:
-                gm = gm & (attention_mask > 0)
             if ASYNC_GLOBAL_COUNT:
-                cnt = gm.sum(1).max()
-                pending = _async_count(torch.stack([cnt, gm[:, 0].all().to(cnt.dtype)]) if want_cls else cnt)
+                # the prologue itself writes each sequence's global count and CLS flag (no mask
+                # reductions as separate launches); copied to pinned memory below, read after the
+                # embedding is queued
+                gstat = torch.empty(B, 2, dtype=torch.int32, device=input_ids.device)
                 gmax = 0
             else:
+                gm = global_attention_mask != 0
+                if attention_mask is not None:
+                    gm = gm & (attention_mask > 0)
                 gmax = int(gm.sum(1).max().item())
                 cls_global = want_cls and bool(gm[:, 0].all())
         else:
             gmax = 0
         ids, pos, tt, ip, flags, gidx = ops.prepare_inputs(
             input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,
-            position_ids, Lp, cfg.pad_token_id, gmax)
+            position_ids, Lp, cfg.pad_token_id, gmax, gstat=gstat)
+        if gstat is not None:
+            pending = _async_count(gstat)
 
         def _globals():
             # the global index table once the count is known (re-runs the prologue with gmax slots;
             # the token streams it rewrites are identical)
             nonlocal gmax, flags, gidx, cls_global
             if pending is not None:
-                gmax = _read_count(pending)
-                if want_cls:
-                    gmax, cls_global = gmax[0], bool(gmax[1])
+                st = _read_count(pending)
+                gmax = max(c for c, _ in st)
+                cls_global = want_cls and all(f for _, f in st)
                 if gmax > 0:
                     _, _, _, _, flags, gidx = ops.prepare_inputs(
                         input_ids, attention_mask, global_attention_mask, token_type_ids, item_position_ids,

@@ -91,9 +91,11 @@ def _rowmajor(t: torch.Tensor, name: str) -> int:
 
 
 def prepare_inputs(input_ids, attention_mask, global_attention_mask, token_type_ids,
-                   item_position_ids, position_ids, Lp: int, pad_id: int, gmax: int):
+                   item_position_ids, position_ids, Lp: int, pad_id: int, gmax: int,
+                   gstat: Optional[torch.Tensor] = None):
     """A2 prologue (models.py:306-329). Returns int32 ids/pos/tt/ip (B,Lp), uint8 flags,
-    int32 gidx (B,gmax)."""
+    int32 gidx (B,gmax). gstat: an int32 (B, 2) tensor to receive each sequence's global-token count
+    and whether its position 0 is global (from the same pass)."""
     lib = _lib.load()
     _dev(input_ids)
     B, L = input_ids.shape
@@ -118,9 +120,11 @@ def prepare_inputs(input_ids, attention_mask, global_attention_mask, token_type_
     ip = torch.empty_like(ids)
     flags = torch.empty(B, Lp, dtype=torch.uint8, device=dev)
     gidx = torch.empty(B, max(gmax, 1), dtype=torch.int32, device=dev)
+    if gstat is not None and (gstat.dtype != torch.int32 or tuple(gstat.shape) != (B, 2) or not gstat.is_contiguous()):
+        raise ValueError("prepare_inputs: gstat must be a contiguous int32 (B, 2) tensor")
     check(lib.rf_prepare_inputs(_p(ids_in), _p(am), _p(gm), _p(tt_in), _p(ip_in), _p(pos_in), B, L,
                                 Lp, pad_id, gmax, _p(ids), _p(pos), _p(tt), _p(ip), _p(flags),
-                                _p(gidx), _stream(ids)), "rf_prepare_inputs")
+                                _p(gidx), _p(gstat), _stream(ids)), "rf_prepare_inputs")
     return ids, pos, tt, ip, flags, gidx[:, :gmax]
 
 
