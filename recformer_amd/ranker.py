@@ -78,8 +78,9 @@ TOPK_MAX_K = 256    # rf_topk_* limits (rf_retrieval.hip TK_KMAX, TK_DENSE_MAX)
 TOPK_MAX_SAMPLE = 2048
 # column chunks after the seed: each TOPK_GROWTH - 1 times the columns already seen (2: doubling). A larger
 # factor means fewer launches and merges but a lower threshold relative to each chunk (about
-# k * (TOPK_GROWTH - 1) candidates per row and chunk)
-TOPK_GROWTH = 2
+# k * (TOPK_GROWTH - 1) candidates per row and chunk). 1M items x 4096 queries, top-50, 16x16x32 family:
+# 9.27 / 9.11 / 9.05 ms at 2 / 4 / 8 (the 32x32x16 family 10.2-10.4 ms at any; gpurun_out/r05f/c5ab.log)
+TOPK_GROWTH = 8
 
 
 @contextlib.contextmanager
