@@ -67,6 +67,7 @@ enum Knob {
   KNOB_MID_TILE,        // EPI_NONE / EPI_BIAS GEMMs whose 256x256 grid leaves CUs idle: 0 the four-wave kernel,
                         // 1 the 128x128 tile kernel, 2 the 256x128 one (captured C3: 17.77 / 18.20 vs
                         // 16.26 / 16.36 ms, r04z: the older tile kernels lose more than the idle CUs cost)
+  KNOB_COLSUM_SLICES,   // column sums (bias gradients): row slices at most (0 = CS_SLICES; A/B of the slice count)
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];

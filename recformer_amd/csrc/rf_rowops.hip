@@ -12,7 +12,7 @@
 namespace rf {
 
 static thread_local char g_err[512];
-int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8, -1, 0, 0, 0, 1, 0, 0, 0};
+int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8, -1, 0, 0, 0, 1, 0, 0, 0, 0};
 const uint64_t* g_seed_dev = nullptr;
 
 void set_error(const char* fmt, ...) {
@@ -614,7 +614,10 @@ __global__ void __launch_bounds__(256) k_scatter_add_rows(int R, int D, const in
   }
 }
 
-constexpr int CS_SLICES = 64;  // k_colsum_fin reduces at most 64 slices
+// row slices of the column-sum stage (at most; 64 rows each at least). 256 slices (every row load of a wave
+// in flight at once) measured no faster in the captured C3 step (16.53 vs 16.49 ms, knob colsum_slices,
+// gpurun_out/r05i): the training bias-gradient sums run beside the weight-gradient stream
+constexpr int CS_SLICES = 64;
 
 template <typename T, bool VECOK>
 __global__ void __launch_bounds__(256) k_colsum_part(int M, int N, const T* __restrict__ x, int64_t ldx,
@@ -678,7 +681,8 @@ __global__ void __launch_bounds__(256) k_colsum_part16(int M, int N, const E* __
   }
 }
 
-// out[n] = sum_z part[z][n]: 64 slices x 4 columns per block, tree-reduced in LDS (fixed order)
+// out[n] = sum_z part[z][n]: 64 slice phases x 4 columns per block (phase z adds slices z, z + 64, ... in
+// order), tree-reduced in LDS (fixed order)
 // scale_n > 0: out[c] for c < scale_n multiplied by scale (a Linear's column scale, e.g. the query's 1/8)
 __global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* __restrict__ part, float* __restrict__ out,
                                                      float* __restrict__ out2, int split, float* __restrict__ out3,
@@ -686,7 +690,10 @@ __global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* _
   __shared__ float red[64][5];
   const int z = threadIdx.x >> 2, k = threadIdx.x & 3;
   const int c = blockIdx.x * 4 + k;
-  red[z][k] = (c < N && z < S) ? part[(int64_t)z * N + c] : 0.f;
+  float a = 0.f;
+  if (c < N)
+    for (int zz = z; zz < S; zz += 64) a += part[(int64_t)zz * N + c];
+  red[z][k] = a;
   __syncthreads();
   for (int o = 32; o > 0; o >>= 1) {
     if (z < o) red[z][k] += red[z + o][k];
@@ -702,7 +709,8 @@ __global__ void __launch_bounds__(256) k_colsum_fin(int S, int N, const float* _
 template <typename T>
 static void colsum(int M, int N, const T* x, int64_t ldx, float* part, float* out, float* out2, int split,
                    hipStream_t s, float* out3 = nullptr, int scale_n = 0, float scale = 1.f) {
-  const int S = max(1, min(CS_SLICES, (M + 63) / 64));
+  const int cap = g_knob[KNOB_COLSUM_SLICES] > 0 ? min(g_knob[KNOB_COLSUM_SLICES], CS_SLICES) : CS_SLICES;
+  const int S = max(1, min(cap, (M + 63) / 64));
   const bool vec = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(T))) == 0;
   if constexpr (sizeof(T) == 2) {
     if (N % 8 == 0 && ldx % 8 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) {
@@ -1051,7 +1059,8 @@ const char* rf_last_error(void) { return rf::g_err; }
 static int knob_index(const char* name) {
   static const char* names[rf::KNOB_COUNT] = {"gemm_gn", "gemm_variant", "band_qpb", "band_path", "gfold_path",
                                               "gfold_qsplit", "gemm_pf", "gemm_mfma32", "rank_w32",
-                                              "gfold_chunk", "gemm_skinny", "epi_tile", "tn_wgs", "mid_tile"};
+                                              "gfold_chunk", "gemm_skinny", "epi_tile", "tn_wgs", "mid_tile",
+                                              "colsum_slices"};
   for (int i = 0; i < rf::KNOB_COUNT; ++i)
     if (name && names[i] && strcmp(name, names[i]) == 0) return i;
   rf::set_error("rf_debug_knob: unknown knob '%s'", name ? name : "(null)");

@@ -103,6 +103,12 @@ def _mm_f32(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
 # a quarter of the chip would idle; the independent dW = dC^T A work fills it (forked and joined with
 # stream events — graph-capturable)
 DW_SIDE_STREAM = True
+# the embedding tables' index sorts (their backward's segment sums) run on that side stream during the
+# forward (_EmbedLN) instead of at the end of the backward
+EMBED_SORT_EARLY = True
+# the global rows' attention backward (rf_global_fold_bwd_full + rf_global_query_bwd: launches of a few
+# hundred workgroups) on that side stream beside the local branch's backward (_Attention.backward)
+GLOBAL_BWD_SIDE = True
 # the attention's gradient of a layer's input added inside the q|k|v projection's dA GEMM (_GradMailbox)
 # instead of autograd's separate bf16 sum: -0.4% per captured C3 step (16.55 vs 16.62 ms, gpurun_out/r04r),
 # The round-4 suite fault with it on (an illegal address in the first training test after the graph tests,
@@ -131,11 +137,19 @@ def _dw_async(fn, ref: torch.Tensor):
     with torch.cuda.stream(side):
         r = fn()
 
+    def record(x):
+        if isinstance(x, torch.Tensor):
+            x.record_stream(main)
+        elif isinstance(x, (list, tuple)):
+            for t in x:
+                record(t)
+        elif isinstance(x, dict):
+            for t in x.values():
+                record(t)
+
     def join():
         main.wait_stream(side)
-        for t in (r if isinstance(r, (list, tuple)) else (r,)):
-            if isinstance(t, torch.Tensor):
-                t.record_stream(main)
+        record(r)
         return r
     return join
 
@@ -570,6 +584,11 @@ class _EmbedLN(torch.autograd.Function):
         h = out[0] if isinstance(out, tuple) else out
         ctx.save_for_backward(ids, pos, tt, ip, word, pe, te, ie, ln_w)
         ctx.eps, ctx.pad = eps, pad_id
+        ctx.sorted = None
+        if EMBED_SORT_EARLY and EMBED_BWD_HIP and h.is_cuda and any(ctx.needs_input_grad[4:8]):
+            # the four index sorts of the tables' gradients depend on the token indices only: queued now on
+            # the side stream, beside the forward, instead of at the tail of the backward
+            ctx.sorted = _dw_async(lambda: [ops.embedding_sort(x) for x in (ids, pos, tt, ip)], h)
         return h
 
     @staticmethod
@@ -580,8 +599,11 @@ class _EmbedLN(torch.autograd.Function):
             # sums over the sorted token indices (rf_segment_rows_sum) — no atomics, no fp32 copy of x
             dx, dw, db = ops.embed_ln_bwd(ids, pos, tt, ip, word.contiguous(), pe.contiguous(), te.contiguous(),
                                           ie.contiguous(), ln_w, ctx.eps, dh.reshape(-1, word.shape[1]))
-            grads = [ops.embedding_grad(dx, idx, table.shape[0], pad)
-                     for table, idx, pad in ((word, ids, ctx.pad), (pe, pos, ctx.pad), (te, tt, None), (ie, ip, None))]
+            srt = ctx.sorted() if ctx.sorted is not None else [None] * 4
+            ctx.sorted = None
+            grads = [ops.embedding_grad(dx, idx, table.shape[0], pad, sorted_index=si)
+                     for (table, idx, pad), si in zip(((word, ids, ctx.pad), (pe, pos, ctx.pad), (te, tt, None),
+                                                       (ie, ip, None)), srt)]
             return (None, None, None, None, *grads, dw, db, None, None)
         i, p, t, q = (x.reshape(-1).long() for x in (ids, pos, tt, ip))
         x = word[i] + pe[p] + te[t] + ie[q]  # recompute the pre-LN sum (fp32)
@@ -925,68 +947,91 @@ class _Attention(torch.autograd.Function):
         # local branch on the HIP backward kernels (rf_attn_bwd.hip); global rows of dout belong
         # to the global branch only (their local output was overwritten)
         d16 = dout.to(q.dtype).contiguous()
+        res = [None] * 7
+        extra = qtail = None
+        need_global = gmax > 0 and (any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]) or ctx.qin)
+        hip_bwd = GLOBAL_BWD_HIP and ctx.fold_ws is not None
+        join_global = None
+        if need_global and hip_bwd and GLOBAL_BWD_SIDE:
+            # the global rows' backward reads dout, h and the forward's fold workspace only, not the local
+            # branch's gradients: its few-block launches run on the side stream beside the local branch's
+            # whole-chip kernels (joined before h's gradient is handed on)
+            join_global = _dw_async(lambda: _Attention._global_branch(ctx, d16, h, qg, wkg, bkg, wvg, bvg, flags,
+                                                                      gidx, B, Lp, H, p_drop, seed, dout, True),
+                                    d16)
         # gradients written in the projection's dtype (bf16): no fp32 copy and cast per layer
         dqkv = torch.empty(B * Lp, 3 * D, dtype=qkv.dtype, device=q.device)
         dq, dk, dv, gds, gpr = ops.band_attention_bwd(q, k, v, out, d16, flags, gidx, B, Lp, H, dqkv=dqkv,
                                                       p_drop=p_drop, seed=seed)
-        res = [None] * 7
         if gmax > 0:
-            if ctx.grows is not None:
-                rows, keep, rows32 = ctx.grows
-            else:
-                rows, keep = _global_rows(gidx, B, Lp)
-                rows32 = torch.where(keep, rows, -1).to(torch.int32)  # -1: empty slot, skipped
             # gradients of the global-key columns, reduced over every query of the sequence and added
             # into dk / dv at the global positions (bf16, as dqkv)
             if GLOBAL_KV_HIP and gds.shape[-1] == gmax:
                 ops.global_kv_grad(gds, gpr, q, d16, gidx, B, Lp, H, dk, dv)
             else:
+                rows32 = ctx.grows[2] if ctx.grows is not None else None
+                if rows32 is None:
+                    rows, keep = _global_rows(gidx, B, Lp)
+                    rows32 = torch.where(keep, rows, -1).to(torch.int32)  # -1: empty slot, skipped
                 # bf16 operands, fp32 accumulation (no fp32 copies of the (B*Lp, D) q and dout)
                 dkg = _global_kv_grad(gds[..., :gmax], q, B, Lp, H)
                 dvg = _global_kv_grad(gpr[..., :gmax], d16, B, Lp, H)
                 # no boolean-mask indexing (it syncs the host): invalid slots add zeros at row 0
                 ops.scatter_add_rows(rows32, dkg.to(dk.dtype).contiguous(), dk, dvg.to(dv.dtype).contiguous(), dv)
             # global branch: closed-form gradient of the fold algebra
-            if any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]) or ctx.qin:
-                hip_bwd = GLOBAL_BWD_HIP and ctx.fold_ws is not None
-                gout = gz = None
-                if not hip_bwd:
-                    gout = dout[rows].float() * keep[:, None].to(torch.float32)
-                if ctx.gz_kind == "hip" and not hip_bwd:  # the forward's mask, from the same kernel
-                    gz = ops.attn_global_keep(gidx, B, Lp, H, p_drop, seed)
-                elif ctx.gz_kind == "torch":
-                    gz = _global_keep(gidx, B, Lp, H, p_drop, seed)
-                if hip_bwd:
-                    with torch.autocast("cuda", enabled=False):
-                        grads = _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B, Lp, H, d16, ctx.fold_ws,
-                                                p_drop, seed)
-                elif GLOBAL_BWD_CLOSED_FORM:
-                    with torch.autocast("cuda", enabled=False):
-                        grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, gz, bvg,
-                                            dh_dtype=h.dtype if GLOBAL_BWD_DH16 else None)
-                else:
-                    gin = [t.detach().requires_grad_(True) for t in (qg, h, wkg, bkg, wvg, bvg)]
-                    with torch.enable_grad(), torch.autocast("cuda", enabled=False):
-                        og = _global_torch(*gin, flags, B, Lp, H, gz)
-                        grads = torch.autograd.grad(og, gin, gout, allow_unused=True)
-                for n, t in enumerate((qg, h, wkg, bkg, wvg, bvg)):
-                    if ctx.needs_input_grad[1 + n] or (n == 1 and ctx.qin):
-                        g = grads[n]
-                        res[1 + n] = None if g is None else g.to(t.dtype)
-                if ctx.masters:  # fp32 gradients straight to the masters (no bf16 round trip)
-                    extra = [grads[2].float() if ctx.needs_input_grad[17] and grads[2] is not None else None,
-                             grads[4].float() if ctx.needs_input_grad[18] and grads[4] is not None else None]
-                if ctx.qin:
-                    res[2], qtail = _Attention._qg_backward(ctx, grads[0], res[2], h, gidx, B, Lp, hip_bwd)
+            if need_global:
+                upd, extra, qtail = (join_global() if join_global is not None else
+                                     _Attention._global_branch(ctx, d16, h, qg, wkg, bkg, wvg, bvg, flags, gidx, B,
+                                                               Lp, H, p_drop, seed, dout, hip_bwd))
+                for n, g in upd.items():
+                    res[n] = g
         if ctx.needs_input_grad[0]:
             res[0] = dqkv.to(qkv.dtype)
         tail = [None] * 18  # the forward's non-tensor inputs, the two masters, the query weights, mb
-        if ctx.masters and gmax > 0 and (any(ctx.needs_input_grad[1:7]) or any(ctx.needs_input_grad[17:19]) or
-                                         ctx.qin):
+        if extra is not None:
             tail[10:12] = extra
-        if ctx.qin and gmax > 0:
+        if qtail is not None:
             tail[12:17] = qtail
         return (*_Attention._post_h(ctx, res, h), *tail)
+
+    @staticmethod
+    def _global_branch(ctx, d16, h, qg, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int, p_drop: float,
+                       seed: int, dout, hip_bwd: bool):
+        """The global rows' backward (closed form of the fold algebra, or autograd through the torch
+        restatement): returns ({input index: gradient} for qg, h, wkg, bkg, wvg, bvg, the fp32 gradients for
+        the two key/value masters (or None), the query projection's tail (or None))."""
+        gout = gz = None
+        if not hip_bwd:
+            rows, keep = ctx.grows[:2] if ctx.grows is not None else _global_rows(gidx, B, Lp)
+            gout = dout[rows].float() * keep[:, None].to(torch.float32)
+        if ctx.gz_kind == "hip" and not hip_bwd:  # the forward's mask, from the same kernel
+            gz = ops.attn_global_keep(gidx, B, Lp, H, p_drop, seed)
+        elif ctx.gz_kind == "torch":
+            gz = _global_keep(gidx, B, Lp, H, p_drop, seed)
+        if hip_bwd:
+            with torch.autocast("cuda", enabled=False):
+                grads = _global_bwd_hip(qg, h, wkg, wvg, bvg, flags, gidx, B, Lp, H, d16, ctx.fold_ws, p_drop, seed)
+        elif GLOBAL_BWD_CLOSED_FORM:
+            with torch.autocast("cuda", enabled=False):
+                grads = _global_bwd(qg, h, wkg, wvg, flags, B, Lp, H, gout, gz, bvg,
+                                    dh_dtype=h.dtype if GLOBAL_BWD_DH16 else None)
+        else:
+            gin = [t.detach().requires_grad_(True) for t in (qg, h, wkg, bkg, wvg, bvg)]
+            with torch.enable_grad(), torch.autocast("cuda", enabled=False):
+                og = _global_torch(*gin, flags, B, Lp, H, gz)
+                grads = torch.autograd.grad(og, gin, gout, allow_unused=True)
+        upd = {}
+        for n, t in enumerate((qg, h, wkg, bkg, wvg, bvg)):
+            if ctx.needs_input_grad[1 + n] or (n == 1 and ctx.qin):
+                g = grads[n]
+                upd[1 + n] = None if g is None else g.to(t.dtype)
+        extra = qtail = None
+        if ctx.masters:  # fp32 gradients straight to the masters (no bf16 round trip)
+            extra = [grads[2].float() if ctx.needs_input_grad[17] and grads[2] is not None else None,
+                     grads[4].float() if ctx.needs_input_grad[18] and grads[4] is not None else None]
+        if ctx.qin:
+            upd[2], qtail = _Attention._qg_backward(ctx, grads[0], upd.get(2), h, gidx, B, Lp, hip_bwd)
+        return upd, extra, qtail
 
     @staticmethod
     def _post_h(ctx, res, h):
