@@ -18,7 +18,7 @@ from ._lib import (RF_BF16, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_GELU_AUX,
 
 __all__ = [
     "dtype_code", "prepare_inputs", "embed_ln", "embed_ln_split", "add_layernorm_split", "join_split",
-    "gemm", "weight_grad", "WeightPack", "embed_ln_bwd", "embedding_sort", "embedding_grad", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
+    "gemm", "weight_grad", "WeightPack", "embed_ln_bwd", "embedding_grad", "colsum", "layernorm", "layernorm_bwd", "drop_add_ln_fwd", "drop_add_ln_bwd", "add_layernorm", "band_attention_bwd", "band_attention",
     "global_attention", "gather_global_rows", "row_inv_norm", "cos_scores", "cos_scores_cand",
     "cross_entropy",
     "cos_scores_bwd",
@@ -456,30 +456,19 @@ def embed_ln_bwd(ids, pos, tt, ip, word, posemb, typeemb, iposemb, ln_w, eps: fl
     return dx, dw, db
 
 
-def embedding_sort(index: torch.Tensor):
-    """The stable sort of token indices embedding_grad sums over: (keys int32, perm int32). It depends on the
-    indices only, so a training forward can run it ahead of the backward (train._EmbedLN)."""
-    keys, perm = torch.sort(index.reshape(-1).to(torch.int32), stable=True)
-    return keys.contiguous(), perm.to(torch.int32).contiguous()
-
-
-def embedding_grad(src: torch.Tensor, index: torch.Tensor, num_rows: int, pad: Optional[int] = None,
-                   sorted_index=None) -> torch.Tensor:
+def embedding_grad(src: torch.Tensor, index: torch.Tensor, num_rows: int, pad: Optional[int] = None) -> torch.Tensor:
     """nn.Embedding's dense weight gradient (num_rows, D) fp32 from row gradients src (M, D) and the
-    token indices (M,), deterministically: a stable sort of the indices (or `sorted_index`, embedding_sort's
-    result for the same indices), then rf_segment_rows_sum adds each index's rows in token order; the
-    padding_idx row stays zero."""
+    token indices (M,), deterministically: a stable sort of the indices, then rf_segment_rows_sum adds
+    each index's rows in token order; the padding_idx row stays zero."""
     lib = _lib.load()
     _dev(src, index)
     M, D = src.shape
     src = src.float().contiguous()
-    keys, perm = embedding_sort(index) if sorted_index is None else sorted_index
-    if keys.numel() != M or perm.numel() != M:
-        raise ValueError(f"embedding_grad: {keys.numel()} sorted indices for {M} rows")
+    keys, perm = torch.sort(index.reshape(-1).to(torch.int32), stable=True)
     out = torch.zeros(num_rows, D, dtype=torch.float32, device=src.device)
     ws = torch.empty(max(lib.rf_segment_rows_sum_workspace(M, D), 16), dtype=torch.uint8, device=src.device)
-    check(lib.rf_segment_rows_sum(M, D, _p(src), _p(perm), _p(keys), -1 if pad is None else int(pad), _p(out),
-                                  num_rows, _p(ws), _stream(src)),
+    check(lib.rf_segment_rows_sum(M, D, _p(src), _p(perm.to(torch.int32).contiguous()), _p(keys.contiguous()),
+                                  -1 if pad is None else int(pad), _p(out), num_rows, _p(ws), _stream(src)),
           "rf_segment_rows_sum")
     return out
 

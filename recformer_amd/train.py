@@ -103,9 +103,6 @@ def _mm_f32(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
 # a quarter of the chip would idle; the independent dW = dC^T A work fills it (forked and joined with
 # stream events — graph-capturable)
 DW_SIDE_STREAM = True
-# the embedding tables' index sorts (their backward's segment sums) run on that side stream during the
-# forward (_EmbedLN) instead of at the end of the backward
-EMBED_SORT_EARLY = True
 # the global rows' attention backward (rf_global_fold_bwd_full + rf_global_query_bwd: launches of a few
 # hundred workgroups) on that side stream beside the local branch's backward (_Attention.backward)
 GLOBAL_BWD_SIDE = True
@@ -119,6 +116,9 @@ GRAD_MAILBOX = True
 # the bias gradients' column sums on the weight-gradient side stream too: measured slower (captured C3
 # 16.48 vs 16.38 ms in one process, gpurun_out/r04s: that stream is the step's critical path), so off
 BIAS_GRAD_SIDE = False
+# ... but for the packed Linears (_GemmP: the q|k|v projection's column sums, 75 MB at C3) it is: there the
+# main stream's dA GEMM (N = 768, K = 2304) outlasts the side stream's dW + reduce
+GEMMP_BIAS_GRAD_SIDE = True
 _SIDE_STREAMS = {}
 
 
@@ -294,7 +294,7 @@ class _GemmP(torch.autograd.Function):
         da = None
         # the dW rows and db entries of the scaled outputs scaled inside the reduction kernels
         scl = (sc, s) if scaled else (0, 1.0)
-        side_b = BIAS_GRAD_SIDE and ctx.needs_input_grad[1] and any(ctx.needs_input_grad[7:])
+        side_b = (BIAS_GRAD_SIDE or GEMMP_BIAS_GRAD_SIDE) and ctx.needs_input_grad[1] and any(ctx.needs_input_grad[7:])
         join = (_dw_async(lambda: (_weight_grad(dc, a, scl).to(ctx.wdt), _bias_grad(dc, scl) if side_b else None),
                           dc) if any(ctx.needs_input_grad[7:]) else None)
         if ctx.needs_input_grad[0]:
@@ -584,11 +584,6 @@ class _EmbedLN(torch.autograd.Function):
         h = out[0] if isinstance(out, tuple) else out
         ctx.save_for_backward(ids, pos, tt, ip, word, pe, te, ie, ln_w)
         ctx.eps, ctx.pad = eps, pad_id
-        ctx.sorted = None
-        if EMBED_SORT_EARLY and EMBED_BWD_HIP and h.is_cuda and any(ctx.needs_input_grad[4:8]):
-            # the four index sorts of the tables' gradients depend on the token indices only: queued now on
-            # the side stream, beside the forward, instead of at the tail of the backward
-            ctx.sorted = _dw_async(lambda: [ops.embedding_sort(x) for x in (ids, pos, tt, ip)], h)
         return h
 
     @staticmethod
@@ -599,11 +594,8 @@ class _EmbedLN(torch.autograd.Function):
             # sums over the sorted token indices (rf_segment_rows_sum) — no atomics, no fp32 copy of x
             dx, dw, db = ops.embed_ln_bwd(ids, pos, tt, ip, word.contiguous(), pe.contiguous(), te.contiguous(),
                                           ie.contiguous(), ln_w, ctx.eps, dh.reshape(-1, word.shape[1]))
-            srt = ctx.sorted() if ctx.sorted is not None else [None] * 4
-            ctx.sorted = None
-            grads = [ops.embedding_grad(dx, idx, table.shape[0], pad, sorted_index=si)
-                     for (table, idx, pad), si in zip(((word, ids, ctx.pad), (pe, pos, ctx.pad), (te, tt, None),
-                                                       (ie, ip, None)), srt)]
+            grads = [ops.embedding_grad(dx, idx, table.shape[0], pad)
+                     for table, idx, pad in ((word, ids, ctx.pad), (pe, pos, ctx.pad), (te, tt, None), (ie, ip, None))]
             return (None, None, None, None, *grads, dw, db, None, None)
         i, p, t, q = (x.reshape(-1).long() for x in (ids, pos, tt, ip))
         x = word[i] + pe[p] + te[t] + ie[q]  # recompute the pre-LN sum (fp32)
