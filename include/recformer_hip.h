@@ -309,6 +309,15 @@ int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int H, const v
                                  const void* wvg, const float* bvg, const uint8_t* flags,
                                  const int32_t* gidx, int gmax, void* workspace, void* out,
                                  int ld_out, float p_drop, uint64_t seed, rf_stream_t stream);
+/* rf_global_attn_fold_fwd_drop in two stages on the same workspace: stage 1 = u and the pass over h
+ * (reads qg, h, wkg; `out` unused), stage 2 = the chunk merge and Wvg, written into out's global rows;
+ * 3 = both. Stage 1 does not touch `out`, so a training forward runs it beside the local attention that
+ * writes out, and stage 2 after it. */
+int rf_global_attn_fold_fwd_stage(int stage, int dtype, int B, int Lp, int D, int H, const void* qg, int ld_qg,
+                                  const void* h, int ldh, const void* wkg, const float* bkg,
+                                  const void* wvg, const float* bvg, const uint8_t* flags,
+                                  const int32_t* gidx, int gmax, void* workspace, void* out,
+                                  int ld_out, float p_drop, uint64_t seed, rf_stream_t stream);
 /* That mask for the backward: z (B, H, gmax, Lp) fp32, z[b,h,g,l] = keep x 1/(1-p) of row
  * (b*H + h)*Lp + max(gidx[b,g], 0), key l. */
 int rf_attn_global_keep(int B, int H, int Lp, const int32_t* gidx, int gmax, float p_drop,

@@ -97,6 +97,8 @@ SIGNATURES = {
                                         P, P, P, P, c_int, P, P, c_int, P]),
     "rf_global_attn_fold_fwd_drop": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, P,
                                              P, P, P, P, c_int, P, P, c_int, c_float, ctypes.c_uint64, P]),
+    "rf_global_attn_fold_fwd_stage": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, P,
+                                              P, P, P, P, c_int, P, P, c_int, c_float, ctypes.c_uint64, P]),
     "rf_attn_global_keep": (c_int, [c_int, c_int, c_int, P, c_int, c_float, ctypes.c_uint64, P, P]),
     "rf_global_attn_fold_h_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, c_float, P, P, P,
                                           P, P, P, c_int, P, P, c_int, P]),

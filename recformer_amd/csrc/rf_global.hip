@@ -1449,13 +1449,14 @@ static int fold_partial_out(int dtype, int B, int Lp, int D, int H, const void* 
   return RF_OK;
 }
 
-extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int H, const void* qg,
-                                            int ld_qg, const void* h, int ldh, const void* wkg,
-                                            const float* bkg, const void* wvg, const float* bvg,
-                                            const uint8_t* flags, const int32_t* gidx, int gmax,
-                                            void* workspace, void* out, int ld_out, float p_drop,
-                                            uint64_t seed, rf_stream_t stream) {
+extern "C" int rf_global_attn_fold_fwd_stage(int stage, int dtype, int B, int Lp, int D, int H, const void* qg,
+                                             int ld_qg, const void* h, int ldh, const void* wkg,
+                                             const float* bkg, const void* wvg, const float* bvg,
+                                             const uint8_t* flags, const int32_t* gidx, int gmax,
+                                             void* workspace, void* out, int ld_out, float p_drop,
+                                             uint64_t seed, rf_stream_t stream) {
   (void)bkg;  // softmax-invariant (see header comment)
+  RF_REQUIRE(stage >= 1 && stage <= 3, "rf_global_attn_fold_fwd_stage: stage %d not in 1..3", stage);
   RF_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "rf_global_attn_fold_fwd: p_drop %f not in [0, 1)", p_drop);
   RF_REQUIRE(p_drop == 0.f || dtype != RF_F32, "rf_global_attn_fold_fwd: attention dropout needs 16-bit operands");
   const AttnDrop dr{seed, drop_thresh(p_drop), p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.f, g_seed_dev};
@@ -1474,7 +1475,8 @@ extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int
   const int nch = (Lp + chr - 1) / chr;
   GfoldWs ws = gfold_carve(workspace, R, nch, H, D);
   hipStream_t s = as_stream(stream);
-  if (dtype == RF_BF16)
+  if (!(stage & 1)) {
+  } else if (dtype == RF_BF16)
     k_gfold_u<bf16><<<dim3(GF_HP, R), 192, 0, s>>>(D, H, R, (const bf16*)qg, ld_qg, (const bf16*)wkg, gidx,
                                                     ws, true);
   else if (dtype == RF_F16)
@@ -1483,10 +1485,20 @@ extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int
     k_gfold_u<float><<<dim3(H, R), 192, 0, s>>>(D, H, R, (const float*)qg, ld_qg, (const float*)wkg, gidx,
                                                  ws, false);
   const int rc =
-      fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, chr, out, ld_out, s, true,
-                       true, dr);
+      fold_partial_out(dtype, B, Lp, D, H, h, ldh, wvg, bvg, flags, gidx, gmax, ws, nch, chr, out, ld_out, s,
+                       (stage & 1) != 0, (stage & 2) != 0, dr);
   if (rc != RF_OK) return rc;
   RF_LAUNCH_CHECK("rf_global_attn_fold_fwd");
+}
+
+extern "C" int rf_global_attn_fold_fwd_drop(int dtype, int B, int Lp, int D, int H, const void* qg,
+                                            int ld_qg, const void* h, int ldh, const void* wkg,
+                                            const float* bkg, const void* wvg, const float* bvg,
+                                            const uint8_t* flags, const int32_t* gidx, int gmax,
+                                            void* workspace, void* out, int ld_out, float p_drop,
+                                            uint64_t seed, rf_stream_t stream) {
+  return rf_global_attn_fold_fwd_stage(3, dtype, B, Lp, D, H, qg, ld_qg, h, ldh, wkg, bkg, wvg, bvg, flags, gidx,
+                                       gmax, workspace, out, ld_out, p_drop, seed, stream);
 }
 
 extern "C" int rf_global_attn_fold_fwd(int dtype, int B, int Lp, int D, int H, const void* qg, int ld_qg,

@@ -651,12 +651,13 @@ def global_attention(qg, kg, vg, flags, gidx, B: int, Lp: int, H: int, out: torc
 
 
 def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: int, H: int,
-                          out: torch.Tensor, tag: Optional[str] = None, p_drop: float = 0.0, seed: int = 0,
-                          ws: Optional[torch.Tensor] = None):
+                          out: Optional[torch.Tensor], tag: Optional[str] = None, p_drop: float = 0.0, seed: int = 0,
+                          ws: Optional[torch.Tensor] = None, stage: int = 3):
     """Global query rows through the key/value-projection fold (rf_global_attn_fold_fwd_drop):
     overwrites ctx rows at the global positions; p_drop > 0: attention-probability dropout with
     the counter-hash mask of `seed` (16-bit dtypes). ws: the fold workspace to use (a training
-    forward keeps it for global_fold_bwd), else a fresh one."""
+    forward keeps it for global_fold_bwd), else a fresh one. stage 1 / 2 (rf_global_attn_fold_fwd_stage):
+    the pass over h only (out unused, may be None) / the merge and output only, on the same ws."""
     lib = _lib.load()
     gmax = gidx.shape[1]
     if gmax == 0:
@@ -671,13 +672,15 @@ def global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B: int, Lp: in
     for t in (wkg, wvg):
         if not t.is_contiguous() or t.dtype != h.dtype:
             raise ValueError("global_attention_fold: weights must be contiguous in the compute dtype")
+    if stage not in (1, 2, 3) or (out is None and stage != 1):
+        raise ValueError(f"global_attention_fold: stage {stage} with out {'None' if out is None else 'given'}")
+    ldo = _rowmajor(out, "out") if out is not None else D
     with _region(tag):
-        rc = lib.rf_global_attn_fold_fwd_drop(dtype_code(h.dtype), B, Lp, D, H, _p(qg), _rowmajor(qg, "qg"),
-                                              _p(h), _rowmajor(h, "h"), _p(wkg), _p(bkg), _p(wvg), _p(bvg),
-                                              _p(flags), _p(gidx.contiguous()), gmax, _p(ws), _p(out),
-                                              _rowmajor(out, "out"), float(p_drop), int(seed) & (2**64 - 1),
-                                              _stream(out))
-    check(rc, "rf_global_attn_fold_fwd_drop")
+        rc = lib.rf_global_attn_fold_fwd_stage(stage, dtype_code(h.dtype), B, Lp, D, H, _p(qg), _rowmajor(qg, "qg"),
+                                               _p(h), _rowmajor(h, "h"), _p(wkg), _p(bkg), _p(wvg), _p(bvg),
+                                               _p(flags), _p(gidx.contiguous()), gmax, _p(ws), _p(out), ldo,
+                                               float(p_drop), int(seed) & (2**64 - 1), _stream(h))
+    check(rc, "rf_global_attn_fold_fwd_stage")
     return out
 
 

@@ -106,6 +106,9 @@ DW_SIDE_STREAM = True
 # the global rows' attention backward (rf_global_fold_bwd_full + rf_global_query_bwd: launches of a few
 # hundred workgroups) on that side stream beside the local branch's backward (_Attention.backward)
 GLOBAL_BWD_SIDE = True
+# the training forward's global-row fold (query projection, u, the pass over h) on that side stream beside
+# the band attention, its merge + output after it (_Attention.forward, rf_global_attn_fold_fwd_stage)
+FOLD_SIDE_TRAIN = True
 # the attention's gradient of a layer's input added inside the q|k|v projection's dA GEMM (_GradMailbox)
 # instead of autograd's separate bf16 sum: -0.4% per captured C3 step (16.55 vs 16.62 ms, gpurun_out/r04r),
 # The round-4 suite fault with it on (an illegal address in the first training test after the graph tests,
@@ -114,11 +117,9 @@ GLOBAL_BWD_SIDE = True
 # (fixed in _zero_bias: nothing made during a capture is cached)
 GRAD_MAILBOX = True
 # the bias gradients' column sums on the weight-gradient side stream too: measured slower (captured C3
-# 16.48 vs 16.38 ms in one process, gpurun_out/r04s: that stream is the step's critical path), so off
+# 16.48 vs 16.38 ms in one process, gpurun_out/r04s: that stream is the step's critical path), so off;
+# for the q|k|v projection's sums alone also slower (15.87 vs 15.81 ms, gpurun_out/r05k)
 BIAS_GRAD_SIDE = False
-# ... but for the packed Linears (_GemmP: the q|k|v projection's column sums, 75 MB at C3) it is: there the
-# main stream's dA GEMM (N = 768, K = 2304) outlasts the side stream's dW + reduce
-GEMMP_BIAS_GRAD_SIDE = True
 _SIDE_STREAMS = {}
 
 
@@ -294,7 +295,7 @@ class _GemmP(torch.autograd.Function):
         da = None
         # the dW rows and db entries of the scaled outputs scaled inside the reduction kernels
         scl = (sc, s) if scaled else (0, 1.0)
-        side_b = (BIAS_GRAD_SIDE or GEMMP_BIAS_GRAD_SIDE) and ctx.needs_input_grad[1] and any(ctx.needs_input_grad[7:])
+        side_b = BIAS_GRAD_SIDE and ctx.needs_input_grad[1] and any(ctx.needs_input_grad[7:])
         join = (_dw_async(lambda: (_weight_grad(dc, a, scl).to(ctx.wdt), _bias_grad(dc, scl) if side_b else None),
                           dc) if any(ctx.needs_input_grad[7:]) else None)
         if ctx.needs_input_grad[0]:
@@ -871,12 +872,13 @@ class _Attention(torch.autograd.Function):
         ctx.masters = wkg_master is not None
         ctx.qin = wqg16 is not None
         ctx.q_scale = q_scale
-        if ctx.qin:
-            D0 = qkv.shape[1] // 3
+
+        def query_global():
             # the global rows of h (rf_gather_global_rows; an empty slot gathers a zero row, whose
             # qg no output reads)
             hg = ops.gather_global_rows(h, gidx, B, Lp)
-            qg = ops.gemm(hg, wqg16, bqg, ops.RF_EPI_BIAS, scale_cols=D0, col_scale=q_scale)
+            return ops.gemm(hg, wqg16, bqg, ops.RF_EPI_BIAS, scale_cols=qkv.shape[1] // 3, col_scale=q_scale)
+        if ctx.qin:
             ctx.qw = (wqg16, wqgT16)
         ctx.fold_ws = None  # the forward fold's workspace when the HIP global backward can use it
         D = qkv.shape[1] // 3
@@ -886,6 +888,31 @@ class _Attention(torch.autograd.Function):
         # the global rows' dropout scale (B, H, G, Lp) fp32 is regenerated in the backward from the
         # seed (ctx.gz_kind), not kept alive on ctx between forward and backward
         ctx.gz_kind = None
+        ws = (_fold_ws(h, B, Lp, H, G) if FOLD_SIDE_TRAIN and fold and G > 0 and q.dtype != torch.float32
+              and not (ctx.drop is not None and G > 32) else None)
+        if ws is not None:
+            # the fold's query projection, u and pass over h (stage 1: nothing the local attention reads or
+            # writes) on the side stream beside the band kernel; its merge and Wvg (stage 2) after it, into
+            # the global rows the band kernel wrote
+            def fold_stage1():
+                qg1 = query_global() if ctx.qin else qg
+                ops.global_attention_fold(qg1.contiguous(), h.contiguous(), wkg.contiguous(), bkg, wvg.contiguous(),
+                                          bvg, flags, gidx, B, Lp, H, None, p_drop=attn_p, seed=seed, ws=ws,
+                                          stage=1)
+                return qg1
+            join = _dw_async(fold_stage1, h)
+            out = ops.band_attention(q, k, v, flags, gidx, B, Lp, H, half_w, p_drop=attn_p, seed=seed)
+            qg = join()
+            ops.global_attention_fold(qg, h, wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H, out, p_drop=attn_p, seed=seed,
+                                      ws=ws, stage=2)
+            ctx.fold_ws = ws
+            ctx.gz_kind = "hip" if ctx.drop is not None else None
+            ctx.save_for_backward(qkv, qg, h, wkg, bkg, wvg, bvg, flags, gidx, out)
+            ctx.dims = (B, Lp, H, half_w)
+            ctx.grows = grows
+            return out
+        if ctx.qin:
+            qg = query_global()
         if ctx.drop is not None and q.dtype != torch.float32 and G > 32:
             # the band kernel's dropout form takes <= 32 global keys: recompute in fp32 (the
             # backward of this case is the fp32 recompute as well)
