@@ -68,6 +68,10 @@ enum Knob {
                         // 1 the 128x128 tile kernel, 2 the 256x128 one (captured C3: 17.77 / 18.20 vs
                         // 16.26 / 16.36 ms, r04z: the older tile kernels lose more than the idle CUs cost)
   KNOB_COLSUM_SLICES,   // column sums (bias gradients): row slices at most (0 = CS_SLICES; A/B of the slice count)
+  KNOB_GEMM_N192,       // EPI_NONE / EPI_BIAS / 16-bit EPI_BIAS_RESID GEMMs whose 256^2 grid leaves CUs idle: 1 the
+                        // four-wave kernel on 256 x 192 tiles when those fill one round; 0 (default): the captured
+                        // C3 step measured slower with it (16.01 vs 15.92 ms, gpurun_out/r05n): the narrower
+                        // tile issues 14 operand DMA pieces per 96 MFMAs instead of 16 per 128
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];

@@ -620,9 +620,17 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
         const float4 x = *reinterpret_cast<const float4*>(r + 4 * q);
         v[4 * q] += x.x; v[4 * q + 1] += x.y; v[4 * q + 2] += x.z; v[4 * q + 3] += x.w;
       }
-    } else if (ZV && NV == 8) {  // the caller's prefetched residual row segment
+    } else if (ZV && (NV == 8 || NV == 6)) {  // the caller's prefetched residual row segment
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += (float)zv[k];
+      for (int k = 0; k < NV; ++k) v[k] += (float)zv[k];
+    } else if (NV == 6) {  // 4-B aligned: three 2-element loads
+      const E* r = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const typename H16<E>::x2 x = *reinterpret_cast<const typename H16<E>::x2*>(r + 2 * q);
+        v[2 * q] += (float)x[0];
+        v[2 * q + 1] += (float)x[1];
+      }
     } else {
       const E* r = reinterpret_cast<const E*>(e.R) + (int64_t)row * e.ldr + c0;
 #pragma unroll
@@ -673,6 +681,19 @@ __device__ __forceinline__ void epi_seg(const EpiArgs& e, int row, int c0, float
 #else
       *reinterpret_cast<typename H16<E>::x8*>(out) = x;
 #endif
+    } else if (NV == 6) {  // the 192-column tile's 6 columns: one 12-B store (4-B aligned)
+      // the fp32 value is rounded to 16 bits as a separate step, as in the 8-column forms: hipcc otherwise
+      // folds the bias FMA and the fp16 conversion into one v_fma_mix (one rounding instead of two: 1 ulp
+      // apart from the 256-column tile in ~2e-5 of the fp16 outputs)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(v[k]));
+      typename H16<E>::x8 x;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = (E)(k < 6 ? v[k < 6 ? k : 0] : 0.f);
+      typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+      typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
+      const u32x4_t w = __builtin_bit_cast(u32x4_t, x);
+      __builtin_nontemporal_store(u32x3_t{w[0], w[1], w[2]}, reinterpret_cast<u32x3_t*>(out));
     } else {
       typename H16<E>::x4 x;
 #pragma unroll
@@ -1081,12 +1102,21 @@ constexpr int W4_CV = 2 * W4_BUF;            // column vectors [parity][3][1 KiB
 constexpr int W4_PF = W4_CV + 6 * 1024;     // L2-prefetch landing area, 256 B per wave (never read)
 constexpr int W4_LDS = W4_PF + 1024;
 
-template <typename E, int EPI, bool CF32, bool RF32, bool IL>
+// NJ = 16-column W fragments per wave: 8 = the 256 x 256 tile; 6 = a 256 x 192 tile (each wave 128 x 96,
+// W halves of 96 rows) for the N = 768 products at the training batch, whose 192 tiles of 256^2 leave a
+// quarter of the 256 CUs idle while 256 tiles of 256 x 192 fill them in one round (EPI_NONE / EPI_BIAS,
+// 16-bit C; a lane then owns 6 consecutive output columns: 12-B stores).
+template <typename E, int EPI, bool CF32, bool RF32, bool IL, int NJ = 8>
 __global__ void __launch_bounds__(256, 1)
     k_gemm_w4(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e,
               int nTm, int nTn) {
   typedef typename H16<E>::x8 V8;
   constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;
+  static_assert(NJ == 8 || (NJ == 6 && IL && !OUT32 && !RF32 &&
+                            (EPI == RF_EPI_NONE || EPI == RF_EPI_BIAS || EPI == RF_EPI_BIAS_RESID)),
+                "k_gemm_w4: the 192-column tile takes the 16-bit EPI_NONE / EPI_BIAS / EPI_BIAS_RESID forms only");
+  constexpr int TN = 32 * NJ;   // tile columns (256 or 192)
+  constexpr int NP = 8 + NJ;    // DMA pieces (and fragment reads) per wave and K-tile: 8 of A, NJ of W
   // epilogue stores per wave (interior tile); EPI_BIAS_GELU_AUX stores the pre-activation too
   constexpr int S = (OUT32 || EPI == RF_EPI_BIAS_GELU_AUX) ? 64 : 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1101,13 +1131,13 @@ __global__ void __launch_bounds__(256, 1)
     const int rem = wg - g * nTm * GN;
     const int tm = rem / gw;
     om0 = tm * 256;
-    on0 = (g * GN + rem - tm * gw) * 256;
+    on0 = (g * GN + rem - tm * gw) * TN;
   };
   int m0, n0, nm0 = 0, nn0 = 0;
   tile_origin(v, m0, n0);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 1, wc = wave & 1;  // A half (rows 128 wr..) and W half (columns 128 wc..)
+  const int wr = wave >> 1, wc = wave & 1;  // A half (rows 128 wr..) and W half (columns 16 NJ wc..)
   const int nk = K >> 6;
   // Operand DMA through buffer resources (buffer_load ... lds): rows past M / N read as zeros
   // (num_records), the per-piece row step and the K-tile offset are scalars (soffset), so a piece
@@ -1122,7 +1152,10 @@ __global__ void __launch_bounds__(256, 1)
   const int half = wave >> 1;
   const int pch = ((lane & 7) ^ (lane >> 3)) * 8;                      // element offset of the chunk
   const int arow_l = half * 128 + (wave & 1) * 64 + (lane >> 3);      // + 8p
-  const int wrow_l = half * 128 + (OUT32 ? 64 * (wave & 1) + 4 * (lane >> 3) : 8 * (lane >> 3) + 4 * (wave & 1));
+  // NJ = 6: W-half rows 48 (w&1) + 8 p + r of the LDS image hold fragment j = 3 (w&1) + (p>>1), column c =
+  // 8 (p&1) + r, i.e. W row 6 c + j = 48 (p&1) + 6 r + 3 (w&1) + (p>>1) of the 96-row half
+  const int wrow_l = NJ == 6 ? half * 96 + 6 * (lane >> 3) + 3 * (wave & 1)
+                             : half * 128 + (OUT32 ? 64 * (wave & 1) + 4 * (lane >> 3) : 8 * (lane >> 3) + 4 * (wave & 1));
   auto voffA = [&](int bm0) { return ((bm0 + arow_l) * lda + pch) * 2; };
   auto voffW = [&](int bn0) { return ((bn0 + wrow_l) * ldw + pch) * 2; };
   int vA = voffA(m0), vW = voffW(n0), vAn = vA, vWn = vW;
@@ -1131,7 +1164,7 @@ __global__ void __launch_bounds__(256, 1)
   // pp = 0,2,4,6,1,3,5,7, i.e. rows +0..3 then +64..67 (+32..35 fp32 out): +1 row, +61 (+29) once).
   // Three row-step scalars stay live instead of 14 loop-invariant products, which hipcc spilled to
   // VGPR lanes and reloaded with v_readlane inside phase B (one per piece).
-  const int stA = 8 * lda * 2, stW1 = ldw * 2, stWj = (OUT32 ? 29 : 61) * ldw * 2;
+  const int stA = 8 * lda * 2, stW1 = ldw * 2, stWj = (NJ == 6 ? 46 : OUT32 ? 29 : 61) * ldw * 2;
   int sA = 0, sW = 0;
   // piece p (0-7 A, 8-15 W) of virtual K-tile kv (>= nk: the next tile's K-tile kv - nk) into buffer
   // buf; pieces 0 and 8 start their chain, so every K-tile issues p = 0..7 and 8..15 in order
@@ -1142,14 +1175,15 @@ __global__ void __launch_bounds__(256, 1)
     const bool nxt = kv >= nk;
     const int kt = nxt ? kv - nk : kv;
     const bool isA = p < 8;
-    const int q = p & 7;
-    const int pp = isA ? q : (q < 4 ? 2 * q : 2 * (q - 4) + 1);
-    char* dst = smem + buf * W4_BUF + (isA ? half : 2 + half) * PP_HALF + ((wave & 1) * 64 + 8 * pp) * 128;
+    const int q = isA ? p : p - 8;
+    const int pp = isA ? q : (q < NJ / 2 ? 2 * q : 2 * (q - NJ / 2) + 1);
+    char* dst = smem + buf * W4_BUF + (isA ? half : 2 + half) * PP_HALF +
+                ((wave & 1) * (isA ? 64 : 8 * NJ) + 8 * pp) * 128;
     if (p == 0) { sA = kt * 128; asm volatile("" : "+s"(sA)); }
     if (p == 8) { sW = kt * 128; asm volatile("" : "+s"(sW)); }
     const int soff = isA ? sA : sW;
     {
-      int st = isA ? stA : (q == 3 ? stWj : stW1);
+      int st = isA ? stA : (q == NJ / 2 - 1 ? stWj : stW1);
       asm volatile("" : "+s"(st));  // no hoisting of per-piece products out of the K-loop
       if (isA) sA += st; else sW += st;
     }
@@ -1183,14 +1217,14 @@ __global__ void __launch_bounds__(256, 1)
   const int off0 = lr * 128 + (((lane >> 4) ^ (lane & 7)) << 4);
   const int off1 = lr * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
   const int aOff = wr * PP_HALF, bOff = (2 + wc) * PP_HALF;
-  V8 a0[8], b0[8], a1[8], b1[8];
-  f32x4 acc[8][8];
-  auto read0 = [&](int buf, int idx) {  // ks = 0 fragment idx (0-7 A, 8-15 W)
+  V8 a0[8], b0[NJ], a1[8], b1[NJ];
+  f32x4 acc[8][NJ];
+  auto read0 = [&](int buf, int idx) {  // ks = 0 fragment idx (0-7 A, 8..8+NJ-1 W)
 #if defined(RF_W4_DIAG) && (RF_W4_DIAG & 4)  // timing diagnostic: no LDS operand reads
     if (idx < 8) asm volatile("" : "=v"(a0[idx])); else asm volatile("" : "=v"(b0[idx - 8]));
     return;
 #endif
-    const char* base = smem + buf * W4_BUF + (idx < 8 ? aOff : bOff) + (idx & 7) * 16 * 128 + off0;
+    const char* base = smem + buf * W4_BUF + (idx < 8 ? aOff : bOff) + (idx < 8 ? idx : idx - 8) * 16 * 128 + off0;
     if (idx < 8) a0[idx] = *reinterpret_cast<const V8*>(base);
     else b0[idx - 8] = *reinterpret_cast<const V8*>(base);
   };
@@ -1199,7 +1233,7 @@ __global__ void __launch_bounds__(256, 1)
     if (idx < 8) asm volatile("" : "=v"(a1[idx])); else asm volatile("" : "=v"(b1[idx - 8]));
     return;
 #endif
-    const char* base = smem + buf * W4_BUF + (idx < 8 ? aOff : bOff) + (idx & 7) * 16 * 128 + off1;
+    const char* base = smem + buf * W4_BUF + (idx < 8 ? aOff : bOff) + (idx < 8 ? idx : idx - 8) * 16 * 128 + off1;
     if (idx < 8) a1[idx] = *reinterpret_cast<const V8*>(base);
     else b1[idx - 8] = *reinterpret_cast<const V8*>(base);
   };
@@ -1228,13 +1262,13 @@ __global__ void __launch_bounds__(256, 1)
   // prologue: K-tiles 0, 1 of the first tile, its column vectors
   dma_cols(m0, n0, 0);
 #pragma unroll
-  for (int p = 0; p < 16; ++p) dma_piece(0, 0, p);
+  for (int p = 0; p < NP; ++p) dma_piece(0, 0, p);
 #pragma unroll
-  for (int p = 0; p < 16; ++p) dma_piece(1, 1, p);
-  wait_vmcnt<16>();
+  for (int p = 0; p < NP; ++p) dma_piece(1, 1, p);
+  wait_vmcnt<NP>();
   bar();
 #pragma unroll
-  for (int i = 0; i < 16; ++i) read0(0, i);
+  for (int i = 0; i < NP; ++i) read0(0, i);
   int kb = 0;      // LDS buffer of the current K-tile (running parity across tiles)
   int tix = 0;     // tile counter (column-vector parity)
   int relax = 0;   // epilogue stores of the previous (interior) tile still counted in vmcnt
@@ -1252,16 +1286,25 @@ __global__ void __launch_bounds__(256, 1)
     auto phaseA = [&](auto zero) {
       // W fragments first: phase B's MFMA order (i outer, j inner) needs all of b1 and a1[0] first
 #pragma unroll
-      for (int i = 0; i < 16; ++i) read1(kb, (i + 8) & 15);
+      for (int i = 0; i < NP; ++i) read1(kb, i < NJ ? 8 + i : i - NJ);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = mfma16(a0[i], b0[j], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j]);
+      if constexpr (NJ == 8) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        for (int g = 0; g < 16; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < NP; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // 3 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8 * NJ - 3 * NP, 0);
       }
     };
     // ---- mid-sync: this wave's reads of buffer kb done; K-tile t+1 (buffer kb^1) landed ----
@@ -1283,9 +1326,9 @@ __global__ void __launch_bounds__(256, 1)
     auto phaseB = [&](int t) {
       if (IL) {
 #pragma unroll
-        for (int p = 0; p < 16; ++p) {
+        for (int p = 0; p < NP; ++p) {
           dma_piece(t + 2, kb, p);
-          read0(kb ^ 1, (p + 8) & 15);  // b0 first (phase A's MFMA order)
+          read0(kb ^ 1, p < NJ ? 8 + p : p - NJ);  // b0 first (phase A's MFMA order)
         }
       } else {
 #pragma unroll
@@ -1298,8 +1341,8 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
-      if (IL) {
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+      if (IL && NJ == 8) {
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
           __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
@@ -1307,6 +1350,16 @@ __global__ void __launch_bounds__(256, 1)
           __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
         }
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+      } else if (IL) {
+#pragma unroll
+        for (int g = 0; g < NP; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 DMA piece
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8 * NJ - 3 * NP, 0);
         __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
       } else {
 #pragma unroll
@@ -1349,16 +1402,25 @@ __global__ void __launch_bounds__(256, 1)
     }
     // epilogue straight from the accumulators (as k_gemm_pp): lane (c = l&15, g = l>>4) holds rows
     // 4g + r of each 16-row block i and the columns [8c, 8c+8) (16-bit) / [4c, 4c+4) u [64+4c, ..)
-    const bool interior = (m0 + 256 <= e.M) && (n0 + 256 <= e.N);
+    const bool interior = (m0 + 256 <= e.M) && (n0 + TN <= e.N);
     int el = lane;
     asm volatile("" : "+v"(el));
     const int erow = m0 + wr * 128 + 4 * (el >> 4);
-    const int ecol = n0 + wc * 128 + (OUT32 ? 4 : 8) * (el & 15);
+    const int ecol = n0 + wc * (16 * NJ) + (OUT32 ? 4 : NJ) * (el & 15);
     float bv[8], gm[8], bt[8];
     const float* cb = reinterpret_cast<const float*>(smem + W4_CV + (tix & 1) * 3 * 1024);
     {
       const int co = ecol - n0;
-      if (OUT32) {
+      if (NJ == 6) {  // 6 columns at a 24-B offset: 8-B reads
+#pragma unroll
+        for (int k = 0; k < 8; ++k) bv[k] = gm[k] = bt[k] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; k += 2) {
+          const f32x2 b = *reinterpret_cast<const f32x2*>(cb + co + k);
+          bv[k] = b[0];
+          bv[k + 1] = b[1];
+        }
+      } else if (OUT32) {
         lds_cols<EPI, 4>(cb, co, bv, gm, bt);
         lds_cols<EPI, 4>(cb, co + 64, bv + 4, gm + 4, bt + 4);
       } else {
@@ -1389,7 +1451,15 @@ __global__ void __launch_bounds__(256, 1)
         const char* zbase = reinterpret_cast<const char*>(e.R) + (int64_t)em0 * e.ldr * (int)sizeof(E);
         auto zload = [&](int k) {
           const int row = erow + (k >> 2) * 16 + (k & 3);
-          return *reinterpret_cast<const V8*>(zbase + (uint32_t)(((row - em0) * e.ldr + ecol) * (int)sizeof(E)));
+          const char* zp = zbase + (uint32_t)(((row - em0) * e.ldr + ecol) * (int)sizeof(E));
+          if constexpr (NJ == 6) {  // the lane's 6 columns: one 12-B load
+            typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+            typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
+            const u32x3_t w = *reinterpret_cast<const u32x3_t*>(zp);
+            return __builtin_bit_cast(V8, u32x4_t{w[0], w[1], w[2], 0u});
+          } else {
+            return *reinterpret_cast<const V8*>(zp);
+          }
         };
         V8 zv[ZD];
 #pragma unroll
@@ -1401,9 +1471,9 @@ __global__ void __launch_bounds__(256, 1)
           if (k + ZD < 32) zv[k % ZD] = zload(k + ZD);
           float vv[8];
 #pragma unroll
-          for (int f = 0; f < 8; ++f) vv[f] = acc[i][f][r];
-          epi_seg<E, EPI, CF32, RF32, 8, CK, true, FSC, true>(e, erow + i * 16 + r, ecol, vv, bv, gm, bt, 0.f, tbase,
-                                                              em0, csc, z);
+          for (int f = 0; f < 8; ++f) vv[f] = f < NJ ? acc[i][f < NJ ? f : 0][r] : 0.f;
+          epi_seg<E, EPI, CF32, RF32, NJ == 6 ? 6 : 8, CK, true, FSC, true>(e, erow + i * 16 + r, ecol, vv, bv, gm, bt,
+                                                                           0.f, tbase, em0, csc, z);
         }
       } else {
 #pragma unroll
@@ -1412,10 +1482,12 @@ __global__ void __launch_bounds__(256, 1)
           for (int r = 0; r < 4; ++r) {
             float vv[8];
 #pragma unroll
-            for (int f = 0; f < 8; ++f) vv[f] = acc[i][f][r];
+            for (int f = 0; f < 8; ++f) vv[f] = f < NJ ? acc[i][f < NJ ? f : 0][r] : 0.f;
             const int row = erow + i * 16 + r;
             const float rsc = EPI == RF_EPI_COS ? cb[256 + row - em0] : 0.f;
-            if (OUT32) {
+            if (NJ == 6) {
+              epi_seg<E, EPI, CF32, RF32, 6, CK, !CK, FSC>(e, row, ecol, vv, bv, gm, bt, rsc, tbase, em0, csc);
+            } else if (OUT32) {
               epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
               epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
             } else {
@@ -1443,18 +1515,19 @@ __global__ void __launch_bounds__(256, 1)
   wait_vmcnt<0>();
 }
 
-template <typename E, int EPI, bool CF32, bool RF32, bool IL>
+template <typename E, int EPI, bool CF32, bool RF32, bool IL, int NJ = 8>
 static void launch_w4(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
                       hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_w4<E, EPI, CF32, RF32, IL>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_w4<E, EPI, CF32, RF32, IL, NJ>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)W4_LDS);
     attr_set = true;
   }
-  const int nTm = (M + 255) / 256, nTn = (N + 255) / 256;
+  const int nTm = (M + 255) / 256, nTn = (N + 32 * NJ - 1) / (32 * NJ);
   const int grid = min(nTm * nTn, num_cus());
-  k_gemm_w4<E, EPI, CF32, RF32, IL><<<grid, 256, W4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
+  k_gemm_w4<E, EPI, CF32, RF32, IL, NJ><<<grid, 256, W4_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm,
+                                                                   nTn);
 }
 
 
@@ -2020,6 +2093,16 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
           return;
         }
         launch_bf16<E, 256, 128, 64, 64, 64, 2, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);
+        return;
+      }
+    }
+    if constexpr (!CF32 && !RF32 && (EPI == RF_EPI_NONE || EPI == RF_EPI_BIAS || EPI == RF_EPI_BIAS_RESID)) {
+      // 256 x 192 tiles when the 256^2 grid leaves CUs idle and the 192-wide one fills at most one round
+      // (the N = 768 products at the training batch: 192 -> 256 tiles at 16k rows)
+      const long tiles192 = (long)((M + 255) / 256) * ((N + 191) / 192);
+      if (w4_ok && g_knob[KNOB_GEMM_N192] && tiles256 < num_cus() && tiles192 > tiles256 && tiles192 <= num_cus() &&
+          e.scale_cols % 192 == 0 && !g_knob[KNOB_GEMM_MFMA32]) {
+        launch_w4<E, EPI, false, false, true, 6>(M, N, K, A, lda, W, ldw, e, s);
         return;
       }
     }

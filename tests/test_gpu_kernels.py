@@ -956,6 +956,7 @@ def test_gemm_four_wave_kernels_all_epilogues(dev, mfma32, dt, M, N, K):
     output, cosine scores), including ragged M / N edges (4100 x 2312), against fp32 torch on the
     same 16-bit operands."""
     old = _lib.set_knob("gemm_mfma32", mfma32)
+    old192 = _lib.set_knob("gemm_n192", 0)  # the 256 x 256 tiles here (the 192-column one: its own test)
     try:
         a = _rand((M, K), dev, dt, 0.5, seed=91)
         w = _rand((N, K), dev, dt, 0.05, seed=92)
@@ -992,6 +993,51 @@ def test_gemm_four_wave_kernels_all_epilogues(dev, mfma32, dt, M, N, K):
         assert float((cs - ref).abs().max()) <= 2e-2
     finally:
         _lib.set_knob("gemm_mfma32", old)
+        _lib.set_knob("gemm_n192", old192)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (16384, 768, 3072), (16347, 760, 768), (10000, 1000, 1024)])
+def test_gemm_192_column_tiles(dev, dt, M, N, K):
+    """The four-wave kernel on 256 x 192 tiles (knob gemm_n192, off by default: the N = 768 products at the training
+    batch, 256 tiles instead of 192 of 256^2) computes every output element with the same MFMA sequence
+    as the 256 x 256 tile: bit-identical to it for EPI_NONE, EPI_BIAS and the 16-bit-residual
+    EPI_BIAS_RESID in bf16 (fp16 with a bias: within 1 ulp, see below), ragged M / N edges included,
+    and within the 16-bit tolerance of fp32 torch. The profiler shows which kernel ran."""
+    from torch.profiler import ProfilerActivity, profile
+    a = _rand((M, K), dev, dt, 0.5, seed=71)
+    w = _rand((N, K), dev, dt, 0.05, seed=72)
+    b = _rand((N,), dev, torch.float32, seed=73)
+    r = _rand((M, N), dev, dt, 1.0, seed=74)  # a 16-bit residual (the training dA GEMM's mailbox form)
+    res = {}
+    old = _lib.set_knob("gemm_n192", 0)
+    try:
+        for knob in (0, 1):
+            _lib.set_knob("gemm_n192", knob)
+            with profile(activities=[ProfilerActivity.CUDA]) as prof:
+                res[knob] = (ops.gemm(a, w, None, ops.RF_EPI_NONE), ops.gemm(a, w, b, ops.RF_EPI_BIAS),
+                             ops.gemm(a, w, b, ops.RF_EPI_BIAS_RESID, resid=r))
+                torch.cuda.synchronize()
+            names = [e.name for e in prof.events() if "k_gemm_w4" in e.name]
+            if names:  # the 192-column instantiation carries NJ = 6 in its mangled name
+                assert any("Li6EEEvi" in n for n in names) == (knob == 1), names
+    finally:
+        _lib.set_knob("gemm_n192", old)
+    for n, (x, y) in enumerate(zip(res[0], res[1])):
+        if dt == torch.bfloat16 or n == 0:
+            assert torch.equal(x, y)
+        else:
+            # fp16 with a bias: the 256-column kernel's fp32 bias add and fp16 rounding are partly fused
+            # by hipcc into one v_fma_mix (one rounding), the 192-column kernel rounds twice (fp32, then
+            # fp16) like the other epilogues: at most 1 ulp apart, in ~1e-5 of the outputs
+            d = (x.float() - y.float()).abs()
+            ulp = torch.finfo(torch.float16).eps * torch.maximum(x.float().abs(), y.float().abs())
+            assert bool((d <= ulp).all()), float((d / ulp.clamp_min(1e-30)).max())
+            assert int((x != y).sum()) <= 1e-4 * x.numel()
+    prod = a.float() @ w.float().t()
+    tol = 4e-3 if dt == torch.float16 else 2e-2
+    for x, ref in zip(res[1], (prod, prod + b, prod + b + r.float())):
+        assert float((x.float() - ref).abs().max()) <= tol * max(1.0, float(ref.abs().max()))
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
