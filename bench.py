@@ -172,6 +172,21 @@ def _thread_counts(spec):
     return out, avail
 
 
+def _cpu_calibration():
+    """The newest committed calibration of the restatement against the real reference (within
+    ±15%; oracle/calibrate_cpu.py, run in the build container, where the reference exists), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "cpu_calibration.json")), reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+            return {"port_over_reference": doc["port_over_reference"], "within_15pct": doc["within_15pct"],
+                    "threads": doc["threads"], "file": os.path.relpath(path, ROOT)}
+        except (OSError, ValueError, KeyError):
+            continue
+    return None
+
+
 def cpu_baseline(sd_cpu, cfg, items_cpu, L, target_s, spec):
     """Time the CPU restatement of the reference (oracle/restatement.py: fp32, the reference's
     algorithm incl. broadcast cosine scoring) on a bounded sample of the same workload, at each
@@ -219,6 +234,7 @@ def cpu_baseline(sd_cpu, cfg, items_cpu, L, target_s, spec):
         samples[T] = n
     best = max(by, key=by.get)
     return {"value": by[best], "unit": "user-seq/s", "cores": best, "kind": "port",
+            "calibration": _cpu_calibration(),
             "by_threads": {str(t): round(v, 3) for t, v in by.items()}, "skipped_threads": skipped,
             "sample": f"{samples[best]} sequences x L={L} (B=1 each) encode+score vs {items_cpu.shape[0]} items, "
                       f"fp32 oracle/restatement.py, {best} threads (fastest of {counts}) on {_cpu_model_name()} "
