@@ -570,11 +570,29 @@ __global__ void __launch_bounds__(256) k_rank_reduce(int B, int ntiles, const in
   const int row = blockIdx.x * 16 + rl;
   int c = 0;
   float e = 0.f;
-  if (row < B)
-    for (int t = grp; t < ntiles; t += 16) {
+  if (row < B) {
+    // 8 tiles' loads in flight per thread (the sums keep the tile order: the same result as one at a
+    // time, which waited a memory round trip per tile: 111 us at 1M items x 4096 queries)
+    int t = grp;
+    for (; t + 7 * 16 < ntiles; t += 8 * 16) {
+      int ci[8];
+      float ei[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        ci[u] = part_cnt[(int64_t)(t + 16 * u) * B + row];
+        ei[u] = part_sexp[(int64_t)(t + 16 * u) * B + row];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        c += ci[u];
+        e += ei[u];
+      }
+    }
+    for (; t < ntiles; t += 16) {
       c += part_cnt[(int64_t)t * B + row];
       e += part_sexp[(int64_t)t * B + row];
     }
+  }
   sc[rl][grp] = c;
   ss[rl][grp] = e;
   __syncthreads();

@@ -257,6 +257,9 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
                                          ops._stream(q)), "rf_topk_merge")
             topv, topi = mv, mi
             tn += lib.rf_score_rank_tiles(n)
+        # the per-row counts are complete: reduce them before the host reads the overflow flags, so the
+        # GPU has that work queued while the host waits (nothing is left to launch after the read)
+        counts = _rank_reduce(lib, B, ntiles, part_cnt, part_sexp, dev, q)
         if plan:
             rows = torch.nonzero(over).flatten()
             if rows.numel():  # many near-equal scores overflowed the lists: exact dense re-rank
@@ -269,12 +272,19 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
                 topi = topi.index_copy(0, rows, fi)
     else:
         _score_rank(q, qn, shard, s_label, inv_t, 2, 0, N, part_cnt, part_sexp, 0, max_val=max_val)
+        counts = _rank_reduce(lib, B, ntiles, part_cnt, part_sexp, dev, q)
+    gt, valid, sexp = counts
+    return {"gt": gt, "valid": valid, "sexp": sexp, "topv": topv, "topi": topi, "shift": inv_t}
+
+
+def _rank_reduce(lib, B: int, ntiles: int, part_cnt, part_sexp, dev, q):
+    """rf_rank_reduce: the per-tile partials summed per row in tile order -> (gt, valid, sexp)."""
     gt = torch.empty(B, dtype=torch.int32, device=dev)
     valid = torch.empty(B, dtype=torch.int32, device=dev)
     sexp = torch.empty(B, dtype=torch.float32, device=dev)
     _lib.check(lib.rf_rank_reduce(B, ntiles, part_cnt.data_ptr(), part_sexp.data_ptr(), gt.data_ptr(),
                                   valid.data_ptr(), sexp.data_ptr(), ops._stream(q)), "rf_rank_reduce")
-    return {"gt": gt, "valid": valid, "sexp": sexp, "topv": topv, "topi": topi, "shift": inv_t}
+    return gt, valid, sexp
 
 
 def merge_topk(vals: torch.Tensor, ids: torch.Tensor, k: int):
