@@ -72,6 +72,8 @@ enum Knob {
                         // four-wave kernel on 256 x 192 tiles when those fill one round; 0 (default): the captured
                         // C3 step measured slower with it (16.01 vs 15.92 ms, gpurun_out/r05n): the narrower
                         // tile issues 14 operand DMA pieces per 96 MFMAs instead of 16 per 128
+  KNOB_ADAM_NT,         // AdamW: non-temporal operand loads / stores (1, default: captured C3 16.03 vs 16.07 ms,
+                        // gpurun_out/r05q) or plain (0)
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];

@@ -31,6 +31,7 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 
 // grad_scale / found_inf: device scalars of a gradient scaler (NULL: none). A step with an inf/NaN
 // gradient (found_inf != 0) writes nothing — every workgroup returns before its first load.
+template <bool NT>
 __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict__ descs,
                                                const int32_t* __restrict__ block_tensor,
                                                const float* __restrict__ grad_scale,
@@ -59,13 +60,26 @@ __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict
   if (vec && n == ADAM_CHUNK) {
     // all loads of the thread's 8 float4 groups issued before the arithmetic
     float4 p[8], g[8], m[8], v[8];
+    // NT: every operand is touched once per step: non-temporal loads and stores (no cache allocation)
+    auto ld = [](const float* a) {
+      if constexpr (NT) {
+        const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a));
+        return make_float4(x[0], x[1], x[2], x[3]);
+      } else {
+        return *reinterpret_cast<const float4*>(a);
+      }
+    };
+    auto st = [](float* a, float4 x) {
+      if constexpr (NT) __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w}, reinterpret_cast<f32x4*>(a));
+      else *reinterpret_cast<float4*>(a) = x;
+    };
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int o = 4 * (threadIdx.x + 256 * i);
-      p[i] = *reinterpret_cast<const float4*>(P + o);
-      g[i] = *reinterpret_cast<const float4*>(G + o);
-      m[i] = *reinterpret_cast<const float4*>(Mm + o);
-      v[i] = *reinterpret_cast<const float4*>(Vv + o);
+      p[i] = ld(P + o);
+      g[i] = ld(G + o);
+      m[i] = ld(Mm + o);
+      v[i] = ld(Vv + o);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -74,9 +88,9 @@ __global__ void __launch_bounds__(256) k_adamw(const rf_adamw_tensor* __restrict
       adam_elem(p[i].z, g[i].z, m[i].z, v[i].z, d, decay, step_size, bc2_sqrt, inv_scale);
       adam_elem(p[i].w, g[i].w, m[i].w, v[i].w, d, decay, step_size, bc2_sqrt, inv_scale);
       const int o = 4 * (threadIdx.x + 256 * i);
-      *reinterpret_cast<float4*>(P + o) = p[i];
-      *reinterpret_cast<float4*>(Mm + o) = m[i];
-      *reinterpret_cast<float4*>(Vv + o) = v[i];
+      st(P + o, p[i]);
+      st(Mm + o, m[i]);
+      st(Vv + o, v[i]);
     }
   } else {
     for (int64_t i = threadIdx.x; i < n; i += 256) {
@@ -100,7 +114,8 @@ extern "C" int rf_adamw_step_amp(const rf_adamw_tensor* tensors, int ntensors, c
   RF_REQUIRE(ntensors >= 0 && nblocks >= 0, "rf_adamw_step: bad counts %d %d", ntensors, nblocks);
   if (nblocks == 0) return RF_OK;
   RF_REQUIRE(tensors && block_tensor, "rf_adamw_step: null pointer");
-  k_adamw<<<nblocks, 256, 0, as_stream(stream)>>>(tensors, block_tensor, grad_scale, found_inf);
+  if (g_knob[KNOB_ADAM_NT]) k_adamw<true><<<nblocks, 256, 0, as_stream(stream)>>>(tensors, block_tensor, grad_scale, found_inf);
+  else k_adamw<false><<<nblocks, 256, 0, as_stream(stream)>>>(tensors, block_tensor, grad_scale, found_inf);
   RF_LAUNCH_CHECK("rf_adamw_step");
 }
 
