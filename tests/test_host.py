@@ -210,3 +210,20 @@ def test_inputs_embeds_table_and_head_mask_host_logic():
         c, _ = R.model_forward(lf.state_dict(), lf.config, **batch_of(g), head_mask=hz)
     assert torch.equal(a, b)
     assert not torch.allclose(a, c)
+
+
+def test_bench_accounting_of_the_step_as_run():
+    """bench.py's algorithmic work per sequence (SURVEY §8d counting) for C2: 176.5 GFLOP with every row
+    through the last layer (70.6 us at 2.5 PF dense bf16), 161.8 GFLOP for the CLS-only last layer the
+    step runs (64.7 us) — the floors e2e_roofline and model_tflops use; and the CPU baseline carries the
+    committed calibration of the restatement against the real reference (within +-15%)."""
+    import bench
+    full = bench.step_flops_per_seq(1024, 768, 3072, 12, 10000, cls_last=False)
+    pruned = bench.step_flops_per_seq(1024, 768, 3072, 12, 10000, cls_last=True)
+    assert abs(full["total"] / 1e9 - 176.5) < 0.1 and abs(pruned["total"] / 1e9 - 161.8) < 0.1
+    assert pruned["score"] == full["score"] == 2 * 10000 * 768
+    assert abs(bench.e2e_floor_us(1024, 768, 3072, 12, 10000, cls_last=False) - 70.6) < 0.05
+    assert abs(bench.e2e_floor_us(1024, 768, 3072, 12, 10000, cls_last=True) - 64.72) < 0.05
+    cal = bench._cpu_calibration()
+    assert cal is not None and cal["within_15pct"] and 0.85 <= cal["port_over_reference"] <= 1.15
+    assert os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), cal["file"]))
