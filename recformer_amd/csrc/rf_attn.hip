@@ -1702,7 +1702,9 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
                                                               (E*)out, ld_out, dr);                        \
     }                                                                                                     \
   } while (0)
-        // pipe3 (three workgroups per CU) unless the knob asks for pipe2 (A/B tools: band_path 0)
+        // pipe3 (three workgroups per CU; bit-identical to pipe2) only when the knob asks for it (band_path 3):
+        // 83.0 vs 85.8 us per launch, but step-neutral in same-process C2 A/Bs (round 4; round 5: -0.2%,
+        // +0.4%, +0.3%, gpurun_out/r05t, r05v) — the GEMM after it runs slower
         const bool band_pipe3 = g_knob[KNOB_BAND_PATH] == 3;
         const size_t lds3 = AQ_MK + (size_t)(qpb + 1) * 16;
         // training (dropout) keeps pipe2: pipe3's dropout form would spill at the 3-wave register budget
