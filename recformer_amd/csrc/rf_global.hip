@@ -35,6 +35,17 @@ constexpr bool RF_GF_DIAG_PH = (RF_GF_DIAG & 4) != 0;  // no P.H products
 #else
 constexpr bool RF_GF_DIAG_SC = false, RF_GF_DIAG_PH = false;
 #endif    // rows per chunk of the fp32 VALU kernel
+// RF_GF_STAMPS (tools/build_variant.sh only, inference): k_gfold_partial_bf16's wave 0 records
+// s_memrealtime (100 MHz) at 16 points into free LDS and copies them to the (unused without dropout)
+// ws.ld slots of its (row, chunk) — tools/gfold_stamps.py reads the timeline.
+#if defined(RF_GF_STAMPS)
+#define GF_STAMP(k)                                                                                   \
+  do {                                                                                                \
+    if (threadIdx.x == 0) gf_lds_st32(red + GF_RED_LD + (k), __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_s_memrealtime())); \
+  } while (0)
+#else
+#define GF_STAMP(k) do { } while (0)
+#endif
 constexpr int GF_HP = 16;     // heads padded to one MFMA column tile (H <= 16)
 constexpr int GF_RED_LD = 176;  // partial kernels' LDS reduction area: dropped sums at red + 176
 constexpr int GF_RED_FLOATS = GF_RED_LD + 64;
@@ -120,6 +131,11 @@ __device__ __forceinline__ void tr_wait() {
 // 16-bit plane type of the u planes for an element type (fp32 mode writes none)
 template <typename T> struct Plane16 { typedef T type; };
 template <> struct Plane16<float> { typedef bf16 type; };
+
+__device__ __forceinline__ void gf_lds_st32(const void* p, float v) {  // LDS store invisible to hipcc's waits
+  asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p),
+               "v"(v) : "memory");
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vm_n() {
@@ -493,14 +509,15 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
   constexpr int PPW = hseg * 8 / 4;      // DMA pieces per wave per half
   if constexpr (nseg % 2 != 0) return;  // D not a multiple of 128: k_gfold_partial_bf16_1 instead
   const int ch = blockIdx.x, r = blockIdx.y, nch = gridDim.x;
+  char* pimg = smem + nseg * 64 * 128;                         // P [64 rows][16 heads] bf16
+  float* red = reinterpret_cast<float*>(pimg + 64 * 16 * 2);    // [max 4x16][sum 4x16][m 16][alpha 16]
+  GF_STAMP(0);
   if (gidx[r] < 0) return;
   const int b = r / gmax;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int q4 = li >> 2, p4 = li & 3;
-  char* pimg = smem + nseg * 64 * 128;                         // P [64 rows][16 heads] bf16
-  float* red = reinterpret_cast<float*>(pimg + 64 * 16 * 2);    // [max 4x16][sum 4x16][m 16][alpha 16]
   float* m_run = red + 128;
   float* alpha_s = red + 144;
   unsigned long long* vmask = reinterpret_cast<unsigned long long*>(red + 160);  // per sub-chunk
@@ -520,9 +537,20 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
              smem + (seg * 64 + (p & 7) * 8) * 128);
     }
   };
-  // u fragments (B operand of S^T = H.U^T): hi and lo planes; heads >= H score 0
-  V8 uh[NK], ul[NK];
-  {
+  // u (B operand of S^T = H.U^T, hi and lo planes; heads >= H score 0). D <= 768: u is DMA'd once per
+  // block into LDS in fragment order ([plane][k-step][lane] x 16 B, conflict-free ds_read_b128) with
+  // the first image, instead of every wave loading all of it into registers — 4x fewer u bytes (the
+  // register loads were 50 MB per C2 launch against the 25 MB first image, and the prologue waited
+  // 4.9 us for them before the image went out: s_memrealtime stamps, tools/gfold_stamps.py).
+#if defined(RF_GF_OLD_PROLOGUE)  // A/B builds only: the round-4 register-u prologue
+  constexpr bool ULDS = false;
+#else
+  constexpr bool ULDS = D <= 768;
+#endif
+  constexpr int UPW = 2 * NK / 4;  // u pieces per wave
+  char* uimg = reinterpret_cast<char*>(red + GF_RED_FLOATS);
+  V8 uh[ULDS ? 1 : NK], ul[ULDS ? 1 : NK];
+  if constexpr (!ULDS) {
     const E* uhi = reinterpret_cast<const E*>(ws.u16) + ((int64_t)r * 2 * GF_HP + li) * D + 8 * g;
     const E* ulo = uhi + (int64_t)GF_HP * D;
 #pragma unroll
@@ -530,17 +558,41 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
       uh[s2] = li < H ? *reinterpret_cast<const V8*>(uhi + 32 * s2) : V8{};
       ul[s2] = li < H ? *reinterpret_cast<const V8*>(ulo + 32 * s2) : V8{};
     }
+    if (wave < nsub) {  // validity ballots of the (up to 4) 64-row sub-chunks
+      const int jr = row_begin + 64 * wave + lane;
+      const bool ok = jr < Lp && flags[(int64_t)b * Lp + jr] != 0;
+      const unsigned long long m = __ballot(ok);
+      if (lane == 0) vmask[wave] = m;
+    }
+    if (threadIdx.x < 16) m_run[threadIdx.x] = GF_NEG_INF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // u fragments and flags, before the DMA stream
+    GF_STAMP(1);
+    dma_half(row_begin, 0);
+    dma_half(row_begin, 1);
+    GF_STAMP(2);
+  } else {
+    const int jf = row_begin + 64 * wave + lane;
+    int fv = (wave < nsub && jf < Lp) ? (int)flags[(int64_t)b * Lp + jf] : 0;
+    // piece (plane, k-step s2): lane (li, g) <- u[plane][head li][32 s2 + 8 g ..]; rows >= H read row
+    // H - 1 (finite; those score columns are never used)
+    const E* ub = reinterpret_cast<const E*>(ws.u16) + ((int64_t)r * 2 * GF_HP + min(li, H - 1)) * D + 8 * g;
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) {
+      const int pc = wave * UPW + i, plane = pc / NK, s2 = pc % NK;
+      glds16(ub + (int64_t)plane * GF_HP * D + 32 * s2, uimg + pc * 1024);
+    }
+    dma_half(row_begin, 0);
+    dma_half(row_begin, 1);
+    GF_STAMP(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // u, the first image and the flags landed
+    asm volatile("" : "+v"(fv));
+    if (wave < nsub) {
+      const unsigned long long m = __ballot(fv != 0);
+      if (lane == 0) vmask[wave] = m;
+    }
+    if (threadIdx.x < 16) m_run[threadIdx.x] = GF_NEG_INF;
+    GF_STAMP(2);
   }
-  if (wave < nsub) {  // validity ballots of the (up to 4) 64-row sub-chunks
-    const int jr = row_begin + 64 * wave + lane;
-    const bool ok = jr < Lp && flags[(int64_t)b * Lp + jr] != 0;
-    const unsigned long long m = __ballot(ok);
-    if (lane == 0) vmask[wave] = m;
-  }
-  if (threadIdx.x < 16) m_run[threadIdx.x] = GF_NEG_INF;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // u fragments and flags, before the DMA stream
-  dma_half(row_begin, 0);
-  dma_half(row_begin, 1);
   float l_run = 0.f, ld_run = 0.f;  // per head li (valid in wave 0, g == 0)
   const uint64_t drow = ((uint64_t)b * H + li) * Lp + (uint64_t)max(gidx[r], 0);  // dropout mask row
   f32x4 acc[nmt];
@@ -556,11 +608,17 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
     wait_vm_n<PPW>();  // half A landed (half B's PPW pieces may still fly)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (sub < 4) GF_STAMP(3 + 3 * sub);
 #pragma unroll
     for (int s2 = 0; s2 < (RF_GF_DIAG_SC ? 0 : NK / 2); ++s2) {
       const V8 a = *reinterpret_cast<const V8*>(smem + gimg(arow, 32 * s2 + 8 * g));
-      st = mfma16(a, uh[s2], st);
-      st = mfma16(a, ul[s2], st);
+      if constexpr (ULDS) {
+        st = mfma16(a, *reinterpret_cast<const V8*>(uimg + (s2 * 64 + lane) * 16), st);
+        st = mfma16(a, *reinterpret_cast<const V8*>(uimg + ((NK + s2) * 64 + lane) * 16), st);
+      } else {
+        st = mfma16(a, uh[s2], st);
+        st = mfma16(a, ul[s2], st);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // half B landed
     __builtin_amdgcn_s_barrier();
@@ -568,8 +626,13 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
 #pragma unroll
     for (int s2 = NK / 2; s2 < (RF_GF_DIAG_SC ? NK / 2 : NK); ++s2) {
       const V8 a = *reinterpret_cast<const V8*>(smem + gimg(arow, 32 * s2 + 8 * g));
-      st = mfma16(a, uh[s2], st);
-      st = mfma16(a, ul[s2], st);
+      if constexpr (ULDS) {
+        st = mfma16(a, *reinterpret_cast<const V8*>(uimg + (s2 * 64 + lane) * 16), st);
+        st = mfma16(a, *reinterpret_cast<const V8*>(uimg + ((NK + s2) * 64 + lane) * 16), st);
+      } else {
+        st = mfma16(a, uh[s2], st);
+        st = mfma16(a, ul[s2], st);
+      }
     }
     const unsigned long long vm = vmask[sub];
     float mx = GF_NEG_INF;
@@ -618,6 +681,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
       m_run[li] = m_new;
     }
     __syncthreads();
+    if (sub < 4) GF_STAMP(4 + 3 * sub);
     // rescale W rows (head 4g + q) by alpha, then W[head][c] += sum_j p[j][head] h[j][c]
     float al[4];
 #pragma unroll
@@ -677,6 +741,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
       if (more) dma_half(j0 + 64, half);
 #endif
     }
+    if (sub < 4) GF_STAMP(5 + 3 * sub);
   }
   if (wave == 0 && g == 0) {
     ws.m[((int64_t)r * nch + ch) * GF_HP + li] = m_run[li];
@@ -694,6 +759,12 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
       for (int q = 0; q < 4; ++q)
         if (4 * g + q < H) wout[(int64_t)(4 * g + q) * D + c0 + li] = acc[i][q];
     }
+#if defined(RF_GF_STAMPS)
+  GF_STAMP(15);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < 16) ws.ld[((int64_t)r * nch + ch) * GF_HP + threadIdx.x] = red[GF_RED_LD + threadIdx.x];
+#endif
 }
 
 // ---- partial pass on a 3-slot ring of 32-row sub-chunks (round 3; D a multiple of 128, <= 768) ------
@@ -1366,15 +1437,16 @@ static int fold_partial_out16(int B, int Lp, int D, int H, const void* h, int ld
     RF_REQUIRE(lds_p <= 160 * 1024, "rf_global_attn_fold: D too large for LDS");
 #define GP_(DD)                                                                                 \
   case DD:                                                                                      \
-    if (DD % 128 == 0 && DD <= 768 && Lp <= 128 && g_knob[KNOB_GFOLD_PATH] != 3) {                \
+    if (DD % 128 == 0 && DD <= 768 && (Lp <= 128 || g_knob[KNOB_GFOLD_PATH] == 4) && g_knob[KNOB_GFOLD_PATH] != 3) {                \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_ring<E, DD>,                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_r);        \
       k_gfold_partial_ring<E, DD><<<dim3(nch, R), 256, lds_r, s>>>(Lp, gmax, chr, (const E*)h, ldh,  \
                                                                 flags, gidx, ws, H, dr);        \
     } else if (DD % 128 == 0) {                                                                 \
+      const size_t lds_pu = lds_p + (DD <= 768 ? (size_t)2 * (DD / 32) * 1024 : 0); /* u image */     \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16<E, DD>,                          \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p);        \
-      k_gfold_partial_bf16<E, DD><<<dim3(nch, R), 256, lds_p, s>>>(Lp, gmax, chr, (const E*)h, ldh,  \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pu);       \
+      k_gfold_partial_bf16<E, DD><<<dim3(nch, R), 256, lds_pu, s>>>(Lp, gmax, chr, (const E*)h, ldh, \
                                                                 flags, gidx, ws, H, dr);        \
     } else {                                                                                    \
       (void)hipFuncSetAttribute((const void*)k_gfold_partial_bf16_1<E, DD>,                        \

@@ -29,7 +29,8 @@ def main():
     w = [(torch.randn(D, D, generator=g) * 0.03).bfloat16().to(dev) for _ in range(3)]
     b = [(torch.randn(D, generator=g) * 0.1).to(dev) for _ in range(3)]
     for name, B, Lp in (("c2", 64, 1024), ("catalog", 4096, 64)):
-        h = torch.randn(B * Lp, D, generator=g).bfloat16().to(dev)
+        pad = int(os.environ.get("RF_GF_PADCOLS", "0"))  # row stride D + pad (HBM channel-spread probe)
+        h = torch.randn(B * Lp, D + pad, generator=g).bfloat16().to(dev)[:, :D]
         flags = torch.ones(B, Lp, dtype=torch.uint8, device=dev)
         flags[:, 0] = 2
         gidx = torch.zeros(B, 1, dtype=torch.int32, device=dev)
