@@ -35,6 +35,14 @@ constexpr bool RF_GF_DIAG_PH = (RF_GF_DIAG & 4) != 0;  // no P.H products
 #else
 constexpr bool RF_GF_DIAG_SC = false, RF_GF_DIAG_PH = false;
 #endif    // rows per chunk of the fp32 VALU kernel
+// the partial pass's image stream: RF_GF_NT (A/B builds) reads it with the non-temporal policy — measured
+// slower (C2: kernel 30.1 vs 27.9 us, step 12.28 vs 12.13 ms, profiles/r05/gfold_partial_ab.txt): the
+// layer's next reader of h then misses the Infinity Cache
+#if defined(RF_GF_NT)
+#define GF_IMG_DMA glds16_nt
+#else
+#define GF_IMG_DMA glds16
+#endif
 // RF_GF_STAMPS (tools/build_variant.sh only, inference): k_gfold_partial_bf16's wave 0 records
 // s_memrealtime (100 MHz) at 16 points into free LDS and copies them to the (unused without dropout)
 // ws.ld slots of its (row, chunk) — tools/gfold_stamps.py reads the timeline.
@@ -533,7 +541,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
       const int seg = half * hseg + (p >> 3), row = (p & 7) * 8 + (lane >> 3);
       const int chk = (lane & 7) ^ (row & 7);
       const int jr = min(j0 + row, Lp - 1);
-      glds16(reinterpret_cast<const char*>(hb) + (uint32_t)((jr * ldh + seg * 64 + chk * 8) * (int)sizeof(E)),
+      GF_IMG_DMA(reinterpret_cast<const char*>(hb) + (uint32_t)((jr * ldh + seg * 64 + chk * 8) * (int)sizeof(E)),
              smem + (seg * 64 + (p & 7) * 8) * 128);
     }
   };
