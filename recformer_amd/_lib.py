@@ -18,6 +18,9 @@ RF_IO_C_F32, RF_IO_R_F32 = 1, 2
 RF_EPI_NONE, RF_EPI_BIAS, RF_EPI_BIAS_GELU, RF_EPI_BIAS_RESID, RF_EPI_COS = 0, 1, 2, 3, 4
 RF_EPI_BIAS_GELU_AUX = 6
 RF_EPI_DGELU = 7
+# rf_abi_version() of the library this binding's SIGNATURES describe; bumped whenever an entry point's
+# arguments change (2: rf_prepare_inputs gained gstat, rf_drop_add_ln_*_t mask_row_mul)
+ABI_VERSION = 2
 
 # symbol -> (restype, argtypes); must match include/recformer_hip.h exactly
 P = c_void_p
@@ -142,6 +145,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             f"librecformer_hip.so not found at {path}: build it with "
             f"`python -c 'import __graft_entry__ as g; g.build()'` (make -C recformer_amd/csrc)")
     lib = ctypes.CDLL(path)
+    lib.rf_abi_version.restype = c_int
+    lib.rf_abi_version.argtypes = []
+    ver = lib.rf_abi_version()
+    if ver != ABI_VERSION:
+        # an older / newer build (e.g. RF_HIP_LIB at a variant library) would read shifted arguments
+        # (an int as the stream handle): refuse it instead of launching on garbage
+        raise RecformerHipError(f"{path}: ABI version {ver}, this binding needs {ABI_VERSION}: rebuild the library")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

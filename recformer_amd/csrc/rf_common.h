@@ -74,6 +74,9 @@ enum Knob {
                         // tile issues 14 operand DMA pieces per 96 MFMAs instead of 16 per 128
   KNOB_ADAM_NT,         // AdamW: non-temporal operand loads / stores (1, default: captured C3 16.03 vs 16.07 ms,
                         // gpurun_out/r05q) or plain (0)
+  KNOB_GEMM_W8,         // 16-bit EPI_NONE / EPI_BIAS / EPI_BIAS_GELU GEMMs on the eight-wave ping-pong kernel
+                        // (k_gemm_w8: two waves per SIMD, one computing while its partner loads): 1 on, 0 the
+                        // four-wave kernel
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];

@@ -582,7 +582,7 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
     const int jf = row_begin + 64 * wave + lane;
     int fv = (wave < nsub && jf < Lp) ? (int)flags[(int64_t)b * Lp + jf] : 0;
     // piece (plane, k-step s2): lane (li, g) <- u[plane][head li][32 s2 + 8 g ..]; rows >= H read row
-    // H - 1 (finite; those score columns are never used)
+    // H - 1 (an in-bounds source), zeroed in LDS once landed (below)
     const E* ub = reinterpret_cast<const E*>(ws.u16) + ((int64_t)r * 2 * GF_HP + min(li, H - 1)) * D + 8 * g;
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
@@ -593,6 +593,14 @@ __global__ void __launch_bounds__(256) k_gfold_partial_bf16(int Lp, int gmax, in
     dma_half(row_begin, 1);
     GF_STAMP(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // u, the first image and the flags landed
+    // padding heads (li >= H) were DMA'd from head H - 1 (a finite in-bounds source): zero their u so
+    // their score columns and workspace slots (m, l, W of heads >= H) are those of u = 0, not copies of
+    // a real head's. No reader uses them (the out / backward kernels loop h < H); this keeps it so.
+    // The same wave wrote these bytes by DMA and waited for them above, so the stores land after them.
+    if (li >= H) {
+#pragma unroll
+      for (int i = 0; i < UPW; ++i) *reinterpret_cast<V8*>(uimg + (wave * UPW + i) * 1024 + lane * 16) = V8{};
+    }
     asm volatile("" : "+v"(fv));
     if (wave < nsub) {
       const unsigned long long m = __ballot(fv != 0);

@@ -220,7 +220,13 @@ class GradBucketer:
                     self._avg_op = dist.ReduceOp.AVG
             except (RuntimeError, ValueError):
                 self._avg_op = None
-        self.zero_grad()
+        # bind every .grad to its bucket view, keeping a gradient that is already there (a bucketer
+        # built mid-accumulation or after a warm-up backward): copied in, not thrown away
+        for ps, views in zip(self.buckets, self._views):
+            for p, v in zip(ps, views):
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                p.grad = v
         self._reset()
 
     def _reset(self):

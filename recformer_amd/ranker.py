@@ -83,6 +83,14 @@ TOPK_MAX_SAMPLE = 2048
 TOPK_GROWTH = 8
 
 
+def growth_for(k: int, cap: int = TOPK_CAP) -> int:
+    """Chunk growth factor for a top-k of k with `cap` candidate slots per row and chunk: TOPK_GROWTH,
+    limited so the expected k * (grow - 1) candidates fill at most half the list (2 at the least)."""
+    if k <= 0:
+        return max(2, int(TOPK_GROWTH))
+    return max(2, min(int(TOPK_GROWTH), 1 + cap // (2 * k)))
+
+
 @contextlib.contextmanager
 def _rank_family(topk: bool):
     """The rank kernel family for one self-contained ranking (label scores + rank counts from the same
@@ -208,9 +216,11 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     # default seed_n = s0; a larger seed_n would lower the first candidate chunks' rate)
     seed_n = s0
     blocks = [(o, min(sample, seed_n - o)) for o in range(0, seed_n, sample)]
-    # column chunks after the seed: each (TOPK_GROWTH - 1) times everything before it
+    # column chunks after the seed: each (grow - 1) times everything before it. A row expects about
+    # k * (grow - 1) candidates per chunk, so the factor is capped to keep that within half the list
+    # (cap): at k = 256 a growth of 8 would overflow nearly every row into the exact re-rank
     plan, off = [], seed_n
-    grow = max(2, int(TOPK_GROWTH))
+    grow = growth_for(k, cap)
     while k > 0 and off < N:
         plan.append((off, min(N - off, max(off * (grow - 1), sample))))
         off += plan[-1][1]
@@ -219,6 +229,7 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     part_cnt = torch.empty(ntiles, B, dtype=torch.int32, device=dev)
     part_sexp = torch.empty(ntiles, B, dtype=torch.float32, device=dev)
     topv = topi = None
+    n_over = 0
     if k > 0:
         dense = torch.empty(B, (s0 + 255) // 256 * 256, dtype=torch.float32, device=dev)  # whole 256-col tiles
         tb = 0
@@ -262,6 +273,7 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
         counts = _rank_reduce(lib, B, ntiles, part_cnt, part_sexp, dev, q)
         if plan:
             rows = torch.nonzero(over).flatten()
+            n_over = rows.numel()
             if rows.numel():  # many near-equal scores overflowed the lists: exact dense re-rank
                 empty_v = torch.full((rows.numel(), k), float("-inf"), device=dev)
                 empty_i = torch.full((rows.numel(), k), -1, dtype=torch.int32, device=dev)
@@ -274,7 +286,10 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
         _score_rank(q, qn, shard, s_label, inv_t, 2, 0, N, part_cnt, part_sexp, 0, max_val=max_val)
         counts = _rank_reduce(lib, B, ntiles, part_cnt, part_sexp, dev, q)
     gt, valid, sexp = counts
-    return {"gt": gt, "valid": valid, "sexp": sexp, "topv": topv, "topi": topi, "shift": inv_t}
+    # overflow: rows whose candidate lists overflowed and were re-ranked densely (a count of slow rows,
+    # not an error: the result is exact either way)
+    return {"gt": gt, "valid": valid, "sexp": sexp, "topv": topv, "topi": topi, "shift": inv_t,
+            "overflow": n_over}
 
 
 def _rank_reduce(lib, B: int, ntiles: int, part_cnt, part_sexp, dev, q):

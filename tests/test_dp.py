@@ -314,12 +314,18 @@ def _wire_worker(rank, ws, port, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
         g = torch.Generator().manual_seed(9)
-        xs = torch.randn(2, 16, 64, generator=g)
+        xs = torch.randn(2, 8 * ws, 64, generator=g)
         res = {}
         for name, cd in (("fp32", None), ("bf16", torch.bfloat16), ("fp16", torch.float16)):
             net = _wire_net()
+            # a warm-up backward before the bucketer exists: its gradients are kept (copied into the views)
+            net(xs[1, :3]).sum().backward()
+            pre = [p.grad.clone() for p in net.parameters()]
             b = dp.GradBucketer(net.parameters(), bucket_bytes=16 << 10, comm_dtype=cd)
             flats = [(f.data_ptr(), f.data_ptr() + f.numel() * f.element_size()) for f in b._flat]
+            kept = all(torch.equal(p.grad, g0) and any(a <= p.grad.data_ptr() < e for a, e in flats)
+                       for p, g0 in zip(net.parameters(), pre))
+            b.zero_grad()
             grads = []
             for w in range(2):
                 if w == 1:
@@ -331,10 +337,24 @@ def _wire_worker(rank, ws, port, out_q):
                 aliased = all(any(a <= p.grad.data_ptr() < e for a, e in flats) for p in net.parameters())
                 grads.append(([p.grad.clone() for p in net.parameters()], aliased))
                 b.zero_grad()
-            res[name] = (grads, b.bucket_bytes_on_wire(), len(b.buckets))
+            res[name] = (grads, b.bucket_bytes_on_wire(), len(b.buckets), kept)
         out_q.put(_plain((rank, res)))
     finally:
         dist.destroy_process_group()
+
+
+def _run_wire(ws):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_wire_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    got = dict(_unplain(q.get(timeout=300)) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return got
 
 
 def test_gradbucketer_16bit_wire_world2():
@@ -342,16 +362,7 @@ def test_gradbucketer_16bit_wire_world2():
     averages the gradients to the 16-bit contract of the fp32 exchange, which equals the full-batch
     gradient; .grad stays a view into the bucket buffers (no flatten / copy-back), also after a
     set-to-None zero_grad; the wire carries half the bytes."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_wire_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    got = dict(_unplain(q.get(timeout=300)) for _ in range(2))
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    got = _run_wire(2)
     xs = torch.randn(2, 16, 64, generator=torch.Generator().manual_seed(9))
     for w in range(2):
         net = _wire_net()
@@ -371,6 +382,48 @@ def test_gradbucketer_16bit_wire_world2():
                     assert (a - b32).abs().max() <= 3 * eps * b32.abs().max() + 1e-12, name
     n32, n16 = got[0]["fp32"][1], got[0]["bf16"][1]
     assert n16 * 2 == n32 and got[0]["fp32"][2] >= 2
+    # gradients present when the bucketer is built are kept in its views (advisor r05), every wire dtype
+    assert all(got[r][name][3] for r in (0, 1) for name in ("fp32", "bf16", "fp16"))
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_gradbucketer_16bit_wire_error_vs_world_size(ws):
+    """How the 16-bit exchange's error grows with the ranks: each rank's term t_r = g_r / ws
+    is rounded once to 16 bits (pack), and the ring adds ws - 1 partial sums, each rounded to 16 bits.
+    Per element, with S = sum_r |t_r| (the sum of the magnitudes entering the reduction):
+        |g_16 - g_32| <= (ws + 1) * (eps / 2 * S + tiny),   eps = 2^-7 (bf16), 2^-10 (fp16)
+    (pack: eps/2 * S; each of the ws - 1 additions: eps/2 * |partial| <= eps/2 * S; tiny = half the wire
+    dtype's subnormal spacing per rounding, which matters for fp16 gradients below 6.1e-5). Checked at world 2 and
+    4 on gloo, whose ring sums in the wire dtype like RCCL's; at world 8 the bound is 9 * eps / 2 * S
+    (3.5% of S in bf16 worst case; the measured error is far below it: the roundings do not all align)."""
+    got = _run_wire(ws)
+    xs = torch.randn(2, 8 * ws, 64, generator=torch.Generator().manual_seed(9))
+    worst = {"bf16": 0.0, "fp16": 0.0}
+    for w in range(2):
+        per_rank = []
+        for r in range(ws):
+            net = _wire_net()
+            net(xs[w, r * 8:(r + 1) * 8]).pow(2).mean().backward()
+            per_rank.append([p.grad / ws for p in net.parameters()])
+        S = [sum(t[i].abs() for t in per_rank) for i in range(len(per_rank[0]))]
+        for r in range(ws):
+            g32 = got[r]["fp32"][0][w][0]
+            for i, (a, ref) in enumerate(zip(g32, [sum(t[i] for t in per_rank) for i in range(len(S))])):
+                assert torch.allclose(a, ref, atol=1e-6, rtol=1e-5)
+            # tiny: half the spacing of the wire dtype's subnormals, per rounding (fp16's start below 6.1e-5)
+            for name, eps, tiny in (("bf16", 2.0 ** -7, 2.0 ** -134), ("fp16", 2.0 ** -10, 2.0 ** -25)):
+                g16 = got[r][name][0][w][0]
+                for a, b32, s in zip(g16, g32, S):
+                    err = (a - b32).abs()
+                    lim = (ws + 1) * ((eps / 2) * s + tiny)
+                    assert bool((err <= lim + 1e-30).all()), (name, ws, float((err / lim).max()))
+                    worst[name] = max(worst[name], float((err / lim).max()))
+    # the ranks agree bit for bit (every rank unpacks the same reduced wire)
+    for name in ("fp32", "bf16", "fp16"):
+        for r in range(1, ws):
+            for a, b in zip(got[0][name][0][1][0], got[r][name][0][1][0]):
+                assert torch.equal(a, b)
+    print(f"world {ws}: max error / bound = {worst['bf16']:.3f} (bf16), {worst['fp16']:.3f} (fp16)")
 
 
 def _combine_worker(rank, ws, port, out_q):

@@ -443,6 +443,42 @@ def test_global_fold_h_stages_match_one_call(dev, dt, B, Lp, H):
         ops.global_attention_fold_h_stage(2, ws, h_keep, *args)
 
 
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,Lp,H", [(3, 192, 3), (4, 1024, 12)])
+def test_global_fold_fwd_stages_match_fused(dev, dt, B, Lp, H, p_drop):
+    """rf_global_attn_fold_fwd_stage(1) then (2) on one workspace — how the training forward runs the
+    fold beside the band attention (train.FOLD_SIDE_TRAIN) — is bit-identical to the one-call stage 3,
+    with and without attention dropout; stage 1 leaves out untouched and stage 2 reads only the
+    workspace (h overwritten in between)."""
+    D = H * 64
+    g = torch.Generator().manual_seed(B * Lp + H)
+    lens = [int(x) for x in torch.randint(1, Lp + 1, (B,), generator=g)]
+    lens[0] = Lp
+    globals_ = [(b, 0) for b in range(B)] + [(b, lens[b] - 1) for b in range(0, B, 2)]
+    _, _, flags, gidx, G = _attn_case(dev, dt, B, Lp, H, lens, globals_, 3)
+    h = _rand((B * Lp, D), dev, dt, 1.0, seed=80)
+    wkg = _rand((D, D), dev, dt, 0.05, seed=81)
+    wvg = _rand((D, D), dev, dt, 0.05, seed=82)
+    bkg = _rand((D,), dev, torch.float32, 0.1, seed=83)
+    bvg = _rand((D,), dev, torch.float32, 0.1, seed=84)
+    qg = _rand((B * G, D), dev, dt, 1.0, seed=85)
+    args = (wkg, bkg, wvg, bvg, flags, gidx, B, Lp, H)
+    ref = torch.full((B * Lp, D), 3.0, dtype=dt, device=dev)
+    ws3 = ops.global_fold_workspace(h, B, Lp, H, gidx.shape[1])
+    ops.global_attention_fold(qg, h, *args, ref, p_drop=p_drop, seed=1234, ws=ws3, stage=3)
+    ws = ops.global_fold_workspace(h, B, Lp, H, gidx.shape[1])
+    out = torch.full((B * Lp, D), 3.0, dtype=dt, device=dev)
+    ops.global_attention_fold(qg, h, *args, None, p_drop=p_drop, seed=1234, ws=ws, stage=1)
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.full_like(out, 3.0))
+    h.normal_()
+    ops.global_attention_fold(qg, h, *args, out, p_drop=p_drop, seed=1234, ws=ws, stage=2)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert (out != 3.0).any()
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,Lp,H", [(300, 64, 12), (70, 192, 3), (5, 1024, 12)])
 def test_global_fold_mfma_matches_gemv(dev, monkeypatch, B, Lp, H, dt):
@@ -944,6 +980,55 @@ def test_weight_pack_matches_torch_casts(dev, dt):
                 w.mul_(1.5)
     with pytest.raises(ValueError):
         ops.WeightPack([dict(src=q.t(), dst=(qb, 0))], dt)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (8192, 768, 3072), (4100, 2312, 768), (65536, 768, 768),
+                                   (300, 520, 128), (70000, 2304, 768), (2048, 256, 192)])
+def test_gemm_eight_wave_kernel(dev, dt, M, N, K):
+    """The eight-wave ping-pong kernel (k_gemm_w8, knob gemm_w8; two waves per SIMD, one computing while its
+    partner loads) for its epilogues (none, bias with a q-column scale, GELU): against fp32 torch on the same
+    16-bit operands, and bit-identical to the four-wave kernel (the same MFMA sequence per accumulator and the
+    same epilogue arithmetic), including ragged M / N edges (4100 x 2312, 300 x 520), a grid of fewer tiles
+    than CUs (300 x 520), several tiles per CU (70000 x 2304) and the shortest K (128 / 192: 2 / 3 K-tiles)."""
+    a = _rand((M, K), dev, dt, 0.5, seed=191)
+    w = _rand((N, K), dev, dt, 0.05, seed=192)
+    b = _rand((N,), dev, torch.float32, seed=193)
+    prod = a.float() @ w.float().t()
+    sc = N // 3 // 16 * 16
+    tol = 4e-3 if dt == torch.float16 else 2e-2
+
+    def rel(x, ref):
+        return float((x.float() - ref).abs().max()) / max(1.0, float(ref.abs().max()))
+
+    def run(knob):
+        old = _lib.set_knob("gemm_w8", knob)
+        try:
+            return (ops.gemm(a, w, None, ops.RF_EPI_NONE),
+                    ops.gemm(a, w, b, ops.RF_EPI_BIAS, scale_cols=sc, col_scale=0.125),
+                    ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU))
+        finally:
+            _lib.set_knob("gemm_w8", old)
+
+    none8, bias8, gelu8 = run(1)
+    assert rel(none8, prod) <= tol
+    ref = prod + b
+    ref[:, :sc] *= 0.125
+    assert rel(bias8, ref) <= tol
+    assert rel(gelu8, F.gelu(prod + b)) <= tol
+    none4, bias4, gelu4 = run(0)
+    assert torch.equal(none8, none4)
+    assert torch.equal(bias8, bias4)
+    assert torch.equal(gelu8, gelu4)
+    # strided operand / output views (the q|k|v column slices the encoder hands over)
+    wide = torch.zeros(M, N + 64, device=dev, dtype=dt)
+    old = _lib.set_knob("gemm_w8", 1)
+    try:
+        ops.gemm(a, w, b, ops.RF_EPI_BIAS, scale_cols=sc, col_scale=0.125, out=wide[:, 16:16 + N])
+    finally:
+        _lib.set_knob("gemm_w8", old)
+    assert torch.equal(wide[:, 16:16 + N], bias4)
+    assert not wide[:, :16].any() and not wide[:, 16 + N:].any()
 
 
 @pytest.mark.parametrize("mfma32", [0, 1])

@@ -89,6 +89,26 @@ def test_shard_rank_matches_restated_ranker_and_sort(dev, monkeypatch, dt, B, N,
     assert torch.equal(parts["topi"], ri)
 
 
+@pytest.mark.parametrize("k", [128, 256])
+def test_shard_rank_large_k_few_overflows(dev, k):
+    """At large k the chunk growth is capped (ranker.growth_for: k * (grow - 1) <= cap / 2), so
+    the candidate lists do not overflow into the dense re-rank for most rows (advisor r05: at
+    k = 256 a growth of 8 overflowed nearly every row); the top-k still equals a full sort."""
+    import recformer_amd.ranker as RK
+    assert RK.growth_for(50) == RK.TOPK_GROWTH and RK.growth_for(256) == 3 and RK.growth_for(128) == 5
+    B, N = 256, 60000
+    q, items, labels = _case(dev, torch.bfloat16, B, N, B + N)
+    shard = CatalogShard(items)
+    sl = label_scores(q, shard, labels, 0.05)
+    parts = shard_rank(q, shard, sl, 0.05, k=k)
+    assert parts["overflow"] <= B // 20, parts["overflow"]
+    dense = _dense_scores(q, shard, sl, 0.05)
+    ids = torch.arange(N, device=dev, dtype=torch.int32).expand(B, N)
+    rv, ri = merge_topk(dense, ids, k)
+    assert torch.equal(parts["topv"], rv)
+    assert torch.equal(parts["topi"], ri)
+
+
 def test_two_shards_combine_to_one(dev):
     """The catalog split in two shards (global ids), label scores summed, counts summed and the
     shards' top-k merged (what combine_shards does across ranks) equals the single-shard result."""

@@ -56,7 +56,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
         assert n in _lib.SIGNATURES, f"{n} declared in the header but not typed in _lib.py"
     assert set(_lib.SIGNATURES) == set(names)
-    assert lib.rf_abi_version() == 1
+    assert lib.rf_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_every_documented_knob_is_readable():

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 6: the eight-wave GEMM's parity, its C2 GEMM bar and a same-process C2 step A/B, plus the new tests
+set -o pipefail
+O=gpurun_out/r06b; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  tests/test_gpu_kernels.py::test_gemm_eight_wave_kernel tests/test_gpu_kernels.py::test_global_fold_fwd_stages_match_fused \
+  tests/test_gpu_retrieval.py::test_shard_rank_large_k_few_overflows tests/test_gpu_train.py::test_side_stream_switches_bit_identical \
+  > $O/pytest.log 2>&1 || { grep -E "^E  |FAILED|Error" $O/pytest.log | head -30; tail -5 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 300 python tools/gemm_c2_bar.py gemm_w8=1 > $O/bar.jsonl 2>&1 || { tail -20 $O/bar.jsonl; exit 1; }
+python3 -c "
+import json
+for l in open('$O/bar.jsonl'):
+    d=json.loads(l); print(d['shape'], d['leg'], d['us'], d['tflops'], d.get('bit_identical_to_default',''))"
+AB_AUTOCAST=1 timeout -k 10 400 python tools/ab_step.py knob:gemm_w8 64 > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; exit 1; }
+cat $O/ab_c2.log
