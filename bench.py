@@ -62,7 +62,47 @@ def parse():
                          "the headline value so kernel progress stays comparable round over round)")
     ap.add_argument("--timing-steps", type=int, default=20,
                     help="steps of the separate HIP-event-instrumented pass (per-kernel times)")
+    ap.add_argument("--batch-sweep", type=str, default="1,16,128",
+                    help="SURVEY §8d batch sweep: per-GPU batch sizes timed eager and as a replayed HIP graph "
+                         "(recformer_amd.graphs.GraphedForward) after the headline legs ('' disables; N=1 only)")
     return ap.parse_args()
+
+
+def batch_sweep(model, cfg, L, sizes, amp, dev):
+    """Per-batch-size latency and throughput of the same encode + score step, eager (one host read of the
+    global-token count per forward) and replayed from a captured HIP graph (inputs copied into the
+    graph's static tensors, no host read). B = 16 is the reference drivers' evaluation batch
+    (finetune.py:185 -> eval, finetune.py:66-96)."""
+    from recformer_amd.graphs import GraphedForward
+    from recformer_amd.synth import synth_batch
+    rows = []
+    for Bs in sizes:
+        bb = {k: v.to(dev) for k, v in synth_batch(Bs, L, cfg.vocab_size, seed=200 + Bs, item_len=21).items()}
+        n = max(10, min(200, 2048 // Bs))
+        with torch.autocast("cuda", dtype=amp):
+            for _ in range(3):
+                model(**bb)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                model(**bb)
+            torch.cuda.synchronize()
+            eager = (time.perf_counter() - t0) / n
+            g = GraphedForward(model, bb, check=False)
+            for _ in range(3):
+                g(**bb)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                g(**bb)
+            torch.cuda.synchronize()
+            graphed = (time.perf_counter() - t0) / n
+            del g
+        torch.cuda.empty_cache()
+        rows.append({"batch": Bs, "steps": n, "eager_ms": round(eager * 1e3, 3),
+                     "eager_seq_s": round(Bs / eager, 1), "graphed_ms": round(graphed * 1e3, 3),
+                     "graphed_seq_s": round(Bs / graphed, 1)})
+    return rows
 
 
 def gemm_flops_per_seq(L, d, ffn, layers, gmax=1, fold=True):
@@ -360,6 +400,9 @@ def main():
             inst_s = time.perf_counter() - ti
             kt = ops.timing_results()
             ops.enable_timing(False)
+        sweep = None
+        if args.batch_sweep and world == 1:
+            sweep = batch_sweep(model, cfg, L, [int(x) for x in args.batch_sweep.split(",") if x.strip()], amp, dev)
     assert scores.shape == (B, args.catalog)
 
     tmax = dp.max_over_ranks(elapsed, device=coll_dev)
@@ -446,6 +489,10 @@ def main():
                                       "us_per_seq_floor": round(floor_full, 2),
                                       "note": "same process, same batch, every row through the last layer "
                                               "(models.PRUNE_LAST_LAYER=False)"}
+        if sweep:
+            out["batch_sweep"] = {"rows": sweep, "note": "same process after the timed legs, same model and mode; "
+                                  "eager = RecformerForSeqRec.forward per batch, graphed = GraphedForward replay "
+                                  "(inputs copied in); B=64 is the headline"}
         out.update({
             "kernels": kernels,
             "kernels_pass": ({"steps": inst_steps, "ms_per_step": round(1e3 * inst_s / inst_steps, 3),

@@ -1018,8 +1018,17 @@ def test_gemm_eight_wave_kernel(dev, dt, M, N, K):
     assert rel(gelu8, F.gelu(prod + b)) <= tol
     none4, bias4, gelu4 = run(0)
     assert torch.equal(none8, none4)
-    assert torch.equal(bias8, bias4)
-    assert torch.equal(gelu8, gelu4)
+    if dt == torch.bfloat16:
+        assert torch.equal(bias8, bias4)
+        assert torch.equal(gelu8, gelu4)
+    else:
+        # fp16: hipcc fuses the four-wave kernel's bias FMA and fp16 rounding into v_fma_mix on some values
+        # (one rounding instead of fp32 then fp16): at most one fp16 ulp apart, and equal elsewhere
+        for x8, x4 in ((bias8, bias4), (gelu8, gelu4)):
+            d = (x8.float() - x4.float()).abs()
+            ulp = torch.maximum(x4.float().abs(), torch.full_like(d, 2.0 ** -14)) * 2.0 ** -10
+            assert bool((d <= ulp).all())
+            assert float((d > 0).float().mean()) < 0.02
     # strided operand / output views (the q|k|v column slices the encoder hands over)
     wide = torch.zeros(M, N + 64, device=dev, dtype=dt)
     old = _lib.set_knob("gemm_w8", 1)
@@ -1027,7 +1036,7 @@ def test_gemm_eight_wave_kernel(dev, dt, M, N, K):
         ops.gemm(a, w, b, ops.RF_EPI_BIAS, scale_cols=sc, col_scale=0.125, out=wide[:, 16:16 + N])
     finally:
         _lib.set_knob("gemm_w8", old)
-    assert torch.equal(wide[:, 16:16 + N], bias4)
+    assert torch.equal(wide[:, 16:16 + N], bias8)
     assert not wide[:, :16].any() and not wide[:, 16 + N:].any()
 
 

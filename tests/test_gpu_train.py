@@ -8,8 +8,10 @@ autocast bf16 — loss 1e-2 rel, gradient cosine >= 0.99 per parameter (>= 0.95 
 gradients of LayerNorm / bias vectors below 1e-3 of the largest gradient).
 """
 import contextlib
+import json
 import math
 import os
+import re
 
 import pytest
 import torch
@@ -403,6 +405,11 @@ def _c2_model(dev):
     return model.to(dev).train()
 
 
+# autocast parity contract for the training backward: per parameter group, the HIP gradient's error
+# against the reference's fp32 gradient is at most this multiple of the reference's own autocast drift
+DRIFT_MULT = 2.0
+
+
 def _c2_check(model, loss, dz, mode, gz, dev, gscale=1.0):
     """The C2 finetune gradients (times gscale) against tests/golden/c2_grads.npz."""
     ref_loss = float(gz["loss"])
@@ -410,12 +417,10 @@ def _c2_check(model, loss, dz, mode, gz, dev, gscale=1.0):
     if mode == "fp32":
         assert abs(float(loss) - ref_loss) <= 1e-3, (float(loss), ref_loss)
         assert float((dz - dz_ref).abs().max()) <= 2e-3 * float(dz_ref.abs().max())
-    else:
-        assert abs(float(loss) - ref_loss) <= 1e-2 * abs(ref_loss), (float(loss), ref_loss)
-        assert F.cosine_similarity(dz.reshape(1, -1), dz_ref.reshape(1, -1)).item() >= 0.99
     params = dict(model.longformer.named_parameters())
     gmax = max(float(gz[f"g:{n}:maxabs"]) for n in gz["names"])
     checked = zero = 0
+    groups = {}
     for n in gz["names"]:
         n = str(n)
         p = params[n]
@@ -437,13 +442,40 @@ def _c2_check(model, loss, dz, mode, gz, dev, gscale=1.0):
             assert float((got - ref).abs().max()) <= 2e-3 * mref, (n, float((got - ref).abs().max()), mref)
             assert abs(nrm - nref) <= 1e-3 * nref, (n, nrm, nref)
         else:
-            assert abs(nrm - nref) <= 5e-2 * nref, (n, nrm, nref)
-            if float(ref.abs().max()) > 1e-6:
-                cos = F.cosine_similarity(got.reshape(1, -1), ref.reshape(1, -1)).item()
-                lim = 0.99 if mref > 1e-3 * gmax else 0.95
-                assert cos >= lim, (n, cos)
+            # per parameter group (the same tensor across the 12 layers): the HIP autocast gradient's
+            # relative L2 error against the reference's fp32 gradient, on the fixture's slices, is held to
+            # DRIFT_MULT x the reference's OWN autocast drift on the same slices (its backward under CPU
+            # torch.autocast in the same 16-bit type, oracle/gen_golden_grads.py)
+            tag = "bf16" if mode == "autocast" else "fp16"
+            key = re.sub(r"layer\.\d+\.", "layer.*.", n)
+            grp = groups.setdefault(key, [[], [], []])
+            grp[0].append(got)
+            grp[1].append(ref)
+            grp[2].append(torch.from_numpy(gz[f"ac_{tag}:g:{n}:val"]))
         checked += 1
     assert checked + zero == len(gz["names"]) == 270 and zero == 29
+    if mode != "fp32":
+        rows = []
+        for key, (got, ref, rac) in groups.items():
+            got, ref, rac = torch.cat(got).double(), torch.cat(ref).double(), torch.cat(rac).double()
+            e_hip = float((got - ref).norm() / ref.norm())
+            e_ref = float((rac - ref).norm() / ref.norm())
+            rows.append({"group": key, "hip_rel_err": e_hip, "ref_autocast_drift": e_ref, "ratio": e_hip / e_ref})
+        tag = "bf16" if mode == "autocast" else "fp16"
+        dz_ac = torch.from_numpy(gz[f"ac_{tag}:dz"])
+        # the loss and dL/dz (the scoring head's input gradient) to the same contract; a floor of 1e-5 relative
+        # keeps a single scalar whose reference drift happens to be ~0 from failing on rounding
+        for name, e_hip, e_ref in (
+                ("loss", abs(float(loss) - ref_loss) / abs(ref_loss),
+                 abs(float(gz[f"ac_{tag}:loss"]) - ref_loss) / abs(ref_loss)),
+                ("dL/dz", float((dz - dz_ref).norm() / dz_ref.norm()), float((dz_ac - dz_ref).norm() / dz_ref.norm()))):
+            rows.append({"group": name, "hip_rel_err": e_hip, "ref_autocast_drift": e_ref,
+                         "ratio": e_hip / max(e_ref, 1e-5)})
+        os.makedirs(os.path.join("gpurun_out", "drift"), exist_ok=True)
+        with open(os.path.join("gpurun_out", "drift", f"c2_grads_{mode}.json"), "w") as f:
+            json.dump(rows, f, indent=1)
+        bad = [r for r in rows if r.get("ratio", 0.0) > DRIFT_MULT]
+        assert not bad, bad
 
 
 def _c2_fixtures():
@@ -459,9 +491,11 @@ def test_c2_finetune_grads_match_reference(dev, mode):
     (tests/golden/c2_grads.npz, oracle/gen_golden_grads.py: models.py full-softmax loss, dropout 0,
     train mode). Per parameter: 256 gradient entries at fixed positions, the L2 norm and max-abs.
     fp32: loss 1e-3 abs, dL/dz and every slice within 2e-3 x max|g| of the parameter, norms 1e-3
-    relative; autocast bf16 (the reference's finetune.py:106-110 setting): loss 1e-2 relative,
-    dL/dz cosine >= 0.99, slice cosine >= 0.99 (0.95 below 1e-3 of the largest gradient),
-    norms within 5%."""
+    relative. autocast bf16 / fp16 (the reference drivers' mixed precision, finetune.py:106-110): per
+    parameter group, and for the loss and dL/dz, the HIP error against the reference's fp32 gradient is
+    at most DRIFT_MULT (2) x the reference's OWN autocast drift in the same 16-bit type on the same
+    entries (c2_grads.npz ac_bf16 / ac_fp16: its backward under CPU torch.autocast). Measured (round 6):
+    ratios 0.07-1.56 (bf16), 0.10-1.36 (fp16); the per-group table goes to gpurun_out/drift/."""
     gz, g12 = _c2_fixtures()
     model = _c2_model(dev)
     keep = {}
