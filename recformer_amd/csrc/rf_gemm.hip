@@ -1236,9 +1236,9 @@ static void launch_w4(int M, int N, int K, const void* A, int lda, const void* W
 
 
 
-// the eight-wave ping-pong kernel (rf_gemm_w8.hip)
-template <typename E, int EPI>
-void launch_w8(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e, hipStream_t s);
+// the eight-wave ping-pong kernel (rf_gemm_w8.hip): EPI_NONE / EPI_BIAS / EPI_BIAS_GELU, 16-bit C
+void gemm_w8(bool half, int epi, int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
+             hipStream_t s);
 
 // ---- k_gemm_w32: the encoder GEMMs on w32_run (rf_w32.h) ----------------------------------------
 template <typename E, int EPI, bool CF32>
@@ -1826,7 +1826,7 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
     }
     if constexpr (!CF32 && !RF32 && (EPI == RF_EPI_NONE || EPI == RF_EPI_BIAS || EPI == RF_EPI_BIAS_GELU)) {
       if (w4_ok && g_knob[KNOB_GEMM_W8] && !g_knob[KNOB_GEMM_MFMA32]) {
-        launch_w8<E, EPI>(M, N, K, A, lda, W, ldw, e, s);
+        gemm_w8(std::is_same<E, f16>::value, EPI, M, N, K, A, lda, W, ldw, e, s);
         return;
       }
     }

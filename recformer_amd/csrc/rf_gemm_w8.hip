@@ -26,7 +26,12 @@ namespace rf {
 // columns (8-B stores, 16 lanes = one 128-B line per row). Same LDS image and swizzle as k_gemm_w4.
 constexpr int W8_BUF = 4 * PP_HALF;   // one K-tile: A rows 0-255 | W image rows 0-255
 constexpr int W8_CV = 2 * W8_BUF;     // column vectors [parity][1 KiB]
+#if defined(RF_W8_STAMPS)
+constexpr int W8_NSTAMP = 128;
+constexpr int W8_LDS = W8_CV + 2 * 1024 + 2 * W8_NSTAMP * 8;
+#else
 constexpr int W8_LDS = W8_CV + 2 * 1024;
+#endif
 
 template <typename E, int EPI>
 __global__ void __launch_bounds__(512, 2)
@@ -39,8 +44,9 @@ __global__ void __launch_bounds__(512, 2)
   const int tiles = nTm * nTn;
   if ((int)blockIdx.x >= tiles) return;
   const int GN = e.gn > 0 ? min(e.gn, nTn) : nTn;
-  auto tile_origin = [&](int vv, int& om0, int& on0) {
-    const int wg = xcd_remap(vv, tiles);
+  // origin of this workgroup's T-th tile (xcd-aware raster as k_gemm_w4); evaluated once per tile
+  auto tile_origin = [&](int T, int& om0, int& on0) {
+    const int wg = xcd_remap((int)blockIdx.x + T * (int)gridDim.x, tiles);
     const int g = wg / (nTm * GN);
     const int gw = min(GN, nTn - g * GN);
     const int rem = wg - g * nTm * GN;
@@ -55,40 +61,50 @@ __global__ void __launch_bounds__(512, 2)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int grp = wave >> 2, wl = wave & 3;
   const int wr = wl >> 1, wq = 2 * grp + (wl & 1);  // compute block: rows 128 wr, columns 64 wq
-  // DMA role: group 0 stages A rows 64 wl + 8 p + lane / 8, group 1 the W image rows 64 wl + 8 p + lane / 8
-  // = W rows 64 wl + 32 (p & 1) + 4 (lane / 8) + (p >> 1) (image row 64 q + 16 j + c holds W row 64 q + 4 c + j)
-  const __amdgpu_buffer_rsrc_t rs =
-      grp == 0 ? __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0,
-                                                   (int)min((int64_t)e.M * lda * 2, (int64_t)0x7FFFFFFF), 0x00020000)
-               : __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0,
-                                                   (int)min((int64_t)e.N * ldw * 2, (int64_t)0x7FFFFFFF), 0x00020000);
-  const int ldo = grp == 0 ? lda : ldw;
+  // Operand DMA of step s (into buffer s & 1), each piece 8 image rows x 128 B, lane: row + lane / 8,
+  // 16-B chunk (lane & 7) ^ (row & 7) from the source (the read swizzle). Group g stages the rows
+  // 128 g + 32 wl + 8 p (p < 4) of the A image and of the W image, 4 + 4 pieces per wave and step: its
+  // W half (the image rows of its own columns) and its A half during its load segment of step s - 1,
+  // except that group 1's A half (rows 128-255, which group 0 reads one segment before group 1) goes out
+  // at the start of its compute segment of step s - 2 (the buffer's previous step was read by then). W image
+  // row r = 64 q + 16 j + c holds W row 64 q + 4 c + j, so lane (r0 + lane / 8) of a piece at r0 (a
+  // multiple of 8) reads W row 4 (lane / 8) + wrow(r0). Every piece has two segments to land before its
+  // first reader: the issuing wave waits for it (counted vmcnt) at the end of its following segment.
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)min((int64_t)e.M * lda * 2, (int64_t)0x7FFFFFFF),
+                                        0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)min((int64_t)e.N * ldw * 2, (int64_t)0x7FFFFFFF),
+                                        0x00020000);
   const int pch = ((lane & 7) ^ (lane >> 3)) * 8;
-  const int drow = grp == 0 ? 64 * wl + (lane >> 3) : 64 * wl + 4 * (lane >> 3);
-  char* dbase = smem + (grp == 0 ? 0 : 2 * PP_HALF) + 64 * wl * 128;
-  // the operand rows (A: tile row origin, W: tile column origin) and K-tile of step s
-  auto step_tile = [&](int s, int& om0, int& on0, int& kt) {
-    const int T = s / nk;
-    kt = s - T * nk;
-    tile_origin((int)blockIdx.x + T * (int)gridDim.x, om0, on0);
-  };
-  auto dma_step = [&](int s) {  // this wave's 8 pieces of step s into buffer s & 1
-    int om0, on0, kt;
-    step_tile(s, om0, on0, kt);
-    const int vo = ((grp == 0 ? om0 : on0) + drow) * ldo * 2 + pch * 2;
-    char* dst = dbase + (s & 1) * W8_BUF;
+  const int r0g = 128 * grp + 32 * wl;                         // this wave's first A / W image row
+  const int voA = ((r0g + (lane >> 3)) * lda + pch) * 2;      // + tile row origin * lda * 2
+  const int voW = (4 * (lane >> 3) * ldw + pch) * 2;           // + (tile column origin + wrow) * ldw * 2
+  auto wrow = [](int r0) { return 64 * (r0 >> 6) + 4 * (r0 & 15) + ((r0 >> 4) & 3); };
+  auto dma_A = [&](int s, int om0, int kt) {
+    char* buf = smem + (s & 1) * W8_BUF;
+    const int vo = voA + om0 * lda * 2;
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int roff = grp == 0 ? 8 * p : 32 * (p & 1) + (p >> 1);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + 8 * p * 128), 16,
-                                               vo, kt * 128 + roff * ldo * 2, 0, 0);
+    for (int p = 0; p < 4; ++p) {
+      const int so = kt * 128 + 8 * p * lda * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(buf + (r0g + 8 * p) * 128),
+                                               16, vo, so, 0, 0);
     }
   };
-  auto dma_cols = [&](int s) {  // wave 0: the column vector of step s's tile into its parity slot
+  auto dma_W = [&](int s, int on0, int kt) {
+    char* buf = smem + (s & 1) * W8_BUF + 2 * PP_HALF;
+    const int vw = voW + on0 * ldw * 2;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int r0 = r0g + 8 * p;
+      const int so = kt * 128 + wrow(r0) * ldw * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (__attribute__((address_space(3))) void*)(buf + r0 * 128), 16,
+                                               vw, so, 0, 0);
+    }
+  };
+  auto dma_cols = [&](int T, int on0) {  // wave 0: tile T's column vector into its parity slot
     if (EPI == RF_EPI_NONE) return;
-    int om0, on0, kt;
-    step_tile(s, om0, on0, kt);
-    glds16(e.bias + min(on0 + 4 * lane, e.N - 4), smem + W8_CV + ((s / nk) & 1) * 1024);
+    glds16(e.bias + min(on0 + 4 * lane, e.N - 4), smem + W8_CV + (T & 1) * 1024);
   };
   const int lr = lane & 15;
   const int off0 = lr * 128 + (((lane >> 4) ^ (lane & 7)) << 4);
@@ -110,44 +126,57 @@ __global__ void __launch_bounds__(512, 2)
       a1[i] = *reinterpret_cast<const V8*>(base + aOff + i * 16 * 128 + dks);
     }
   };
-  auto compute = [&](bool first) {
+  auto compute = [&]() {
     __builtin_amdgcn_s_setprio(1);
-    if (first) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a0[i], b0[j], f32x4{0.f, 0.f, 0.f, 0.f});
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
-    }
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+#if defined(RF_W8_STAMPS)  // diagnostic build (tools/w8_stamps.py): waves 0 and 4 stamp s_memtime around
+  // every barrier into LDS (no vector-memory op, so the counted vmcnt waits stay exact), flushed at the end
+  unsigned long long* lst = reinterpret_cast<unsigned long long*>(smem + W8_CV + 2048) + grp * W8_NSTAMP;
+  int nstp = 0;
+  auto stamp = [&]() {
+    if (wl == 0 && nstp < W8_NSTAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (lane == 0) lst[nstp] = t;
+    }
+    ++nstp;
+  };
+#else
+  auto stamp = [&]() {};
+#endif
   auto bar = [&]() {
     __builtin_amdgcn_sched_barrier(0);
+    stamp();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    stamp();
     __builtin_amdgcn_sched_barrier(0);
   };
   constexpr int NST = 32;  // epilogue stores per wave (interior tile): 8 blocks x 4 rows
-  // epilogue of the tile of step s (its last K-tile just computed): lane (c = l & 15, g = l >> 4) holds
-  // rows 4 g + r of each 16-row block i and the output columns 4 c .. 4 c + 3 of the wave's 64
-  auto epilogue = [&](int s) {
-    int m0, n0, kt;
-    step_tile(s, m0, n0, kt);
+  // epilogue of tile T at (m0, n0): lane (c = l & 15, g = l >> 4) holds rows 4 g + r of each 16-row block
+  // i and the output columns 4 c .. 4 c + 3 of the wave's 64. Returns the stores it left in flight.
+  auto epilogue = [&](int T, int m0, int n0) {
     const bool interior = (m0 + 256 <= e.M) && (n0 + 256 <= e.N);
     int el = lane;
     asm volatile("" : "+v"(el));
     const int erow = m0 + wr * 128 + 4 * (el >> 4);
     const int ecol = n0 + wq * 64 + 4 * (el & 15);
     float bv[4], gm[4], bt[4];
-    const float* cb = reinterpret_cast<const float*>(smem + W8_CV + ((s / nk) & 1) * 1024);
+    const float* cb = reinterpret_cast<const float*>(smem + W8_CV + (T & 1) * 1024);
     lds_cols<EPI, 4>(cb, ecol - n0, bv, gm, bt);
     constexpr bool FSC = EPI == RF_EPI_BIAS || EPI == RF_EPI_BIAS_GELU;
     float csc = 1.f;
@@ -173,68 +202,109 @@ __global__ void __launch_bounds__(512, 2)
     return interior ? NST : 0;
   };
   auto wait_lgkm0 = []() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-  // the counted wait of a load segment: its DMA pieces (issued first) landed, the epilogue's stores
-  // (issued after them) may stay in flight
-  auto wait_dma = [&](int nst) {
-    if (nst >= NST) wait_vmcnt<NST>();
-    else wait_vmcnt<0>();
+  // counted wait: every vector-memory op of this wave but the `younger` newest has completed (DMA pieces
+  // come in fours, an interior epilogue issues NST stores)
+  auto wait_n = [&](int younger) {
+    switch (younger) {
+      case 4: wait_vmcnt<4>(); break;
+      case NST: wait_vmcnt<NST>(); break;
+      case NST + 4: wait_vmcnt<NST + 4>(); break;
+      default: wait_vmcnt<0>(); break;
+    }
   };
 
-  // prologue: step 0 (both operands), tile 0's column vector; group 0 reads step 0 and DMAs A of step 1.
-  // Both groups then run the same loop shape (load segment, barrier, compute segment, barrier; only the
-  // accumulators are carried across iterations), group 0 one segment ahead: it computes step 0 first.
-  dma_step(0);
-  if (wave == 0) dma_cols(0);
+  // tile bookkeeping of step m (read / computed this iteration): its tile T and origin, the tile before
+  // (for its epilogue) and the tile after (for the DMA of steps m + 1, m + 2 and the next column vector)
+  int T = 0, kt = 0, cm0, cn0, pm0 = 0, pn0 = 0, nm0 = 0, nn0 = 0;
+  tile_origin(0, cm0, cn0);
+  if (ntile > 1) tile_origin(1, nm0, nn0);
+  // prologue: step 0 (every wave its halves), tile 0's column vector; then step 1 (group 0 its halves, group 1
+  // its A half, which must land before group 0 reads step 1) while group 0 reads step 0; group 0 computes
+  // step 0 (one segment ahead of group 1)
+  dma_A(0, cm0, 0);
+  dma_W(0, cn0, 0);
+  if (wave == 0) dma_cols(0, cn0);
   wait_vmcnt<0>();
   bar();
+  if (J > 1) {
+    const bool same = nk > 1;
+    dma_A(1, same ? cm0 : nm0, same ? 1 : 0);
+    if (grp == 0) dma_W(1, same ? cn0 : nn0, same ? 1 : 0);
+  }
   if (grp == 0) {
-    if (J > 1) dma_step(1);
     read_step(0);
     wait_lgkm0();
-    wait_vmcnt<0>();
   }
   bar();
+  int nst = 0;
+  zero_acc();  // tile 0 (later tiles: after each epilogue)
   if (grp == 0) {
-    compute(true);
+    compute();
+    wait_vmcnt<0>();
     bar();
   }
-  // group 0's iteration m: load segment of step m (A of m + 1, epilogue of m - 1 if it ended a tile, the
-  // fragments of m) beside group 1's compute of m - 1, then its compute of m beside group 1's load of m.
-  // Group 1's iteration m: load segment of step m (W of m + 1, epilogue of m - 1, fragments of m) beside
-  // group 0's compute of m, then its compute of m beside group 0's load of m + 1.
-  for (int m = grp == 0 ? 1 : 0; m < J; ++m) {
-    const int kt = m % nk;
-    if (m + 1 < J) dma_step(m + 1);
+  // Iteration m: the load segment of step m (beside the partner's compute: group 0's beside group 1's
+  // compute of m - 1, group 1's beside group 0's compute of m) — the DMA of step m + 1, the previous
+  // tile's epilogue when step m starts a tile, the fragments of step m — then the compute segment of
+  // step m (group 1: headed by its A half of step m + 2). Only the accumulators are carried across
+  // iterations.
+  const int m_first = grp == 0 ? 1 : 0;
+  for (int m = m_first; m < J; ++m) {
+    if (m > 0) kt = kt + 1 == nk ? 0 : kt + 1;  // kt = m % nk (kt of step 0 set above)
+    const bool tstart = kt == 0 && m > 0;
+    if (tstart) {
+      ++T;
+      pm0 = cm0; pn0 = cn0;
+      cm0 = nm0; cn0 = nn0;
+      if (T + 1 < ntile) tile_origin(T + 1, nm0, nn0);
+    }
+    const bool n1 = m + 1 < J;
+    if (n1) {
+      const bool same = kt + 1 < nk;
+      if (grp == 0) dma_A(m + 1, same ? cm0 : nm0, same ? kt + 1 : 0);
+      dma_W(m + 1, same ? cn0 : nn0, same ? kt + 1 : 0);
+    }
     // the next tile's column vector (wave 0, at the tile's second K-tile: its parity slot was last read by
     // group 1's epilogue of the tile before, one segment earlier; nk >= 2)
-    if (wave == 0 && kt == 1 && m - 1 + nk < J) dma_cols(m - 1 + nk);
-    int nst = 0;
-    if (kt == 0 && m > 0) nst = epilogue(m - 1);
-    if (kt == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (wave == 0 && kt == 1 && T + 1 < ntile) dma_cols(T + 1, nn0);
+    nst = 0;
+    if (tstart) {
+      nst = epilogue(T - 1, pm0, pn0);
+      zero_acc();
     }
     __builtin_amdgcn_sched_barrier(0);  // the fragment reads after the epilogue (register pressure)
     read_step(m);
+    if (grp == 1) wait_n((n1 ? 4 : 0) + nst);  // its A half of step m + 1 (issued a segment ago) landed
     wait_lgkm0();
-    wait_dma(nst);
     bar();
-    compute(false);
+    bool n2 = false;
+    if (grp == 1 && m + 2 < J) {
+      const bool same = kt + 2 < nk;
+      dma_A(m + 2, same ? cm0 : nm0, same ? kt + 2 : kt + 2 - nk);
+      n2 = true;
+    }
+    compute();
+    wait_n(nst + (n2 ? 4 : 0));  // this wave's pieces of the load segment (step m + 1) landed
     bar();
   }
   if (grp == 0) {  // group 0's last load segment: the last tile's epilogue, beside group 1's last compute
-    epilogue(J - 1);
+    epilogue(T, cm0, cn0);
     bar();
   } else {
-    epilogue(J - 1);
+    epilogue(T, cm0, cn0);
   }
+#if defined(RF_W8_STAMPS)
+  if (e.stamps && wl == 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = lane; i < W8_NSTAMP; i += 64)
+      e.stamps[((size_t)blockIdx.x * 2 + grp) * W8_NSTAMP + i] = i < nstp ? lst[i] : 0ull;
+  }
+#endif
   wait_vmcnt<0>();
 }
 
 template <typename E, int EPI>
-void launch_w8(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
+static void launch_w8(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
                       hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
@@ -247,14 +317,19 @@ void launch_w8(int M, int N, int K, const void* A, int lda, const void* W, int l
   k_gemm_w8<E, EPI><<<grid, 512, W8_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
 }
 
-#define RF_W8_INST(E, EPI)                                                                                     \
-  template void launch_w8<E, EPI>(int, int, int, const void*, int, const void*, int, const EpiArgs&, hipStream_t);
-RF_W8_INST(bf16, RF_EPI_NONE)
-RF_W8_INST(bf16, RF_EPI_BIAS)
-RF_W8_INST(bf16, RF_EPI_BIAS_GELU)
-RF_W8_INST(f16, RF_EPI_NONE)
-RF_W8_INST(f16, RF_EPI_BIAS)
-RF_W8_INST(f16, RF_EPI_BIAS_GELU)
-#undef RF_W8_INST
+// the entry rf_gemm.hip calls (a plain function: the kernel templates are instantiated implicitly here,
+// as the dispatcher of rf_gemm.hip does for its own kernels)
+void gemm_w8(bool half, int epi, int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
+             hipStream_t s) {
+  if (half) {
+    if (epi == RF_EPI_NONE) launch_w8<f16, RF_EPI_NONE>(M, N, K, A, lda, W, ldw, e, s);
+    else if (epi == RF_EPI_BIAS) launch_w8<f16, RF_EPI_BIAS>(M, N, K, A, lda, W, ldw, e, s);
+    else launch_w8<f16, RF_EPI_BIAS_GELU>(M, N, K, A, lda, W, ldw, e, s);
+  } else {
+    if (epi == RF_EPI_NONE) launch_w8<bf16, RF_EPI_NONE>(M, N, K, A, lda, W, ldw, e, s);
+    else if (epi == RF_EPI_BIAS) launch_w8<bf16, RF_EPI_BIAS>(M, N, K, A, lda, W, ldw, e, s);
+    else launch_w8<bf16, RF_EPI_BIAS_GELU>(M, N, K, A, lda, W, ldw, e, s);
+  }
+}
 
 }  // namespace rf

@@ -76,6 +76,7 @@ TOPK_SAMPLE = 2048  # dense seed block that sets each row's first candidate thre
 TOPK_CAP = 1024     # candidate list per row and chunk
 TOPK_MAX_K = 256    # rf_topk_* limits (rf_retrieval.hip TK_KMAX, TK_DENSE_MAX)
 TOPK_MAX_SAMPLE = 2048
+TILE_CAND_CAP = 32  # rf_retrieval.hip RK_TCAP: candidates staged per (row, 256-column tile)
 # column chunks after the seed: each TOPK_GROWTH - 1 times the columns already seen (2: doubling). A larger
 # factor means fewer launches and merges but a lower threshold relative to each chunk (about
 # k * (TOPK_GROWTH - 1) candidates per row and chunk). 1M items x 4096 queries, top-50, 16x16x32 family:
@@ -212,9 +213,12 @@ def shard_rank(queries: torch.Tensor, shard: CatalogShard, s_label: torch.Tensor
     inv_t = 1.0 / temp
     dev = q.device
     s0 = min(N, sample) if k > 0 else 0
-    # the dense seed: blocks of `sample` columns, their top-k merged block by block (one block at the
-    # default seed_n = s0; a larger seed_n would lower the first candidate chunks' rate)
-    seed_n = s0
+    # the dense seed: blocks of `sample` columns, their top-k merged block by block. After a seed of n_s
+    # columns a row expects k * 256 / n_s candidates per 256-column tile, and the kernel stages at most
+    # TILE_CAND_CAP (RK_TCAP) per (row, tile) before the row overflows into the dense re-rank: the seed is
+    # sized to keep that expectation at a quarter of the cap (one block up to k = 64; 4 blocks at k = 256)
+    need = 256 * k * 4 // TILE_CAND_CAP  # columns for k * 256 / n_s <= TILE_CAND_CAP / 4
+    seed_n = min(N, max(s0, -(-need // sample) * sample)) if k > 0 else 0
     blocks = [(o, min(sample, seed_n - o)) for o in range(0, seed_n, sample)]
     # column chunks after the seed: each (grow - 1) times everything before it. A row expects about
     # k * (grow - 1) candidates per chunk, so the factor is capped to keep that within half the list

@@ -7,7 +7,7 @@ name=$1; src=$2; shift 2
 cd "$(dirname "$0")/../recformer_amd/csrc"
 mkdir -p build/var ../../tools/var
 objs=""
-for f in rf_rowops rf_embed_bwd rf_gemm rf_gemm_tn rf_attn rf_attn_bwd rf_global rf_retrieval rf_optim rf_pack; do
+for f in rf_rowops rf_embed_bwd rf_gemm rf_gemm_w8 rf_gemm_tn rf_attn rf_attn_bwd rf_global rf_retrieval rf_optim rf_pack; do
   if [ "$f.hip" = "$src" ]; then
     # the retired GEMM main loops (knob gemm_variant 1-7) exist only in these A/B builds
     extra=""; [ "$f" = rf_gemm ] && extra="-DRF_GEMM_EXPERIMENTS"

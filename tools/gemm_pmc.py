@@ -3,7 +3,7 @@ passes and kernel traces of the GEMMs alone): qkv (65536 x 2304 x 768, bias + q-
 (65536 x 768 x 768, bias), FFN1 (65536 x 3072 x 768, bias + GELU), FFN2 (65536 x 768 x 3072, bias).
 Operands at the bench's scales (activations ~N(0, 1) LayerNorm outputs, weights ~N(0, 0.02)), bf16.
 
-    python tools/gemm_pmc.py [reps] [shape,...]
+    RF_KNOBS=name=v,... python tools/gemm_pmc.py [reps] [shape,...]
 """
 import os
 import sys
@@ -20,6 +20,10 @@ SHAPES = {"qkv": (65536, 2304, 768, ops.RF_EPI_BIAS, 768), "out": (65536, 768, 7
 
 
 def main():
+    from recformer_amd import _lib
+    for kv in filter(None, os.environ.get("RF_KNOBS", "").split(",")):  # e.g. RF_KNOBS=gemm_w8=1
+        k, v = kv.split("=")
+        _lib.set_knob(k, int(v))
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
     names = sys.argv[2].split(",") if len(sys.argv) > 2 else list(SHAPES)
     dev = torch.device("cuda")
