@@ -207,8 +207,10 @@ __global__ void __launch_bounds__(512, 2)
   auto wait_n = [&](int younger) {
     switch (younger) {
       case 4: wait_vmcnt<4>(); break;
+      case 8: wait_vmcnt<8>(); break;
       case NST: wait_vmcnt<NST>(); break;
       case NST + 4: wait_vmcnt<NST + 4>(); break;
+      case NST + 8: wait_vmcnt<NST + 8>(); break;
       default: wait_vmcnt<0>(); break;
     }
   };
@@ -273,8 +275,14 @@ __global__ void __launch_bounds__(512, 2)
       zero_acc();
     }
     __builtin_amdgcn_sched_barrier(0);  // the fragment reads after the epilogue (register pressure)
+#if defined(RF_W8_LATE)
+    // A/B: every wait in the load segment, before the reads: all but this segment's pieces and stores
+    wait_n((n1 ? (grp == 0 ? 8 : 4) : 0) + nst);
+    read_step(m);
+#else
     read_step(m);
     if (grp == 1) wait_n((n1 ? 4 : 0) + nst);  // its A half of step m + 1 (issued a segment ago) landed
+#endif
     wait_lgkm0();
     bar();
     bool n2 = false;
@@ -284,7 +292,9 @@ __global__ void __launch_bounds__(512, 2)
       n2 = true;
     }
     compute();
+#if !defined(RF_W8_LATE)
     wait_n(nst + (n2 ? 4 : 0));  // this wave's pieces of the load segment (step m + 1) landed
+#endif
     bar();
   }
   if (grp == 0) {  // group 0's last load segment: the last tile's epilogue, beside group 1's last compute
