@@ -1702,9 +1702,11 @@ extern "C" int rf_band_attn_fwd_drop(int dtype, int B, int Lp, int H, int hd, in
                                                               (E*)out, ld_out, dr);                        \
     }                                                                                                     \
   } while (0)
-        // pipe3 (three workgroups per CU; bit-identical to pipe2) only when the knob asks for it (band_path 3):
-        // 83.0 vs 85.8 us per launch, but step-neutral in same-process C2 A/Bs (round 4; round 5: -0.2%,
-        // +0.4%, +0.3%, gpurun_out/r05t, r05v) — the GEMM after it runs slower
+        // pipe3 (three workgroups per CU; bit-identical to pipe2) by default (band_path 3; 0 = pipe2): round 6's
+        // kernel traces of whole C2 steps, one setting per process in ABBA order (tools/gpu/band_trace.sh,
+        // profiles/r06/band_trace_abba.txt): band 83.2 / 83.3 vs 86.7 / 87.1 us, every other kernel within
+        // 0.5 us (no slower GEMM after it), kernel time per 50 steps 608.0 / 610.3 vs 611.7 / 611.7 ms,
+        // 12.100 / 12.142 vs 12.149 / 12.163 ms per step (the earlier A/Bs, -0.2 .. +0.4%, were within noise)
         const bool band_pipe3 = g_knob[KNOB_BAND_PATH] == 3;
         const size_t lds3 = AQ_MK + (size_t)(qpb + 1) * 16;
         // training (dropout) keeps pipe2: pipe3's dropout form would spill at the 3-wave register budget

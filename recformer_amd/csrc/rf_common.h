@@ -50,7 +50,7 @@ enum Knob {
   KNOB_GEMM_GN = 0,     // ping-pong GEMM raster: column-group width (6)
   KNOB_GEMM_VARIANT,    // bf16 GEMM kernel family (8 = four-wave interleaved, 6 = four-wave, 5 = ping-pong, 7 = BK32 ring)
   KNOB_BAND_QPB,        // band attention query blocks per workgroup (0 = auto)
-  KNOB_BAND_PATH,       // band attention kernel: 0 pipe2, 1 pipe (v1), 2 one-shot
+  KNOB_BAND_PATH,       // band attention kernel: 3 pipe3 (default), 0 pipe2, 1 pipe (v1), 2 one-shot
   KNOB_GFOLD_PATH,      // global fold: 0 auto, 1 GEMV, 2 MFMA, 3 auto without the ring partial kernel, 4 ring at any Lp
   KNOB_GFOLD_QSPLIT,    // global fold query/key kernel: max column splits (8)
   KNOB_GEMM_PF,         // four-wave GEMM L2 prefetch: -1 auto (2 for K >= 2048), else distance in K-tiles (0 = off), + 256: W rows too

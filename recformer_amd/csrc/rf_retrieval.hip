@@ -656,12 +656,15 @@ __device__ void wave_topk(const uint32_t* keys, const int32_t* ids, int n, int k
     hi = wave_max_u(hi);
     need = kk;
     while (hi > lo) {
-      const uint64_t w = ((uint64_t)(hi - lo)) / 256 + 1;
+      // bins of 2^sh keys, sh the least with (hi - lo) >> sh < 256: a shift per element instead of a 64-bit
+      // division (the selection is the same: the bin holding the kk-th largest key, then its range)
+      const uint32_t span = hi - lo;
+      const int sh = max(0, 24 - (int)__builtin_clz(span));  // bit length of span minus 8
       for (int b = lane; b < 256; b += 64) hist[b] = 0;
       __builtin_amdgcn_wave_barrier();
       for (int e = lane; e < n; e += 64) {
         const uint32_t key = keys[e];
-        if (key >= lo && key <= hi) atomicAdd(&hist[(int)((key - lo) / w)], 1);
+        if (key >= lo && key <= hi) atomicAdd(&hist[(int)((key - lo) >> sh)], 1);
       }
       __builtin_amdgcn_wave_barrier();
       // bins from the top: lane l owns bins 255 - 4l .. 252 - 4l; suffix sums across lanes
@@ -695,8 +698,8 @@ __device__ void wave_topk(const uint32_t* keys, const int32_t* ids, int n, int k
       bsel = __shfl(bsel, src, 64);
       above = __shfl(above, src, 64);
       need -= above;
-      const uint64_t nlo = (uint64_t)lo + (uint64_t)bsel * w;
-      const uint64_t nhi = min((uint64_t)hi, nlo + w - 1);
+      const uint64_t nlo = (uint64_t)lo + ((uint64_t)bsel << sh);
+      const uint64_t nhi = min((uint64_t)hi, nlo + (1ull << sh) - 1);
       lo = (uint32_t)nlo;
       hi = (uint32_t)nhi;
       __builtin_amdgcn_wave_barrier();

@@ -12,7 +12,7 @@
 namespace rf {
 
 static thread_local char g_err[512];
-int g_knob[KNOB_COUNT] = {6, 8, 0, 0, 0, 8, -1, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0};
+int g_knob[KNOB_COUNT] = {6, 8, 0, 3, 0, 8, -1, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0};
 const uint64_t* g_seed_dev = nullptr;
 
 void set_error(const char* fmt, ...) {
