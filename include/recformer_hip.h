@@ -59,7 +59,7 @@ const uint64_t* rf_set_seed_source(const uint64_t* step_counter);
 int rf_abi_version(void);
 /* Diagnostics (A/B tools; the product never sets them): set a launch-path tuning knob ("gemm_gn",
  * "gemm_variant", "band_qpb", "band_path", "gfold_path", "gfold_qsplit", "gemm_pf", "gemm_mfma32",
- * "rank_w32", "gfold_chunk", "gemm_skinny", "epi_tile", "tn_wgs", "mid_tile", "colsum_slices", "gemm_n192", "adam_nt", "gemm_w8") for the process;
+ * "rank_w32", "gfold_chunk", "gemm_skinny", "epi_tile", "tn_wgs", "mid_tile", "colsum_slices", "gemm_n192", "adam_nt", "gemm_w8", "gemm_w4p") for the process;
  * returns the previous value
  * (INT32_MIN and rf_last_error() for an unknown name). The compiled defaults are the measured choices;
  * no launch reads the environment. */

@@ -77,6 +77,8 @@ enum Knob {
   KNOB_GEMM_W8,         // 16-bit EPI_NONE / EPI_BIAS / EPI_BIAS_GELU GEMMs on the eight-wave ping-pong kernel
                         // (k_gemm_w8: two waves per SIMD, one computing while its partner loads): 1 on, 0 the
                         // four-wave kernel
+  KNOB_GEMM_W4P,        // 16-bit EPI_NONE / EPI_BIAS / EPI_BIAS_GELU GEMMs on the four-wave kernel with k-step-split
+                        // LDS planes (k_gemm_w4p: operand DMA spread over both phases): 1 on, 0 k_gemm_w4
   KNOB_COUNT
 };
 extern int g_knob[KNOB_COUNT];

@@ -1239,6 +1239,9 @@ static void launch_w4(int M, int N, int K, const void* A, int lda, const void* W
 // the eight-wave ping-pong kernel (rf_gemm_w8.hip): EPI_NONE / EPI_BIAS / EPI_BIAS_GELU, 16-bit C
 void gemm_w8(bool half, int epi, int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
              hipStream_t s);
+// the four-wave kernel on k-step-split LDS planes (rf_gemm_w8.hip, knob gemm_w4p); false: not instantiated there
+bool gemm_w4p(bool half, int epi, bool cf32, int M, int N, int K, const void* A, int lda, const void* W, int ldw,
+              const EpiArgs& e, hipStream_t s);
 
 // ---- k_gemm_w32: the encoder GEMMs on w32_run (rf_w32.h) ----------------------------------------
 template <typename E, int EPI, bool CF32>
@@ -1829,6 +1832,11 @@ static void dispatch_tile(int M, int N, int K, const void* A, int lda, const voi
         gemm_w8(std::is_same<E, f16>::value, EPI, M, N, K, A, lda, W, ldw, e, s);
         return;
       }
+    }
+    if constexpr (!RF32) {
+      if (w4_ok && g_knob[KNOB_GEMM_W4P] && !g_knob[KNOB_GEMM_MFMA32] &&
+          gemm_w4p(std::is_same<E, f16>::value, EPI, CF32, M, N, K, A, lda, W, ldw, e, s))
+        return;
     }
     if (w4_ok) launch_w4<E, EPI, CF32, RF32, true>(M, N, K, A, lda, W, ldw, e, s);
     else launch_bf16<E, 256, 256, 128, 64, 32, 4, EPI, CF32, RF32>(M, N, K, A, lda, W, ldw, e, s);

@@ -343,3 +343,349 @@ void gemm_w8(bool half, int epi, int M, int N, int K, const void* A, int lda, co
 }
 
 }  // namespace rf
+
+namespace rf {
+
+// ---- the four-wave kernel on ks-split LDS planes (knob gemm_w4p) -----------------------------------------
+// k_gemm_w4's 256 x 256 tile, 4 waves of 128 x 128 (one per SIMD), the same MFMA sequence per accumulator
+// (so bit-identical outputs), with the operand image of a K-tile split by k-step: plane ks holds k
+// [32 ks, 32 ks + 32) of the 256 A and the 256 W rows as 64-B rows (TileGeo<32>'s chunk swizzle). A plane is
+// free as soon as every wave has read its fragments, so each phase refills the plane the PREVIOUS phase
+// finished with: phase A(t) (MFMAs on k-step 0, reads of k-step 1 of K-tile t) DMAs plane 0 of K-tile t + 2;
+// phase B(t) (k-step 1, reads of k-step 0 of t + 1) DMAs plane 1 of t + 2 — 8 pieces per wave per phase
+// instead of 16 in phase B only (k_gemm_w4), with one barrier per phase, and every piece two barriers
+// (three phases) ahead of its first read. tools/micro/mfma_dma.hip: the w4 loop shape runs 3,286 cycles
+// per K-tile with its 16 pieces in one phase, 2,816 with 8 + 8 (2,782 without any DMA).
+constexpr int WP_BUF = 4 * PP_HALF;       // one K-tile: plane 0 | plane 1, each A rows 0-255 | W image rows 0-255
+constexpr int WP_PLANE = 2 * PP_HALF;     // 32 KiB: 512 rows x 64 B
+constexpr int WP_CV = 2 * WP_BUF;         // column vectors [parity][3][1 KiB]
+constexpr int WP_LDS = WP_CV + 6 * 1024;
+
+template <typename E, int EPI, bool CF32>
+__global__ void __launch_bounds__(256, 1)
+    k_gemm_w4p(int K, const E* __restrict__ A, int lda, const E* __restrict__ W, int ldw, EpiArgs e, int nTm,
+               int nTn) {
+  typedef typename H16<E>::x8 V8;
+  constexpr bool RF32 = false;
+  constexpr bool OUT32 = CF32 || EPI == RF_EPI_COS;
+  constexpr int NJ = 8, TN = 256;
+  constexpr int S = (OUT32 || EPI == RF_EPI_BIAS_GELU_AUX) ? 64 : 32;  // epilogue stores per wave (interior)
+  constexpr int C = (EPI == RF_EPI_NONE || EPI == RF_EPI_DGELU) ? 0 : 1;  // column-vector DMA per wave and tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles = nTm * nTn;
+  int v = blockIdx.x;
+  if (v >= tiles) return;
+  const int GN = e.gn > 0 ? min(e.gn, nTn) : nTn;
+  auto tile_origin = [&](int vv, int& om0, int& on0) {
+    const int wg = xcd_remap(vv, tiles);
+    const int g = wg / (nTm * GN);
+    const int gw = min(GN, nTn - g * GN);
+    const int rem = wg - g * nTm * GN;
+    const int tm = rem / gw;
+    om0 = tm * 256;
+    on0 = (g * GN + rem - tm * gw) * TN;
+  };
+  int m0, n0, nm0 = 0, nn0 = 0;
+  tile_origin(v, m0, n0);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;  // compute block: A rows 128 wr, W image rows 128 wc
+  const int nk = K >> 6;
+  // DMA: a piece is 16 plane rows x 64 B (lane: row + lane / 4, 16-B slot lane & 3, fetched from source
+  // chunk slot ^ f(row), f(r) = (-(r >> 2)) & 3 — TileGeo<32>'s swizzle, row = the plane row, a multiple of
+  // 16 plus lane / 4). Wave w stages A rows 64 w .. 64 w + 63 (pieces p = 0..3) and the W image rows of
+  // fragments f = 4 (w & 1) + p of W-half w >> 1 (image row 16 f + j of a half holds W row 8 j + f, or
+  // 64 (f >> 2) + 4 j + (f & 3) for fp32 out: whole-line epilogue stores, as k_gemm_w4's wperm).
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)min((int64_t)e.M * lda * 2, (int64_t)0x7FFFFFFF),
+                                        0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)min((int64_t)e.N * ldw * 2, (int64_t)0x7FFFFFFF),
+                                        0x00020000);
+  const int jl = lane >> 2;                                              // plane row within a piece
+  const int sch = ((lane & 3) ^ ((-(jl >> 2)) & 3)) * 8;                 // source chunk (elements)
+  const int arow_l = 64 * wave + jl;                                     // + 16 p
+  const int whalf = wave >> 1;
+  const int wrow_l = 128 * whalf + (OUT32 ? 4 * jl : 8 * jl);           // + wfrag(f)
+  auto wfrag = [](int f) { return OUT32 ? 64 * (f >> 2) + (f & 3) : f; };
+  auto voffA = [&](int bm0) { return ((bm0 + arow_l) * lda + sch) * 2; };
+  auto voffW = [&](int bn0) { return ((bn0 + wrow_l) * ldw + sch) * 2; };
+  int vA = voffA(m0), vW = voffW(n0), vAn = vA, vWn = vW;
+  auto launder = [&]() { asm volatile("" : "+v"(vA), "+v"(vW), "+v"(vAn), "+v"(vWn)); };
+  // piece p (0-3 A, 4-7 W) of plane ks of virtual K-tile kv (>= nk: the next tile's K-tile kv - nk), issued
+  // p = 0..7 in order: the soffsets run as two chains (A: +16 rows per piece, W: +1 row per piece) so only
+  // three row-step scalars stay live (per-piece products were kept as SGPR spills in VGPR lanes and
+  // reloaded with v_readlane inside the MFMA stream — k_gemm_w4's round-3 finding)
+  const int stA = 16 * lda * 2, stW = ldw * 2, wb = wfrag(4 * (wave & 1)) * ldw * 2;
+  int sA = 0, sW = 0;
+  auto dma_piece = [&](int kv, int ks, int p) {
+    const bool nxt = kv >= nk;
+    const int kt = nxt ? kv - nk : kv;
+    char* plane = smem + (kv & 1) * WP_BUF + ks * WP_PLANE;
+    if (p == 0) { sA = kt * 128 + ks * 64; asm volatile("" : "+s"(sA)); }
+    if (p == 4) { sW = kt * 128 + ks * 64 + wb; asm volatile("" : "+s"(sW)); }
+    if (p < 4) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(plane + (64 * wave + 16 * p) * 64),
+                                               16, nxt ? vAn : vA, sA, 0, 0);
+      int st = stA;
+      asm volatile("" : "+s"(st));
+      sA += st;
+    } else {
+      const int f = 4 * (wave & 1) + (p - 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsW, (__attribute__((address_space(3))) void*)(plane + PP_HALF + (128 * whalf + 16 * f) * 64), 16,
+          nxt ? vWn : vW, sW, 0, 0);
+      int st = stW;
+      asm volatile("" : "+s"(st));
+      sW += st;
+    }
+  };
+  auto dma_cols = [&](int tm0, int tn0, int par) {
+    if (C == 0) return;
+    const int vec = wave % 3;
+    const float* src = EPI == RF_EPI_COS ? e.rw : e.bias;
+    int idx = min(tn0 + 4 * lane, e.N - 4);
+    if (EPI == RF_EPI_BIAS_RESID_LN && vec == 1) src = e.lgamma;
+    if (EPI == RF_EPI_BIAS_RESID_LN && vec == 2) src = e.lbeta;
+    if (EPI == RF_EPI_COS && vec == 1) {
+      src = e.ra;
+      idx = min(tm0 + 4 * lane, e.M - 4);
+    }
+    glds16(src + idx, smem + WP_CV + (par * 3 + vec) * 1024);
+  };
+  // fragment reads: 16 rows (lane & 15) x the 4 chunks (lane >> 4) of a plane's 64-B rows, swizzled
+  const int lr = lane & 15;
+  const int offr = lr * 64 + (((lane >> 4) ^ ((-(lr >> 2)) & 3)) << 4);
+  const int aOff = 128 * wr * 64 + offr, bOff = PP_HALF + 128 * wc * 64 + offr;
+  V8 a0[8], b0[8], a1[8], b1[8];
+  f32x4 acc[8][8];
+  auto readp = [&](int kv, int ks, int idx) {  // fragment idx (0-7 A, 8-15 W) of plane ks of K-tile kv
+    const char* plane = smem + (kv & 1) * WP_BUF + ks * WP_PLANE;
+    const V8 x = *reinterpret_cast<const V8*>(plane + (idx < 8 ? aOff + idx * 16 * 64 : bOff + (idx - 8) * 16 * 64));
+    if (ks == 0) {
+      if (idx < 8) a0[idx] = x; else b0[idx - 8] = x;
+    } else {
+      if (idx < 8) a1[idx] = x; else b1[idx - 8] = x;
+    }
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // the counted wait before a barrier: everything but the `younger` newest vector-memory ops of this wave
+  auto sync = [&](int younger) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int R1 = 16 + S + C < 63 ? 16 + S + C : 63;  // vmcnt is 6 bits: a larger count waits more, safely
+    if (younger == 16) wait_vmcnt<16>();
+    else if (younger == 16 + S + C) wait_vmcnt<R1>();
+    else wait_vmcnt<0>();
+    bar();
+  };
+
+  // prologue: both planes of K-tiles 0 and 1, the first tile's column vectors; k-step 0 of K-tile 0
+  dma_cols(m0, n0, 0);
+#pragma unroll
+  for (int kv = 0; kv < 2; ++kv)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int p = 0; p < 8; ++p) dma_piece(kv, ks, p);
+  wait_vmcnt<0>();
+  bar();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) readp(0, 0, i);
+  int tix = 0;
+  int relax = 0;  // vector-memory ops of the previous tile's epilogue (+ column DMA) still counted in vmcnt
+  bool first_tile = true;
+  for (;;) {
+    const bool has_next = v + (int)gridDim.x < tiles;
+    if (has_next) {
+      tile_origin(v + gridDim.x, nm0, nn0);
+    } else {
+      nm0 = m0;
+      nn0 = n0;
+    }
+    vAn = voffA(nm0);
+    vWn = voffW(nn0);
+    // ---- phase A(t): k-step 0 MFMAs of K-tile t; k-step 1 fragments of t; plane 0 of K-tile t + 2 ----
+    auto phaseA = [&](int t, auto zero) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        dma_piece(t + 2, 0, p);
+        readp(t, 1, p < 4 ? 8 + 2 * p : 2 * (p - 4));  // W fragments first (phase B's MFMA order)
+        readp(t, 1, p < 4 ? 8 + 2 * p + 1 : 2 * (p - 4) + 1);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = mfma16(a0[i], b0[j], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j]);
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 DMA piece
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 DS reads
+      }
+    };
+    // ---- phase B(t): k-step 1 MFMAs of K-tile t; k-step 0 fragments of t + 1; plane 1 of K-tile t + 2 ----
+    auto phaseB = [&](int t) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        dma_piece(t + 2, 1, p);
+        readp(t + 1, 0, p < 4 ? 8 + 2 * p : 2 * (p - 4));
+        readp(t + 1, 0, p < 4 ? 8 + 2 * p + 1 : 2 * (p - 4) + 1);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+    };
+    // S(t) before phase A(t): every wave's reads of plane 0 of K-tile t (phase B(t - 1)) done, plane 1 of K-tile
+    // t landed; M(t) before phase B(t): the reads of plane 1 of t done, plane 0 of t + 1 landed. The first
+    // three barriers of a tile also count the previous tile's epilogue stores and column DMA (relax).
+    if (!first_tile) sync(16 + relax);
+    launder();
+    phaseA(0, std::true_type{});
+    sync(16 + relax);
+    launder();
+    phaseB(0);
+    for (int t = 1; t < nk; ++t) {
+      sync(t == 1 ? 16 + relax : 16);
+      launder();
+      phaseA(t, std::false_type{});
+      sync(16);
+      launder();
+      phaseB(t);
+    }
+    first_tile = false;
+    // epilogue straight from the accumulators (k_gemm_w4's): lane (c = l & 15, g = l >> 4) holds rows
+    // 4 g + r of each 16-row block i and the columns [8c, 8c+8) (16-bit) / [4c, 4c+4) u [64+4c, ..)
+    const bool interior = (m0 + 256 <= e.M) && (n0 + TN <= e.N);
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const int erow = m0 + wr * 128 + 4 * (el >> 4);
+    const int ecol = n0 + wc * 128 + (OUT32 ? 4 : 8) * (el & 15);
+    float bv[8], gm[8], bt[8];
+    const float* cb = reinterpret_cast<const float*>(smem + WP_CV + (tix & 1) * 3 * 1024);
+    {
+      const int co = ecol - n0;
+      if (OUT32) {
+        lds_cols<EPI, 4>(cb, co, bv, gm, bt);
+        lds_cols<EPI, 4>(cb, co + 64, bv + 4, gm + 4, bt + 4);
+      } else {
+        lds_cols<EPI, 8>(cb, co, bv, gm, bt);
+      }
+    }
+    const int em0 = m0;
+    const void* tbase = reinterpret_cast<const E*>(e.C) + (int64_t)m0 * e.ldc;
+    constexpr bool FSC = !OUT32 && (EPI == RF_EPI_BIAS || EPI == RF_EPI_BIAS_GELU || EPI == RF_EPI_BIAS_GELU_AUX);
+    float csc = 1.f;
+    if (FSC) {
+      csc = ecol < e.scale_cols ? e.col_scale : 1.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bv[k] *= csc;
+    }
+    auto epilogue = [&](auto check) {
+      constexpr bool CK = decltype(check)::value;
+      constexpr bool ZP = !CK && !OUT32 && EPI == RF_EPI_DGELU;
+      if constexpr (ZP) {
+        constexpr int ZD = 16;
+        const char* zbase = reinterpret_cast<const char*>(e.R) + (int64_t)em0 * e.ldr * (int)sizeof(E);
+        auto zload = [&](int k) {
+          const int row = erow + (k >> 2) * 16 + (k & 3);
+          return *reinterpret_cast<const V8*>(zbase + (uint32_t)(((row - em0) * e.ldr + ecol) * (int)sizeof(E)));
+        };
+        V8 zv[ZD];
+#pragma unroll
+        for (int k = 0; k < ZD; ++k) zv[k] = zload(k);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+          const int i = k >> 2, r = k & 3;
+          const V8 z = zv[k % ZD];
+          if (k + ZD < 32) zv[k % ZD] = zload(k + ZD);
+          float vv[8];
+#pragma unroll
+          for (int f = 0; f < 8; ++f) vv[f] = acc[i][f][r];
+          epi_seg<E, EPI, CF32, RF32, 8, CK, true, FSC, true>(e, erow + i * 16 + r, ecol, vv, bv, gm, bt, 0.f, tbase,
+                                                              em0, csc, z);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float vv[8];
+#pragma unroll
+            for (int f = 0; f < 8; ++f) vv[f] = acc[i][f][r];
+            const int row = erow + i * 16 + r;
+            const float rsc = EPI == RF_EPI_COS ? cb[256 + row - em0] : 0.f;
+            if (OUT32) {
+              epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol, vv, bv, gm, bt, rsc);
+              epi_seg<E, EPI, CF32, RF32, 4, CK>(e, row, ecol + 64, vv + 4, bv + 4, gm + 4, bt + 4, rsc);
+            } else {
+              epi_seg<E, EPI, CF32, RF32, 8, CK, !CK, FSC>(e, row, ecol, vv, bv, gm, bt, rsc, tbase, em0, csc);
+            }
+          }
+      }
+    };
+    if (interior) epilogue(std::false_type{});
+    else epilogue(std::true_type{});
+    asm volatile("" ::: "memory");
+    // the next tile's column vectors into the other parity slot (last read by the previous tile's epilogue,
+    // before this tile's first barrier); waited for by the next tile's S(1) barrier at the latest
+    if (has_next) dma_cols(nm0, nn0, (tix + 1) & 1);
+    ++tix;
+    if (!has_next) break;
+    v += gridDim.x;
+    m0 = nm0;
+    n0 = nn0;
+    vA = vAn;
+    vW = vWn;
+    relax = interior ? S + C : 0;
+  }
+  wait_vmcnt<0>();
+}
+
+template <typename E, int EPI, bool CF32>
+static void launch_w4p(int M, int N, int K, const void* A, int lda, const void* W, int ldw, const EpiArgs& e,
+                       hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_w4p<E, EPI, CF32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)WP_LDS);
+    attr_set = true;
+  }
+  const int nTm = (M + 255) / 256, nTn = (N + 255) / 256;
+  const int grid = min(nTm * nTn, num_cus());
+  k_gemm_w4p<E, EPI, CF32><<<grid, 256, WP_LDS, s>>>(K, (const E*)A, lda, (const E*)W, ldw, e, nTm, nTn);
+}
+
+// rf_gemm.hip's entry: the 16-bit-output forms of the encoder GEMMs (EPI_NONE / BIAS / BIAS_GELU); false when
+// the combination is not instantiated here (the caller then takes k_gemm_w4)
+bool gemm_w4p(bool half, int epi, bool cf32, int M, int N, int K, const void* A, int lda, const void* W, int ldw,
+              const EpiArgs& e, hipStream_t s) {
+  if (cf32) return false;
+#define WP_(EE)                                                                                      \
+  switch (epi) {                                                                                     \
+    case RF_EPI_NONE: launch_w4p<EE, RF_EPI_NONE, false>(M, N, K, A, lda, W, ldw, e, s); return true; \
+    case RF_EPI_BIAS: launch_w4p<EE, RF_EPI_BIAS, false>(M, N, K, A, lda, W, ldw, e, s); return true; \
+    case RF_EPI_BIAS_GELU: launch_w4p<EE, RF_EPI_BIAS_GELU, false>(M, N, K, A, lda, W, ldw, e, s); return true; \
+    default: return false;                                                                           \
+  }
+  if (half) {
+    WP_(f16)
+  } else {
+    WP_(bf16)
+  }
+#undef WP_
+}
+
+}  // namespace rf

@@ -12,7 +12,7 @@
 namespace rf {
 
 static thread_local char g_err[512];
-int g_knob[KNOB_COUNT] = {6, 8, 0, 3, 0, 8, -1, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0};
+int g_knob[KNOB_COUNT] = {6, 8, 0, 3, 0, 8, -1, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0};
 const uint64_t* g_seed_dev = nullptr;
 
 void set_error(const char* fmt, ...) {
@@ -1060,7 +1060,7 @@ static int knob_index(const char* name) {
   static const char* names[rf::KNOB_COUNT] = {"gemm_gn", "gemm_variant", "band_qpb", "band_path", "gfold_path",
                                               "gfold_qsplit", "gemm_pf", "gemm_mfma32", "rank_w32",
                                               "gfold_chunk", "gemm_skinny", "epi_tile", "tn_wgs", "mid_tile",
-                                              "colsum_slices", "gemm_n192", "adam_nt", "gemm_w8"};
+                                              "colsum_slices", "gemm_n192", "adam_nt", "gemm_w8", "gemm_w4p"};
   for (int i = 0; i < rf::KNOB_COUNT; ++i)
     if (name && names[i] && strcmp(name, names[i]) == 0) return i;
   rf::set_error("rf_debug_knob: unknown knob '%s'", name ? name : "(null)");

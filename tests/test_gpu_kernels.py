@@ -1040,6 +1040,47 @@ def test_gemm_eight_wave_kernel(dev, dt, M, N, K):
     assert not wide[:, :16].any() and not wide[:, 16 + N:].any()
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (8192, 768, 3072), (4100, 2312, 768), (65536, 768, 768),
+                                   (300, 520, 128), (70000, 2304, 768), (2048, 256, 192)])
+def test_gemm_split_plane_kernel(dev, dt, M, N, K):
+    """The four-wave kernel on k-step-split LDS planes (k_gemm_w4p, knob gemm_w4p: the operand DMA spread
+    over both phases of a K-tile) for its epilogues (none, bias with a q-column scale, GELU): against fp32
+    torch on the same 16-bit operands and bit-identical to k_gemm_w4 (same MFMA sequence, same epilogue code),
+    ragged M / N edges, fewer tiles than CUs, several tiles per CU, the shortest K (2 / 3 K-tiles)."""
+    a = _rand((M, K), dev, dt, 0.5, seed=291)
+    w = _rand((N, K), dev, dt, 0.05, seed=292)
+    b = _rand((N,), dev, torch.float32, seed=293)
+    prod = a.float() @ w.float().t()
+    sc = N // 3 // 16 * 16
+    tol = 4e-3 if dt == torch.float16 else 2e-2
+
+    def rel(x, ref):
+        return float((x.float() - ref).abs().max()) / max(1.0, float(ref.abs().max()))
+
+    def run(knob):
+        old = _lib.set_knob("gemm_w4p", knob)
+        try:
+            return (ops.gemm(a, w, None, ops.RF_EPI_NONE),
+                    ops.gemm(a, w, b, ops.RF_EPI_BIAS, scale_cols=sc, col_scale=0.125),
+                    ops.gemm(a, w, b, ops.RF_EPI_BIAS_GELU))
+        finally:
+            _lib.set_knob("gemm_w4p", old)
+
+    outs = run(1)
+    assert rel(outs[0], prod) <= tol
+    ref = prod + b
+    ref[:, :sc] *= 0.125
+    assert rel(outs[1], ref) <= tol
+    assert rel(outs[2], F.gelu(prod + b)) <= tol
+    for x, y in zip(outs, run(0)):
+        if dt == torch.bfloat16:
+            assert torch.equal(x, y)
+        else:  # fp16: at most one ulp where hipcc fuses a bias FMA with the fp16 rounding differently
+            d = (x.float() - y.float()).abs()
+            assert bool((d <= torch.maximum(y.float().abs(), torch.full_like(d, 2.0 ** -14)) * 2.0 ** -10).all())
+
+
 @pytest.mark.parametrize("mfma32", [0, 1])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (8192, 768, 3072), (4100, 2312, 768), (65536, 768, 768)])
