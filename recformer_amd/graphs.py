@@ -54,6 +54,11 @@ __all__ = ["GraphedForward", "CapturedTrainStep", "static_gmax"]
 # watchdog thread raised, and its exception terminated the process while the main thread sat in
 # capture_end (the round-4 abort of the captured one-rank RCCL step, gpurun_out/r04f2/pytest.log).
 CAPTURE_MODE = "thread_local"
+# CapturedTrainStep's backward with the weight gradients deferred to the side stream (train.deferred_weight_grads):
+# off — measured slower (captured C3 17.04 vs 15.77 ms in one process, gpurun_out/r06k: the dW GEMMs then
+# queue up beside the main stream's kernels, which the per-Linear join used to pace, and the end-of-backward
+# join waits for the whole queue)
+DEFER_DW = False
 
 
 class GraphedForward:
@@ -253,11 +258,14 @@ class CapturedTrainStep:
             out = loss / self.k if self.k > 1 else loss
             if self.scaler is not None:
                 out = self.scaler.scale(out)
-            if self.bucketer is not None and not last:
-                with self.bucketer.no_sync():
+            # the Linear weight gradients accumulate on the side stream with one join at the end of the
+            # backward (train.DEFER_DW; DP bucketers' hooked parameters keep autograd's accumulation)
+            with train.deferred_weight_grads(DEFER_DW):
+                if self.bucketer is not None and not last:
+                    with self.bucketer.no_sync():
+                        out.backward()
+                else:
                     out.backward()
-            else:
-                out.backward()
             if last:
                 self._optimizer_part()
             return loss

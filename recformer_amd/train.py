@@ -34,6 +34,7 @@ equal torch's RNG draws, so dropout-on runs match the reference in distribution,
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import weakref
 from typing import Optional, Tuple
@@ -153,6 +154,72 @@ def _dw_async(fn, ref: torch.Tensor):
         record(r)
         return r
     return join
+
+
+# weight gradients accumulated into the masters' .grad on the side stream, with ONE join at the end of the
+# backward pass (an autograd engine callback) instead of one per Linear: the main stream no longer waits
+# for each layer's dW before going on (the weight-gradient stream was the step's critical path).
+# Only for leaf masters without post-accumulate hooks (a DP GradBucketer's hooks, or non-leaf masters such
+# as pretraining's shared casts, keep the per-Linear join and autograd's accumulation). Off by default: the
+# Linears then return no gradient for their weights to autograd, so torch.autograd.grad(loss, params) would
+# see none; the training drivers that own the step turn it on around their backward
+# (deferred_weight_grads(): graphs.CapturedTrainStep, tools/train_bench.py).
+DEFER_DW = False
+_DEFER = {"queued": False}
+
+
+@contextlib.contextmanager
+def deferred_weight_grads(on: bool = True):
+    """Within: loss.backward() accumulates the Linear weight gradients into .grad on the side stream with
+    one join when the backward pass ends (DEFER_DW)."""
+    global DEFER_DW
+    old, DEFER_DW = DEFER_DW, on
+    try:
+        yield
+    finally:
+        DEFER_DW = old
+
+
+def _defer_ok(masters, need) -> bool:
+    if not (DEFER_DW and DW_SIDE_STREAM):
+        return False
+    for m, n in zip(masters, need):
+        if n and (m is None or not m.is_leaf or not m.is_cuda or getattr(m, "_post_accumulate_grad_hooks", None)
+                  or m.dtype != torch.float32):
+            return False
+    return True
+
+
+def _accum_grad(p: torch.Tensor, g: torch.Tensor) -> None:
+    """p.grad += g on the current (side) stream; the first gradient is stored as it is (AccumulateGrad's
+    steal), detached from any graph."""
+    if p.grad is None:
+        p.grad = g.detach()
+    else:
+        p.grad.add_(g)
+
+
+def _dw_deferred(fn, ref: torch.Tensor) -> None:
+    """Run fn() (weight-gradient work that accumulates into leaf .grad tensors itself) on the side stream
+    after the main stream's work so far; the main stream waits for the side stream once, when the backward
+    pass ends (queued engine callback), before any optimizer or scaler reads a gradient."""
+    main = torch.cuda.current_stream(ref.device)
+    side = _SIDE_STREAMS.get(ref.device)
+    if side is None:
+        side = _SIDE_STREAMS[ref.device] = torch.cuda.Stream(ref.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in out:
+        if isinstance(t, torch.Tensor):
+            t.record_stream(main)
+    if not _DEFER["queued"]:
+        _DEFER["queued"] = True
+
+        def join():
+            _DEFER["queued"] = False
+            main.wait_stream(side)
+        torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 def _weight_grad(dc: torch.Tensor, a: torch.Tensor, scale=(0, 1.0)) -> torch.Tensor:
@@ -284,6 +351,7 @@ class _GemmP(torch.autograd.Function):
         ctx.sc = (scale_cols, col_scale)
         ctx.rows = [m.shape[0] for m in masters]
         ctx.wdt = masters[0].dtype
+        ctx.masters = masters
         return ops.gemm(a.contiguous(), w16, b, ops.RF_EPI_BIAS, scale_cols=scale_cols, col_scale=col_scale)
 
     @staticmethod
@@ -296,8 +364,24 @@ class _GemmP(torch.autograd.Function):
         # the dW rows and db entries of the scaled outputs scaled inside the reduction kernels
         scl = (sc, s) if scaled else (0, 1.0)
         side_b = BIAS_GRAD_SIDE and ctx.needs_input_grad[1] and any(ctx.needs_input_grad[7:])
-        join = (_dw_async(lambda: (_weight_grad(dc, a, scl).to(ctx.wdt), _bias_grad(dc, scl) if side_b else None),
-                          dc) if any(ctx.needs_input_grad[7:]) else None)
+        need_w = ctx.needs_input_grad[7:]
+        join = None
+        if any(need_w) and not side_b and dc.is_cuda and _defer_ok(ctx.masters, need_w):
+            rows, masters = ctx.rows, ctx.masters
+
+            def side_work():
+                dw = _weight_grad(dc, a, scl).to(ctx.wdt)
+                r0 = 0
+                for m, n, nd in zip(masters, rows, need_w):
+                    if nd:
+                        _accum_grad(m, dw[r0:r0 + n])
+                    r0 += n
+                return (dw,)
+            _dw_deferred(side_work, dc)
+            need_w = (False,) * len(need_w)  # accumulated on the side stream, returned as None
+        elif any(need_w):
+            join = _dw_async(lambda: (_weight_grad(dc, a, scl).to(ctx.wdt), _bias_grad(dc, scl) if side_b else None),
+                             dc)
         if ctx.needs_input_grad[0]:
             other = ctx.mb.g if ctx.mb is not None else None
             if other is not None:  # dA + the attention's gradient of the same input, in the epilogue
@@ -314,7 +398,7 @@ class _GemmP(torch.autograd.Function):
         if dw is not None:
             r0 = 0
             for i, n in enumerate(ctx.rows):
-                dws[i] = dw[r0:r0 + n] if ctx.needs_input_grad[7 + i] else None
+                dws[i] = dw[r0:r0 + n] if need_w[i] else None
                 r0 += n
         return (da, db, None, None, None, None, None, *dws)
 
@@ -490,6 +574,7 @@ class _FFN(torch.autograd.Function):
         ctx.save_for_backward(a, u, z, w1_16 if w1t is None else w1t, w2_16 if w2t is None else w2t)
         ctx.packed = (w1t is not None, w2t is not None)
         ctx.wdt = (w1.dtype, w2.dtype)
+        ctx.masters = (w1, w2)
         return t2
 
     @staticmethod
@@ -503,13 +588,29 @@ class _FFN(torch.autograd.Function):
         # both weight gradients on the side stream, beside da = dz.W1 (N = 768: a quarter of the CUs
         # idle at 16k tokens); dw2 waits for nothing but dt2, dw1 for dz
         side_b = BIAS_GRAD_SIDE and ctx.needs_input_grad[3]
-        join = _dw_async(lambda: (_weight_grad(dt2, u).to(ctx.wdt[1]) if ctx.needs_input_grad[4] else None,
-                                  _weight_grad(dz, a).to(ctx.wdt[0]) if ctx.needs_input_grad[1] else None,
-                                  ops.colsum(dz) if side_b else None), dz)
+        need1, need2 = ctx.needs_input_grad[1], ctx.needs_input_grad[4]
+        w1m, w2m = ctx.masters
+        join = None
+        if (need1 or need2) and not side_b and dz.is_cuda and _defer_ok((w1m, w2m), (need1, need2)):
+            def side_work():
+                dw2 = _weight_grad(dt2, u).to(ctx.wdt[1]) if need2 else None
+                if need2:
+                    _accum_grad(w2m, dw2)
+                dw1 = _weight_grad(dz, a).to(ctx.wdt[0]) if need1 else None
+                if need1:
+                    _accum_grad(w1m, dw1)
+                return (dw2, dw1)
+            _dw_deferred(side_work, dz)
+        else:
+            join = _dw_async(lambda: (_weight_grad(dt2, u).to(ctx.wdt[1]) if need2 else None,
+                                      _weight_grad(dz, a).to(ctx.wdt[0]) if need1 else None,
+                                      ops.colsum(dz) if side_b else None), dz)
         da = ops.gemm(dz, w1t, None, ops.RF_EPI_NONE) if ctx.needs_input_grad[0] else None
         db1 = ops.colsum(dz) if ctx.needs_input_grad[3] and not side_b else None
-        dw2, dw1, db1s = join()
-        db1 = db1s if side_b else db1
+        dw2 = dw1 = None
+        if join is not None:
+            dw2, dw1, db1s = join()
+            db1 = db1s if side_b else db1
         return da, dw1, None, db1, dw2, None, db2, None, None
 
 

@@ -838,9 +838,10 @@ def test_cls_last_layer_training_matches_full(dev, monkeypatch, dtype, p_drop):
 def test_side_stream_switches_bit_identical(dev, monkeypatch, dtype):
     """The training step's side-stream placements change where kernels run, not what they compute:
     the fold's first stage beside the band attention (train.FOLD_SIDE_TRAIN: stage 1 + stage 2 instead of
-    the one-call fold) and the global rows' backward on the weight-gradient stream (train.GLOBAL_BWD_SIDE)
-    give bit-identical losses and gradients in every on/off combination, with hidden and attention dropout
-    on (a missing stream dependency would show as a sometimes-different gradient)."""
+    the one-call fold), the global rows' backward on the weight-gradient stream (train.GLOBAL_BWD_SIDE) and
+    the Linear weight gradients accumulated on that stream with one join at the end of the backward
+    (train.deferred_weight_grads) give bit-identical losses and gradients in each combination, with hidden
+    and attention dropout on (a missing stream dependency would show as a sometimes-different gradient)."""
     from recformer_amd import train as T
     g = load_golden("c1_ragged")
     batch = {k: v.to(dev) for k, v in batch_of(g).items()}
@@ -849,26 +850,28 @@ def test_side_stream_switches_bit_identical(dev, monkeypatch, dtype):
     items = torch.randn(40, CFG["hidden_size"]) * 0.5
     lf = hashed_model(dict(CFG, hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.1), seed=1)
     res = {}
-    for fold_side in (True, False):
-        for bwd_side in (True, False):
-            monkeypatch.setattr(T, "FOLD_SIDE_TRAIN", fold_side)
-            monkeypatch.setattr(T, "GLOBAL_BWD_SIDE", bwd_side)
-            m = RecformerForSeqRec(lf.config)
-            m.longformer.load_state_dict(lf.state_dict())
-            m.config.finetune_negative_sample_size = 0
-            m.init_item_embedding(items.clone())
-            m = m.to(dev).train()
-            for rep in range(2):  # twice: a race would rarely repeat its result
-                m.zero_grad(set_to_none=True)
-                torch.manual_seed(321)
-                with torch.autocast("cuda", dtype=dtype):
-                    loss = m(**batch, labels=labels)
+    for fold_side, bwd_side, defer in ((True, True, True), (True, True, False), (False, False, True),
+                                       (False, False, False), (True, False, True), (False, True, False)):
+        monkeypatch.setattr(T, "FOLD_SIDE_TRAIN", fold_side)
+        monkeypatch.setattr(T, "GLOBAL_BWD_SIDE", bwd_side)
+        m = RecformerForSeqRec(lf.config)
+        m.longformer.load_state_dict(lf.state_dict())
+        m.config.finetune_negative_sample_size = 0
+        m.init_item_embedding(items.clone())
+        m = m.to(dev).train()
+        for rep in range(2):  # twice: a race would rarely repeat its result
+            # rep 1 accumulates onto zeroed (not None) gradients: the deferred path's add_ form
+            m.zero_grad(set_to_none=rep == 0)
+            torch.manual_seed(321)
+            with torch.autocast("cuda", dtype=dtype):
+                loss = m(**batch, labels=labels)
+            with T.deferred_weight_grads(defer):
                 loss.backward()
-                torch.cuda.synchronize()
-                res[(fold_side, bwd_side, rep)] = (loss.detach().float().cpu(),
-                                                   {k: p.grad.detach().clone() for k, p in
-                                                    m.longformer.named_parameters() if p.grad is not None})
-    ref_loss, ref_g = res[(True, True, 0)]
+            torch.cuda.synchronize()
+            res[(fold_side, bwd_side, defer, rep)] = (loss.detach().float().cpu(),
+                                                      {k: p.grad.detach().clone() for k, p in
+                                                       m.longformer.named_parameters() if p.grad is not None})
+    ref_loss, ref_g = res[(True, True, True, 0)]
     for key, (loss, grads) in res.items():
         assert torch.equal(loss, ref_loss), key
         assert grads.keys() == ref_g.keys(), key

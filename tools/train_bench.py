@@ -108,7 +108,9 @@ def main():
         (name=a,b: values a / b)."""
         from recformer_amd import _lib, models, train
         if a.ab:
-            mod, name = (models, a.ab[len("models."):]) if a.ab.startswith("models.") else (train, a.ab)
+            from recformer_amd import graphs as G
+            mod, name = ((models, a.ab[len("models."):]) if a.ab.startswith("models.") else
+                         (G, a.ab[len("graphs."):]) if a.ab.startswith("graphs.") else (train, a.ab))
             if not hasattr(mod, name):
                 raise SystemExit(f"unknown switch {a.ab}")
             setattr(mod, name, val)
