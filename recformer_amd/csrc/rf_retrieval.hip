@@ -19,8 +19,9 @@
 //                   (MODE 2: metrics without a top-k).
 //   k_rank_reduce   sums the per-tile partials per row in tile order (deterministic).
 //   k_topk_dense / k_topk_merge
-//                   exact top-k per row (value descending, ties by lower item index) by a radix
-//                   select over order-preserving 32-bit keys in LDS; the merge reads the seed
+//                   exact top-k per row (value descending, ties by lower item index) by a ballot-
+//                   counted binary search over order-preserving 32-bit keys held in registers (one
+//                   wave per row); the merge reads the seed
 //                   top-k and every tile's candidate slots and flags rows whose slots overflowed
 //                   (the caller re-ranks those rows densely).
 // Element types: bf16 and fp16 operands (v_mfma_f32_16x16x32_bf16 / _f16), fp32 scores.
@@ -343,9 +344,10 @@ __global__ void __launch_bounds__(512, 1) k_score_rank(int K, const T* __restric
 // k_rank_w32: A = the shard's item rows [col0, col0 + ncols) (M), W = the queries (N), so a lane holds
 // 4 query columns x 64 item rows of every 256 x 256 tile: the per-query counts and exp-sums are
 // in-lane sums over items, one shuffle across the lane halves and one LDS exchange between the two
-// waves of a query half — no score matrix, no per-row cross-lane reductions. Candidates (MODE 1) go
-// straight to the query's global list with one atomic each (about k per row per column chunk), a
-// row whose list overflows is flagged by the merge as before; MODE 0 also stores the dense scores.
+// waves of a query half — no score matrix, no per-row cross-lane reductions. Candidates (MODE 1) are
+// compacted per wave into LDS slots and appended to the queries' global lists after the tile (one
+// atomic each, about k per row per column chunk); a row whose list overflows is flagged by the merge
+// as before; MODE 0 also stores the dense scores.
 // k_label_score32 computes the labels' own scores with the same MFMA (32x32x16, the same operand
 // roles, K ascending in 16-chunks, the chain starting from zero) and the same epilogue expression, so
 // the strict ranks compare bit-identical values. (The 16x16x32 kernels above are kept for D not a
@@ -381,6 +383,13 @@ struct RankKernArgs {
   RankW32Args a;
 };
 constexpr int RANK_KARG_OFF = (int)offsetof(RankKernArgs, a);
+
+// k_rank_w32's epilogue scratch (W32_SCR_BYTES): [0, 8 KiB) the count / exp-sum exchange between the
+// two waves of a query half, then MODE 1's per-wave candidate slots
+constexpr int RW_CL = 8192;
+constexpr int RW_CL_CAP = 543;  // candidates per wave and tile (about 3 per query in the densest chunk), + trash
+constexpr int RW_CL_WAVE = (RW_CL_CAP + 1) * 8;
+static_assert(RW_CL + 4 * RW_CL_WAVE <= W32_SCR_BYTES, "rank epilogue scratch");
 
 template <int MODE>
 struct RankW32Pol {
@@ -429,6 +438,15 @@ struct RankW32Pol {
       tau[jb] = MODE == 1 ? a.tau[qq] : 0.f;
     }
     const int ib = t.wr * 128 + 4 * g;  // tile-relative item row of register 0 of block 0
+    // MODE 1: this wave's candidates are staged in the epilogue scratch as (score, item << 8 | query)
+    // by a ballot compaction (no atomics, LDS addresses only inside the unrolled loop: the direct
+    // global appends of round 4 held 64-bit list addresses across it and spilled), then appended to
+    // the queries' global lists after the loop; a query whose candidates miss the wave's slots is
+    // poisoned (> capr) for the exact re-rank
+    uint2* cl = reinterpret_cast<uint2*>(t.scr + RW_CL + t.wave * RW_CL_WAVE);
+    int ncand = 0;
+    uint32_t lost = 0;                                        // MODE 1: queries jb with candidates past the slots
+    const uint32_t pkb = (uint32_t)((ib << 8) | (4 * c));     // + (pr << 8) + jb: item << 8 | query
     int gt[4] = {0, 0, 0, 0}, vc[4] = {0, 0, 0, 0};
     float se[4] = {0.f, 0.f, 0.f, 0.f};
     // MODE 0: dense scores through a buffer resource: a query past B is past num_records, an item past
@@ -446,8 +464,6 @@ struct RankW32Pol {
       const int item = t.m0 + ib + pr;  // column of this launch's range [0, ncols)
       const bool iok = item < a.ncols;
       const float rcv = t.cb[ib + pr];
-      uint32_t cb4 = 0;
-      float svs[4];
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
         // items past ncols score -inf: no count, exp2(-inf) = 0 — one select, no branch around the exp
@@ -463,30 +479,66 @@ struct RankW32Pol {
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv), rsD, lb + (uint32_t)((jb * (int)a.ldd + pr) * 4),
                                                 0, 0);
         }
-        if (MODE == 1) cb4 |= (qok[jb] && sv >= tau[jb]) ? (1u << jb) : 0u;
-        svs[jb] = sv;
+        if (MODE == 1) {
+          // a (query, item) pair is a candidate with probability ~k (grow - 1) / chunk (0.3-2.4%): the
+          // ballot is taken per query column and the compaction runs only where some lane has one
+          // (a wave-uniform branch); within it every lane stores, a lane without a candidate (or past
+          // the slots) into the wave's trash slot, and the count advances by the ballot's popcount
+          const bool cnd = qok[jb] && iok && sv >= tau[jb];
+          const uint64_t m = __builtin_amdgcn_ballot_w64(cnd);
+          if (m) {
+            const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)ncand));
+            const bool keep = cnd && slot < RW_CL_CAP;
+            lost |= (cnd && !keep) ? (1u << jb) : 0u;
+            cl[keep ? slot : RW_CL_CAP] = make_uint2(__float_as_uint(sv), pkb + (uint32_t)((pr << 8) + jb));
+            ncand += (int)__popcll(m);
+          }
+          asm volatile("" : "+v"(lost));
+        }
       }
       if (MODE == 1) {
-        // candidates (about k per query and column chunk) go straight to the per-query lists: the write
-        // block runs only in the rows where some lane of the wave has one (a wave-uniform branch, exec
-        // masking inside), one global atomic per candidate; a list past capr flags its query for an
-        // exact re-rank (the merge)
-        if (__builtin_amdgcn_ballot_w64(cb4 != 0u)) {
+        // the counts in place: the candidate branches would otherwise let their arithmetic sink to the
+        // end of the loop, every score of the tile live until then (spills)
 #pragma unroll
-          for (int jb = 0; jb < 4; ++jb) {
-            if (cb4 & (1u << jb)) {
-              const int q = q0 + jb;
-              const int pos = atomicAdd(a.rcnt + q, 1);
-              if (pos < a.capr) {
-                a.cval[(int64_t)q * a.capr + pos] = svs[jb];
-                a.cidx[(int64_t)q * a.capr + pos] = a.idx_base + a.col0 + t.m0 + ib + pr;
-              }
-            }
-          }
-        }
+        for (int jb = 0; jb < 4; ++jb) asm volatile("" : "+v"(gt[jb]), "+v"(vc[jb]), "+v"(se[jb]));
       }
       __builtin_amdgcn_sched_barrier(0);
     });
+    if (MODE == 1) {  // the counts are complete here: otherwise their arithmetic sinks past the flush below
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) asm volatile("" : "+v"(gt[jb]), "+v"(vc[jb]), "+v"(se[jb]));
+    }
+    if (MODE == 1) {
+      // append the staged candidates to the queries' lists: one global atomic each, predicated through
+      // buffer offsets (>= 2^31: dropped) instead of divergent branches — a branch here costs the whole
+      // kernel its registers (the allocator then spills the prologue's values across the K-loop)
+      __builtin_amdgcn_wave_barrier();
+      constexpr uint32_t OOR = 0x80000000u;
+      const int nc = min(ncand, RW_CL_CAP);
+      const int qb = t.n0 + t.wc * 128;
+      const int lim = (int)min((int64_t)a.B * a.capr * 4, (int64_t)0x7FFFFFFF);
+      const __amdgpu_buffer_rsrc_t rsN = __builtin_amdgcn_make_buffer_rsrc((void*)a.rcnt, (short)0, a.B * 4, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)a.cval, (short)0, lim, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rsI = __builtin_amdgcn_make_buffer_rsrc((void*)a.cidx, (short)0, lim, 0x00020000);
+      const int idb = a.idx_base + a.col0 + t.m0;
+      for (int e0 = 0; e0 < nc; e0 += 64) {  // wave-uniform trip count
+        const int e = e0 + el;
+        const bool ok = e < nc;
+        const uint2 x = cl[ok ? e : RW_CL_CAP];
+        const int q = qb + (int)(x.y & 255u);
+        const int pos = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rsN, ok ? q * 4 : (int)OOR, 0, 0);
+        const uint32_t off = (ok && pos < a.capr) ? (uint32_t)((q * a.capr + pos) * 4) : OOR;
+        __builtin_amdgcn_raw_buffer_store_b32(x.x, rsV, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(idb + (int)(x.y >> 8)), rsI, off, 0, 0);
+      }
+      if (ncand > RW_CL_CAP) {  // wave-uniform: poison the queries whose candidates missed the slots
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+          (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(a.capr + 1, rsN,
+                                                               ((lost >> jb) & 1u) ? (q0 + jb) * 4 : (int)OOR, 0, 0);
+      }
+    }
     // lane halves (item rows 4g..), then the two waves (wr) of this query half through LDS
     int pk[4];
 #pragma unroll
@@ -610,8 +662,9 @@ __global__ void __launch_bounds__(256) k_rank_reduce(int B, int ntiles, const in
   }
 }
 
-// ---- exact top-k per row, one wave per row ----------------------------------------------------
-// order-preserving key: larger float -> larger unsigned key
+// ---- exact top-k per row, one wave per row, keys in registers ---------------------------------
+// order-preserving key: larger float -> larger unsigned key (0 only for a negative NaN: here the
+// "missing entry" marker)
 __device__ __forceinline__ uint32_t fkey(float f) {
   const uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -629,119 +682,134 @@ __device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
   return v;
 }
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// lanes below this one in a ballot mask
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Top-k of the n (key, id) pairs in this wave's LDS arrays: value descending, ties by lower id;
-// missing entries (-inf, -1). The k-th largest key is found by a radix select on the observed
-// key RANGE (each pass splits [lo, hi] into 256 bins: close scores spread over the bins instead of
-// piling into one bin of the top byte), then the entries above it and the lowest-id ties are
-// ranked. hist: 256 ints, sel: >= k ints, tie: >= n ints of this wave's scratch.
-__device__ void wave_topk(const uint32_t* keys, const int32_t* ids, int n, int k, int* hist, int* sel, int* tie,
-                          float* out_v, int32_t* out_i) {
+constexpr int TK_DENSE_MAX = 2048;  // entries per row of a dense block
+constexpr int TK_MERGE_MAX = 2048;  // seed list + candidates per row
+constexpr int TK_KMAX = 256;
+constexpr int TK_WAVES = 4;         // rows per workgroup
+// per-wave LDS: the selected keys and ids (TK_KMAX each), the ids of the entries tied at the threshold
+constexpr int TK_WAVE_WORDS = 2 * TK_KMAX + TK_MERGE_MAX;
+
+// final order of the kk selected entries: key descending, id ascending, as one 64-bit comparison key
+// (key << 32 | ~id). Entry a = 64 t + lane is held by its lane (R registers, kk <= 64 R); every entry b
+// is read from its lane (v_readlane into SGPRs: no LDS round trip per comparison)
+template <int R>
+__device__ __forceinline__ void rank_selected(const uint32_t* sk, const int32_t* si, int kk, float* out_v,
+                                              int32_t* out_i) {
   const int lane = threadIdx.x & 63;
-  const int kk = min(k, n);
-  uint32_t tau = 0;
-  int need = 0;
-  if (kk > 0) {
-    uint32_t lo = 0xFFFFFFFFu, hi = 0;
-    for (int e = lane; e < n; e += 64) {
-      lo = min(lo, keys[e]);
-      hi = max(hi, keys[e]);
+  uint64_t mc[R];
+  int rank[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) {
+    const int a = t * 64 + lane;
+    mc[t] = a < kk ? ((uint64_t)sk[a] << 32) | (uint32_t)~si[a] : 0ull;
+    rank[t] = 0;
+  }
+#pragma unroll
+  for (int tb = 0; tb < R; ++tb) {
+    const int nb = min(64, kk - tb * 64);
+    const int lo = (int)(uint32_t)mc[tb], hi = (int)(uint32_t)(mc[tb] >> 32);
+    for (int bl = 0; bl < nb; ++bl) {
+      const uint64_t cb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, bl) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane(lo, bl);
+#pragma unroll
+      for (int t = 0; t < R; ++t) rank[t] += cb > mc[t] ? 1 : 0;
     }
-    lo = wave_min_u(lo);
-    hi = wave_max_u(hi);
-    need = kk;
-    while (hi > lo) {
-      // bins of 2^sh keys, sh the least with (hi - lo) >> sh < 256: a shift per element instead of a 64-bit
-      // division (the selection is the same: the bin holding the kk-th largest key, then its range)
-      const uint32_t span = hi - lo;
-      const int sh = max(0, 24 - (int)__builtin_clz(span));  // bit length of span minus 8
-      for (int b = lane; b < 256; b += 64) hist[b] = 0;
-      __builtin_amdgcn_wave_barrier();
-      for (int e = lane; e < n; e += 64) {
-        const uint32_t key = keys[e];
-        if (key >= lo && key <= hi) atomicAdd(&hist[(int)((key - lo) >> sh)], 1);
-      }
-      __builtin_amdgcn_wave_barrier();
-      // bins from the top: lane l owns bins 255 - 4l .. 252 - 4l; suffix sums across lanes
-      int c4[4], own = 0;
+  }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        c4[j] = hist[255 - 4 * lane - j];
-        own += c4[j];
-      }
-      int incl = own;  // inclusive prefix over lanes 0..lane (= bins from the top)
+  for (int t = 0; t < R; ++t) {
+    if (t * 64 + lane < kk) {
+      out_v[rank[t]] = kfloat((uint32_t)(mc[t] >> 32));
+      out_i[rank[t]] = (int32_t)~(uint32_t)mc[t];
+    }
+  }
+}
+
+// Top-k of one row's n entries (entry p at key_at(p), id_at(p); key 0 = missing): values descending,
+// ties by lower id; missing outputs (-inf, -1). The n keys sit in registers, S per lane (entry
+// j * 64 + lane), so the k-th largest key is found by a binary search over the key range whose
+// counts are ballots (#{key >= t}: one compare and one popcount per register, wave-uniform, no LDS,
+// no atomics; it stops early once exactly k keys reach t). The entries above the threshold, then the
+// lowest-id ties, are compacted into LDS and ranked against each other through lane reads.
+template <int S, typename KeyAt, typename IdAt>
+__device__ __forceinline__ void row_topk(int n, int k, KeyAt key_at, IdAt id_at, uint32_t* sk, int32_t* si,
+                                         int32_t* tid, float* out_v, int32_t* out_i) {
+  const int lane = threadIdx.x & 63;
+  uint32_t key[S];
+  uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+  int nv = 0;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int x = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += x;
-      }
-      const int excl = incl - own;
-      int bsel = -1, above = 0;
-      if (excl < need && incl >= need) {
-        int cum = excl;
+  for (int j = 0; j < S; ++j) {
+    const int p = j * 64 + lane;
+    key[j] = p < n ? key_at(p) : 0u;
+  }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (bsel < 0 && cum + c4[j] >= need) {
-            bsel = 255 - 4 * lane - j;
-            above = cum;
-          }
-          cum += c4[j];
+  for (int j = 0; j < S; ++j) {
+    if (key[j]) {
+      lo = min(lo, key[j]);
+      hi = max(hi, key[j]);
+    }
+    nv += __popcll(__ballot(key[j] != 0u));
+  }
+  const int kk = min(k, nv);
+  if (kk > 0) {
+    lo = __builtin_amdgcn_readfirstlane(wave_min_u(lo));
+    hi = __builtin_amdgcn_readfirstlane(wave_max_u(hi));
+    // tau: the largest t with #{key >= t} >= kk, i.e. the kk-th largest key; `exact`: #{key >= tau} == kk
+    bool exact = nv == kk;
+    while (!exact && lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1) + 1u;  // in (lo, hi]
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < S; ++j) c += __popcll(__ballot(key[j] >= mid));
+      if (c >= kk) {
+        lo = mid;
+        exact = c == kk;
+      } else {
+        hi = mid - 1u;
+      }
+    }
+    const uint32_t tau = lo;
+    int ngt = 0, nt = 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int p = j * 64 + lane;
+      const bool g = key[j] != 0u && (exact ? key[j] >= tau : key[j] > tau);
+      const bool q = !exact && key[j] == tau;
+      const uint64_t mg = __ballot(g), mq = __ballot(q);
+      if (g) {
+        const int o = ngt + lanes_below(mg);
+        sk[o] = key[j];
+        si[o] = id_at(p);
+      }
+      if (q) tid[nt + lanes_below(mq)] = id_at(p);
+      ngt += __popcll(mg);
+      nt += __popcll(mq);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int need = kk - ngt;
+    if (need > 0) {  // the `need` ties with the lowest ids (all of them when nt == need)
+      for (int a = lane; a < nt; a += 64) {
+        const int ia = tid[a];
+        int r = a;
+        if (nt > need) {
+          r = 0;
+          for (int b = 0; b < nt && r < need; ++b) r += tid[b] < ia ? 1 : 0;
+        }
+        if (r < need) {
+          sk[ngt + r] = tau;
+          si[ngt + r] = ia;
         }
       }
-      const unsigned long long found = __ballot(bsel >= 0);
-      const int src = __ffsll((long long)found) - 1;
-      bsel = __shfl(bsel, src, 64);
-      above = __shfl(above, src, 64);
-      need -= above;
-      const uint64_t nlo = (uint64_t)lo + ((uint64_t)bsel << sh);
-      const uint64_t nhi = min((uint64_t)hi, nlo + (1ull << sh) - 1);
-      lo = (uint32_t)nlo;
-      hi = (uint32_t)nhi;
       __builtin_amdgcn_wave_barrier();
     }
-    tau = lo;
-  }
-  // entries above tau (kk - need of them) and the ties
-  int ngt = 0, nt = 0;
-  for (int e0 = 0; e0 < n && kk > 0; e0 += 64) {
-    const int e = e0 + lane;
-    const uint32_t key = e < n ? keys[e] : 0u;
-    const bool g = e < n && key > tau, q = e < n && key == tau;
-    const unsigned long long mg = __ballot(g), mq = __ballot(q);
-    const unsigned long long below = (1ull << lane) - 1ull;
-    if (g) sel[ngt + __popcll(mg & below)] = e;
-    if (q) tie[nt + __popcll(mq & below)] = e;
-    ngt += __popcll(mg);
-    nt += __popcll(mq);
-  }
-  __builtin_amdgcn_wave_barrier();
-  for (int a = lane; a < nt; a += 64) {  // the `need` ties with the lowest ids
-    const int ea = tie[a];
-    int r = a;
-    if (nt > need) {
-      r = 0;
-      for (int b = 0; b < nt && r < need; ++b) r += ids[tie[b]] < ids[ea] ? 1 : 0;
-    }
-    if (r < need) sel[ngt + r] = ea;
-  }
-  __builtin_amdgcn_wave_barrier();
-  for (int a = lane; a < kk; a += 64) {  // final order: key descending, id ascending
-    const int ea = sel[a];
-    const uint32_t ka = keys[ea];
-    const int ia = ids[ea];
-    int r = 0;
-    for (int b = 0; b < kk; ++b) {
-      const int eb = sel[b];
-      const uint32_t kb = keys[eb];
-      r += (kb > ka || (kb == ka && ids[eb] < ia)) ? 1 : 0;
-    }
-    out_v[r] = kfloat(ka);
-    out_i[r] = ia;
+    if (kk <= 64) rank_selected<1>(sk, si, kk, out_v, out_i);
+    else if (kk <= 128) rank_selected<2>(sk, si, kk, out_v, out_i);
+    else rank_selected<4>(sk, si, kk, out_v, out_i);
   }
   for (int a = kk + lane; a < k; a += 64) {
     out_v[a] = -__builtin_inff();
@@ -749,82 +817,65 @@ __device__ void wave_topk(const uint32_t* keys, const int32_t* ids, int n, int k
   }
 }
 
-constexpr int TK_DENSE_MAX = 2048;  // entries per row of a dense block (per wave)
-constexpr int TK_MERGE_MAX = 2048;  // seed list + candidates per row (per wave)
-constexpr int TK_KMAX = 256;
-constexpr int TK_WAVES = 4;         // rows per workgroup
-// per-wave LDS: keys, ids, ties (n each), hist 256, sel k
-constexpr int TK_WAVE_LDS = TK_DENSE_MAX * 12 + 256 * 4 + TK_KMAX * 4;
-
-__global__ void __launch_bounds__(256) k_topk_dense(int B, int n, const float* __restrict__ vals, int64_t ldv,
-                                                    const int32_t* __restrict__ idx, int64_t ldi, int32_t idx_base,
-                                                    int k, float* __restrict__ out_v, int32_t* __restrict__ out_i) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int row = blockIdx.x * TK_WAVES + wave;
-  if (row >= B) return;
-  char* base = smem + wave * TK_WAVE_LDS;
-  uint32_t* keys = reinterpret_cast<uint32_t*>(base);
-  int32_t* ids = reinterpret_cast<int32_t*>(base + TK_DENSE_MAX * 4);
-  int* tie = reinterpret_cast<int*>(base + TK_DENSE_MAX * 8);
-  int* hist = reinterpret_cast<int*>(base + TK_DENSE_MAX * 12);
-  int* sel = hist + 256;
-  for (int e = lane; e < n; e += 64) {
-    keys[e] = fkey(vals[(int64_t)row * ldv + e]);
-    ids[e] = idx ? idx[(int64_t)row * ldi + e] : idx_base + e;
-  }
-  __builtin_amdgcn_wave_barrier();
-  wave_topk(keys, ids, n, k, hist, sel, tie, out_v + (int64_t)row * k, out_i + (int64_t)row * k);
+// the register count per lane that holds n entries (one instantiation per size class)
+template <typename KeyAt, typename IdAt>
+__device__ __forceinline__ void row_topk_n(int n, int k, KeyAt key_at, IdAt id_at, int32_t* lds, float* out_v,
+                                           int32_t* out_i) {
+  uint32_t* sk = reinterpret_cast<uint32_t*>(lds);
+  int32_t* si = lds + TK_KMAX;
+  int32_t* tid = lds + 2 * TK_KMAX;
+  if (n <= 512) row_topk<8>(n, k, key_at, id_at, sk, si, tid, out_v, out_i);
+  else if (n <= 1024) row_topk<16>(n, k, key_at, id_at, sk, si, tid, out_v, out_i);
+  else row_topk<32>(n, k, key_at, id_at, sk, si, tid, out_v, out_i);
 }
 
-__global__ void __launch_bounds__(256) k_topk_merge(int B, int k0, const float* __restrict__ v0,
-                                                    const int32_t* __restrict__ i0, const float* __restrict__ cval,
-                                                    const int32_t* __restrict__ cidx, const int32_t* __restrict__ rcnt,
-                                                    int capr, int k, float* __restrict__ out_v,
-                                                    int32_t* __restrict__ out_i, int32_t* __restrict__ overflow) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__global__ void __launch_bounds__(64 * TK_WAVES) k_topk_dense(int B, int n, const float* __restrict__ vals,
+                                                              int64_t ldv, const int32_t* __restrict__ idx,
+                                                              int64_t ldi, int32_t idx_base, int k,
+                                                              float* __restrict__ out_v, int32_t* __restrict__ out_i) {
+  __shared__ int32_t lds[TK_WAVES * TK_WAVE_WORDS];
+  const int wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * TK_WAVES + wave;
+  if (row >= B) return;
+  const float* vr = vals + (int64_t)row * ldv;
+  const int32_t* ir = idx ? idx + (int64_t)row * ldi : nullptr;
+  row_topk_n(
+      n, k, [&](int p) { return fkey(vr[p]); }, [&](int p) { return ir ? ir[p] : idx_base + p; },
+      lds + wave * TK_WAVE_WORDS, out_v + (int64_t)row * k, out_i + (int64_t)row * k);
+}
+
+__global__ void __launch_bounds__(64 * TK_WAVES) k_topk_merge(int B, int k0, const float* __restrict__ v0,
+                                                              const int32_t* __restrict__ i0,
+                                                              const float* __restrict__ cval,
+                                                              const int32_t* __restrict__ cidx,
+                                                              const int32_t* __restrict__ rcnt, int capr, int k,
+                                                              float* __restrict__ out_v, int32_t* __restrict__ out_i,
+                                                              int32_t* __restrict__ overflow) {
+  __shared__ int32_t lds[TK_WAVES * TK_WAVE_WORDS];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * TK_WAVES + wave;
   if (row >= B) return;
-  char* base = smem + wave * TK_WAVE_LDS;
-  uint32_t* keys = reinterpret_cast<uint32_t*>(base);
-  int32_t* ids = reinterpret_cast<int32_t*>(base + TK_MERGE_MAX * 4);
-  int* tie = reinterpret_cast<int*>(base + TK_MERGE_MAX * 8);
-  int* hist = reinterpret_cast<int*>(base + TK_MERGE_MAX * 12);
-  int* sel = hist + 256;
   const int c = rcnt[row];
   float* ov = out_v + (int64_t)row * k;
   int32_t* oi = out_i + (int64_t)row * k;
+  const float* sv = v0 + (int64_t)row * k0;
+  const int32_t* sd = i0 + (int64_t)row * k0;
   if (c > capr || k0 + c > TK_MERGE_MAX) {
     // overflowed: keep the previous list (a valid lower bound for the next threshold) and flag the
     // row for an exact dense re-rank
     for (int e = lane; e < k; e += 64) {
-      ov[e] = e < k0 ? v0[(int64_t)row * k0 + e] : -__builtin_inff();
-      oi[e] = e < k0 ? i0[(int64_t)row * k0 + e] : -1;
+      ov[e] = e < k0 ? sv[e] : -__builtin_inff();
+      oi[e] = e < k0 ? sd[e] : -1;
     }
     if (lane == 0) overflow[row] = 1;
     return;
   }
-  int n = 0;
-  for (int e0 = 0; e0 < k0; e0 += 64) {  // seed list (entries with id < 0 are empty)
-    const int e = e0 + lane;
-    const int id = e < k0 ? i0[(int64_t)row * k0 + e] : -1;
-    const bool ok = id >= 0;
-    const unsigned long long m = __ballot(ok);
-    if (ok) {
-      const int p = n + __popcll(m & ((1ull << lane) - 1ull));
-      keys[p] = fkey(v0[(int64_t)row * k0 + e]);
-      ids[p] = id;
-    }
-    n += __popcll(m);
-  }
-  for (int e = lane; e < c; e += 64) {
-    keys[n + e] = fkey(cval[(int64_t)row * capr + e]);
-    ids[n + e] = cidx[(int64_t)row * capr + e];
-  }
-  n += c;
-  __builtin_amdgcn_wave_barrier();
-  wave_topk(keys, ids, n, k, hist, sel, tie, ov, oi);
+  // entries 0..k0-1: the running list (id < 0: empty slot, missing), then the c candidates
+  const float* cv = cval + (int64_t)row * capr - k0;
+  const int32_t* cd = cidx + (int64_t)row * capr - k0;
+  row_topk_n(
+      k0 + c, k, [&](int p) { return p < k0 ? (sd[p] >= 0 ? fkey(sv[p]) : 0u) : fkey(cv[p]); },
+      [&](int p) { return p < k0 ? sd[p] : cd[p]; }, lds + wave * TK_WAVE_WORDS, ov, oi);
 }
 
 }  // namespace rf
@@ -957,21 +1008,12 @@ extern "C" int rf_rank_reduce(int B, int ntiles, const int32_t* part_cnt, const 
   RF_LAUNCH_CHECK("rf_rank_reduce");
 }
 
-static void topk_lds_attr(const void* fn) {
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, TK_WAVES * TK_WAVE_LDS);
-}
-
 extern "C" int rf_topk_dense(int B, int n, const float* vals, int64_t ldv, const int32_t* idx, int64_t ldi,
                              int32_t idx_base, int k, float* out_v, int32_t* out_i, rf_stream_t stream) {
   RF_REQUIRE(B >= 0 && n >= 0 && n <= TK_DENSE_MAX && k > 0 && k <= TK_KMAX,
              "rf_topk_dense: n=%d must be <= %d and k=%d in [1, %d]", n, TK_DENSE_MAX, k, TK_KMAX);
   if (B == 0) return RF_OK;
-  static bool attr = false;
-  if (!attr) {
-    topk_lds_attr((const void*)k_topk_dense);
-    attr = true;
-  }
-  k_topk_dense<<<(B + TK_WAVES - 1) / TK_WAVES, 64 * TK_WAVES, TK_WAVES * TK_WAVE_LDS, as_stream(stream)>>>(
+  k_topk_dense<<<(B + TK_WAVES - 1) / TK_WAVES, 64 * TK_WAVES, 0, as_stream(stream)>>>(
       B, n, vals, ldv, idx, ldi, idx_base, k, out_v, out_i);
   RF_LAUNCH_CHECK("rf_topk_dense");
 }
@@ -982,12 +1024,7 @@ extern "C" int rf_topk_merge(int B, int k0, const float* v0, const int32_t* i0, 
   RF_REQUIRE(B >= 0 && k0 >= 0 && k0 <= TK_KMAX && capr > 0 && k > 0 && k <= TK_KMAX,
              "rf_topk_merge: bad arguments");
   if (B == 0) return RF_OK;
-  static bool attr = false;
-  if (!attr) {
-    topk_lds_attr((const void*)k_topk_merge);
-    attr = true;
-  }
-  k_topk_merge<<<(B + TK_WAVES - 1) / TK_WAVES, 64 * TK_WAVES, TK_WAVES * TK_WAVE_LDS, as_stream(stream)>>>(
+  k_topk_merge<<<(B + TK_WAVES - 1) / TK_WAVES, 64 * TK_WAVES, 0, as_stream(stream)>>>(
       B, k0, v0, i0, cval, cidx, rcnt, capr, k, out_v, out_i, overflow);
   RF_LAUNCH_CHECK("rf_topk_merge");
 }

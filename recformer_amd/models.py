@@ -280,6 +280,21 @@ def _read_count(p):
     buf, ev = p
     ev.synchronize()
     return int(buf) if buf.dim() == 0 else buf.tolist()
+# 16-bit inference: the FFN output Linear (K = 3072 -> 768, bias only, TF:1122-1130) as a plain
+# library GEMM (torch.addmm -> hipBLASLt, bf16 bias in its epilogue: autocast's Linear does the
+# same) instead of rf_gemm; the one layer GEMM without a fused epilogue worth keeping, and the one
+# shape where the library's main loop was faster on the same box (profiles/r06/gemm_c2_bar_r06a.jsonl)
+FFN2_LIBRARY = False
+
+
+def _ffn2_library(f: torch.Tensor, lw: dict, tag: str) -> torch.Tensor:
+    b = lw.get("b_2_lp")
+    if b is None:
+        b = lw["b_2_lp"] = lw["b_2"].to(f.dtype)
+    with ops._region(tag):
+        return torch.addmm(b, f, lw["w_2"].t())
+
+
 # pretraining training: the LM-head decoder + masked-LM cross entropy on the HIP kernels
 # (train._DecoderCE) for 16-bit compute; False = torch ops (F.linear + F.cross_entropy)
 DECODER_CE_HIP = True
@@ -665,7 +680,10 @@ class RecformerModel(nn.Module):
                 t = ops.gemm(ctx, w_o, lw["b_o"], ops.RF_EPI_BIAS, tag="gemm_out")
                 ops.add_layernorm_split(t, h, h_lo, lw["ln1_w"], lw["ln1_b"], eps, tag="layernorm")
                 f = ops.gemm(h, lw["w_1"], lw["b_1"], ops.RF_EPI_BIAS_GELU, tag="gemm_ffn1")
-                t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS, tag="gemm_ffn2")
+                if FFN2_LIBRARY:
+                    t2 = _ffn2_library(f, lw, "gemm_ffn2")
+                else:
+                    t2 = ops.gemm(f, lw["w_2"], lw["b_2"], ops.RF_EPI_BIAS, tag="gemm_ffn2")
                 _, _, h32 = ops.add_layernorm_split(t2, h, h_lo, lw["ln2_w"], lw["ln2_b"], eps,
                                                     planes=not last_layer,
                                                     want_f32=last_layer or output_hidden_states,

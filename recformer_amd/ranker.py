@@ -96,8 +96,10 @@ def growth_for(k: int, cap: int = TOPK_CAP) -> int:
 def _rank_family(topk: bool):
     """The rank kernel family for one self-contained ranking (label scores + rank counts from the same
     arithmetic, so the strict counts and exact ties stay the full-matrix Ranker's): the 32x32x16 loop
-    for counts only (1M x 4096: 6.96 vs 7.89 ms), the 16x16x32 one with a top-k (9.5 vs 10.5-10.8 ms;
-    gpurun_out/r04h/ab_c5.log). label_scores / shard_rank called directly follow the knob rank_w32."""
+    for counts only (1M x 4096: 6.96 vs 7.89 ms), the 16x16x32 one with a top-k (round 6, both with the
+    register top-k and the 32x32x16 candidate epilogue without spills: 125k 1.361 vs 1.456 ms, 1M 8.838
+    vs 9.419 ms; profiles/r06/c5_family_ab.jsonl). label_scores / shard_rank called directly follow the
+    knob rank_w32."""
     old = _lib.set_knob("rank_w32", 0 if topk else 1)
     try:
         yield

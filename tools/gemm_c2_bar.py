@@ -57,7 +57,9 @@ def main():
                          col_scale=0.125 if sc else 1.0, out=out)
             return f
 
+        b16 = b.bfloat16()
         legs = [("hipblaslt_plain", lambda: torch.mm(a, w.t(), out=out), ()),
+                ("hipblaslt_bias", lambda: torch.addmm(b16, a, w.t(), out=out), ()),
                 ("hip_plain", ours(ops.RF_EPI_NONE), ()),
                 ("hip_epilogue", ours(epi), ())]
         for kv in variants:

@@ -75,8 +75,8 @@ def main():
             t_top = timeit(lambda: shard_rank(q, shard, sl, 0.05, k=args.k))
             ref = shard_rank(q, shard, sl, 0.05, k=args.k)
         # A/B of the top-k plan (the same result required): growth factors x kernel families
-        for fam in filter(None, args.family.split(",")) or ([""] if args.growth else []):
-            for gr in filter(None, args.growth.split(",")) or [str(RK.TOPK_GROWTH)]:
+        for fam in [f for f in args.family.split(",") if f] or ([""] if args.growth else []):
+            for gr in [x for x in args.growth.split(",") if x] or [str(RK.TOPK_GROWTH)]:
                 old_g = RK.TOPK_GROWTH
                 RK.TOPK_GROWTH = int(gr)
                 ctx = (contextlib.nullcontext() if not fam else
