@@ -59,6 +59,15 @@ CAPTURE_MODE = "thread_local"
 # queue up beside the main stream's kernels, which the per-Linear join used to pace, and the end-of-backward
 # join waits for the whole queue)
 DEFER_DW = False
+# the optimizer update overlapped with the backward (CapturedTrainStep without a scaler, clipping,
+# accumulation or a DP bucketer): a parameter whose gradient is final (its post-accumulate hook, fired
+# once per backward) joins a pending set; every OPT_CHUNK elements the set is updated on a side stream
+# (optim.AdamW.step_params) while the backward of the layers below still runs, the rest after the
+# backward. Same kernel, same per-element arithmetic: the parameters are bit-identical to the serial step.
+# Off: measured slower (captured C3 16.24 vs 15.74 ms in one process, profiles/r06/c3_ab_overlap_opt.txt):
+# the HBM-bound update's workgroups take CUs from the backward's persistent GEMMs on the critical path
+OVERLAP_OPTIMIZER = False
+OPT_CHUNK = 4 << 20
 
 
 class GraphedForward:
@@ -246,6 +255,14 @@ class CapturedTrainStep:
         self.output = None
         self._pos = 0  # micro-batches run in the current accumulation window
         lib = _lib.load()
+        self._ov = None
+        if (OVERLAP_OPTIMIZER and scaler is None and max_grad_norm is None and bucketer is None and self.k == 1
+                and hasattr(optimizer, "step_params") and all(p.is_leaf for p in self.params)):
+            self._ov = {"on": False, "count": {}, "order": [], "chunks": None, "of": {}, "left": [],
+                        "stepped": set(), "stream": torch.cuda.Stream(dev), "hooks": []}
+            for p in self.params:
+                if p.requires_grad:
+                    self._ov["hooks"].append(p.register_post_accumulate_grad_hook(self._grad_ready))
 
         def micro(last: bool):
             """One micro-batch: forward, (scaled) backward; the last of a window also steps."""
@@ -260,14 +277,29 @@ class CapturedTrainStep:
                 out = self.scaler.scale(out)
             # the Linear weight gradients accumulate on the side stream with one join at the end of the
             # backward (train.DEFER_DW; DP bucketers' hooked parameters keep autograd's accumulation)
+            ov = self._ov
+            if ov is not None:
+                # the first backward only records the order and count of the gradient accumulations;
+                # afterwards the parameters accumulated exactly once are updated chunk by chunk as their
+                # gradients become final
+                ov["count"].clear()
+                ov["order"].clear()
+                ov["on"] = ov["chunks"] is not None
+                if ov["on"]:
+                    ov["left"] = [len(c) for c in ov["chunks"]]
+                    ov["stepped"] = set()
             with train.deferred_weight_grads(DEFER_DW):
                 if self.bucketer is not None and not last:
                     with self.bucketer.no_sync():
                         out.backward()
                 else:
                     out.backward()
+            if ov is not None and ov["chunks"] is None and not torch.cuda.is_current_stream_capturing():
+                self._plan_chunks()
             if last:
                 self._optimizer_part()
+            if ov is not None:
+                ov["on"] = False  # a backward outside the step (not this step's) must not update anything
             return loss
 
         def window():
@@ -328,8 +360,62 @@ class CapturedTrainStep:
         self.cls_global = self.cls_global and bool(getattr(lf, "_last_pruned", False))
         self.replays = 0
 
+    def _plan_chunks(self) -> None:
+        """After the counting backward: the parameters accumulated exactly once, in accumulation order,
+        cut into chunks of >= OPT_CHUNK elements; each chunk's launch plan is prepared now (outside any
+        capture)."""
+        ov = self._ov
+        chunks, cur, n = [], [], 0
+        for p in ov["order"]:
+            if ov["count"][id(p)] != 1:
+                continue
+            cur.append(p)
+            n += p.numel()
+            if n >= OPT_CHUNK:
+                chunks.append(cur)
+                cur, n = [], 0
+        if cur:
+            chunks.append(cur)
+        ov["chunks"] = chunks
+        ov["of"] = {id(p): i for i, c in enumerate(chunks) for p in c}
+        for c in chunks:
+            self.opt.prepare_params(c)
+        self.opt.prepare_params([p for p in self.params if id(p) not in ov["of"]])
+
+    def _grad_ready(self, p: torch.Tensor) -> None:
+        """Post-accumulate hook: p's gradient of this backward is complete (OVERLAP_OPTIMIZER)."""
+        ov = self._ov
+        if ov["chunks"] is None:
+            ov["count"][id(p)] = ov["count"].get(id(p), 0) + 1
+            if ov["count"][id(p)] == 1:
+                ov["order"].append(p)
+            return
+        if not ov["on"]:
+            return
+        i = ov["of"].get(id(p))
+        if i is None:
+            return
+        ov["left"][i] -= 1
+        if ov["left"][i] == 0:  # the chunk's gradients are all final: update it beside the backward
+            c = ov["chunks"][i]
+            ov["stream"].wait_stream(torch.cuda.current_stream(p.device))
+            with torch.cuda.stream(ov["stream"]):
+                self.opt.step_params(c)
+            ov["stepped"].add(i)
+
     def _optimizer_part(self):
         """Gradient exchange, unscale + clip, optimizer step, scale update, gradient zeroing."""
+        ov = self._ov
+        if ov is not None and ov["on"]:
+            # overlapped: the parameters outside the chunks (a gradient accumulated more than once, or none
+            # in the counting pass) here, a chunk that did not complete too, then the main stream joins
+            # the side stream
+            self.opt.step_params([p for p in self.params if id(p) not in ov["of"]])
+            for i, c in enumerate(ov["chunks"]):
+                if i not in ov["stepped"]:
+                    self.opt.step_params(c)
+            torch.cuda.current_stream(self.counter.device).wait_stream(ov["stream"])
+            return
         if self.bucketer is not None:
             self.bucketer.finish()
         sc = self.scaler
@@ -367,6 +453,10 @@ class CapturedTrainStep:
         if getattr(self, "graph", None) is None:
             return
         torch.cuda.synchronize(self.counter.device)
+        if self._ov is not None:
+            for h in self._ov["hooks"]:
+                h.remove()
+            self._ov = None
         for g in (self.graph_acc, self.graph):
             if g is not None:
                 g.reset()

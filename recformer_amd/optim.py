@@ -50,6 +50,18 @@ _DESC = np.dtype([("param", "<u8"), ("grad", "<u8"), ("exp_avg", "<u8"), ("exp_a
 assert _DESC.itemsize == 104
 
 
+class _Plan:
+    """One parameter subset's launch plan: the block -> tensor table and the last descriptors."""
+
+    def __init__(self):
+        self.table_key = None
+        self.first: Optional[np.ndarray] = None
+        self.table: Optional[np.ndarray] = None
+        self.blob_key = None
+        self.blob = None  # (pinned host copy, device copy) of the last descriptors
+        self.spare = None  # pinned buffer reserved for a captured step's descriptors
+
+
 class AdamW(torch.optim.Optimizer):
     """torch.optim.AdamW's interface (lr, betas, eps, weight_decay, amsgrad=False, maximize),
     one rf_adamw_step launch per step()."""
@@ -74,11 +86,9 @@ class AdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                       amsgrad=False, maximize=maximize, capturable=capturable))
         self._chunk: Optional[int] = None
-        self._table_key = None
-        self._table: Optional[np.ndarray] = None
-        self._blob_key = None
-        self._blob = None  # (pinned host copy, device copy) of the last descriptors
-        self._spare = None  # pinned buffer reserved for a captured step's descriptors
+        # launch plans (descriptor table + its host / device copies), one per parameter subset stepped:
+        # None = every parameter (step()), or the id tuple of a step_params() subset
+        self._plans = {}
         self._graph_blobs = []  # descriptor blobs a captured graph reads: kept for the optimizer's lifetime
         self._hyper = None  # device (groups, 2) fp32: lr, 1 - lr * weight_decay of each capturable group
         self._hyper_vals = None  # the host values last uploaded into _hyper
@@ -125,7 +135,38 @@ class AdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._run(None)
+        return loss
+
+    @torch.no_grad()
+    def step_params(self, params) -> None:
+        """The update of `params` alone (a subset of the groups' parameters, each updated as step() would):
+        CapturedTrainStep steps a layer's parameters while the backward of the layers below still runs.
+        No GradScaler interplay (grad_scale / found_inf are not read): the caller steps subsets only
+        without a scaler."""
+        if getattr(self, "grad_scale", None) is not None or getattr(self, "found_inf", None) is not None:
+            raise RuntimeError("recformer_amd.optim.AdamW.step_params: not with a GradScaler")
+        self._run(tuple(id(p) for p in params))
+
+    def prepare_params(self, params) -> None:
+        """Reserve step_params(params)'s launch plan outside a capture (the pinned buffer its captured
+        descriptor copy replays from), so a graph may capture that subset's first step."""
+        params = list(params)
+        pl = self._plans.get(tuple(id(p) for p in params))
+        if pl is None:
+            pl = self._plans[tuple(id(p) for p in params)] = _Plan()
+        if self._chunk is None:
+            self._chunk = int(_lib.load().rf_adamw_chunk())
+        size = len(params) * _DESC.itemsize + 4 * sum((p.numel() + self._chunk - 1) // self._chunk for p in params)
+        if pl.spare is None or pl.spare.numel() < size:
+            pl.spare = torch.empty(max(size, 1), dtype=torch.uint8, pin_memory=True)
+
+    def _run(self, subset) -> None:
         lib = _lib.load()
+        pl = self._plans.get(subset)
+        if pl is None:
+            pl = self._plans[subset] = _Plan()
+        only = None if subset is None else set(subset)
         if self._chunk is None:
             self._chunk = int(lib.rf_adamw_chunk())
         chunk = self._chunk
@@ -134,7 +175,7 @@ class AdamW(torch.optim.Optimizer):
         found_inf = getattr(self, "found_inf", None)
         if not any(g.get("capturable", False) for g in self.param_groups) and found_inf is not None:
             if float(found_inf) != 0.0:  # GradScaler's skip; host step counts must not advance
-                return loss
+                return
             found_inf = None
         rows, device, dev_steps = [], None, []
         hyper_needed = any(g.get("capturable", False) for g in self.param_groups)
@@ -146,7 +187,7 @@ class AdamW(torch.optim.Optimizer):
             if isinstance(lr, torch.Tensor):
                 lr = float(lr)
             for p in group["params"]:
-                if p.grad is None:
+                if p.grad is None or (only is not None and id(p) not in only):
                     continue
                 g = p.grad
                 if g.is_sparse:
@@ -178,22 +219,22 @@ class AdamW(torch.optim.Optimizer):
                              step_ptr, hyper_ptr, p.numel(), dec_d, b1, 1 - b1, b2, 1 - b2, eps, lr_d, step_size,
                              bc2s, 1 if group["maximize"] else 0))
         if not rows:
-            return loss
+            return
         if dev_steps:
             torch._foreach_add_(dev_steps, 1.0)
         numels = tuple(r[6] for r in rows)
-        if numels != self._table_key:
+        if numels != pl.table_key:
             nblk = np.array([(n + chunk - 1) // chunk for n in numels], dtype=np.int64)
-            self._first = np.concatenate([[0], np.cumsum(nblk)[:-1]]).astype(np.int64)
-            self._table = np.repeat(np.arange(len(numels), dtype=np.int32), nblk)
-            self._table_key = numels
+            pl.first = np.concatenate([[0], np.cumsum(nblk)[:-1]]).astype(np.int64)
+            pl.table = np.repeat(np.arange(len(numels), dtype=np.int32), nblk)
+            pl.table_key = numels
         stream = torch.cuda.current_stream(device).cuda_stream
         capturing = torch.cuda.is_current_stream_capturing()
         key = tuple(rows) if dev_steps else None
-        if key is not None and key == self._blob_key:
+        if key is not None and key == pl.blob_key:
             # capturable and nothing changed: the device descriptors of the last step stand (no copy,
             # so nothing host-side enters a captured graph)
-            base, nd = self._blob[1].data_ptr(), len(rows)
+            base, nd = pl.blob[1].data_ptr(), len(rows)
         else:
             d = np.zeros(len(rows), dtype=_DESC)
             cols = list(zip(*rows))
@@ -201,41 +242,40 @@ class AdamW(torch.optim.Optimizer):
                      "beta2", "w2", "eps", "lr", "step_size", "bc2_sqrt", "maximize")
             for name, col in zip(names, cols):
                 d[name] = col
-            d["first_block"] = self._first
+            d["first_block"] = pl.first
             # one host->device copy: descriptors then the block -> tensor table, from pinned memory kept
             # with the device copy (a captured graph replays the copy from it). Pinned memory cannot be
             # allocated while a stream captures: uncaptured steps stage through a fresh pinned tensor
             # (torch's host allocator guards its reuse) and keep one spare, unused buffer for a capture.
-            blob = np.concatenate([d.view(np.uint8), self._table.view(np.uint8)])
+            blob = np.concatenate([d.view(np.uint8), pl.table.view(np.uint8)])
             if capturing:
-                host = self._spare
+                host = pl.spare
                 if host is None or host.numel() < blob.size:
                     raise RuntimeError("recformer_amd.optim.AdamW: run one uncaptured step before capturing")
-                self._spare = None
+                pl.spare = None
                 host = host[: blob.size]
                 host.numpy()[:] = blob
             else:
                 host = torch.from_numpy(blob).pin_memory()
-                if self._spare is None or self._spare.numel() < blob.size:
-                    self._spare = torch.empty(blob.size, dtype=torch.uint8, pin_memory=True)
+                if pl.spare is None or pl.spare.numel() < blob.size:
+                    pl.spare = torch.empty(blob.size, dtype=torch.uint8, pin_memory=True)
             dev_blob = torch.empty(blob.size, dtype=torch.uint8, device=device)
             dev_blob.copy_(host, non_blocking=True)
-            self._blob, self._blob_key = (host, dev_blob), key
+            pl.blob, pl.blob_key = (host, dev_blob), key
             base, nd = dev_blob.data_ptr(), len(rows)
-        if capturing and not any(b is self._blob for b in self._graph_blobs):
+        if capturing and not any(b is pl.blob for b in self._graph_blobs):
             # a graph replays from these (the pinned source of its descriptor copy, or the device
             # descriptors it reuses): neither may return to torch's caching allocators while the
-            # optimizer lives, whatever later uncaptured steps do with _blob
-            self._graph_blobs.append(self._blob)
+            # optimizer lives, whatever later uncaptured steps do with the plan's blob
+            self._graph_blobs.append(pl.blob)
         gs = grad_scale.data_ptr() if grad_scale is not None else 0
         fi = found_inf.data_ptr() if found_inf is not None else 0
         for t in (grad_scale, found_inf):
             if t is not None and (t.dtype != torch.float32 or t.device != device or t.numel() != 1):
                 raise ValueError("recformer_amd.optim.AdamW: grad_scale / found_inf must be fp32 scalars on the "
                                  "parameters' device")
-        check(lib.rf_adamw_step_amp(base, nd, base + nd * _DESC.itemsize, int(self._table.size), gs, fi, stream),
+        check(lib.rf_adamw_step_amp(base, nd, base + nd * _DESC.itemsize, int(pl.table.size), gs, fi, stream),
               "rf_adamw_step")
         if dev_steps and found_inf is not None:
             torch._foreach_sub_(dev_steps, [found_inf] * len(dev_steps))  # a skipped step is not counted
         self._launches += 1
-        return loss

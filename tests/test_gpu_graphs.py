@@ -348,3 +348,29 @@ def test_captured_dp_step_nccl_single_rank(dev, wire):
         if step is not None:
             step.close()  # the captured RCCL kernels go before their communicator
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("chunk", [1000, 1 << 30])
+def test_overlapped_optimizer_bit_identical(dev, chunk, monkeypatch):
+    """graphs.OVERLAP_OPTIMIZER: the AdamW update of each chunk of parameters whose gradients are final runs
+    on a side stream during the backward (optim.AdamW.step_params); the parameters after the captured
+    steps are bit-identical to the serial step's (small chunks: many launches beside the backward)."""
+    batch = _batch(dev)
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(graphs, "OVERLAP_OPTIMIZER", on)
+        monkeypatch.setattr(graphs, "OPT_CHUNK", chunk)
+        a = _model(dev)
+        oa = AdamW([p for p in a.parameters() if p.requires_grad], lr=1e-3, weight_decay=0.01, capturable=True)
+        step = graphs.CapturedTrainStep(a, oa, batch, warmup=2)
+        assert (step._ov is not None) == on
+        if on:
+            assert len(step._ov["chunks"]) >= (2 if chunk == 1000 else 1)
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        res.append([p.detach().clone() for p in a.parameters()])
+        assert all(float(s["step"]) == 5.0 for s in oa.state.values())
+        step.close()
+    for pa, pb in zip(*res):
+        assert torch.equal(pa, pb)
