@@ -1,6 +1,6 @@
 """C2 forward steps (bench.py's workload: RecformerForSeqRec encode + score, 12L/768d, L = 1024, B = 64, fp32
 parameters under autocast bf16) with library knobs from RF_KNOBS, for kernel traces of one setting per
-process (tools/gpu/band_trace.sh):
+process (tools/gpu/run.sh bandab):
 
     RF_KNOBS=band_path=3 python tools/c2_steps.py [steps] [warmup]
 """

@@ -20,6 +20,11 @@
 #              "r03 r04") against the working tree, every row through the last layer, order A B C C B A
 #   gemmpmc    the four C2 GEMMs alone (tools/gemm_pmc.py): kernel trace + SQ wait / instruction / LDS and
 #              HBM-byte PMC passes, one rocprofv3 run per pass
+#   gemmbar    same-box GEMM bar at the C2 shapes: hipBLASLt plain / bias vs the HIP kernels, legs round-robin
+#              in one process, knob variants from $KNOBS (tools/gemm_c2_bar.py)
+#   bandab     band attention pipe2 vs pipe3 (knob band_path 0 / 3): kernel traces of C2 steps, ABBA by process
+#   c5ab       C5 retrieval, rank kernel families w16 / w32 with the top-k, same results required, plus a
+#              kernel trace of the 125k shard (tools/retrieval_bench.py --family, tools/trace_seq.py)
 #   ab32       same-process A/B of the 32x32x16 GEMM kernel (knob gemm_mfma32): C2 forward, captured C3;
 #              C5 retrieval with the 32x32x16 rank kernel (knob rank_w32) alternated by process
 set -o pipefail
@@ -152,6 +157,25 @@ print(json.dumps({'tree': '$t', 'value': d['value'], 'ms_per_step': d['ms_per_st
       python3 tools/retrieval_bench.py > $O/retrieval_trace.log 2>&1 || fail $O/retrieval_trace.log 20
     timeout -k 10 600 python tools/catalog_bench.py > $O/catalog.log 2>&1 || fail $O/catalog.log 20
     tail -2 $O/catalog.log ;;
+  gemmbar)
+    timeout -k 10 400 python tools/gemm_c2_bar.py ${KNOBS:-} > $O/bar.jsonl 2>&1 || fail $O/bar.jsonl
+    cut -c1-160 $O/bar.jsonl ;;
+  bandab)
+    for run in 0a 3a 3b 0b; do
+      bp=${run:0:1}
+      ( cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && RF_KNOBS=band_path=$bp timeout -k 10 300 \
+        rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$run -o c2 -- python3 tools/c2_steps.py 40 10 \
+        > $O/run_$run.log 2>&1 ) || fail $O/run_$run.log
+      grep ms/step $O/run_$run.log
+      python3 tools/summarize_profile.py $O/trace_$run --config 64,1024,12 > $O/summary_$run.txt 2>&1 || true
+    done ;;
+  c5ab)
+    timeout -k 10 400 python tools/retrieval_bench.py --family w16,w32 > $O/retrieval.log 2>&1 || fail $O/retrieval.log
+    grep -E '"ms"' $O/retrieval.log | cut -c1-200
+    ( cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 300 rocprofv3 --kernel-trace \
+      --output-format csv -d $O/trace -o r -- python3 tools/retrieval_bench.py --items 125000 > $O/trace.log 2>&1 ) \
+      || fail $O/trace.log
+    python3 tools/trace_seq.py $O/trace/r_kernel_trace.csv 0 45 | tail -36 ;;
   torchops)
     timeout -k 10 300 python tools/torch_ops_trace.py > $O/torchops.txt 2>&1 || fail $O/torchops.txt 20
     head -80 $O/torchops.txt ;;
