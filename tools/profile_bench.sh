@@ -3,7 +3,9 @@
 # bench run; writes gpurun_out/prof_<tag>/ and a per-kernel summary JSON.
 set -e
 TAG=${1:-r01}
-ARGS="--steps ${PROF_STEPS:-30} --warmup 10 --cpu-baseline-seconds 0 --no-kernel-timing ${BENCH_ARGS:-}"
+# no batch sweep under the profiler: its replayed HIP graphs crash rocprofv3's PMC passes (SIGSEGV in
+# CUDAGraph.replay, gpurun_out/prof_r06f/fetch.log), and the sweep is not the profiled workload
+ARGS="--steps ${PROF_STEPS:-30} --warmup 10 --cpu-baseline-seconds 0 --no-kernel-timing --batch-sweep= ${BENCH_ARGS:-}"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
