@@ -729,12 +729,76 @@ __device__ __forceinline__ void rank_selected(const uint32_t* sk, const int32_t*
   }
 }
 
+// The threshold search and the selection over keys held S per lane (entry j * 64 + lane; key 0 =
+// missing), kk <= #valid keys, lo / hi bounds of the kk-th largest key (wave-uniform): tau = the largest
+// t with #{key >= t} >= kk by a binary search whose counts are ballots (one compare and one popcount per
+// register, no LDS, no atomics; it stops once exactly kk keys reach t), then the keys above tau and the
+// lowest-id ties compacted into sk / si (ties' ids through tieb) and ranked. pos_of(j) is the entry's
+// position in the row (its id through id_at).
+template <int S, typename PosOf, typename IdAt>
+__device__ __forceinline__ void search_select(const uint32_t (&key)[S], int kk, bool exact, uint32_t lo, uint32_t hi,
+                                              PosOf pos_of, IdAt id_at, uint32_t* sk, int32_t* si, int32_t* tieb,
+                                              float* out_v, int32_t* out_i) {
+  const int lane = threadIdx.x & 63;
+  while (!exact && lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1) + 1u;  // in (lo, hi]
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) c += __popcll(__ballot(key[j] >= mid));
+    if (c >= kk) {
+      lo = mid;
+      exact = c == kk;
+    } else {
+      hi = mid - 1u;
+    }
+  }
+  const uint32_t tau = lo;
+  int ngt = 0, nt = 0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const bool g = key[j] != 0u && (exact ? key[j] >= tau : key[j] > tau);
+    const bool q = !exact && key[j] == tau;
+    const uint64_t mg = __ballot(g), mq = __ballot(q);
+    if (g) {
+      const int o = ngt + lanes_below(mg);
+      sk[o] = key[j];
+      si[o] = id_at(pos_of(j));
+    }
+    if (q) tieb[nt + lanes_below(mq)] = id_at(pos_of(j));
+    ngt += __popcll(mg);
+    nt += __popcll(mq);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int need = kk - ngt;
+  if (need > 0) {  // the `need` ties with the lowest ids (all of them when nt == need)
+    for (int a = lane; a < nt; a += 64) {
+      const int ia = tieb[a];
+      int r = a;
+      if (nt > need) {
+        r = 0;
+        for (int b = 0; b < nt && r < need; ++b) r += tieb[b] < ia ? 1 : 0;
+      }
+      if (r < need) {
+        sk[ngt + r] = tau;
+        si[ngt + r] = ia;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (kk <= 64) rank_selected<1>(sk, si, kk, out_v, out_i);
+  else if (kk <= 128) rank_selected<2>(sk, si, kk, out_v, out_i);
+  else rank_selected<4>(sk, si, kk, out_v, out_i);
+}
+
+constexpr int TK_CMAX = 256;  // compacted candidates of a long row (keys, then positions, in front of the ties)
+
 // Top-k of one row's n entries (entry p at key_at(p), id_at(p); key 0 = missing): values descending,
-// ties by lower id; missing outputs (-inf, -1). The n keys sit in registers, S per lane (entry
-// j * 64 + lane), so the k-th largest key is found by a binary search over the key range whose
-// counts are ballots (#{key >= t}: one compare and one popcount per register, wave-uniform, no LDS,
-// no atomics; it stops early once exactly k keys reach t). The entries above the threshold, then the
-// lowest-id ties, are compacted into LDS and ranked against each other through lane reads.
+// ties by lower id; missing outputs (-inf, -1). The n keys sit in registers, S per lane. Long rows
+// (S >= 16) with kk <= 64 first narrow the range: the kk-th largest of the 64 lane maxima is a lower
+// bound of the kk-th largest key (the lane maxima are a subset of the keys), found by the same search
+// over one register; the keys at or above it — a few percent of a dense row — are compacted into LDS
+// and the search and selection run on those, four registers per lane instead of S (rows with more than
+// TK_CMAX of them keep the full form). Same tau, same selection: bit-identical either way.
 template <int S, typename KeyAt, typename IdAt>
 __device__ __forceinline__ void row_topk(int n, int k, KeyAt key_at, IdAt id_at, uint32_t* sk, int32_t* si,
                                          int32_t* tid, float* out_v, int32_t* out_i) {
@@ -759,57 +823,51 @@ __device__ __forceinline__ void row_topk(int n, int k, KeyAt key_at, IdAt id_at,
   if (kk > 0) {
     lo = __builtin_amdgcn_readfirstlane(wave_min_u(lo));
     hi = __builtin_amdgcn_readfirstlane(wave_max_u(hi));
-    // tau: the largest t with #{key >= t} >= kk, i.e. the kk-th largest key; `exact`: #{key >= tau} == kk
-    bool exact = nv == kk;
-    while (!exact && lo < hi) {
-      const uint32_t mid = lo + ((hi - lo) >> 1) + 1u;  // in (lo, hi]
-      int c = 0;
+    bool done = false;
+    if (S >= 16 && kk <= 64 && nv > kk) {
+      uint32_t lm = 0u;
 #pragma unroll
-      for (int j = 0; j < S; ++j) c += __popcll(__ballot(key[j] >= mid));
-      if (c >= kk) {
-        lo = mid;
-        exact = c == kk;
-      } else {
-        hi = mid - 1u;
+      for (int j = 0; j < S; ++j) lm = max(lm, key[j]);
+      uint32_t a = lo, b = hi;  // the kk-th largest lane maximum (a lane without keys holds 0 < lo)
+      while (a < b) {
+        const uint32_t mid = a + ((b - a) >> 1) + 1u;
+        if (__popcll(__ballot(lm >= mid)) >= kk) a = mid;
+        else b = mid - 1u;
       }
-    }
-    const uint32_t tau = lo;
-    int ngt = 0, nt = 0;
+      int c0 = 0;
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
-      const int p = j * 64 + lane;
-      const bool g = key[j] != 0u && (exact ? key[j] >= tau : key[j] > tau);
-      const bool q = !exact && key[j] == tau;
-      const uint64_t mg = __ballot(g), mq = __ballot(q);
-      if (g) {
-        const int o = ngt + lanes_below(mg);
-        sk[o] = key[j];
-        si[o] = id_at(p);
-      }
-      if (q) tid[nt + lanes_below(mq)] = id_at(p);
-      ngt += __popcll(mg);
-      nt += __popcll(mq);
-    }
-    __builtin_amdgcn_wave_barrier();
-    const int need = kk - ngt;
-    if (need > 0) {  // the `need` ties with the lowest ids (all of them when nt == need)
-      for (int a = lane; a < nt; a += 64) {
-        const int ia = tid[a];
-        int r = a;
-        if (nt > need) {
-          r = 0;
-          for (int b = 0; b < nt && r < need; ++b) r += tid[b] < ia ? 1 : 0;
+      for (int j = 0; j < S; ++j) c0 += __popcll(__ballot(key[j] >= a));
+      if (c0 <= TK_CMAX) {
+        uint32_t* ck = reinterpret_cast<uint32_t*>(tid);
+        int32_t* cp = tid + TK_CMAX;
+        int o = 0;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          const bool g = key[j] >= a;
+          const uint64_t m = __ballot(g);
+          if (g) {
+            const int e = o + lanes_below(m);
+            ck[e] = key[j];
+            cp[e] = j * 64 + lane;
+          }
+          o += __popcll(m);
         }
-        if (r < need) {
-          sk[ngt + r] = tau;
-          si[ngt + r] = ia;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t k2[TK_CMAX / 64];
+#pragma unroll
+        for (int t = 0; t < TK_CMAX / 64; ++t) {
+          const int e = t * 64 + lane;
+          k2[t] = e < c0 ? ck[e] : 0u;
         }
+        search_select<TK_CMAX / 64>(
+            k2, kk, c0 == kk, a, hi, [&](int t) { return cp[t * 64 + lane]; }, id_at, sk, si, tid + 2 * TK_CMAX,
+            out_v, out_i);
+        done = true;
       }
-      __builtin_amdgcn_wave_barrier();
     }
-    if (kk <= 64) rank_selected<1>(sk, si, kk, out_v, out_i);
-    else if (kk <= 128) rank_selected<2>(sk, si, kk, out_v, out_i);
-    else rank_selected<4>(sk, si, kk, out_v, out_i);
+    if (!done)
+      search_select<S>(key, kk, nv == kk, lo, hi, [&](int j) { return j * 64 + lane; }, id_at, sk, si, tid, out_v,
+                       out_i);
   }
   for (int a = kk + lane; a < k; a += 64) {
     out_v[a] = -__builtin_inff();
